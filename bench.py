@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MF-SGD param updates/s, 10M users x 1M items, rank 64.
+
+Metric and config from BASELINE.json: "param updates/sec (whole node), MF-SGD
+10M x 1M rank-64 at 1/2/4/8 MI355X".  One update = one rating-SGD step
+(one user row + one item row of 64 fp32 each).  Synthetic ratings, random
+init, fp32 parameters and compute (``--wire bf16`` optionally halves the
+all-to-all bytes at N > 1; default fp32).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Weak scaling: every GPU processes ``--batch`` ratings per step (its users'
+ratings, as ``psOnlineMF`` partitions input by ``user % W``); value = total
+updates/s over all GPUs, timed between barriers + device syncs, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1 << 22, help="ratings per GPU per step")
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--pool", type=int, default=8, help="data pool = pool * batch ratings per GPU")
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from flink_parameter_server_1_amd import ops
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    if comm.device.type == "cuda" and not ops.native_available():
+        raise RuntimeError("gfx950 kernel library not built: run python csrc/build.py")
+    n = comm.world
+    if a.gpus != n:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
+                   user_update=a.user_update)
+    model = DistributedMF(cfg, comm)
+    data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
+    dev = comm.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    step = 0
+    for _ in range(a.warmup):
+        model.step(*data.batch(step, a.batch))
+        step += 1
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        model.step(*data.batch(step, a.batch))
+        step += 1
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt_max = comm.max_over_ranks(dt)
+    total_updates = a.batch * a.steps * n
+    value = total_updates / dt_max
+    if comm.rank == 0:
+        out = {
+            "metric": "param updates/sec (whole node), MF-SGD 10Mx1M rank-64",
+            "value": value,
+            "unit": "updates/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt_max / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (uniform users/items, U[0,1) ratings; random-init U[-0.01,0.01) factors)",
+            "config": {
+                "model": f"mf-sgd users={a.users} items={a.items} rank={a.dim}",
+                "global_batch": a.batch * n,
+                "seq_len": None,
+                "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded)",
+                "wire_dtype": a.wire if n > 1 else "none (local PS shard)",
+                "scalar_params_per_s": value * 2 * a.dim,
+                "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
+                if n > 1 else None,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

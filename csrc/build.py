@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Build the native libraries in-tree (no JIT cache, no hipify).
+
+* ``libfps_kernels.so`` — every ``csrc/kernels/*.hip`` compiled by
+  ``hipcc --offload-arch=gfx950`` into one shared object exposing a C ABI
+  (``fps_*`` launchers taking device pointers + a ``hipStream_t``).  Loaded
+  with ctypes by ``flink_parameter_server_1_amd.ops`` *after* torch, so the
+  HIP runtime torch already loaded (same SONAME ``libamdhip64.so.7``) serves it.
+* ``libfps_host.so`` — ``csrc/host/*.cpp`` (C++17, g++): the host runtime
+  pieces (synthetic data generators, ``id;value`` text codec, sharded
+  hash store, ...).
+
+Usage: ``python csrc/build.py [--force] [--only kernels|host]``.
+Outputs land in ``flink_parameter_server_1_amd/_lib/``.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "flink_parameter_server_1_amd", "_lib")
+ARCH = os.environ.get("FPS_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm not installed?)")
+
+
+def _digest(paths, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _up_to_date(target: str, digest: str) -> bool:
+    stamp = target + ".stamp"
+    return os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == digest
+
+
+def _write_stamp(target: str, digest: str):
+    with open(target + ".stamp", "w") as f:
+        f.write(digest + "\n")
+
+
+def build_kernels(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    target = os.path.join(OUT, "libfps_kernels.so")
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels")]
+    digest = _digest(srcs + hdrs, " ".join(flags))
+    if not force and _up_to_date(target, digest):
+        return target
+    cmd = [_hipcc()] + flags + srcs + ["-o", target + ".tmp"]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(target + ".tmp", target)
+    _write_stamp(target, digest)
+    return target
+
+
+def build_host(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
+    target = os.path.join(OUT, "libfps_host.so")
+    if not srcs:
+        return ""
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-march=x86-64-v2", "-I",
+             os.path.join(CSRC, "host")]
+    digest = _digest(srcs + hdrs, cxx + " ".join(flags))
+    if not force and _up_to_date(target, digest):
+        return target
+    cmd = [cxx] + flags + srcs + ["-o", target + ".tmp"]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(target + ".tmp", target)
+    _write_stamp(target, digest)
+    return target
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["kernels", "host"])
+    a = ap.parse_args(argv)
+    if a.only in (None, "kernels"):
+        print(build_kernels(a.force))
+    if a.only in (None, "host"):
+        print(build_host(a.force))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

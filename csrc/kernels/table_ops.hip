@@ -1,0 +1,269 @@
+// PS shard table kernels (gfx950): init, pull-serve gather, push apply,
+// per-step key de-duplication + bucketing for the all-to-all.
+//
+//   K9  init_rows      -- deterministic hash-RNG init by global id
+//   K2  gather_rows    -- pull serve: rows of the HBM shard -> wire buffer
+//   K3  apply_rows     -- push apply: add / set / sgd / adagrad
+//   K1  dedup_*        -- unique keys per destination shard + slot per request
+//
+// Row layout: a row of D fp32 is owned by TPR lanes (TPR = pow2 >= D, <= 64),
+// NV = ceil(D / TPR) values per lane.  D = 64 -> one float per lane, one
+// 256-B coalesced transaction per row and per atomic wave-instruction.
+#include "common.h"
+
+using namespace fps;
+
+namespace {
+
+template <int TPR>
+__device__ __forceinline__ void row_coords(int64_t& first, int64_t& step, int& j0) {
+  constexpr int RPW = 64 / TPR;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  first = wave * RPW + lane / TPR;
+  step = nwaves * RPW;
+  j0 = lane % TPR;
+}
+
+template <int TPR>
+__global__ void __launch_bounds__(256) init_rows_kernel(float* __restrict__ table, int64_t n_rows, int D,
+                                                        int64_t id_base, int64_t id_stride, float lo, float hi,
+                                                        uint32_t seed) {
+  int64_t r, step; int j0;
+  row_coords<TPR>(r, step, j0);
+  const float span = hi - lo;
+  for (; r < n_rows; r += step) {
+    const int64_t gid = id_base + r * id_stride;
+    float* row = table + r * (int64_t)D;
+    for (int j = j0; j < D; j += TPR) row[j] = lo + span * hash_uniform(seed, gid, (uint32_t)j);
+  }
+}
+
+template <int TPR, bool OUT_BF16, typename IDX>
+__global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, const IDX* __restrict__ idx,
+                                                          int64_t n, int D, void* __restrict__ out,
+                                                          uint8_t* __restrict__ touched) {
+  int64_t r, step; int j0;
+  row_coords<TPR>(r, step, j0);
+  for (; r < n; r += step) {
+    const int64_t row = (int64_t)idx[r];
+    const float* src = table + row * D;
+    if (OUT_BF16) {
+      uint16_t* dst = (uint16_t*)out + r * D;
+      for (int j = j0; j < D; j += TPR) dst[j] = f32_to_bf16(src[j]);
+    } else {
+      float* dst = (float*)out + r * D;
+      for (int j = j0; j < D; j += TPR) dst[j] = src[j];
+    }
+    if (touched != nullptr && j0 == 0) touched[row] = 1;
+  }
+}
+
+// op: 0 = add (atomic), 1 = set, 2 = sgd w -= lr*g (atomic), 3 = adagrad
+// (acc += g^2, w -= lr*g/sqrt(acc+eps); keys must be unique in the launch).
+template <int TPR, bool IN_BF16, int OP>
+__global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ table, float* __restrict__ state,
+                                                         const int32_t* __restrict__ idx, int64_t n, int D,
+                                                         const void* __restrict__ delta, float lr, float eps,
+                                                         uint8_t* __restrict__ touched) {
+  int64_t r, step; int j0;
+  row_coords<TPR>(r, step, j0);
+  for (; r < n; r += step) {
+    const int64_t row = (int64_t)idx[r];
+    if (row < 0) continue;  // padding slot
+    float* dst = table + row * D;
+    for (int j = j0; j < D; j += TPR) {
+      float g = IN_BF16 ? bf16_to_f32(((const uint16_t*)delta)[r * D + j]) : ((const float*)delta)[r * D + j];
+      if (OP == 0) {
+        atomic_add_noret(dst + j, g);
+      } else if (OP == 1) {
+        dst[j] = g;
+      } else if (OP == 2) {
+        atomic_add_noret(dst + j, -lr * g);
+      } else {
+        float* acc = state + row * D + j;
+        float a = *acc + g * g;
+        *acc = a;
+        dst[j] -= lr * g * rsqrtf(a + eps);
+      }
+    }
+    if (touched != nullptr && j0 == 0) touched[row] = 1;
+  }
+}
+
+// ---- de-duplication of request keys (one step, epoch-tagged map, no spins)
+// map[key] = epoch << 32 | (0xffffffff - owner_request_index); atomicMax makes
+// the newest epoch win and, inside it, the smallest request index.
+__global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, int64_t n, unsigned long long* __restrict__ map,
+                                   uint32_t epoch) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[b];
+    const unsigned long long v = ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (uint32_t)b);
+    atomicMax(map + k, v);
+  }
+}
+
+// owners take a slot inside their destination shard's group
+__device__ __forceinline__ void key_dest(int32_t k, int W, int part_kind, int64_t block, int& d, int32_t& local) {
+  if (part_kind == 0) { d = k % W; local = k / W; }
+  else { d = (int)(k / block); if (d >= W) d = W - 1; local = (int32_t)(k - (int64_t)d * block); }
+}
+
+__global__ void dedup_assign_kernel(const int32_t* __restrict__ keys, int64_t n, const unsigned long long* __restrict__ map,
+                                    int W, int part_kind, int64_t block, int32_t* __restrict__ counts,
+                                    int32_t* __restrict__ owner_slot) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[b];
+    const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+    if (owner != (uint32_t)b) continue;
+    int d; int32_t local;
+    key_dest(k, W, part_kind, block, d, local);
+    owner_slot[b] = atomicAdd(counts + d, 1);
+  }
+}
+
+// exclusive prefix of the W counts (W <= 1024; one tiny block)
+__global__ void dedup_scan_kernel(const int32_t* __restrict__ counts, int W, int32_t* __restrict__ prefix) {
+  if (threadIdx.x == 0) {
+    int32_t acc = 0;
+    for (int d = 0; d < W; ++d) { prefix[d] = acc; acc += counts[d]; }
+    prefix[W] = acc;
+  }
+}
+
+// compact position of every request; owners also write their unique local
+// key, so uniq[0:total] is grouped by destination shard in ascending order
+__global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, int64_t n, const unsigned long long* __restrict__ map,
+                                     int W, int part_kind, int64_t block, const int32_t* __restrict__ prefix,
+                                     const int32_t* __restrict__ owner_slot, int32_t* __restrict__ uniq,
+                                     int32_t* __restrict__ pos) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[b];
+    const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+    int d; int32_t local;
+    key_dest(k, W, part_kind, block, d, local);
+    const int32_t p = prefix[d] + owner_slot[owner];
+    pos[b] = p;
+    if (owner == (uint32_t)b) uniq[p] = local;
+  }
+}
+
+// shard id + per-shard count + stable rank inside the shard, for callers
+// that ship raw (non-deduplicated) keys.
+__global__ void bucketize_kernel(const int32_t* __restrict__ keys, int64_t n, int W, int part_kind, int64_t block,
+                                 int32_t* __restrict__ shard, int32_t* __restrict__ counts) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[b] < 0 ? -keys[b] : keys[b];
+    int d;
+    if (part_kind == 0) d = k % W;
+    else { d = (int)(k / block); if (d >= W) d = W - 1; }
+    shard[b] = d;
+    atomicAdd(counts + d, 1);
+  }
+}
+
+}  // namespace
+
+#define TPR_SWITCH(D, ...)                                   \
+  do {                                                       \
+    if ((D) <= 4) { constexpr int TPR = 4; __VA_ARGS__; }     \
+    else if ((D) <= 8) { constexpr int TPR = 8; __VA_ARGS__; } \
+    else if ((D) <= 16) { constexpr int TPR = 16; __VA_ARGS__; } \
+    else if ((D) <= 32) { constexpr int TPR = 32; __VA_ARGS__; } \
+    else { constexpr int TPR = 64; __VA_ARGS__; }            \
+  } while (0)
+
+static inline int rows_grid(int64_t n, int TPR) {
+  const int64_t rows_per_block = 4 * (64 / TPR);  // 256 threads = 4 waves
+  return grid_for(n, (int)rows_per_block, 256 * 32);
+}
+
+FPS_API int fps_init_rows(float* table, int64_t n_rows, int D, int64_t id_base, int64_t id_stride, float lo, float hi,
+                          uint32_t seed, void* stream) {
+  if (n_rows <= 0) return 0;
+  TPR_SWITCH(D, hipLaunchKernelGGL(init_rows_kernel<TPR>, dim3(rows_grid(n_rows, TPR)), dim3(256), 0,
+                                   (hipStream_t)stream, table, n_rows, D, id_base, id_stride, lo, hi, seed));
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int fps_gather_rows(const float* table, const void* idx, int idx_is_64, int64_t n, int D, void* out,
+                            int out_bf16, uint8_t* touched, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  TPR_SWITCH(D, {
+    const int g = rows_grid(n, TPR);
+    if (idx_is_64) {
+      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched);
+      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched);
+    } else {
+      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched);
+      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched);
+    }
+  });
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int TPR>
+static void launch_apply(float* table, float* state, const int32_t* idx, int64_t n, int D, const void* delta,
+                         int delta_bf16, int op, float lr, float eps, uint8_t* touched, hipStream_t s) {
+  const int g = rows_grid(n, TPR);
+  if (delta_bf16) {
+    switch (op) {
+      case 0: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 0>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      default: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
+    }
+  } else {
+    switch (op) {
+      case 0: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 0>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      default: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
+    }
+  }
+}
+
+FPS_API int fps_apply_rows(float* table, float* state, const int32_t* idx, int64_t n, int D, const void* delta,
+                           int delta_bf16, int op, float lr, float eps, uint8_t* touched, void* stream) {
+  if (n <= 0) return 0;
+  if (op == 3 && state == nullptr) return (int)hipErrorInvalidValue;
+  TPR_SWITCH(D, launch_apply<TPR>(table, state, idx, n, D, delta, delta_bf16, op, lr, eps, touched, (hipStream_t)stream));
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// counts[W] must be zeroed by the caller; prefix has W+1 entries
+// (prefix[W] = number of unique keys); uniq/pos/owner_slot have n entries.
+FPS_API int fps_dedup(const int32_t* keys, int64_t n, unsigned long long* map, uint32_t epoch, int W, int part_kind,
+                      int64_t block, int32_t* counts, int32_t* prefix, int32_t* owner_slot, int32_t* uniq,
+                      int32_t* pos, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int g = grid_for(n > 0 ? n : 1, 256, 256 * 16);
+  if (n > 0) {
+    hipLaunchKernelGGL(dedup_claim_kernel, dim3(g), dim3(256), 0, s, keys, n, map, epoch);
+    hipLaunchKernelGGL(dedup_assign_kernel, dim3(g), dim3(256), 0, s, keys, n, (const unsigned long long*)map, W,
+                       part_kind, block, counts, owner_slot);
+  }
+  hipLaunchKernelGGL(dedup_scan_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)counts, W, prefix);
+  if (n > 0)
+    hipLaunchKernelGGL(dedup_resolve_kernel, dim3(g), dim3(256), 0, s, keys, n, (const unsigned long long*)map, W,
+                       part_kind, block, (const int32_t*)prefix, (const int32_t*)owner_slot, uniq, pos);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int fps_bucketize(const int32_t* keys, int64_t n, int W, int part_kind, int64_t block, int32_t* shard,
+                          int32_t* counts, void* stream) {
+  if (n <= 0) return 0;
+  const int g = grid_for(n, 256, 256 * 16);
+  hipLaunchKernelGGL(bucketize_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, keys, n, W, part_kind, block, shard,
+                     counts);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int fps_abi_version() { return 1; }

@@ -1,0 +1,152 @@
+"""Online MF-SGD on the tensor engine (the north-star workload).
+
+Same model and data flow as ``psOnlineMF``
+(``M/matrix/factorization/PSOnlineMatrixFactorization.scala:39-75``):
+
+* ratings are partitioned by ``user % W`` (``:62-64``), so each worker owns
+  the user vectors of its users (worker-resident table, P3);
+* item vectors live on the PS, hash-sharded ``item % W``, updated by pushing
+  deltas that the PS adds (``SimplePSLogic`` with vector sum, ``:58-60``);
+* per rating: ``e = r - u.i``, ``u += lr*e*i``, push ``lr*e*u`` to the item
+  (``SGDUpdater``), init U[-0.01, 0.01) (``RangedRandomFactorInitializer``).
+
+Execution per micro-batch of B ratings on each GPU:
+
+* ``W == 1`` — the item shard is local: one fused kernel reads u and i,
+  stores u (Hogwild inside the batch; optional atomics) and atomically adds
+  di into the item row (``ops.mf_sgd_local``).  No wire buffers at all.
+* ``W > 1`` — ``TensorPS.pull`` (dedup + 2 all-to-alls), fused SGD on the
+  pulled rows accumulating per-unique-item deltas (``ops.mf_sgd_pulled``),
+  ``TensorPS.push`` (all-to-all + atomic apply).
+
+Throughput unit: rating-SGD updates/s (each updates one user row and one item
+row of ``dim`` floats), see BASELINE.md.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from ... import ops
+from ...parallel.comm import Comm
+from ...parallel.table import ShardedTable
+from ...parallel.tensor_ps import TensorPS
+
+
+@dataclass
+class MFConfig:
+    num_users: int = 10_000_000
+    num_items: int = 1_000_000
+    dim: int = 64
+    learning_rate: float = 0.01
+    lam: float = 0.0
+    range_min: float = -0.01
+    range_max: float = 0.01
+    seed: int = 0
+    user_update: str = "store"        # "store" (Hogwild) | "atomic"
+    wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
+
+
+_WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+class DistributedMF:
+    def __init__(self, cfg: MFConfig, comm: Optional[Comm] = None):
+        self.cfg = cfg
+        self.comm = comm or Comm()
+        W, r, dev = self.comm.world, self.comm.rank, self.comm.device
+        init = ("uniform", cfg.range_min, cfg.range_max)
+        # worker-resident user shard: users u with u % W == r, local row u // W
+        self.users = ShardedTable(cfg.num_users, cfg.dim, r, W, "hash", init, cfg.seed, dev, track_touched=False)
+        # PS item shard
+        self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.seed + 7919, dev, optimizer="add")
+        self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
+        self.user_atomic = cfg.user_update == "atomic"
+        self.updates = 0
+
+    @property
+    def U(self):
+        return self.users.weight
+
+    @property
+    def I(self):
+        return self.items.weight
+
+    def step(self, uid_local: torch.Tensor, iid: torch.Tensor, rating: torch.Tensor):
+        """One micro-batch. ``uid_local`` = row in this worker's user shard,
+        ``iid`` = global item id (int32), ``rating`` fp32."""
+        c = self.cfg
+        if self.comm.world == 1:
+            ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
+        else:
+            rows, plan = self.ps.pull(iid)
+            delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+            ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
+                              self.user_atomic)
+            self.ps.push(plan, delta)
+        self.updates += uid_local.numel()
+
+    @torch.no_grad()
+    def sq_err(self, uid_local, iid, rating) -> float:
+        """Sum of squared errors of this rank's ratings (items pulled when remote)."""
+        if self.comm.world == 1:
+            return float(ops.mf_sq_err(self.U, self.I, uid_local, iid, rating).item())
+        vals = self.ps.pull_values(iid)
+        e = rating - (self.U[uid_local.long()] * vals).sum(1)
+        return float((e.double() ** 2).sum())
+
+    def rmse(self, uid_local, iid, rating) -> float:
+        se = self.comm.sum_over_ranks(self.sq_err(uid_local, iid, rating))
+        n = self.comm.sum_over_ranks(float(uid_local.numel()))
+        return (se / max(n, 1.0)) ** 0.5
+
+    def user_vectors(self):
+        ids = self.users.global_ids(torch.arange(self.users.n_local, device=self.U.device))
+        return ids, self.U
+
+    def item_vectors(self, only_touched=True):
+        return self.items.dump(only_touched)
+
+
+@dataclass
+class SyntheticRatings:
+    """On-device synthetic rating stream of one rank (users of this rank only).
+
+    ``truth_dim > 0`` draws ratings from a hidden low-rank model so RMSE can
+    fall; otherwise ratings are U[0, 1) (implicit-feedback-like), which is all
+    a throughput run needs.
+    """
+
+    num_users: int
+    num_items: int
+    n: int
+    rank: int = 0
+    world: int = 1
+    seed: int = 1234
+    truth_dim: int = 0
+    device: str = "cpu"
+    uid: torch.Tensor = field(init=False)
+    iid: torch.Tensor = field(init=False)
+    rating: torch.Tensor = field(init=False)
+
+    def __post_init__(self):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed * 1000003 + self.rank)
+        n_local_users = (self.num_users - self.rank + self.world - 1) // self.world
+        self.uid = torch.randint(0, n_local_users, (self.n,), generator=g, device=self.device, dtype=torch.int32)
+        self.iid = torch.randint(0, self.num_items, (self.n,), generator=g, device=self.device, dtype=torch.int32)
+        if self.truth_dim > 0:
+            gt = torch.Generator(device="cpu")
+            gt.manual_seed(self.seed)
+            Ut = torch.rand(self.num_users, self.truth_dim, generator=gt) / self.truth_dim ** 0.5
+            It = torch.rand(self.num_items, self.truth_dim, generator=gt) / self.truth_dim ** 0.5
+            ug = self.rank + self.world * self.uid.long().cpu()
+            self.rating = (Ut[ug] * It[self.iid.long().cpu()]).sum(1).to(self.device)
+        else:
+            self.rating = torch.rand(self.n, generator=g, device=self.device, dtype=torch.float32)
+
+    def batch(self, i: int, size: int):
+        s = (i * size) % max(self.n - size + 1, 1)
+        return self.uid[s:s + size], self.iid[s:s + size], self.rating[s:s + size]

@@ -1,0 +1,164 @@
+"""Tensor ops of the fast path: gfx950 HIP kernels on device tensors, the
+plain-PyTorch reference (``ops.reference``) on CPU tensors.
+
+Dispatch is by the tensor's device.  A CUDA(HIP) tensor *always* goes to the
+native kernel; if the library is missing that raises (no silent eager
+fallback on a GPU box).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+from . import reference as R
+
+_OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3}
+
+
+def native_available() -> bool:
+    return N.available()
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _c(t):
+    if not t.is_contiguous():
+        raise ValueError("kernel inputs must be contiguous")
+    return t
+
+
+def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: float = 0.0, hi: float = 1.0,
+              seed: int = 0) -> torch.Tensor:
+    """Fill ``table[r] = U[lo,hi)`` keyed by global id ``id_base + r*id_stride`` (K9)."""
+    n, d = table.shape
+    if _on_gpu(table):
+        lib = N.require()
+        N.check(lib.fps_init_rows(_c(table).data_ptr(), n, d, id_base, id_stride, lo, hi, seed & 0xFFFFFFFF,
+                                  N.stream_ptr(table.device)), "init_rows")
+        return table
+    return R.init_rows(table, id_base, id_stride, lo, hi, seed)
+
+
+def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
+                touched: torch.Tensor = None) -> torch.Tensor:
+    """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2)."""
+    n = idx.numel()
+    d = table.shape[1]
+    if out is None:
+        out = torch.empty((n, d), dtype=out_dtype, device=table.device)
+    if _on_gpu(table):
+        lib = N.require()
+        N.check(lib.fps_gather_rows(_c(table).data_ptr(), _c(idx).data_ptr(), int(idx.dtype == torch.int64), n, d,
+                                    _c(out).data_ptr(), int(out.dtype == torch.bfloat16), N.ptr(touched),
+                                    N.stream_ptr(table.device)), "gather_rows")
+        return out
+    out.copy_(R.gather_rows(table, idx, out.dtype, touched))
+    return out
+
+
+def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: str = "add", lr: float = 0.0,
+               eps: float = 1e-10, state: torch.Tensor = None, touched: torch.Tensor = None) -> torch.Tensor:
+    """Push apply (K3): ``add`` (atomic), ``set``, ``sgd`` (w -= lr*g, atomic),
+    ``adagrad`` (unique idx).  ``idx < 0`` marks padding rows."""
+    n = idx.numel()
+    d = table.shape[1]
+    if _on_gpu(table):
+        if idx.dtype != torch.int32:
+            idx = idx.to(torch.int32)
+        lib = N.require()
+        N.check(lib.fps_apply_rows(_c(table).data_ptr(), N.ptr(state), _c(idx).data_ptr(), n, d, _c(delta).data_ptr(),
+                                   int(delta.dtype == torch.bfloat16), _OPS[op], lr, eps, N.ptr(touched),
+                                   N.stream_ptr(table.device)), "apply_rows")
+        return table
+    return R.apply_rows(table, idx, delta, op, lr, eps, state, touched)
+
+
+class DedupWorkspace:
+    """Per-step key de-duplication + shard grouping for one worker (K1).
+
+    ``map`` is an epoch-tagged ``uint64[num_ids]`` claim table (nothing is
+    cleared between steps).  ``run(keys)`` returns device tensors
+    ``counts[W], prefix[W+1], uniq[U], pos[B]``: the unique *local* keys
+    grouped by owning shard (contiguous, so they are directly the all-to-all
+    send buffer with splits ``counts``) and each request's row in it.
+    """
+
+    def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu"):
+        self.num_ids, self.W, self.part_kind, self.block = num_ids, W, part_kind, block
+        self.device = torch.device(device)
+        self.epoch = 0
+        self.cap = 0
+        if self.device.type == "cuda":
+            self.map = torch.zeros(num_ids, dtype=torch.int64, device=device)
+            self.counts = torch.zeros(W, dtype=torch.int32, device=device)
+            self.prefix = torch.zeros(W + 1, dtype=torch.int32, device=device)
+
+    def _grow(self, n):
+        if n > self.cap:
+            self.cap = max(n, int(self.cap * 1.25))
+            self.owner_slot = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.uniq = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.pos = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+
+    def run(self, keys: torch.Tensor):
+        if self.device.type != "cuda":
+            return R.dedup(keys, self.W, self.part_kind, self.block)
+        n = keys.numel()
+        self._grow(max(n, 1))
+        self.epoch += 1
+        self.counts.zero_()
+        lib = N.require()
+        N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch & 0xFFFFFFFF, self.W,
+                              self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
+                              self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(),
+                              N.stream_ptr(self.device)), "dedup")
+        return self.counts, self.prefix, self.uniq, self.pos[:n]
+
+
+def bucketize(keys: torch.Tensor, W: int, part_kind: int = 0, block: int = 1):
+    """Shard id per key and per-shard counts."""
+    if _on_gpu(keys):
+        shard = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+        counts = torch.zeros(W, dtype=torch.int32, device=keys.device)
+        lib = N.require()
+        N.check(lib.fps_bucketize(_c(keys).data_ptr(), keys.numel(), W, part_kind, block, shard.data_ptr(),
+                                  counts.data_ptr(), N.stream_ptr(keys.device)), "bucketize")
+        return shard, counts
+    return R.bucketize(keys, W, part_kind, block)
+
+
+def mf_sgd_local(U, I, uid, iid, r, lr: float, lam: float = 0.0, user_atomic: bool = False):
+    """Fused MF SGD step with the item shard local (pull = read, push = atomic add) (K4)."""
+    if _on_gpu(U):
+        lib = N.require()
+        N.check(lib.fps_mf_sgd_local(_c(U).data_ptr(), _c(I).data_ptr(), _c(uid).data_ptr(), _c(iid).data_ptr(),
+                                     _c(r).data_ptr(), uid.numel(), U.shape[1], lr, lam, int(user_atomic),
+                                     N.stream_ptr(U.device)), "mf_sgd_local")
+        return
+    R.mf_sgd_local(U, I, uid, iid, r, lr, lam, user_atomic)
+
+
+def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr: float, lam: float = 0.0, user_atomic: bool = False):
+    """MF SGD on pulled item rows; item deltas accumulate into ``delta[pos]`` (K4)."""
+    if _on_gpu(U):
+        lib = N.require()
+        N.check(lib.fps_mf_sgd_pulled(_c(U).data_ptr(), _c(uid).data_ptr(), _c(r).data_ptr(), _c(rows).data_ptr(),
+                                      int(rows.dtype == torch.bfloat16), _c(pos).data_ptr(), _c(delta).data_ptr(),
+                                      uid.numel(), U.shape[1], lr, lam, int(user_atomic), N.stream_ptr(U.device)),
+                "mf_sgd_pulled")
+        return
+    R.mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam, user_atomic)
+
+
+def mf_sq_err(U, I, uid, iid, r) -> torch.Tensor:
+    """Sum of squared rating errors (device scalar on GPU) (K14)."""
+    if _on_gpu(U):
+        out = torch.zeros(1, dtype=torch.float64, device=U.device)
+        lib = N.require()
+        N.check(lib.fps_mf_sq_err(_c(U).data_ptr(), _c(I).data_ptr(), _c(uid).data_ptr(), _c(iid).data_ptr(),
+                                  _c(r).data_ptr(), uid.numel(), U.shape[1], out.data_ptr(), N.stream_ptr(U.device)),
+                "mf_sq_err")
+        return out
+    return torch.tensor([R.mf_sq_err(U, I, uid, iid, r)], dtype=torch.float64)

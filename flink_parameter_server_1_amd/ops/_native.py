@@ -1,0 +1,96 @@
+"""ctypes binding of the in-tree gfx950 kernel library ``_lib/libfps_kernels.so``.
+
+The library exposes a plain C ABI (``fps_*`` launchers: device pointers, sizes
+and a ``hipStream_t``) so it does not depend on torch's C++ ABI and builds in
+seconds with hipcc.  It must be loaded *after* ``import torch``: torch ships
+the HIP runtime (``libamdhip64.so.7``) and the library binds to that loaded
+copy, so kernels run on torch's device/context and streams.
+
+On a GPU box a missing / unloadable library is an error (``require()``),
+never a silent fallback to eager PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the library load, see docstring)
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+KERNELS_SO = os.path.join(_LIB_DIR, "libfps_kernels.so")
+
+_lock = threading.Lock()
+_lib = None
+_err = None
+
+c_int, c_i64, c_f32, c_u32, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32, ctypes.c_void_p
+
+_SIGNATURES = {
+    "fps_abi_version": [],
+    "fps_init_rows": [c_vp, c_i64, c_int, c_i64, c_i64, c_f32, c_f32, c_u32, c_vp],
+    "fps_gather_rows": [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_int, c_vp, c_vp],
+    "fps_apply_rows": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_f32, c_f32, c_vp, c_vp],
+    "fps_dedup": [c_vp, c_i64, c_vp, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_bucketize": [c_vp, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp],
+    "fps_mf_sgd_local": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
+    "fps_mf_sgd_pulled": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
+    "fps_mf_sq_err": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp],
+}
+#: optional symbols (added by later kernel files); bound when present
+OPTIONAL = {}
+
+
+def register(name, argtypes):
+    OPTIONAL[name] = argtypes
+
+
+def load():
+    """Load the kernel library once; returns the ctypes handle or None."""
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        return _lib
+    with _lock:
+        if _lib is not None or _err is not None:
+            return _lib
+        if not os.path.exists(KERNELS_SO):
+            _err = FileNotFoundError(f"{KERNELS_SO} missing: run `python csrc/build.py`")
+            return None
+        try:
+            lib = ctypes.CDLL(KERNELS_SO)
+            for name, args in list(_SIGNATURES.items()) + list(OPTIONAL.items()):
+                fn = getattr(lib, name, None)
+                if fn is None:
+                    if name in _SIGNATURES:
+                        raise AttributeError(f"{name} missing from {KERNELS_SO}")
+                    continue
+                fn.argtypes = args
+                fn.restype = c_int
+            _lib = lib
+        except OSError as e:  # pragma: no cover
+            _err = e
+    return _lib
+
+
+def require():
+    lib = load()
+    if lib is None:
+        raise RuntimeError(f"gfx950 kernel library unavailable: {_err}")
+    return lib
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,147 @@
+"""Plain-PyTorch reference implementations of every kernel in ``csrc/kernels``.
+
+They define the semantics the HIP kernels are tested against (numerics tests
+compare the gfx950 kernel with these on the same inputs) and are the CPU
+execution path of the tensor engine (gloo multi-process tests, CPU boxes).
+"""
+from __future__ import annotations
+
+import torch
+
+M32 = 0xFFFFFFFF
+
+
+def fmix32(x: torch.Tensor) -> torch.Tensor:
+    """murmur3 finalizer on int64 tensors holding uint32 values."""
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & M32
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def hash_uniform(seed: int, ids: torch.Tensor, j: torch.Tensor) -> torch.Tensor:
+    """U[0,1) for every (id, j) pair; ids [N,1] int64, j [1,D] int64 -> [N, D] fp32."""
+    h0 = fmix32(torch.tensor((seed ^ 0x9E3779B9) & M32, dtype=torch.int64))
+    h = fmix32(h0 ^ (ids & M32))
+    h = fmix32(h ^ ((ids >> 32) & M32) ^ 0x27D4EB2F)
+    h = fmix32((h + j * 0x9E3779B9) & M32)
+    return (h >> 8).to(torch.float32) * (1.0 / 16777216.0)
+
+
+def init_rows(table: torch.Tensor, id_base: int, id_stride: int, lo: float, hi: float, seed: int):
+    n, d = table.shape
+    ids = (id_base + torch.arange(n, dtype=torch.int64) * id_stride).view(-1, 1)
+    j = torch.arange(d, dtype=torch.int64).view(1, -1)
+    table.copy_((lo + (hi - lo) * hash_uniform(seed, ids, j)).to(table.device))
+    return table
+
+
+def init_values(ids: torch.Tensor, dim: int, lo: float, hi: float, seed: int) -> torch.Tensor:
+    j = torch.arange(dim, dtype=torch.int64).view(1, -1)
+    return lo + (hi - lo) * hash_uniform(seed, ids.to(torch.int64).view(-1, 1).cpu(), j)
+
+
+def gather_rows(table, idx, out_dtype=torch.float32, touched=None):
+    idx = idx.long()
+    if touched is not None:
+        touched[idx] = 1
+    return table[idx].to(out_dtype)
+
+
+OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3}
+
+
+def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touched=None):
+    idx = idx.long()
+    keep = idx >= 0
+    idx, delta = idx[keep], delta[keep].to(torch.float32)
+    if touched is not None:
+        touched[idx] = 1
+    if op == "add":
+        table.index_add_(0, idx, delta)
+    elif op == "set":
+        table[idx] = delta
+    elif op == "sgd":
+        table.index_add_(0, idx, -lr * delta)
+    elif op == "adagrad":
+        state[idx] += delta * delta
+        table[idx] -= lr * delta * torch.rsqrt(state[idx] + eps)
+    else:
+        raise ValueError(op)
+    return table
+
+
+def shard_of(keys: torch.Tensor, W: int, part_kind: int, block: int):
+    k = keys.long().abs()
+    if part_kind == 0:
+        return k % W, k // W
+    d = torch.clamp(k // block, max=W - 1)
+    return d, k - d * block
+
+
+def dedup(keys: torch.Tensor, W: int, part_kind: int, block: int):
+    """Unique keys grouped by destination shard (compact layout).
+
+    Returns ``counts[W] int32, prefix[W+1] int32, uniq[U] int32 (local keys,
+    shard-major), pos[B] int32`` with ``uniq[pos[b]] == local(keys[b])``.
+    Inside a shard group unique keys keep first-occurrence order (the GPU
+    kernel's order there is arbitrary).
+    """
+    keys = keys.long()
+    uniq_g, first_idx = _unique_first(keys)
+    dest, local = shard_of(uniq_g, W, part_kind, block)
+    counts = torch.bincount(dest, minlength=W)
+    order = torch.argsort(dest * (keys.numel() + 1) + first_idx, stable=True)
+    slot_of = torch.empty_like(order)
+    slot_of[order] = torch.arange(order.numel())
+    uniq = local[order].to(torch.int32)
+    inv = torch.searchsorted(uniq_g, keys)
+    pos = slot_of[inv].to(torch.int32)
+    prefix = torch.zeros(W + 1, dtype=torch.int32)
+    prefix[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return counts.to(torch.int32), prefix, uniq, pos
+
+
+def _unique_first(keys):
+    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    first = torch.full((uniq.numel(),), keys.numel(), dtype=torch.long)
+    first.scatter_reduce_(0, inv, torch.arange(keys.numel()), reduce="amin")
+    return uniq, first
+
+
+def bucketize(keys, W, part_kind, block):
+    d, _ = shard_of(keys, W, part_kind, block)
+    return d.to(torch.int32), torch.bincount(d, minlength=W).to(torch.int32)
+
+
+def mf_sgd_local(U, I, uid, iid, r, lr, lam=0.0, user_atomic=False):
+    uid, iid = uid.long(), iid.long()
+    u, i = U[uid], I[iid]
+    e = r - (u * i).sum(1)
+    du = lr * (e[:, None] * i - lam * u)
+    di = lr * (e[:, None] * u - lam * i)
+    if user_atomic:
+        U.index_add_(0, uid, du)
+    else:
+        U[uid] = u + du
+    I.index_add_(0, iid, di)
+
+
+def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
+    uid, pos = uid.long(), pos.long()
+    u, i = U[uid], rows[pos].to(torch.float32)
+    e = r - (u * i).sum(1)
+    du = lr * (e[:, None] * i - lam * u)
+    di = lr * (e[:, None] * u - lam * i)
+    if user_atomic:
+        U.index_add_(0, uid, du)
+    else:
+        U[uid] = u + du
+    delta.index_add_(0, pos, di)
+
+
+def mf_sq_err(U, I, uid, iid, r) -> float:
+    e = r - (U[uid.long()] * I[iid.long()]).sum(1)
+    return float((e.double() ** 2).sum())

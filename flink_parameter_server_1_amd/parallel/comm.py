@@ -1,0 +1,123 @@
+"""Process-group plumbing of the tensor engine.
+
+One process per GPU; ``torch.distributed`` with the ``nccl`` backend, which
+on ROCm *is* RCCL over xGMI.  The PS traffic is any-worker -> any-shard, so
+the primitive is the variable-split all-to-all (``all_to_all_single``): on a
+fully connected 8-GPU xGMI mesh every rank pair has its own link and an
+all-to-all drives all 7 links of a GPU at once, where a ring collective
+would be bound by one link.  Three all-to-all phases per micro-batch:
+
+  X1  keys   worker -> owner shard    (int32, deduplicated per step)
+  X2  rows   owner -> worker          (same splits reversed; keys implicit
+                                       because answers come back in request
+                                       order -- the reference's FIFO property)
+  X1' deltas worker -> owner shard    (fp32 or bf16 rows, pre-reduced per key)
+
+Gloo provides the same calls on CPU (multi-process tests).  ``world == 1``
+short-circuits every exchange to a local copy.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, group=None, device=None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.rank, self.world, self.backend = 0, 1, "local"
+        if device is None:
+            if torch.cuda.is_available():
+                device = torch.device("cuda", torch.cuda.current_device())
+            else:
+                device = torch.device("cpu")
+        self.device = torch.device(device)
+        self.bytes_sent = 0
+
+    # ------------------------------------------------------------- set-up
+    @staticmethod
+    def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> "Comm":
+        """Initialise the default group from torchrun env vars (or world=1)."""
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        use_gpu = torch.cuda.is_available()
+        if use_gpu:
+            torch.cuda.set_device(local_rank)
+            device = torch.device("cuda", local_rank)
+        else:
+            device = torch.device("cpu")
+        if world > 1 and not dist.is_initialized():
+            backend = backend or ("nccl" if use_gpu else "gloo")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(**kw)
+        return Comm(device=device)
+
+    # ------------------------------------------------------------- collectives
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
+        """Every rank tells every other how many rows it will send it."""
+        if self.world == 1:
+            return send_counts.clone()
+        recv = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv, send_counts, group=self.group)
+        return recv
+
+    def all_to_all(self, send: torch.Tensor, send_splits: Sequence[int], recv_splits: Sequence[int],
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Variable-split all-to-all along dim 0 (rows of any trailing shape)."""
+        n_out = int(sum(recv_splits))
+        if out is None:
+            out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+        if self.world == 1:
+            out[:n_out].copy_(send[:n_out])
+            return out
+        row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
+        self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
+        dist.all_to_all_single(out[:n_out], send[: int(sum(send_splits))], list(map(int, recv_splits)),
+                               list(map(int, send_splits)), group=self.group)
+        return out
+
+    def all_reduce(self, t: torch.Tensor, op=None) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
+        if self.world == 1:
+            return [t]
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t, group=self.group)
+        return outs
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def sum_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, group=self.group)
+        return float(t.item())

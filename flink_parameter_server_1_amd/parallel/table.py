@@ -1,0 +1,108 @@
+"""HBM-resident PS shard tables.
+
+A ``ShardedTable`` is the device counterpart of the PS logics in
+``ps/logics.py``: each rank owns one shard of a ``[num_ids, dim]`` parameter
+table, laid out densely in HBM (288 GB per MI355X -- a 100B-parameter fp32
+table is ~50 GB per GPU over 8).  Lazy "init on first pull" of the reference
+(``M/server/SimplePSLogic.scala:13-14``) becomes a deterministic init of
+every row keyed by its *global* id (hash RNG, ``ops.init_rows``), which
+yields the same value whenever the row is first touched and whichever shard
+holds it.  A ``touched`` byte per row reproduces the close-time dump of only
+the touched parameters (``SimplePSLogicWithClose`` / ``RangePSLogicWithClose``).
+
+Partitioning: ``hash`` (``|id| % P``, the reference default) or ``range``
+(``|id| // ceil(F/P)``, ``rangePartitionerPS``).  Local row of an id:
+hash -> ``id // P``; range -> ``id - shard * block``.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..core.partitioners import HashPartitioner, RangePartitioner
+
+
+class ShardedTable:
+    PART_KIND = {"hash": 0, "range": 1}
+
+    def __init__(self, num_ids: int, dim: int, rank: int = 0, world: int = 1, partition: str = "hash",
+                 init: Tuple = ("uniform", -0.01, 0.01), seed: int = 0, device="cpu", optimizer: str = "add",
+                 track_touched: bool = True, dtype=torch.float32):
+        if partition not in self.PART_KIND:
+            raise ValueError(partition)
+        self.num_ids, self.dim, self.rank, self.world = int(num_ids), int(dim), rank, world
+        self.partition = partition
+        self.part_kind = self.PART_KIND[partition]
+        self.part = HashPartitioner(world) if partition == "hash" else RangePartitioner(world, num_ids)
+        self.block = 1 if partition == "hash" else self.part.block
+        self.n_local = self.part.shard_size(self.num_ids, rank)
+        self.device = torch.device(device)
+        self.optimizer = optimizer
+        self.seed = seed
+        self.init_spec = init
+        self.weight = torch.empty((self.n_local, self.dim), dtype=dtype, device=self.device)
+        self.reset_parameters()
+        self.state = torch.zeros_like(self.weight) if optimizer == "adagrad" else None
+        self.touched = torch.zeros(self.n_local, dtype=torch.uint8, device=self.device) if track_touched else None
+
+    # ----------------------------------------------------------- id mapping
+    @property
+    def id_base(self) -> int:
+        return self.rank if self.partition == "hash" else self.rank * self.block
+
+    @property
+    def id_stride(self) -> int:
+        return self.world if self.partition == "hash" else 1
+
+    def global_ids(self, local: torch.Tensor) -> torch.Tensor:
+        return self.id_base + local.long() * self.id_stride
+
+    def local_of(self, ids: torch.Tensor) -> torch.Tensor:
+        return self.part.local_index(ids.long())
+
+    # ----------------------------------------------------------- lifecycle
+    def reset_parameters(self):
+        kind = self.init_spec[0]
+        if kind == "uniform":
+            _, lo, hi = self.init_spec
+            ops.init_rows(self.weight, self.id_base, self.id_stride, float(lo), float(hi), self.seed)
+        elif kind == "zeros":
+            self.weight.zero_()
+        elif kind == "const":
+            self.weight.fill_(float(self.init_spec[1]))
+        else:
+            raise ValueError(f"unknown init {kind}")
+
+    # ----------------------------------------------------------- PS side
+    def serve(self, local_keys: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
+        """Pull serve (K2): rows for the requested local keys."""
+        return ops.gather_rows(self.weight, local_keys, out_dtype=wire_dtype, touched=self.touched)
+
+    def apply(self, local_keys: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None):
+        """Push apply (K3) with the table's update rule."""
+        ops.apply_rows(self.weight, local_keys, deltas, op or self.optimizer, lr=lr, state=self.state,
+                       touched=self.touched)
+
+    def load(self, ids: torch.Tensor, values: torch.Tensor):
+        """Model load (``transformWithModelLoad``): set rows owned by this shard."""
+        ids = ids.to(self.device).long()
+        mine = self.part.shard_tensor(ids) == self.rank
+        loc = self.local_of(ids[mine]).to(torch.int32)
+        ops.apply_rows(self.weight, loc, values.to(self.device)[mine].to(torch.float32).contiguous(), "set",
+                       touched=self.touched)
+
+    def dump(self, only_touched: bool = True):
+        """(global ids, values) of this shard -- the close-time model output."""
+        if only_touched and self.touched is not None:
+            loc = torch.nonzero(self.touched, as_tuple=False).flatten()
+        else:
+            loc = torch.arange(self.n_local, device=self.device)
+        return self.global_ids(loc), self.weight[loc]
+
+    def nbytes(self) -> int:
+        n = self.weight.numel() * self.weight.element_size()
+        if self.state is not None:
+            n += self.state.numel() * 4
+        return n
