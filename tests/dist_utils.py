@@ -1,0 +1,51 @@
+"""Spawn a gloo process group on CPU (the Flink mini-cluster analogue)."""
+import os
+import socket
+import tempfile
+import traceback
+
+import torch.multiprocessing as mp
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _entry(rank, world, port, fn, args, out_dir):
+    import pickle
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = fn(rank, world, *args)
+        err = None
+    except Exception:  # pragma: no cover - reported by the parent
+        res, err = None, traceback.format_exc()
+    with open(os.path.join(out_dir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump((res, err), f)
+    dist.destroy_process_group()
+
+
+def run_ranks(fn, world, *args):
+    """Run ``fn(rank, world, *args)`` on ``world`` gloo ranks; returns the list of results."""
+    import pickle
+
+    out_dir = tempfile.mkdtemp(prefix="fps_dist_")
+    mp.spawn(_entry, args=(world, free_port(), fn, args, out_dir), nprocs=world, join=True)
+    results = []
+    for r in range(world):
+        with open(os.path.join(out_dir, f"r{r}.pkl"), "rb") as f:
+            res, err = pickle.load(f)
+        if err:
+            raise AssertionError(f"rank {r} failed:\n{err}")
+        results.append(res)
+    return results
