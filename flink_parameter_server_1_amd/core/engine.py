@@ -83,7 +83,7 @@ class WorkerTask:
         self.sender = sender
         self.receiver = receiver
         self.engine = engine
-        self.data = deque()
+        self.data = None  # iterator over this subtask's input partition
         self.answers = deque()
         self.client = _WorkerClient(self, engine)
         self.data_done = False
@@ -151,8 +151,8 @@ def split_input(data, n: int, partitioner: Optional[Callable] = None) -> List[de
     if isinstance(data, PartitionedInput):
         if len(data.parts) != n:
             raise ValueError(f"input has {len(data.parts)} partitions, expected {n}")
-        return [deque(p) for p in data.parts]
-    parts = [deque() for _ in range(n)]
+        return list(data.parts)
+    parts = [[] for _ in range(n)]
     if partitioner is None:
         for i, rec in enumerate(data):
             parts[i % n].append(rec)
@@ -163,10 +163,12 @@ def split_input(data, n: int, partitioner: Optional[Callable] = None) -> List[de
 
 
 class PartitionedInput:
-    """Marks an input already split per worker subtask."""
+    """Marks an input already split per worker subtask.  Partitions may be
+    lazy iterables (generators, ``utils.sleep_blocker.block``); the engine
+    consumes them incrementally, interleaved with pull answers."""
 
     def __init__(self, parts: Sequence[Iterable]):
-        self.parts = [list(p) for p in parts]
+        self.parts = list(parts)
 
 
 class LocalRuntime:
@@ -193,7 +195,7 @@ class LocalRuntime:
         for w in local_workers:
             t = WorkerTask(w, _instantiate(worker_logic, w), copy.deepcopy(worker_sender),
                            copy.deepcopy(worker_receiver), self)
-            t.data = data_parts[w] if data_parts is not None else deque()
+            t.data = iter(data_parts[w]) if data_parts is not None else None
             self.workers[w] = t
         for p in local_ps:
             self.servers[p] = PSTask(p, _instantiate(ps_logic, p), copy.deepcopy(ps_sender),
@@ -239,11 +241,16 @@ class LocalRuntime:
             while ans and n < b:
                 t.handle_answer(ans.popleft())
                 n += 1
-            d = t.data
             m = 0
-            while d and m < b:
-                t.handle_data(d.popleft())
-                m += 1
+            src = t.data
+            if src is not None:  # lazily consumed input partition
+                for rec in src:
+                    t.handle_data(rec)
+                    m += 1
+                    if m >= b:
+                        break
+                else:
+                    t.data = None
             if n or m:
                 progressed = True
         for t in self.servers.values():
@@ -260,7 +267,7 @@ class LocalRuntime:
 
     def _locally_idle(self) -> bool:
         for t in self.workers.values():
-            if t.answers or t.data:
+            if t.answers or t.data is not None:
                 return False
         for t in self.servers.values():
             if t.inbox:

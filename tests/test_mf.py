@@ -1,0 +1,151 @@
+"""MF model library on the per-record engine — port of
+T/matrix/factorization/PSOfflineMatrixFactorizationTest.scala plus tests the
+reference lacks (online MF, LEMP pruning vs brute force, top-K apps, merge)."""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from flink_parameter_server_1_amd.core.messages import Left, Right, left_values, right_values
+from flink_parameter_server_1_amd.models.mf import apps
+from flink_parameter_server_1_amd.models.mf.core import (FactorIsNotANumberException, JavaRandom, Rating,
+                                                         PseudoRandomFactorInitializer, SGDUpdater, TopKQueue,
+                                                         attach_length, vector_sum)
+from flink_parameter_server_1_amd.models.mf.pruning import COORD, INCR, LC, LENGTH, LI, LEMPPruningStrategy
+from flink_parameter_server_1_amd.models.mf.workers import CollectTopKFromEachWorker, lemp_top_k
+from sortedcontainers import SortedList
+
+
+def reference_offline_ratings():
+    """The reference test's data set: java.util.Random(47), 100 draws, duplicates removed."""
+    r = JavaRandom(47)
+    rs = [Rating.from_tuple((r.next_int(20), r.next_int(15), r.next_double())) for _ in range(100)]
+    uniq = {}
+    for x in rs:
+        uniq.setdefault((x.user, x.item), x)
+    return list(uniq.values())
+
+
+def rmse_from_stream(ratings, out):
+    users, items = {}, {}
+    for e in out:
+        k, v = e.value
+        (users if e.is_left else items)[k] = v
+    s = sum((float(np.dot(users[x.user], items[x.item])) - x.rating) ** 2 for x in ratings)
+    return math.sqrt(s / len(ratings))
+
+
+def test_java_random_parity():
+    r = JavaRandom(42)
+    assert r.next_double() == 0.7275636800328681
+    assert JavaRandom(0).next_double() == 0.730967787376657
+    v = PseudoRandomFactorInitializer(3).next_factor(42)
+    assert v[0] == 0.7275636800328681
+
+
+def test_offline_mf_rmse_below_half():
+    ratings = reference_offline_ratings()
+    assert 80 <= len(ratings) <= 100
+    out = apps.ps_offline_mf(ratings, num_factors=15, learning_rate=0.01, iterations=10, range_min=0.0,
+                             range_max=1.0, pull_limit=10, worker_parallelism=4, ps_parallelism=4, seed=3)
+    rmse = rmse_from_stream(ratings, out)
+    assert rmse <= 0.5, rmse
+
+
+def test_online_mf_learns_and_emits_every_update():
+    rng = random.Random(1)
+    truth_u = {u: np.array([rng.random() for _ in range(4)]) for u in range(30)}
+    truth_i = {i: np.array([rng.random() for _ in range(4)]) for i in range(20)}
+    ratings = [Rating(u, i, float(truth_u[u] @ truth_i[i]) / 4) for _ in range(12) for u in range(30)
+               for i in rng.sample(range(20), 3)]
+    out = apps.ps_online_mf(ratings, num_factors=4, range_min=0.0, range_max=0.5, learning_rate=0.1,
+                            pull_limit=50, worker_parallelism=3, ps_parallelism=2, seed=0)
+    assert len(left_values(out)) == len(ratings) and len(right_values(out)) == len(ratings)
+    first = rmse_from_stream(ratings[:50], out[:0] + [Left((u, np.full(4, 0.25))) for u in range(30)] +
+                             [Right((i, np.full(4, 0.25))) for i in range(20)])
+    assert rmse_from_stream(ratings, out) < first
+
+
+def test_online_mf_negative_sampling_pulls_extra():
+    ratings = [Rating(u, i, 1.0) for u in range(5) for i in range(8)]
+    out = apps.ps_online_mf(ratings, num_factors=3, learning_rate=0.05, negative_sample_rate=2, user_memory=4,
+                            worker_parallelism=1, ps_parallelism=1, seed=1)
+    # every positive and every negative rating produces one worker output
+    assert len(left_values(out)) > len(ratings)
+
+
+def test_vector_sum_nan_raises():
+    with pytest.raises(FactorIsNotANumberException):
+        vector_sum(np.array([1.0]), np.array([float("nan")]))
+
+
+def test_sgd_updater():
+    du, di = SGDUpdater(0.1).delta(1.0, np.array([1.0, 0.0]), np.array([0.5, 0.5]))
+    np.testing.assert_allclose(du, [0.025, 0.025])
+    np.testing.assert_allclose(di, [0.05, 0.0])
+
+
+def test_pruning_from_string():
+    assert LEMPPruningStrategy.from_string("length") == LENGTH()
+    assert LEMPPruningStrategy.from_string("coord") == COORD()
+    assert LEMPPruningStrategy.from_string("incr:3") == INCR(3)
+    assert LEMPPruningStrategy.from_string("lc:2.5") == LC(2.5)
+    assert LEMPPruningStrategy.from_string("li:5:2.5") == LI(5, 2.5)
+    with pytest.raises(ValueError):
+        LEMPPruningStrategy.from_string("nope")
+
+
+@pytest.mark.parametrize("strategy", [LENGTH(), COORD(), INCR(3), LC(1.5), LI(4, 1.5)])
+def test_lemp_equals_brute_force(strategy):
+    rng = np.random.default_rng(7)
+    model = {i: attach_length(rng.normal(size=10) * rng.uniform(0.1, 3.0)) for i in range(400)}
+    items = SortedList((-lv[0], i) for i, lv in model.items())
+    for _ in range(20):
+        u = attach_length(rng.normal(size=10))
+        got = lemp_top_k(u, items, model, 15, 32, strategy)
+        scores = sorted(((float(u[1] @ lv[1]), i) for i, lv in model.items()), reverse=True)[:15]
+        assert sorted(i for _, i in got.items()) == sorted(i for _, i in scores)
+
+
+def test_collect_top_k_merges_and_filters_seen():
+    from flink_parameter_server_1_amd.models.mf.core import RichRating
+
+    c = CollectTopKFromEachWorker(K=2, memory=5, worker_parallelism=2)
+    out = []
+    r0 = RichRating(1, 10, 1.0, 0, 0.0)
+    r1 = RichRating(1, 10, 1.0, 1, 0.0)
+    c.flat_map(Left((r0, TopKQueue([(0.9, 10), (0.5, 11)]))), out.append)
+    assert out == []
+    c.flat_map(Left((r1, TopKQueue([(0.7, 12), (0.1, 13)]))), out.append)
+    assert out == [(1, 10, 0, [(0.9, 10), (0.7, 12)])]
+    # item 10 is now seen by user 1
+    c.flat_map(Left((RichRating(1, 11, 1.0, 0, 1.0), TopKQueue([(0.9, 10), (0.5, 11)]))), out.append)
+    c.flat_map(Left((RichRating(1, 11, 1.0, 1, 1.0), TopKQueue([(0.7, 12)]))), out.append)
+    assert out[-1][3] == [(0.7, 12), (0.5, 11)]
+
+
+def test_top_k_generator_app_matches_brute_force():
+    rng = np.random.default_rng(3)
+    users = {u: attach_length(rng.normal(size=6)) for u in range(10)}
+    items = {i: attach_length(rng.normal(size=6)) for i in range(60)}
+    model = [Left((u, lv)) for u, lv in users.items()] + [Right((i, lv)) for i, lv in items.items()]
+    ratings = [Rating(u, 0, 1.0, t) for t, u in enumerate(range(10))]
+    res = apps.ps_top_k_generator(ratings, model, K=5, worker_k=5, bucket_size=7, pruning_algorithm=COORD(),
+                                  worker_parallelism=3, ps_parallelism=2)
+    assert len(res) == 10
+    for (item, ts, topk), r in zip(sorted(res, key=lambda x: x[1]), ratings):
+        u = users[r.user][1]
+        brute = sorted(((float(u @ lv[1]), i) for i, lv in items.items()), reverse=True)[:5]
+        assert [i for _, i in topk] == [i for _, i in brute]
+
+
+def test_online_learner_and_generator_runs():
+    rng = random.Random(5)
+    ratings = [Rating(rng.randrange(15), rng.randrange(30), 1.0, t) for t in range(120)]
+    res = apps.ps_online_learner_and_generator(ratings, num_factors=5, learning_rate=0.05, negative_sample_rate=2,
+                                               K=4, worker_k=4, bucket_size=5, worker_parallelism=2,
+                                               ps_parallelism=2, seed=2)
+    assert len(res) == len(ratings)
+    assert all(len(t[3]) <= 4 for t in res)
+    assert any(len(t[3]) == 4 for t in res[40:])
