@@ -126,3 +126,50 @@ def test_multiclass_long_id_outputs_ids():
                                             passive_aggressive_method=m, pull_limit=10, label_count=L,
                                             feature_count=F, range_partitioning=True)
     assert sorted(left_values(out)) == [(7, 0), (8, 1)]
+
+
+def _dict_data(n, F, seed, multi=False, L=3):
+    rng = np.random.default_rng(seed)
+    w = np.random.default_rng(99).normal(size=(F, L if multi else 1))
+    out = []
+    for _ in range(n):
+        idx = rng.choice(F, size=6, replace=False)
+        vals = rng.normal(size=6)
+        x = {int(i): float(v) for i, v in zip(idx, vals)}
+        s = vals @ w[idx]
+        out.append((x, int(np.argmax(s)) if multi else (1 if s[0] > 0 else -1)))
+    return out
+
+
+@pytest.mark.parametrize("paf_type", [0, 1, 2])
+def test_offline_binary_app(paf_type):
+    from flink_parameter_server_1_amd.models.pa.offline import pa_binary_classification_offline
+
+    train = _dict_data(400, 30, 1)
+    test = _dict_data(100, 30, 2)
+    out = pa_binary_classification_offline(train, [x for x, _ in test], worker_parallelism=2, ps_parallelism=2,
+                                           iterations=5, paf_type=paf_type, paf_const=1, pull_limit=100, seed=0)
+    preds = {tuple(sorted(v.items())): lab for v, lab in left_values(out)}
+    acc = np.mean([preds[tuple(sorted(x.items()))] == y for x, y in test])
+    assert len(preds) == len(test) and acc >= 0.8, acc
+
+
+def test_offline_multiclass_app():
+    from flink_parameter_server_1_amd.models.pa.offline import pa_multi_classification_offline
+
+    train = _dict_data(600, 30, 1, multi=True)
+    test = _dict_data(100, 30, 2, multi=True)
+    out = pa_multi_classification_offline(train, [x for x, _ in test], label_count=3, worker_parallelism=2,
+                                          ps_parallelism=3, iterations=5, paf_type=1, paf_const=1.0,
+                                          pull_limit=100, seed=0)
+    preds = {tuple(sorted(v.items())): lab for v, lab in left_values(out)}
+    acc = np.mean([preds[tuple(sorted(x.items()))] == y for x, y in test])
+    assert acc >= 0.7, acc
+
+
+def test_filter_paii_is_float_division():
+    from flink_parameter_server_1_amd.models.pa.offline import PassiveAggressiveFilter
+
+    f = PassiveAggressiveFilter.build_pafii(2)
+    d = f.delta({1: 1.0}, {1: 0.0}, 1)
+    assert d[1] == pytest.approx(1.0 / (1.0 + 0.25))  # reference: 1/(2*2) == 0 in Int
