@@ -39,6 +39,9 @@ def main(argv=None):
     ap.add_argument("--pool", type=int, default=8, help="data pool = pool * batch ratings per GPU")
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
+    ap.add_argument("--sgd-mode", default="auto", choices=["auto", "grouped", "flat"])
+    ap.add_argument("--force-ps-path", action="store_true",
+                    help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     a = ap.parse_args(argv)
 
     import torch
@@ -54,7 +57,7 @@ def main(argv=None):
     if a.gpus != n:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
-                   user_update=a.user_update)
+                   user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -99,7 +102,8 @@ def main(argv=None):
                 "global_batch": a.batch * n,
                 "seq_len": None,
                 "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded)",
-                "wire_dtype": a.wire if n > 1 else "none (local PS shard)",
+                "wire_dtype": a.wire if (n > 1 or a.force_ps_path) else "none (local PS shard)",
+                "sgd_mode": model.sgd_mode,
                 "scalar_params_per_s": value * 2 * a.dim,
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
                 if n > 1 else None,

@@ -47,6 +47,8 @@ class MFConfig:
     seed: int = 0
     user_update: str = "store"        # "store" (Hogwild) | "atomic"
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
+    force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
+    sgd_mode: str = "auto"            # "auto" | "grouped" | "flat"
 
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
@@ -64,6 +66,15 @@ class DistributedMF:
         self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.seed + 7919, dev, optimizer="add")
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
         self.user_atomic = cfg.user_update == "atomic"
+        # "grouped": ratings of a micro-batch sorted by item, each item row updated
+        # in registers (no item atomics, exact per-item order); "flat": one rating
+        # per lane group with atomic item updates.  Grouped is the GPU default;
+        # the CPU reference of grouped is a Python loop, so CPU runs use flat.
+        mode = cfg.sgd_mode
+        if mode == "auto":
+            mode = "grouped" if dev.type == "cuda" and not self.user_atomic else "flat"
+        self.sgd_mode = mode
+        self.grouper = ops.CSRGrouper(dev)
         self.updates = 0
 
     @property
@@ -78,13 +89,23 @@ class DistributedMF:
         """One micro-batch. ``uid_local`` = row in this worker's user shard,
         ``iid`` = global item id (int32), ``rating`` fp32."""
         c = self.cfg
-        if self.comm.world == 1:
-            ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
+        grouped = self.sgd_mode == "grouped"
+        if self.comm.world == 1 and not c.force_ps_path:
+            if grouped:
+                ptr, order = self.grouper.run(iid, self.items.n_local)
+                ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
+            else:
+                ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
         else:
             rows, plan = self.ps.pull(iid)
-            delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
-            ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
-                              self.user_atomic)
+            if grouped:
+                ptr, order = self.grouper.run(plan.pos, plan.n_unique)
+                delta = torch.empty((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+                ops.mf_sgd_grouped(self.U, rows, uid_local, rating, ptr, order, c.learning_rate, c.lam, delta)
+            else:
+                delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+                ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
+                                  self.user_atomic)
             self.ps.push(plan, delta)
         self.updates += uid_local.numel()
 

@@ -152,6 +152,58 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr: float, lam: float = 0.0, user
     R.mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam, user_atomic)
 
 
+class CSRGrouper:
+    """Counting sort of request indices by key (``key`` in ``[0, n_groups)``) with
+    reusable device buffers; returns ``(ptr[G+1] int32, order[B] int32)``."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.cap_g = 0
+        self.cap_b = 0
+
+    def run(self, keys: torch.Tensor, n_groups: int):
+        if self.device.type != "cuda":
+            return R.csr_group(keys, n_groups)
+        n = keys.numel()
+        if n_groups + 1 > self.cap_g:
+            self.cap_g = max(n_groups + 1, int(self.cap_g * 1.25))
+            self.cnt = torch.empty(self.cap_g, dtype=torch.int32, device=self.device)
+            self.cursor = torch.empty(self.cap_g, dtype=torch.int32, device=self.device)
+            self.ptr = torch.empty(self.cap_g, dtype=torch.int32, device=self.device)
+        if n > self.cap_b:
+            self.cap_b = max(n, int(self.cap_b * 1.25))
+            self.order = torch.empty(self.cap_b, dtype=torch.int32, device=self.device)
+        cnt = self.cnt[:n_groups]
+        cnt.zero_()
+        lib = N.require()
+        s = N.stream_ptr(self.device)
+        N.check(lib.fps_csr_count(_c(keys).data_ptr(), n, cnt.data_ptr(), s), "csr_count")
+        ptr = self.ptr[: n_groups + 1]
+        ptr[:1].zero_()
+        torch.cumsum(cnt, 0, out=ptr[1:])
+        cur = self.cursor[:n_groups]
+        cur.zero_()
+        N.check(lib.fps_csr_scatter(keys.data_ptr(), n, ptr.data_ptr(), cur.data_ptr(), self.order.data_ptr(), s),
+                "csr_scatter")
+        return ptr, self.order[:n]
+
+
+def mf_sgd_grouped(U, I, uid, r, ptr, order, lr: float, lam: float = 0.0, delta: torch.Tensor = None):
+    """Item-grouped MF SGD (K4, grouped form): group ``g`` = row ``g`` of ``I``; its
+    ratings (``order[ptr[g]:ptr[g+1]]``) update the row sequentially in registers.
+    ``delta`` given -> ``I`` is a pulled-rows buffer and ``delta[g] = final - pulled``;
+    otherwise ``I`` (local shard) is updated in place."""
+    G = ptr.numel() - 1
+    if _on_gpu(U):
+        mode = 0 if delta is None else (2 if I.dtype == torch.bfloat16 else 1)
+        lib = N.require()
+        N.check(lib.fps_mf_sgd_grouped(_c(U).data_ptr(), _c(I).data_ptr(), mode, _c(uid).data_ptr(),
+                                       _c(r).data_ptr(), _c(ptr).data_ptr(), _c(order).data_ptr(), G, U.shape[1], lr,
+                                       lam, N.ptr(delta), N.stream_ptr(U.device)), "mf_sgd_grouped")
+        return
+    R.mf_sgd_grouped(U, I, uid, r, ptr, order, lr, lam, delta)
+
+
 def mf_sq_err(U, I, uid, iid, r) -> torch.Tensor:
     """Sum of squared rating errors (device scalar on GPU) (K14)."""
     if _on_gpu(U):

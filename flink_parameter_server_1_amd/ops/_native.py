@@ -36,6 +36,9 @@ _SIGNATURES = {
     "fps_mf_sgd_local": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
     "fps_mf_sgd_pulled": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
     "fps_mf_sq_err": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp],
+    "fps_csr_count": [c_vp, c_i64, c_vp, c_vp],
+    "fps_csr_scatter": [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "fps_mf_sgd_grouped": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {}

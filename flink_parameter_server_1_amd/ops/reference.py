@@ -142,6 +142,39 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
     delta.index_add_(0, pos, di)
 
 
+def csr_group(keys: torch.Tensor, n_groups: int):
+    """Counting sort: ``ptr[G+1]`` offsets and ``order`` = request indices grouped by key."""
+    k = keys.long()
+    order = torch.argsort(k, stable=True).to(torch.int32)
+    cnt = torch.bincount(k, minlength=n_groups)
+    ptr = torch.zeros(n_groups + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    return ptr, order
+
+
+def mf_sgd_grouped(U, I, uid, r, ptr, order, lr, lam=0.0, delta=None):
+    """Per group (item / unique slot) sequential SGD in ``order``; ``delta`` given =
+    pulled mode (``I`` read only, ``delta[g] = final - initial``), else ``I`` updated in place."""
+    uid, ptr, order = uid.long(), ptr.long(), order.long()
+    G = ptr.numel() - 1
+    for g in range(G):
+        a, b = int(ptr[g]), int(ptr[g + 1])
+        if a == b:
+            continue
+        i0 = I[g].to(torch.float32).clone()
+        i = i0.clone()
+        for s in range(a, b):
+            rb = int(order[s])
+            u = U[uid[rb]].clone()
+            e = float(r[rb]) - float(torch.dot(u, i))
+            U[uid[rb]] = u + lr * (e * i - lam * u)
+            i = i + lr * (e * u - lam * i)
+        if delta is not None:
+            delta[g] = i - i0
+        else:
+            I[g] = i
+
+
 def mf_sq_err(U, I, uid, iid, r) -> float:
     e = r - (U[uid.long()] * I[iid.long()]).sum(1)
     return float((e.double() ** 2).sum())
