@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""BASELINE config #3: word2vec skip-gram negative sampling, 1M vocab, dim 300, PS-sharded.
+
+    python bench/bench_w2v.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+    (N > 1 under torch.distributed.run: one PS shard per GPU, RCCL all-to-all)
+
+Reports (center, context) pair-updates/s for the whole job: each pair updates
+one input row and 1 + ``negatives`` output rows (block-shared negatives, MFMA
+kernel, see csrc/kernels/sgns.hip).  Synthetic Zipf topic corpus, random init.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--vocab", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=300)
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU per step")
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--lr", type=float, default=0.005)
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    dev = comm.device
+    m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
+                                   wire_dtype=a.wire), comm=comm)
+    toks = synthetic_corpus(max(a.pairs // a.window, 1 << 16) * 2, a.vocab, seed=comm.rank, device=dev)
+    c, o = skipgram_pairs(toks, a.window)
+    n = c.numel()
+
+    def batch(i):
+        s = (i * a.pairs) % max(n - a.pairs, 1)
+        return c[s:s + a.pairs], o[s:s + a.pairs]
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    loss0 = m.step(*batch(0), with_loss=True)
+    for i in range(a.warmup):
+        m.step(*batch(i + 1))
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        m.step(*batch(i + 1 + a.warmup))
+    sync()
+    comm.barrier()
+    dt = comm.max_over_ranks(time.perf_counter() - t0)
+    loss1 = m.step(*batch(0), with_loss=True)
+    if comm.rank == 0:
+        total = a.pairs * a.steps * comm.world
+        print(json.dumps({
+            "metric": "word2vec SGNS pair-updates/sec (whole node)", "value": total / dt, "unit": "pairs/s",
+            "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
+            "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
+            "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared 32/block)",
+                       "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -110,16 +110,46 @@ __device__ __forceinline__ void key_dest(int32_t k, int W, int part_kind, int64_
   else { d = (int)(k / block); if (d >= W) d = W - 1; local = (int32_t)(k - (int64_t)d * block); }
 }
 
+// Wave-aggregated slot allocation: the lanes of a wave that target the same
+// shard take their slots with ONE atomicAdd (leader lane), ranks by popcount.
+// A per-lane atomicAdd on W (often 1) counters serialises the whole batch on a
+// single address (measured 11 ms for 1M owners on one counter).
+__device__ __forceinline__ int32_t wave_alloc(bool want, int d, int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(want);
+  int32_t slot = -1;
+  while (pending) {  // uniform: every lane sees the same ballots
+    const int leader = __ffsll((long long)pending) - 1;
+    const int dd = __shfl(d, leader, 64);
+    const unsigned long long m = __ballot(want && d == dd);
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(counts + dd, (int32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (want && d == dd) slot = base + (int32_t)__popcll(m & ((1ull << lane) - 1ull));
+    pending &= ~m;
+  }
+  return slot;
+}
+
 __global__ void dedup_assign_kernel(const int32_t* __restrict__ keys, int64_t n, const unsigned long long* __restrict__ map,
                                     int W, int part_kind, int64_t block, int32_t* __restrict__ counts,
                                     int32_t* __restrict__ owner_slot) {
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = keys[b];
-    const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
-    if (owner != (uint32_t)b) continue;
-    int d; int32_t local;
-    key_dest(k, W, part_kind, block, d, local);
-    owner_slot[b] = atomicAdd(counts + d, 1);
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // wave-uniform loop bound: every lane of a wave runs the same trip count
+  for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); w0 < n; w0 += stride) {
+    const int64_t b = w0 + lane;
+    bool own = false;
+    int d = 0;
+    if (b < n) {
+      const int32_t k = keys[b];
+      const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+      int32_t local;
+      key_dest(k, W, part_kind, block, d, local);
+      own = owner == (uint32_t)b;
+    }
+    const int32_t s = wave_alloc(own, d, counts);
+    if (own) owner_slot[b] = s;
   }
 }
 
@@ -153,13 +183,18 @@ __global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, int64_t n
 // that ship raw (non-deduplicated) keys.
 __global__ void bucketize_kernel(const int32_t* __restrict__ keys, int64_t n, int W, int part_kind, int64_t block,
                                  int32_t* __restrict__ shard, int32_t* __restrict__ counts) {
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = keys[b] < 0 ? -keys[b] : keys[b];
-    int d;
-    if (part_kind == 0) d = k % W;
-    else { d = (int)(k / block); if (d >= W) d = W - 1; }
-    shard[b] = d;
-    atomicAdd(counts + d, 1);
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); w0 < n; w0 += stride) {
+    const int64_t b = w0 + lane;
+    int d = 0;
+    if (b < n) {
+      const int32_t k = keys[b] < 0 ? -keys[b] : keys[b];
+      if (part_kind == 0) d = k % W;
+      else { d = (int)(k / block); if (d >= W) d = W - 1; }
+      shard[b] = d;
+    }
+    wave_alloc(b < n, d, counts);
   }
 }
 

@@ -1,0 +1,121 @@
+"""Word2vec skip-gram with negative sampling on the parameter server (BASELINE config #3).
+
+Not in the reference's model library; it is the north-star's third workload
+("word2vec SGNS, 1M vocab, dim 300, 8 PS shards over xGMI") and has the same
+shape as the MF worker loop (K4+K5 with a sigmoid loss).
+
+Parameters: input vectors ``W_in[V, D]`` (init U[-0.5/D, 0.5/D)) and output
+vectors ``W_out[V, D]`` (zeros), each a hash-sharded PS table.  One step on a
+micro-batch of (center, context) pairs:
+
+1. draw 32 shared negatives per 32 pairs from unigram^0.75 (alias table, K5);
+2. pull the center rows from ``W_in`` and context + negative rows from
+   ``W_out`` (deduplicated all-to-all, ``TensorPS``);
+3. ``ops.sgns_step`` (MFMA, K6) computes per-row deltas;
+4. push both delta sets; the PS adds them.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ... import ops
+from ...parallel.comm import Comm
+from ...parallel.table import ShardedTable
+from ...parallel.tensor_ps import TensorPS
+
+_WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+@dataclass
+class SGNSConfig:
+    vocab_size: int = 1_000_000
+    dim: int = 300
+    window: int = 5
+    negatives: int = 5            # per-pair negatives the shared block emulates
+    learning_rate: float = 0.025
+    unigram_power: float = 0.75
+    seed: int = 0
+    wire_dtype: str = "fp32"
+
+
+class DistributedSGNS:
+    BLOCK = 32  # pairs per block == shared negatives per block (kernel constant)
+
+    def __init__(self, cfg: SGNSConfig, counts: Optional[torch.Tensor] = None, comm: Optional[Comm] = None):
+        self.cfg = cfg
+        self.comm = comm or Comm()
+        W, r, dev = self.comm.world, self.comm.rank, self.comm.device
+        D = cfg.dim
+        self.w_in = ShardedTable(cfg.vocab_size, D, r, W, "hash", ("uniform", -0.5 / D, 0.5 / D), cfg.seed, dev)
+        self.w_out = ShardedTable(cfg.vocab_size, D, r, W, "hash", ("zeros",), cfg.seed + 1, dev)
+        wire = _WIRE[cfg.wire_dtype]
+        self.ps_in = TensorPS(self.w_in, self.comm, wire)
+        self.ps_out = TensorPS(self.w_out, self.comm, wire)
+        if counts is None:  # Zipf-like default frequency profile
+            counts = 1.0 / torch.arange(1, cfg.vocab_size + 1, dtype=torch.float64)
+        prob, alias = ops.build_alias_table((counts.double() ** cfg.unigram_power).numpy())
+        self.prob, self.alias = prob.to(dev), alias.to(dev)
+        self.counter = 0
+        self.pairs_seen = 0
+
+    def step(self, centers: torch.Tensor, contexts: torch.Tensor, lr: Optional[float] = None,
+             with_loss: bool = False):
+        c = self.cfg
+        lr = c.learning_rate if lr is None else lr
+        P = centers.numel()
+        nb = (P + self.BLOCK - 1) // self.BLOCK
+        negs = ops.sample_alias(self.prob, self.alias, nb * self.BLOCK, seed=c.seed + 17 * self.comm.rank,
+                                counter=self.counter)
+        self.counter += 1
+        rows_in, plan_in = self.ps_in.pull(centers)
+        rows_out, plan_out = self.ps_out.pull(torch.cat([contexts.to(torch.int32), negs]))
+        dev = rows_in.device
+        d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
+        d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
+        pos_o = plan_out.pos[:P].contiguous()
+        pos_neg = plan_out.pos[P:].contiguous()
+        loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
+                             c.negatives / self.BLOCK, d_in, d_out, with_loss=with_loss)
+        self.ps_in.push(plan_in, d_in)
+        self.ps_out.push(plan_out, d_out)
+        self.pairs_seen += P
+        if with_loss:
+            return float(loss.item()) / max(P, 1)
+        return None
+
+    def embeddings(self, only_touched: bool = True):
+        return self.w_in.dump(only_touched)
+
+
+def skipgram_pairs(tokens: torch.Tensor, window: int, generator: Optional[torch.Generator] = None):
+    """(center, context) pairs with word2vec's random reduced window b ~ U{1..window}."""
+    T = tokens.numel()
+    b = torch.randint(1, window + 1, (T,), generator=generator, device=tokens.device)
+    cs, os_ = [], []
+    for o in range(1, window + 1):
+        idx = torch.arange(T - o, device=tokens.device)
+        fwd = b[idx] >= o           # context t+o of center t
+        bwd = b[idx + o] >= o       # context t of center t+o
+        cs += [tokens[idx][fwd], tokens[idx + o][bwd]]
+        os_ += [tokens[idx + o][fwd], tokens[idx][bwd]]
+    return torch.cat(cs).to(torch.int32), torch.cat(os_).to(torch.int32)
+
+
+def synthetic_corpus(n_tokens: int, vocab_size: int, n_topics: int = 64, topic_len: int = 50, seed: int = 0,
+                     device="cpu") -> torch.Tensor:
+    """Zipf-frequency tokens in topic runs: words co-occur with their topic's words,
+    so embeddings have structure to learn."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    topic_of_word = torch.randint(0, n_topics, (vocab_size,), generator=g)
+    order = torch.argsort(topic_of_word, stable=True)
+    starts = torch.searchsorted(topic_of_word[order], torch.arange(n_topics))
+    sizes = torch.bincount(topic_of_word, minlength=n_topics)
+    n_runs = (n_tokens + topic_len - 1) // topic_len
+    topics = torch.randint(0, n_topics, (n_runs,), generator=g).repeat_interleave(topic_len)[:n_tokens]
+    # Zipf inside the topic via u^3 skew
+    u = torch.rand(n_tokens, generator=g) ** 3
+    rank = (u * sizes[topics].clamp(min=1)).long()
+    return order[starts[topics] + rank].to(torch.int32).to(device)

@@ -204,6 +204,67 @@ def mf_sgd_grouped(U, I, uid, r, ptr, order, lr: float, lam: float = 0.0, delta:
     R.mf_sgd_grouped(U, I, uid, r, ptr, order, lr, lam, delta)
 
 
+def sample_uniform_reject(n: int, k: int, n_items: int, positive=None, user=None, ring=None, mem: int = 0,
+                          seed: int = 0, counter: int = 0, device="cpu") -> torch.Tensor:
+    """``k`` uniform negatives per row, avoiding the positive and the user's ring (K5)."""
+    device = torch.device(device)
+    if device.type == "cuda":
+        out = torch.empty(n * k, dtype=torch.int32, device=device)
+        lib = N.require()
+        N.check(lib.fps_sample_uniform_reject(n, k, n_items, N.ptr(positive), N.ptr(user), N.ptr(ring), mem,
+                                              seed & 0xFFFFFFFF, counter, out.data_ptr(), N.stream_ptr(device)),
+                "sample_uniform_reject")
+        return out
+    return R.sample_uniform_reject(n, k, n_items, positive, user, ring, mem, seed, counter)
+
+
+def build_alias_table(weights):
+    """Walker/Vose alias table of a discrete distribution -> (prob fp32, alias int32) on CPU."""
+    import numpy as np
+
+    w = np.asarray(weights, dtype=np.float64)
+    V = w.size
+    p = w * V / w.sum()
+    prob = np.zeros(V)
+    alias = np.zeros(V, dtype=np.int64)
+    small = [i for i in range(V) if p[i] < 1.0]
+    large = [i for i in range(V) if p[i] >= 1.0]
+    while small and large:
+        s, g = small.pop(), large.pop()
+        prob[s], alias[s] = p[s], g
+        p[g] -= 1.0 - p[s]
+        (small if p[g] < 1.0 else large).append(g)
+    for i in large + small:
+        prob[i], alias[i] = 1.0, i
+    return torch.from_numpy(prob.astype(np.float32)), torch.from_numpy(alias.astype(np.int32))
+
+
+def sample_alias(prob: torch.Tensor, alias: torch.Tensor, n: int, seed: int = 0, counter: int = 0) -> torch.Tensor:
+    if prob.is_cuda:
+        out = torch.empty(n, dtype=torch.int32, device=prob.device)
+        lib = N.require()
+        N.check(lib.fps_sample_alias(_c(prob).data_ptr(), _c(alias).data_ptr(), prob.numel(), n, seed & 0xFFFFFFFF,
+                                     counter, out.data_ptr(), N.stream_ptr(prob.device)), "sample_alias")
+        return out
+    return R.sample_alias(prob, alias, n, seed, counter)
+
+
+def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: float, d_in, d_out,
+              with_loss: bool = False):
+    """Block-shared-negative skip-gram step on MFMA (K6); deltas accumulate into
+    ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has 32 rows per 32 pairs."""
+    D = rows_in.shape[1]
+    if rows_in.is_cuda:
+        loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
+        lib = N.require()
+        N.check(lib.fps_sgns_step(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
+                                  int(rows_in.dtype == torch.bfloat16), _c(pos_c).data_ptr(), _c(pos_o).data_ptr(),
+                                  _c(pos_neg).data_ptr(), pos_c.numel(), D, lr, neg_weight, _c(d_in).data_ptr(),
+                                  _c(d_out).data_ptr(), N.ptr(loss), N.stream_ptr(rows_in.device)), "sgns_step")
+        return loss
+    return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out)])
+
+
 def mf_sq_err(U, I, uid, iid, r) -> torch.Tensor:
     """Sum of squared rating errors (device scalar on GPU) (K14)."""
     if _on_gpu(U):

@@ -175,6 +175,70 @@ def mf_sgd_grouped(U, I, uid, r, ptr, order, lr, lam=0.0, delta=None):
             I[g] = i
 
 
+def _u32(x):
+    return torch.as_tensor(x, dtype=torch.int64) & M32
+
+
+def rnd(seed: int, counter: int, i: torch.Tensor, salt) -> torch.Tensor:
+    """Counter-based RNG of ``csrc/kernels/sampling.hip`` (uint32 per index)."""
+    i = i.to(torch.int64)
+    h = fmix32(_u32(seed ^ 0x68BC21EB))
+    h = fmix32(h ^ _u32(counter & M32))
+    h = fmix32(h ^ _u32((counter >> 32) & M32) ^ (i & M32))
+    salt = torch.as_tensor(salt, dtype=torch.int64)
+    h = fmix32(h ^ ((i >> 32) & M32) ^ ((salt * 0x9E3779B9) & M32))
+    return h
+
+
+def sample_uniform_reject(n, k, n_items, positive=None, user=None, ring=None, mem=0, seed=0, counter=0):
+    t = torch.arange(n * k, dtype=torch.int64)
+    b = t // k
+    pos = positive.long()[b] if positive is not None else torch.full_like(t, -1)
+    out = torch.zeros(n * k, dtype=torch.int64)
+    done = torch.zeros(n * k, dtype=torch.bool)
+    rows = ring.long().view(-1, mem)[user.long()[b]] if (ring is not None and user is not None and mem) else None
+    for tries in range(32):
+        cand = (rnd(seed, counter, t, tries) * n_items) >> 32
+        bad = cand == pos
+        if rows is not None:
+            bad |= (rows == cand[:, None]).any(1)
+        take = ~done
+        out[take] = cand[take]
+        done |= ~bad
+    return out.to(torch.int32)
+
+
+def sample_alias(prob, alias, n, seed=0, counter=0):
+    t = torch.arange(n, dtype=torch.int64)
+    V = prob.numel()
+    col = (rnd(seed, counter, t, 1) * V) >> 32
+    u = (rnd(seed, counter, t, 2) >> 8).to(torch.float32) * (1.0 / 16777216.0)
+    return torch.where(u < prob[col], col, alias.long()[col]).to(torch.int32)
+
+
+def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out):
+    """Block-shared-negative SGNS (32 pairs x 32 negatives per block); returns the loss."""
+    P = pos_c.numel()
+    loss = 0.0
+    Hall = rows_in.float()[pos_c.long()]
+    Oall = rows_out.float()[pos_o.long()]
+    for blk in range((P + 31) // 32):
+        sl = slice(32 * blk, min(P, 32 * blk + 32))
+        H, O = Hall[sl], Oall[sl]
+        negs = pos_neg.long()[32 * blk: 32 * blk + 32]
+        Nn = rows_out.float()[negs]
+        sp = (H * O).sum(1)
+        S = H @ Nn.T
+        gpos = lr * (1 - torch.sigmoid(sp))
+        G = -lr * neg_weight * torch.sigmoid(S)
+        d_in.index_add_(0, pos_c.long()[sl], G @ Nn + gpos[:, None] * O)
+        d_out.index_add_(0, negs, G.T @ H)
+        d_out.index_add_(0, pos_o.long()[sl], gpos[:, None] * H)
+        loss += float(-torch.log(torch.sigmoid(sp) + 1e-12).sum()
+                      - neg_weight * torch.log(1 - torch.sigmoid(S) + 1e-12).sum())
+    return loss
+
+
 def mf_sq_err(U, I, uid, iid, r) -> float:
     e = r - (U[uid.long()] * I[iid.long()]).sum(1)
     return float((e.double() ** 2).sum())

@@ -85,11 +85,13 @@ class Comm:
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Variable-split all-to-all along dim 0 (rows of any trailing shape)."""
         n_out = int(sum(recv_splits))
-        if out is None:
-            out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
         if self.world == 1:
+            if out is None:  # nothing leaves the rank: hand the buffer through
+                return send[:n_out]
             out[:n_out].copy_(send[:n_out])
             return out
+        if out is None:
+            out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
         row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
         self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
         dist.all_to_all_single(out[:n_out], send[: int(sum(send_splits))], list(map(int, recv_splits)),

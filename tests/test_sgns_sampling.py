@@ -1,0 +1,115 @@
+"""Word2vec SGNS + negative sampling: CPU reference semantics, GPU kernels vs reference, gloo distributed."""
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_ranks
+from flink_parameter_server_1_amd import ops
+from flink_parameter_server_1_amd.ops import reference as R
+
+
+def test_alias_table_distribution():
+    w = np.array([5.0, 1.0, 3.0, 1.0])
+    prob, alias = ops.build_alias_table(w)
+    s = ops.sample_alias(prob, alias, 200_000, seed=3)
+    freq = torch.bincount(s.long(), minlength=4).double() / s.numel()
+    np.testing.assert_allclose(freq.numpy(), w / w.sum(), atol=0.01)
+
+
+def test_uniform_reject_avoids_positive_and_ring():
+    pos = torch.tensor([0, 1, 2, 3], dtype=torch.int32)
+    user = torch.tensor([0, 1, 0, 1], dtype=torch.int32)
+    ring = torch.tensor([[4, 5], [6, -1]], dtype=torch.int32).flatten()
+    out = ops.sample_uniform_reject(4, 50, 8, pos, user, ring, 2, seed=1).view(4, 50)
+    for b in range(4):
+        banned = {int(pos[b])} | ({4, 5} if user[b] == 0 else {6})
+        assert not (set(out[b].tolist()) & banned)
+
+
+def test_sgns_cpu_learns_cooccurrence():
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    cfg = SGNSConfig(vocab_size=2000, dim=16, window=3, learning_rate=0.025)
+    m = DistributedSGNS(cfg)
+    toks = synthetic_corpus(40000, 2000, n_topics=10, seed=1)
+    c, o = skipgram_pairs(toks, 3, torch.Generator().manual_seed(0))
+    first = m.step(c[:2048], o[:2048], with_loss=True)
+    for s in range(0, c.numel() - 1024, 1024):
+        m.step(c[s:s + 1024], o[s:s + 1024])
+    last = m.step(c[:2048], o[:2048], with_loss=True)
+    assert last < 0.8 * first, (first, last)
+
+
+def _dist_sgns(rank, world):
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=2000, dim=8, window=2, learning_rate=0.025))
+    toks = synthetic_corpus(12000, 2000, n_topics=6, seed=rank)
+    c, o = skipgram_pairs(toks, 2, torch.Generator().manual_seed(rank))
+    first = m.step(c[:1024], o[:1024], with_loss=True)
+    for s in range(0, c.numel() - 512, 512):
+        m.step(c[s:s + 512], o[s:s + 512])
+    return first, m.step(c[:1024], o[:1024], with_loss=True)
+
+
+def test_sgns_distributed_gloo():
+    res = run_ranks(_dist_sgns, 2)
+    for first, last in res:
+        assert last < first
+
+
+# ----------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [16, 64, 100, 300])
+@pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
+def test_sgns_kernel_matches_reference(D, wire):
+    torch.manual_seed(D)
+    Uin, Uout, P = 300, 400, 200
+    rows_in = (torch.randn(Uin, D) * 0.3).to(wire)
+    rows_out = (torch.randn(Uout, D) * 0.3).to(wire)
+    pos_c = torch.randint(0, Uin, (P,), dtype=torch.int32)
+    pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
+    pos_neg = torch.randint(0, Uout, (((P + 31) // 32) * 32,), dtype=torch.int32)
+    d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
+    loss_r = R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, 0.05, 5 / 32, d_in_r, d_out_r)
+    dev = "cuda"
+    d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
+    loss = ops.sgns_step(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), 0.05,
+                         5 / 32, d_in, d_out, with_loss=True)
+    torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=2e-6)
+    torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=2e-6)
+    assert abs(float(loss) - loss_r) / loss_r < 1e-4
+
+
+@pytest.mark.gpu
+def test_sampling_kernels_match_reference():
+    prob, alias = ops.build_alias_table(np.arange(1, 101, dtype=np.float64))
+    a = ops.sample_alias(prob.cuda(), alias.cuda(), 10000, seed=5, counter=7).cpu()
+    b = R.sample_alias(prob, alias, 10000, 5, 7)
+    assert torch.equal(a, b)
+    pos = torch.randint(0, 50, (300,), dtype=torch.int32)
+    user = torch.randint(0, 10, (300,), dtype=torch.int32)
+    ring = torch.randint(-1, 50, (10 * 4,), dtype=torch.int32)
+    g = ops.sample_uniform_reject(300, 5, 50, pos.cuda(), user.cuda(), ring.cuda(), 4, seed=2, counter=9,
+                                  device="cuda").cpu()
+    c = R.sample_uniform_reject(300, 5, 50, pos, user, ring, 4, 2, 9)
+    assert torch.equal(g, c)
+
+
+@pytest.mark.gpu
+def test_sgns_gpu_training_reduces_loss():
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=20000, dim=128, window=4, learning_rate=0.01),
+                        comm=Comm(device=torch.device("cuda")))
+    toks = synthetic_corpus(400000, 20000, n_topics=50, seed=1, device="cuda")
+    c, o = skipgram_pairs(toks, 4)
+    first = m.step(c[:8192], o[:8192], with_loss=True)
+    for s in range(0, c.numel() - 8192, 8192):
+        m.step(c[s:s + 8192], o[s:s + 8192])
+    last = m.step(c[:8192], o[:8192], with_loss=True)
+    assert last < 0.8 * first, (first, last)
