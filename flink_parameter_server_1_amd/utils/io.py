@@ -1,0 +1,258 @@
+"""Model formats, data readers and checkpoint / resume.
+
+* ``id;value`` text — one coordinate per line in coordinate order per id,
+  users and items in separate files: the reference's dump format
+  (``T/matrix/factorization/PSOnlineMatrixFactorizationImplicitTest.scala:76-91``),
+  read by its notebooks.  ``write_factors_text`` / ``read_factors_text``.
+* model streams — ``(id, value)`` iterables for ``transform_with_model_load``
+  (``model_stream_from_text``) and the last-writer-wins fold of an output
+  stream (``fold_model``).
+* binary shard snapshots — ``ids int64[n] + values fp32[n, d]`` with a header
+  (partitioner kind, num ids, dim, world, rank, step).  ``restore_table``
+  re-shards: it reads every shard file and keeps the ids this rank owns, so a
+  checkpoint written at P shards restores at any P'.
+* ``Checkpointer`` — periodic snapshots of named tables + a JSON manifest,
+  atomic publish (tmp + rename), ``restore_latest``.  The reference has no
+  runtime checkpointing at all (``README.md:67-69``).
+* rating logs — ``ts user item [rating]`` lines (space/comma/tab), the input
+  format of the reference's experiment drivers (``read_ratings``).
+* PA prediction log lines ``###PS###t;<label>;[k -> v,...]``
+  (``M/passive/aggressive/classification/binary/PABinaryClassificationOffline.scala:356``).
+
+Heavy lifting is in C++ (``csrc/host/fps_host.cpp``) with Python fallbacks.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import time
+from typing import Dict, Iterable, Iterator, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import native_host as NH
+
+
+# ------------------------------------------------------------------ id;value text
+def write_factors_text(path: str, ids, values, append: bool = False) -> None:
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.int64))
+    vals = np.ascontiguousarray(np.asarray(values, dtype=np.float32)).reshape(ids.size, -1)
+    L = NH.lib()
+    if L is not None:
+        rc = L.fps_write_factors_text(path.encode(), NH._p(ids), NH._p(vals), ids.size, vals.shape[1], int(append))
+        if rc != 0:
+            raise OSError(f"cannot write {path}")
+        return
+    with open(path, "a" if append else "w") as f:
+        for i, row in zip(ids.tolist(), vals):
+            for v in row:
+                f.write(f"{i};{float(v):.9g}\n")
+
+
+def read_factors_text(path: str) -> Dict[int, np.ndarray]:
+    """``{id: vector}``; consecutive lines with the same id form the vector."""
+    L = NH.lib()
+    if L is not None:
+        n = L.fps_read_id_value_text(path.encode(), 0, None, None)
+        if n < 0:
+            raise FileNotFoundError(path)
+        ids = np.empty(n, dtype=np.int64)
+        vals = np.empty(n, dtype=np.float64)
+        n = L.fps_read_id_value_text(path.encode(), n, NH._p(ids), NH._p(vals))
+        ids, vals = ids[:n], vals[:n]
+    else:
+        rows = [ln.strip().split(";") for ln in open(path) if ln.strip()]
+        ids = np.array([int(r[0]) for r in rows], dtype=np.int64)
+        vals = np.array([float(r[1]) for r in rows], dtype=np.float64)
+    out: Dict[int, list] = {}
+    if ids.size:
+        cut = np.flatnonzero(np.diff(ids)) + 1
+        for seg_i, seg_v in zip(np.split(ids, cut), np.split(vals, cut)):
+            out.setdefault(int(seg_i[0]), []).extend(seg_v.tolist())
+    return {k: np.asarray(v) for k, v in out.items()}
+
+
+def model_stream_from_text(path: str) -> Iterator[Tuple[int, np.ndarray]]:
+    """``(id, vector)`` records for ``transform_with_model_load``."""
+    yield from read_factors_text(path).items()
+
+
+def fold_model(stream, side: str = "right") -> Dict[int, object]:
+    """Last-writer-wins fold of an output stream (the model the stream describes)."""
+    out = {}
+    for e in stream:
+        if (side == "right" and e.is_right) or (side == "left" and e.is_left):
+            k, v = e.value
+            out[k] = v
+    return out
+
+
+def write_prediction_log(lines: Iterable[Tuple[dict, object]], path: Optional[str] = None) -> List[str]:
+    res = [f"###PS###t;{label};[{','.join(f'{k} -> {v}' for k, v in sorted(vec.items()))}]"
+           for vec, label in lines]
+    if path:
+        with open(path, "w") as f:
+            f.write("\n".join(res) + "\n")
+    return res
+
+
+# ------------------------------------------------------------------ rating logs
+def read_ratings(path: str, default_rating: float = 1.0):
+    """``ts user item [rating]`` lines -> numpy arrays (ts, user, item, rating)."""
+    L = NH.lib()
+    if L is not None:
+        n = L.fps_count_lines(path.encode())
+        if n < 0:
+            raise FileNotFoundError(path)
+        ts = np.empty(n, dtype=np.int64)
+        u = np.empty(n, dtype=np.int32)
+        i = np.empty(n, dtype=np.int32)
+        r = np.empty(n, dtype=np.float32)
+        m = L.fps_parse_ratings(path.encode(), n, NH._p(ts), NH._p(u), NH._p(i), NH._p(r), default_rating)
+        return ts[:m], u[:m], i[:m], r[:m]
+    rows = []
+    for ln in open(path):
+        parts = ln.replace(",", " ").replace("\t", " ").split()
+        if len(parts) >= 3:
+            rows.append((int(parts[0]), int(parts[1]), int(parts[2]),
+                         float(parts[3]) if len(parts) > 3 else default_rating))
+    a = np.array(rows, dtype=np.float64).reshape(-1, 4)
+    return a[:, 0].astype(np.int64), a[:, 1].astype(np.int32), a[:, 2].astype(np.int32), a[:, 3].astype(np.float32)
+
+
+def synthetic_ratings_host(n: int, n_local_users: int, n_items: int, seed: int = 0, offset: int = 0):
+    """Multithreaded C++ synthetic rating generator (host-side data loader)."""
+    u = np.empty(n, dtype=np.int32)
+    i = np.empty(n, dtype=np.int32)
+    r = np.empty(n, dtype=np.float32)
+    L = NH.lib()
+    if L is None:
+        rng = np.random.default_rng(seed + offset)
+        return (rng.integers(0, n_local_users, n, dtype=np.int32), rng.integers(0, n_items, n, dtype=np.int32),
+                rng.random(n, dtype=np.float32))
+    L.fps_gen_ratings(n, n_local_users, n_items, seed & 0xFFFFFFFF, offset, NH._p(u), NH._p(i), NH._p(r))
+    return u, i, r
+
+
+# ------------------------------------------------------------------ snapshots
+def save_snapshot(path: str, ids: torch.Tensor, values: torch.Tensor, *, part_kind: int, num_ids: int, world: int,
+                  rank: int, step: int = 0) -> None:
+    ids_np = np.ascontiguousarray(ids.detach().to("cpu", torch.int64).numpy())
+    vals_np = np.ascontiguousarray(values.detach().to("cpu", torch.float32).numpy()).reshape(ids_np.size, -1)
+    L = NH.lib()
+    if L is not None:
+        rc = L.fps_write_snapshot(path.encode(), part_kind, num_ids, vals_np.shape[1], world, rank, step,
+                                  NH._p(ids_np), NH._p(vals_np), ids_np.size)
+        if rc != 0:
+            raise OSError(f"snapshot write failed ({rc}): {path}")
+        return
+    meta = dict(part_kind=part_kind, num_ids=num_ids, dim=vals_np.shape[1], world=world, rank=rank, step=step)
+    np.savez(path + ".npz", ids=ids_np, values=vals_np, meta=json.dumps(meta))
+    os.replace(path + ".npz", path)
+
+
+def load_snapshot(path: str):
+    """-> (meta dict, ids int64[n], values fp32[n, d])."""
+    L = NH.lib()
+    if L is not None:
+        meta = np.zeros(7, dtype=np.int64)
+        if L.fps_read_snapshot_header(path.encode(), NH._p(meta)) == 0:
+            keys = ["part_kind", "num_ids", "dim", "world", "rank", "n_rows", "step"]
+            m = dict(zip(keys, meta.tolist()))
+            ids = np.empty(m["n_rows"], dtype=np.int64)
+            vals = np.empty((m["n_rows"], m["dim"]), dtype=np.float32)
+            if L.fps_read_snapshot(path.encode(), NH._p(ids), NH._p(vals), m["n_rows"]) != 0:
+                raise OSError(f"corrupt snapshot {path}")
+            return m, ids, vals
+    z = np.load(path, allow_pickle=False)
+    m = json.loads(str(z["meta"]))
+    return m, z["ids"], z["values"]
+
+
+def save_table(table, path: str, step: int = 0, only_touched: bool = False) -> None:
+    ids, vals = table.dump(only_touched)
+    save_snapshot(path, ids, vals, part_kind=table.part_kind, num_ids=table.num_ids, world=table.world,
+                  rank=table.rank, step=step)
+
+
+def restore_table(table, pattern: str) -> int:
+    """Load every shard file matching ``pattern`` and keep this rank's ids (re-sharding)."""
+    n = 0
+    for f in sorted(glob.glob(pattern)):
+        _, ids, vals = load_snapshot(f)
+        if ids.size:
+            table.load(torch.from_numpy(ids), torch.from_numpy(vals))
+            n += int((table.part.shard_tensor(torch.from_numpy(ids)) == table.rank).sum())
+    return n
+
+
+class Checkpointer:
+    """Periodic snapshots of named ``ShardedTable``s.
+
+    Layout: ``<dir>/step_<k>/<name>.shard<rank>-of-<world>.bin`` + ``manifest.json``
+    written by rank 0 after a barrier (the snapshot is complete when the
+    manifest exists).  ``restore_latest`` re-shards to the current world size.
+    """
+
+    def __init__(self, directory: str, tables: Dict[str, object], comm=None, every_steps: int = 0, keep: int = 2):
+        self.dir = directory
+        self.tables = tables
+        self.comm = comm
+        self.every = every_steps
+        self.keep = keep
+        os.makedirs(directory, exist_ok=True)
+
+    def _rank_world(self):
+        if self.comm is None:
+            return 0, 1
+        return self.comm.rank, self.comm.world
+
+    def maybe_save(self, step: int, extra: Optional[dict] = None) -> bool:
+        if self.every and step % self.every == 0 and step > 0:
+            self.save(step, extra)
+            return True
+        return False
+
+    def save(self, step: int, extra: Optional[dict] = None) -> str:
+        rank, world = self._rank_world()
+        d = os.path.join(self.dir, f"step_{step:09d}")
+        os.makedirs(d, exist_ok=True)
+        for name, t in self.tables.items():
+            save_table(t, os.path.join(d, f"{name}.shard{rank}-of-{world}.bin"), step)
+        if self.comm is not None:
+            self.comm.barrier()
+        if rank == 0:
+            manifest = {"step": step, "world": world, "tables": sorted(self.tables), "time": time.time(),
+                        "extra": extra or {}}
+            with open(os.path.join(d, "manifest.json.tmp"), "w") as f:
+                json.dump(manifest, f)
+            os.replace(os.path.join(d, "manifest.json.tmp"), os.path.join(d, "manifest.json"))
+            self._gc()
+        if self.comm is not None:
+            self.comm.barrier()
+        return d
+
+    def _gc(self):
+        done = sorted(p for p in glob.glob(os.path.join(self.dir, "step_*"))
+                      if os.path.exists(os.path.join(p, "manifest.json")))
+        for p in done[:-self.keep] if self.keep else []:
+            for f in glob.glob(os.path.join(p, "*")):
+                os.remove(f)
+            os.rmdir(p)
+
+    def latest(self) -> Optional[str]:
+        done = sorted(p for p in glob.glob(os.path.join(self.dir, "step_*"))
+                      if os.path.exists(os.path.join(p, "manifest.json")))
+        return done[-1] if done else None
+
+    def restore_latest(self) -> Optional[dict]:
+        d = self.latest()
+        if d is None:
+            return None
+        with open(os.path.join(d, "manifest.json")) as f:
+            manifest = json.load(f)
+        for name, t in self.tables.items():
+            restore_table(t, os.path.join(d, f"{name}.shard*-of-*.bin"))
+        return manifest
