@@ -4,8 +4,10 @@
 Metric and config from BASELINE.json: "param updates/sec (whole node), MF-SGD
 10M x 1M rank-64 at 1/2/4/8 MI355X".  One update = one rating-SGD step
 (one user row + one item row of 64 fp32 each).  Synthetic ratings, random
-init, fp32 parameters and compute (``--wire bf16`` optionally halves the
-all-to-all bytes at N > 1; default fp32).
+init, fp32 parameters and compute.  At N > 1 the pulled item rows and pushed
+deltas cross xGMI as bf16 by default (``--wire``; tables and arithmetic stay
+fp32), and the pull of micro-batch k+1 overlaps the SGD of micro-batch k
+(``--no-pipeline`` disables it).
 
     python bench.py --gpus N --steps K --warmup W
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -37,7 +39,9 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--pool", type=int, default=8, help="data pool = pool * batch ratings per GPU")
-    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="all-to-all row dtype; auto = bf16 at N>1")
+    ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "grouped", "flat"])
     ap.add_argument("--force-ps-path", action="store_true",
@@ -56,8 +60,11 @@ def main(argv=None):
     n = comm.world
     if a.gpus != n:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    if a.wire == "auto":
+        a.wire = "bf16" if n > 1 else "fp32"
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
-                   user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode)
+                   user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
+                   pipeline=not a.no_pipeline)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -70,12 +77,14 @@ def main(argv=None):
     for _ in range(a.warmup):
         model.step(*data.batch(step, a.batch))
         step += 1
+    model.flush()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         model.step(*data.batch(step, a.batch))
         step += 1
+    model.flush()  # the last micro-batch's SGD + push run inside the timed region
     sync()
     comm.barrier()
     sync()
@@ -104,6 +113,7 @@ def main(argv=None):
                 "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded)",
                 "wire_dtype": a.wire if (n > 1 or a.force_ps_path) else "none (local PS shard)",
                 "sgd_mode": model.sgd_mode,
+                "pipelined": model.pipeline,
                 "scalar_params_per_s": value * 2 * a.dim,
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
                 if n > 1 else None,

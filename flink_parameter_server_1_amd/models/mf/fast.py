@@ -49,6 +49,7 @@ class MFConfig:
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "grouped" | "flat"
+    pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
 
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
@@ -75,6 +76,8 @@ class DistributedMF:
             mode = "flat"
         self.sgd_mode = mode
         self.grouper = ops.CSRGrouper(dev)
+        self.pipeline = cfg.pipeline and (W > 1 or cfg.force_ps_path)
+        self._pending = None
         self.updates = 0
 
     @property
@@ -90,28 +93,53 @@ class DistributedMF:
         ``iid`` = global item id (int32), ``rating`` fp32."""
         c = self.cfg
         grouped = self.sgd_mode == "grouped"
+        uid_local, iid, rating = uid_local.contiguous(), iid.contiguous(), rating.contiguous()
         if self.comm.world == 1 and not c.force_ps_path:
             if grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
             else:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
+        elif self.pipeline:
+            # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD
+            # of batch k; k's push follows.  Staleness bound: one micro-batch.
+            nxt = (self.ps.pull_async(iid), uid_local, rating)
+            if self._pending is not None:
+                self._finish(self._pending)
+            self._pending = nxt
         else:
             rows, plan = self.ps.pull(iid)
-            if grouped:
-                ptr, order = self.grouper.run(plan.pos, plan.n_unique)
-                delta = torch.empty((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
-                ops.mf_sgd_grouped(self.U, rows, uid_local, rating, ptr, order, c.learning_rate, c.lam, delta)
-            else:
-                delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
-                ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
-                                  self.user_atomic)
-            self.ps.push(plan, delta)
+            self._compute_push(rows, plan, uid_local, rating)
         self.updates += uid_local.numel()
+
+    def _finish(self, pending):
+        (rows, work, plan), uid_local, rating = pending
+        if work is not None:
+            work.wait()
+        self._compute_push(rows, plan, uid_local, rating)
+
+    def _compute_push(self, rows, plan, uid_local, rating):
+        c = self.cfg
+        if self.sgd_mode == "grouped":
+            ptr, order = self.grouper.run(plan.pos, plan.n_unique)
+            delta = torch.empty((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+            ops.mf_sgd_grouped(self.U, rows, uid_local, rating, ptr, order, c.learning_rate, c.lam, delta)
+        else:
+            delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+            ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
+                              self.user_atomic)
+        self.ps.push(plan, delta)
+
+    def flush(self):
+        """Complete the in-flight micro-batch of the pipelined path."""
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            self._finish(p)
 
     @torch.no_grad()
     def sq_err(self, uid_local, iid, rating) -> float:
         """Sum of squared errors of this rank's ratings (items pulled when remote)."""
+        self.flush()
         if self.comm.world == 1:
             return float(ops.mf_sq_err(self.U, self.I, uid_local, iid, rating).item())
         vals = self.ps.pull_values(iid)

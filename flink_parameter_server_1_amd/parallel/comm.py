@@ -98,6 +98,19 @@ class Comm:
                                list(map(int, send_splits)), group=self.group)
         return out
 
+    def all_to_all_async(self, send: torch.Tensor, send_splits: Sequence[int], recv_splits: Sequence[int]):
+        """Non-blocking all-to-all: returns ``(out, work)``; ``work.wait()`` orders the
+        caller's stream after the transfer (no host block).  ``work`` is None at world 1."""
+        n_out = int(sum(recv_splits))
+        if self.world == 1:
+            return send[:n_out], None
+        out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+        row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
+        self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
+        work = dist.all_to_all_single(out, send[: int(sum(send_splits))], list(map(int, recv_splits)),
+                                      list(map(int, send_splits)), group=self.group, async_op=True)
+        return out, work
+
     def all_reduce(self, t: torch.Tensor, op=None) -> torch.Tensor:
         if self.world > 1:
             dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)

@@ -52,7 +52,10 @@ class TensorPS:
         self.dedup = ops.DedupWorkspace(table.num_ids, comm.world, table.part_kind, table.block, table.device)
         self.stats = {"pulls": 0, "unique": 0, "steps": 0}
 
-    def plan(self, keys: torch.Tensor) -> PullPlan:
+    def plan(self, keys: torch.Tensor, persistent: bool = False) -> PullPlan:
+        """Dedup + split exchange + key all-to-all.  ``persistent`` copies the
+        request->row map out of the reusable dedup workspace, so the plan
+        survives the next ``plan`` call (pipelined steps)."""
         keys = keys.to(torch.int32).contiguous()
         counts, prefix, uniq, pos = self.dedup.run(keys)
         recv_counts = self.comm.exchange_counts(counts)
@@ -61,6 +64,10 @@ class TensorPS:
         send_splits, recv_splits = both[:W], both[W:]
         n_unique = int(sum(send_splits))
         recv_keys = self.comm.all_to_all(uniq[:n_unique], send_splits, recv_splits)
+        if persistent:
+            pos = pos.clone()
+            if W == 1:
+                recv_keys = recv_keys.clone()
         self.stats["pulls"] += keys.numel()
         self.stats["unique"] += n_unique
         self.stats["steps"] += 1
@@ -72,6 +79,15 @@ class TensorPS:
         served = self.table.serve(plan.recv_keys, self.wire_dtype)
         rows = self.comm.all_to_all(served, plan.recv_splits, plan.send_splits)
         return rows, plan
+
+    def pull_async(self, keys: torch.Tensor):
+        """Start a pull whose row all-to-all runs on the communicator's stream while
+        the caller keeps computing; returns ``(rows, work, plan)`` -- wait on
+        ``work`` (if not None) before reading ``rows``."""
+        plan = self.plan(keys, persistent=True)
+        served = self.table.serve(plan.recv_keys, self.wire_dtype)
+        rows, work = self.comm.all_to_all_async(served, plan.recv_splits, plan.send_splits)
+        return rows, work, plan
 
     def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0):
         """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply."""
