@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""BASELINE config #4: Passive-Aggressive binary classifier, 1B-dim sparse features, async push/pull.
+
+    python bench/bench_pa.py [--features 1000000000] [--batch 65536] [--nnz 64] [--steps K]
+    (multi-GPU under torch.distributed.run: the feature table is range-sharded over the GPUs)
+
+Reports examples/s and feature-updates/s (nnz pulled + pushed per example) for
+the whole job.  Synthetic CSR batches with labels from a hidden sparse linear
+model; zero-initialised weights (the reference's ``initBinary``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--features", type=int, default=1_000_000_000)
+    ap.add_argument("--batch", type=int, default=1 << 16, help="examples per GPU per step")
+    ap.add_argument("--nnz", type=int, default=64)
+    ap.add_argument("--zipf", type=float, default=2.0)
+    ap.add_argument("--kind", default="binary", choices=["binary", "ova", "pb", "ml"])
+    ap.add_argument("--labels", type=int, default=1)
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from flink_parameter_server_1_amd.models.pa.fast import DistributedPA, PAConfig, synthetic_sparse_batch
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    dev = comm.device
+    m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire),
+                      comm)
+    batches = [synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=comm.rank + 1, step=s, label_count=a.labels,
+                                      device=dev, zipf=a.zipf) for s in range(4)]
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for s in range(a.warmup):
+        m.train_step(*batches[s % 4])
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        m.train_step(*batches[s % 4])
+    sync()
+    comm.barrier()
+    dt = comm.max_over_ranks(time.perf_counter() - t0)
+    ip, idx, val, lab = synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=999, step=0, label_count=a.labels,
+                                               device=dev, zipf=a.zipf)
+    pred = m.predict(ip, idx, val)
+    acc = float(((pred.to(torch.int8) == lab) if a.kind == "binary" else (pred == lab)).float().mean())
+    if comm.rank == 0:
+        ex = a.batch * a.steps * comm.world
+        print(json.dumps({
+            "metric": "PA examples/sec (whole node)", "value": ex / dt, "unit": "examples/s",
+            "feature_updates_per_s": ex * a.nnz / dt, "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
+            "data": "synthetic sparse CSR (hidden linear model labels)", "holdout_accuracy": acc,
+            "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
+                       "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire},
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

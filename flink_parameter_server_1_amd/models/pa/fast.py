@@ -1,0 +1,113 @@
+"""Passive-Aggressive on the tensor engine (BASELINE config #4: 1B-dim sparse features).
+
+Same learning rules and data flow as ``PassiveAggressiveParameterServer``
+(``M/passive/aggressive/PassiveAggressiveParameterServer.scala:239-370``):
+a worker pulls the weights of every active feature of its examples, computes
+the PA step and pushes per-feature deltas that the PS adds; the PS table is
+range-partitioned by default (``rangePartitionerPS``, ``:372-384``).  Here a
+micro-batch of examples travels as CSR tensors; the features are
+deduplicated and pulled with one all-to-all (``TensorPS``), one wave per
+example runs the PA step on the GPU (``ops.pa_binary`` / ``ops.pa_multi``,
+K10-K12), and the per-unique-feature deltas are pushed back.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ... import ops
+from ...parallel.comm import Comm
+from ...parallel.table import ShardedTable
+from ...parallel.tensor_ps import TensorPS
+
+_WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+@dataclass
+class PAConfig:
+    feature_count: int
+    kind: str = "binary"          # binary | ova | pb | ml
+    label_count: int = 1
+    variant: str = "PA"           # PA | PA-I | PA-II (binary / ova)
+    aggressiveness: float = 1.0   # C
+    partition: str = "range"      # range | hash
+    wire_dtype: str = "fp32"
+
+
+class DistributedPA:
+    def __init__(self, cfg: PAConfig, comm: Optional[Comm] = None, cost: Optional[torch.Tensor] = None):
+        self.cfg = cfg
+        self.comm = comm or Comm()
+        self.L = 1 if cfg.kind == "binary" else cfg.label_count
+        if self.L > 64:
+            raise ValueError("multiclass kernels keep the classes on the 64 lanes: label_count <= 64")
+        W, r, dev = self.comm.world, self.comm.rank, self.comm.device
+        self.table = ShardedTable(cfg.feature_count, self.L, r, W, cfg.partition, ("zeros",), 0, dev,
+                                  optimizer="add")
+        self.ps = TensorPS(self.table, self.comm, _WIRE[cfg.wire_dtype])
+        if cfg.kind in ("pb", "ml"):
+            if cost is None:
+                cost = 1.0 - torch.eye(self.L)
+            self.cost = cost.to(dev, torch.float32).contiguous()
+        else:
+            self.cost = None
+        self.examples = 0
+
+    def _run(self, indptr, indices, values, labels, train: bool, with_loss=False):
+        c = self.cfg
+        rows, plan = self.ps.pull(indices)
+        w = rows.float().contiguous()
+        delta = torch.zeros((plan.n_unique, self.L), dtype=torch.float32, device=w.device)
+        if c.kind == "binary":
+            pred, loss = ops.pa_binary(indptr, values, plan.pos, w.view(-1), labels, c.variant, c.aggressiveness,
+                                       delta.view(-1), with_loss)
+        else:
+            pred, loss = ops.pa_multi(indptr, values, plan.pos, w, labels, c.kind, c.variant, c.aggressiveness,
+                                      self.cost, delta, with_loss)
+        if train:
+            self.ps.push(plan, delta)
+            self.examples += indptr.numel() - 1
+        return pred, loss
+
+    def train_step(self, indptr, indices, values, labels, with_loss=False):
+        """Labels: binary +1/-1 (int8, 0 = predict only); multiclass class id (int32, -1 = predict only)."""
+        return self._run(indptr, indices, values, labels, True, with_loss)
+
+    def predict(self, indptr, indices, values):
+        B = indptr.numel() - 1
+        dev = values.device
+        y = (torch.zeros(B, dtype=torch.int8, device=dev) if self.cfg.kind == "binary"
+             else torch.full((B,), -1, dtype=torch.int32, device=dev))
+        return self._run(indptr, indices, values, y, False)[0]
+
+    def dump(self, only_touched=True):
+        return self.table.dump(only_touched)
+
+
+def synthetic_sparse_batch(B: int, nnz: int, feature_count: int, seed: int, step: int, label_count: int = 1,
+                           device="cpu", zipf: float = 1.0):
+    """CSR batch with labels from a hidden sparse linear model (hash-defined per feature),
+    so a PA learner has signal.  Features drawn ``F * u^(1+zipf)`` (skewed toward low ids)."""
+    g = torch.Generator(device=device)
+    g.manual_seed((seed * 1_000_003 + step) & 0x7FFFFFFF)
+    u = torch.rand(B * nnz, generator=g, device=device)
+    idx = torch.clamp((u ** (1.0 + zipf) * feature_count).long(), max=feature_count - 1)
+    vals = torch.rand(B * nnz, generator=g, device=device) + 0.1
+    indptr = torch.arange(0, B * nnz + 1, nnz, dtype=torch.int64, device=device)
+    # hidden model: per-feature class preferences from a hash of the id
+    from ...ops.reference import fmix32
+
+    h = fmix32((idx & 0xFFFFFFFF) ^ 0x5BD1E995)
+    if label_count == 1:
+        s = ((h & 0xFFFF).float() / 65535.0 - 0.5)
+        margin = torch.zeros(B, device=device).index_add_(0, torch.arange(B, device=device).repeat_interleave(nnz),
+                                                          vals * s)
+        labels = torch.where(margin > 0, 1, -1).to(torch.int8)
+    else:
+        cls = (h % label_count)
+        scores = torch.zeros(B, label_count, device=device)
+        scores.index_put_((torch.arange(B, device=device).repeat_interleave(nnz), cls), vals, accumulate=True)
+        labels = torch.argmax(scores, 1).to(torch.int32)
+    return indptr, idx.to(torch.int32), vals, labels

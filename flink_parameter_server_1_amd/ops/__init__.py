@@ -85,12 +85,17 @@ class DedupWorkspace:
     send buffer with splits ``counts``) and each request's row in it.
     """
 
+    #: id spaces above this use a sort-based dedup instead of a dense claim map
+    #: (1B-feature PA tables would otherwise need an 8 GB map per worker)
+    DENSE_MAP_MAX_IDS = 1 << 28
+
     def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu"):
         self.num_ids, self.W, self.part_kind, self.block = num_ids, W, part_kind, block
         self.device = torch.device(device)
         self.epoch = 0
         self.cap = 0
-        if self.device.type == "cuda":
+        self.sort_based = num_ids > self.DENSE_MAP_MAX_IDS
+        if self.device.type == "cuda" and not self.sort_based:
             self.map = torch.zeros(num_ids, dtype=torch.int64, device=device)
             self.counts = torch.zeros(W, dtype=torch.int32, device=device)
             self.prefix = torch.zeros(W + 1, dtype=torch.int32, device=device)
@@ -102,9 +107,27 @@ class DedupWorkspace:
             self.uniq = torch.empty(self.cap, dtype=torch.int32, device=self.device)
             self.pos = torch.empty(self.cap, dtype=torch.int32, device=self.device)
 
+    def _run_sorted(self, keys: torch.Tensor):
+        """Radix-sort dedup (torch.unique on device) for huge id spaces."""
+        uniq_g, inv = torch.unique(keys.long(), sorted=True, return_inverse=True)
+        d, local = R.shard_of(uniq_g, self.W, self.part_kind, self.block)
+        if self.part_kind == 0 and self.W > 1:
+            order = torch.argsort(d, stable=True)
+            slot_of = torch.empty_like(order)
+            slot_of[order] = torch.arange(order.numel(), device=order.device)
+            uniq, pos = local[order], slot_of[inv]
+        else:  # range partitioning: sorted keys are already grouped by shard
+            uniq, pos = local, inv
+        counts = torch.bincount(d, minlength=self.W).to(torch.int32)
+        prefix = torch.zeros(self.W + 1, dtype=torch.int32, device=keys.device)
+        prefix[1:] = torch.cumsum(counts, 0)
+        return counts, prefix, uniq.to(torch.int32), pos.to(torch.int32)
+
     def run(self, keys: torch.Tensor):
         if self.device.type != "cuda":
             return R.dedup(keys, self.W, self.part_kind, self.block)
+        if self.sort_based:
+            return self._run_sorted(keys)
         n = keys.numel()
         self._grow(max(n, 1))
         self.epoch += 1
@@ -263,6 +286,42 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
                                   _c(d_out).data_ptr(), N.ptr(loss), N.stream_ptr(rows_in.device)), "sgns_step")
         return loss
     return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out)])
+
+
+PA_VARIANTS = {"PA": 0, "PA-I": 1, "PA-II": 2}
+PA_MODES = {"ova": 0, "pb": 1, "ml": 2}
+
+
+def pa_binary(indptr, xval, pos, w, y, variant: str, C: float, delta, with_loss: bool = False):
+    """Binary PA on a CSR micro-batch (K10); returns ``(pred int8[B], loss or None)``."""
+    B = indptr.numel() - 1
+    if xval.is_cuda:
+        pred = torch.empty(B, dtype=torch.int8, device=xval.device)
+        loss = torch.zeros(1, device=xval.device) if with_loss else None
+        lib = N.require()
+        N.check(lib.fps_pa_binary(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(w).data_ptr(),
+                                  _c(y).data_ptr(), B, PA_VARIANTS[variant], C, _c(delta).data_ptr(),
+                                  pred.data_ptr(), N.ptr(loss), N.stream_ptr(xval.device)), "pa_binary")
+        return pred, loss
+    pred, loss = R.pa_binary(indptr, xval, pos, w, y, PA_VARIANTS[variant], C, delta)
+    return pred, torch.tensor([loss])
+
+
+def pa_multi(indptr, xval, pos, W, y, mode: str, variant: str, C: float, cost, delta, with_loss: bool = False):
+    """Multiclass PA (OVA / cost PB / cost ML) on a CSR micro-batch (K11/K12); L <= 64."""
+    B = indptr.numel() - 1
+    L = W.shape[1]
+    if xval.is_cuda:
+        pred = torch.empty(B, dtype=torch.int32, device=xval.device)
+        loss = torch.zeros(1, device=xval.device) if with_loss else None
+        lib = N.require()
+        N.check(lib.fps_pa_multi(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(W).data_ptr(), L,
+                                 _c(y).data_ptr(), B, PA_MODES[mode], PA_VARIANTS[variant], C, N.ptr(cost),
+                                 _c(delta).data_ptr(), pred.data_ptr(), N.ptr(loss), N.stream_ptr(xval.device)),
+                "pa_multi")
+        return pred, loss
+    pred, loss = R.pa_multi(indptr, xval, pos, W, y, PA_MODES[mode], PA_VARIANTS[variant], C, cost, delta)
+    return pred, torch.tensor([loss])
 
 
 def mf_sq_err(U, I, uid, iid, r) -> torch.Tensor:

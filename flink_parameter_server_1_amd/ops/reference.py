@@ -239,6 +239,63 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_
     return loss
 
 
+def _pa_tau(variant, loss, n2, C):
+    if variant == 0:
+        return torch.where(n2 > 0, loss / n2.clamp(min=1e-30), torch.zeros_like(loss))
+    if variant == 1:
+        return torch.where(n2 > 0, torch.clamp(loss / n2.clamp(min=1e-30), max=C), torch.zeros_like(loss))
+    return loss / (n2 + 1.0 / (2.0 * C))
+
+
+def pa_binary(indptr, xval, pos, w, y, variant, C, delta):
+    """Returns (pred int8 [B], summed hinge loss); accumulates into ``delta[U]``."""
+    B = indptr.numel() - 1
+    seg = torch.repeat_interleave(torch.arange(B), (indptr[1:] - indptr[:-1]).long())
+    m = torch.zeros(B).index_add_(0, seg, xval * w[pos.long()])
+    n2 = torch.zeros(B).index_add_(0, seg, xval * xval)
+    pred = torch.where(m > 0, 1, -1).to(torch.int8)
+    yf = y.float()
+    loss = torch.clamp(1 - yf * m, min=0) * (y != 0)
+    mult = _pa_tau(variant, loss, n2, C) * yf
+    delta.index_add_(0, pos.long(), mult[seg] * xval)
+    return pred, float(loss.sum())
+
+
+def pa_multi(indptr, xval, pos, W, y, mode, variant, C, cost, delta):
+    B = indptr.numel() - 1
+    L = W.shape[1]
+    seg = torch.repeat_interleave(torch.arange(B), (indptr[1:] - indptr[:-1]).long())
+    d = torch.zeros(B, L).index_add_(0, seg, xval[:, None] * W[pos.long()])
+    n2 = torch.zeros(B).index_add_(0, seg, xval * xval)
+    pred = torch.argmax(d, 1).to(torch.int32)
+    total = 0.0
+    lab = y.long()
+    has = lab >= 0
+    if mode == 0:
+        yc = -torch.ones(B, L)
+        yc[has, lab[has]] = 1.0
+        loss = torch.clamp(1 - d * yc, min=0) * has[:, None]
+        mult = _pa_tau(variant, loss, n2[:, None].expand_as(loss), C) * yc
+        delta.index_add_(0, pos.long(), xval[:, None] * mult[seg])
+        total = float(loss.sum())
+    else:
+        labc = lab.clamp(min=0)
+        dy = d[torch.arange(B), labc]
+        score = d if mode == 1 else d - dy[:, None] + torch.sqrt(cost[labc])
+        q = torch.argmax(score, 1)
+        act = has & (q != labc)
+        loss = d[torch.arange(B), q] - dy + torch.sqrt(cost[labc, q])
+        tau = torch.where(n2 > 0, loss / (2 * n2.clamp(min=1e-30)), torch.zeros_like(loss)) * act
+        v = tau[seg] * xval
+        rows = pos.long()
+        dl = torch.zeros(xval.numel(), L)
+        dl[torch.arange(xval.numel()), labc[seg]] += v
+        dl[torch.arange(xval.numel()), q[seg]] -= v
+        delta.index_add_(0, rows, dl)
+        total = float((loss * act).sum())
+    return pred, total
+
+
 def mf_sq_err(U, I, uid, iid, r) -> float:
     e = r - (U[uid.long()] * I[iid.long()]).sum(1)
     return float((e.double() ** 2).sum())

@@ -1,0 +1,131 @@
+"""Passive-Aggressive on the tensor engine: kernels vs reference (GPU), learning on CPU / gloo,
+parity of the batched step with the per-record algorithms."""
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_ranks
+from flink_parameter_server_1_amd import ops
+from flink_parameter_server_1_amd.models.pa.fast import DistributedPA, PAConfig, synthetic_sparse_batch
+from flink_parameter_server_1_amd.ops import reference as R
+
+
+def _acc(m, kind, L, dev="cpu", F=5000):
+    ip, idx, val, lab = synthetic_sparse_batch(2000, 20, F, seed=99, step=0, label_count=L, device=dev)
+    pred = m.predict(ip, idx, val)
+    if kind == "binary":
+        return float((pred.to(torch.int8) == lab).float().mean())
+    return float((pred == lab).float().mean())
+
+
+@pytest.mark.parametrize("kind,L,variant", [("binary", 1, "PA"), ("binary", 1, "PA-I"), ("binary", 1, "PA-II"),
+                                            ("ova", 4, "PA"), ("ova", 4, "PA-II"), ("pb", 4, "PA"),
+                                            ("ml", 4, "PA")])
+def test_pa_fast_learns_cpu(kind, L, variant):
+    F = 5000
+    m = DistributedPA(PAConfig(feature_count=F, kind=kind, label_count=L, variant=variant, aggressiveness=1.0))
+    before = _acc(m, kind, L)
+    for s in range(30):
+        m.train_step(*synthetic_sparse_batch(256, 20, F, seed=1, step=s, label_count=L))
+    after = _acc(m, kind, L)
+    floor = 0.6 if kind == "binary" else 0.4  # chance: 0.5 / 0.25
+    assert after > floor and after > before + 0.1, (before, after)
+
+
+def test_batched_binary_step_equals_per_record_algorithm():
+    """One example per batch == PassiveAggressiveBinaryAlgorithm.delta on the pulled weights."""
+    from flink_parameter_server_1_amd.models.pa.algorithms import PassiveAggressiveBinaryAlgorithm
+    from flink_parameter_server_1_amd.models.pa.sparse import SparseVector
+
+    m = DistributedPA(PAConfig(feature_count=100, kind="binary", variant="PA-I", aggressiveness=0.3))
+    alg = PassiveAggressiveBinaryAlgorithm.build_pai(0.3)
+    w = np.zeros(100)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        idx = np.sort(rng.choice(100, 7, replace=False))
+        val = rng.random(7) + 0.1
+        y = bool(rng.random() < 0.5)
+        for i, d in alg.delta(SparseVector(idx, val, 100), w, y):
+            w[i] += d
+        m.train_step(torch.tensor([0, 7]), torch.tensor(idx, dtype=torch.int32), torch.tensor(val, dtype=torch.float32),
+                     torch.tensor([1 if y else -1], dtype=torch.int8))
+    ids, vals = m.dump(False)
+    np.testing.assert_allclose(vals.flatten().numpy()[np.argsort(ids.numpy())], w, rtol=1e-4, atol=1e-6)
+
+
+def _dist_pa(rank, world):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    F = 8000
+    m = DistributedPA(PAConfig(feature_count=F, kind="ova", label_count=3), Comm())
+    for s in range(25):
+        m.train_step(*synthetic_sparse_batch(128, 20, F, seed=rank + 1, step=s, label_count=3))
+    return _acc(m, "ova", 3, F=F)
+
+
+def test_pa_fast_distributed_gloo():
+    res = run_ranks(_dist_pa, 2)
+    assert all(a > 0.45 for a in res), res  # 3 classes: chance 0.33
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["PA", "PA-I", "PA-II"])
+def test_pa_binary_kernel_matches_reference(variant):
+    torch.manual_seed(1)
+    B, U = 300, 500
+    lens = torch.randint(1, 90, (B,))
+    indptr = torch.zeros(B + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    pos = torch.randint(0, U, (nnz,), dtype=torch.int32)
+    xval = torch.rand(nnz)
+    w = torch.randn(U) * 0.1
+    y = torch.where(torch.rand(B) < 0.5, 1, -1).to(torch.int8)
+    y[::7] = 0
+    dr = torch.zeros(U)
+    pr, lr_ = R.pa_binary(indptr, xval, pos, w, y, ops.PA_VARIANTS[variant], 0.7, dr)
+    d = torch.zeros(U, device="cuda")
+    p, l = ops.pa_binary(indptr.cuda(), xval.cuda(), pos.cuda(), w.cuda(), y.cuda(), variant, 0.7, d, True)
+    assert torch.equal(p.cpu(), pr)
+    torch.testing.assert_close(d.cpu(), dr, rtol=1e-4, atol=1e-5)
+    assert abs(float(l) - lr_) / max(lr_, 1e-6) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["ova", "pb", "ml"])
+@pytest.mark.parametrize("L", [3, 10, 64])
+def test_pa_multi_kernel_matches_reference(mode, L):
+    torch.manual_seed(L)
+    B, U = 200, 300
+    lens = torch.randint(1, 40, (B,))
+    indptr = torch.zeros(B + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    pos = torch.randint(0, U, (nnz,), dtype=torch.int32)
+    xval = torch.rand(nnz)
+    W = torch.randn(U, L) * 0.1
+    y = torch.randint(0, L, (B,), dtype=torch.int32)
+    y[::5] = -1
+    cost = torch.rand(L, L) * (1 - torch.eye(L))
+    dr = torch.zeros(U, L)
+    pr, lr_ = R.pa_multi(indptr, xval, pos, W, y, ops.PA_MODES[mode], 1, 0.5, cost, dr)
+    d = torch.zeros(U, L, device="cuda")
+    p, l = ops.pa_multi(indptr.cuda(), xval.cuda(), pos.cuda(), W.cuda(), y.cuda(), mode, "PA-I", 0.5, cost.cuda(),
+                        d, True)
+    assert torch.equal(p.cpu(), pr)
+    torch.testing.assert_close(d.cpu(), dr, rtol=1e-4, atol=1e-5)
+    assert abs(float(l) - lr_) / max(lr_, 1e-6) < 1e-3
+
+
+@pytest.mark.gpu
+def test_pa_fast_gpu_learns_and_sort_dedup():
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    F = 1 << 29  # above the dense-map limit: exercises the sort-based dedup
+    m = DistributedPA(PAConfig(feature_count=F, kind="binary"), Comm(device=torch.device("cuda")))
+    assert m.ps.dedup.sort_based
+    for s in range(40):
+        m.train_step(*synthetic_sparse_batch(4096, 32, F, seed=1, step=s, device="cuda", zipf=4.0))
+    ip, idx, val, lab = synthetic_sparse_batch(4096, 32, F, seed=7, step=0, device="cuda", zipf=4.0)
+    acc = float((m.predict(ip, idx, val).to(torch.int8) == lab).float().mean())
+    assert acc > 0.7, acc
