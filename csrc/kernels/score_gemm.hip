@@ -1,0 +1,100 @@
+// Inner-product scoring on MFMA for top-K retrieval (gfx950).  Kernel K8 (scoring part).
+//
+//   S[b, i] = <Q[b, :], X[i, :]>      Q [B, D] fp32, X [N, D] fp32, S [B, N] fp32
+//
+// The LEMP top-K worker scores each query user against a length-sorted bucket
+// of item vectors (M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:46-110);
+// on the GPU a bucket is a [B x bucket] GEMM.  fp32 in / fp32 accumulate with
+// v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, so scores match the CPU
+// reference bit-for-bit up to summation order).  Workgroup tile 64 x 64,
+// 4 waves in a 2 x 2 grid of 32 x 32 MFMA tiles; K staged through LDS in
+// 32-wide slabs with rows padded to an odd dword stride (conflict-free
+// row-strided operand reads); 16-B global loads; XCD-aware block remap so the
+// blocks sharing an item panel run on one XCD's L2.
+#include "common.h"
+
+using namespace fps;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int TB = 64;   // tile rows (queries) and cols (items)
+constexpr int KB = 32;   // k slab
+constexpr int LDK = KB + 1;
+
+__device__ __forceinline__ int acc_row(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__global__ void __launch_bounds__(256) score_gemm_kernel(const float* __restrict__ Q, const float* __restrict__ X,
+                                                         float* __restrict__ S, int B, int N, int D, int64_t ldS) {
+  __shared__ float Qs[TB * LDK];
+  __shared__ float Xs[TB * LDK];
+  const int nbx = (N + TB - 1) / TB, nby = (B + TB - 1) / TB;
+  const int nwg = nbx * nby;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  // query tiles fastest: the (few) blocks that read one item panel are
+  // consecutive logical ids, i.e. on one XCD, so X is fetched into one L2
+  const int by = wg % nby, bx = wg / nby;
+  const int i0 = bx * TB, q0 = by * TB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  floatx16 acc = {0};
+  for (int k0 = 0; k0 < D; k0 += KB) {
+    // stage 64 rows x 32 floats of Q and X: 256 threads x 4 floats x 2 passes each
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int e = (pass * 256 + tid);  // 0..511 -> (row, float4 column)
+      const int r = e >> 3, c4 = (e & 7) * 4;
+      const int kq = k0 + c4;
+      float qv[4] = {0.f, 0.f, 0.f, 0.f}, xv[4] = {0.f, 0.f, 0.f, 0.f};
+      const int qrow = q0 + r, xrow = i0 + r;
+      if (qrow < B) {
+        if (kq + 3 < D && ((((int64_t)qrow * D + kq) & 3) == 0)) {
+          const float4 f = *(const float4*)(Q + (int64_t)qrow * D + kq);
+          qv[0] = f.x; qv[1] = f.y; qv[2] = f.z; qv[3] = f.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qv[j] = kq + j < D ? Q[(int64_t)qrow * D + kq + j] : 0.f;
+        }
+      }
+      if (xrow < N) {
+        if (kq + 3 < D && ((((int64_t)xrow * D + kq) & 3) == 0)) {
+          const float4 f = *(const float4*)(X + (int64_t)xrow * D + kq);
+          xv[0] = f.x; xv[1] = f.y; xv[2] = f.z; xv[3] = f.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = kq + j < D ? X[(int64_t)xrow * D + kq + j] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Qs[r * LDK + c4 + j] = qv[j];
+        Xs[r * LDK + c4 + j] = xv[j];
+      }
+    }
+    __syncthreads();
+    const int ar = wr * 32 + (lane & 31), br = wc * 32 + (lane & 31), kh = lane >> 5;
+#pragma unroll
+    for (int kk = 0; kk < KB; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Qs[ar * LDK + kk + kh], Xs[br * LDK + kk + kh], acc, 0, 0, 0);
+    __syncthreads();
+  }
+  const int col = i0 + wc * 32 + (lane & 31);
+  if (col < N) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = q0 + wr * 32 + acc_row(lane, r);
+      if (row < B) S[(int64_t)row * ldS + col] = acc[r];
+    }
+  }
+}
+
+}  // namespace
+
+FPS_API int fps_score_gemm(const float* Q, const float* X, float* S, int B, int N, int D, int64_t ldS, void* stream) {
+  if (B <= 0 || N <= 0) return 0;
+  const int nwg = ((N + TB - 1) / TB) * ((B + TB - 1) / TB);
+  hipLaunchKernelGGL(score_gemm_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, Q, X, S, B, N, D, ldS);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}

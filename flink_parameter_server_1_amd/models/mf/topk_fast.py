@@ -1,0 +1,98 @@
+"""Top-K recommendation on the GPU: LEMP bucket scan with MFMA scoring (K8) + merge (K13).
+
+The reference's top-K worker (``M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:35-114``)
+scans length-sorted buckets of worker-resident item vectors per query user,
+stops when ``|bucket head| * |u| <= k-th best score`` and filters candidates
+with LEMP pruning (``M/matrix/factorization/pruning/LEMPPruningFunctions.scala``).
+On MI355X a whole query *batch* is scored against a bucket with one MFMA GEMM
+(``ops.score_gemm``), merged into the running top-K (``torch.topk`` on
+``[B, k + bucket]``), and the LEMP length bound is applied per query at bucket
+granularity: the scan stops once every query in the batch is settled.  The
+result is exact (equal to brute force), which is what the CPU pruning
+strategies also guarantee; they only change how much work is skipped.
+
+``DistributedTopK`` reproduces the scatter-gather of ``psTopKGenerator`` /
+``psOnlineLearnerAndGenerator``: item vectors are sharded over the ranks
+(worker-resident), every rank scores the same broadcast query batch against
+its shard, partial top-Ks are ``all_gather``-ed and merged with the users'
+seen items excluded (``CollectTopKFromEachWorker``, ``M/matrix/factorization/utils/CollectTopKFromEachWorker.scala:41-45``).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ... import ops
+
+
+class LempTopK:
+    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536):
+        vecs = item_vecs.float().contiguous()
+        lengths = torch.linalg.vector_norm(vecs, dim=1)
+        order = torch.argsort(lengths, descending=True)
+        self.vecs = vecs[order].contiguous()
+        self.ids = item_ids.to(vecs.device).long()[order]
+        self.lengths = lengths[order]
+        self.bucket = bucket_size
+        self.buckets_scanned = 0
+
+    def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None):
+        """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
+        use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering."""
+        Q = Q.float().contiguous()
+        B = Q.shape[0]
+        dev = Q.device
+        qlen = torch.linalg.vector_norm(Q, dim=1)
+        best_s = torch.full((B, k), float("-inf"), device=dev)
+        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+        N = self.vecs.shape[0]
+        S = None
+        for s in range(0, N, self.bucket):
+            e = min(N, s + self.bucket)
+            # LEMP bucket bound: no item of this or later buckets can beat the k-th best
+            if s > 0 and bool((qlen * self.lengths[s] <= best_s[:, -1]).all()):
+                break
+            n = e - s
+            if S is None or S.shape[1] < n:
+                S = torch.empty((B, self.bucket), device=dev)
+            ops.score_gemm(Q, self.vecs[s:e], S[:, :n])
+            cand_s = torch.cat([best_s, S[:, :n]], 1)
+            top_s, top_j = torch.topk(cand_s, min(k, cand_s.shape[1]), dim=1)
+            cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
+            best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
+            self.buckets_scanned += 1
+        return best_s, best_i
+
+
+def merge_top_k(scores: torch.Tensor, ids: torch.Tensor, k: int, exclude_ids: Optional[torch.Tensor] = None):
+    """Merge partial top-K lists ``[B, m]`` into the best ``k``; ``exclude_ids`` [B, E]
+    (padded with -1) are dropped first (K13)."""
+    s = scores.clone()
+    if exclude_ids is not None and exclude_ids.numel():
+        hit = (ids[:, :, None] == exclude_ids[:, None, :]).any(-1)
+        s[hit] = float("-inf")
+    s[ids < 0] = float("-inf")
+    top_s, j = torch.topk(s, min(k, s.shape[1]), dim=1)
+    return top_s, torch.gather(ids, 1, j)
+
+
+class DistributedTopK:
+    """Item shards per rank, broadcast queries, all-gather + merge."""
+
+    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, comm=None, bucket_size: int = 65536):
+        from ...parallel.comm import Comm
+
+        self.comm = comm or Comm()
+        self.local = LempTopK(item_ids, item_vecs, bucket_size)
+
+    def query(self, Q: torch.Tensor, K: int, worker_k: Optional[int] = None,
+              exclude_ids: Optional[torch.Tensor] = None):
+        wk = worker_k or K
+        s, i = self.local.query(Q, wk)
+        if self.comm.world > 1:
+            ss = torch.cat(self.comm.all_gather(s.contiguous()), 1)
+            ii = torch.cat(self.comm.all_gather(i.contiguous()), 1)
+        else:
+            ss, ii = s, i
+        return merge_top_k(ss, ii, K, exclude_ids)

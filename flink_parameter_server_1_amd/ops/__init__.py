@@ -288,6 +288,25 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
     return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out)])
 
 
+def score_gemm(Q: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """``out[b, i] = <Q[b], X[i]>`` on MFMA (fp32 in/accumulate, K8 scoring).  ``out`` may be
+    a column slice of a wider buffer (row stride taken from it)."""
+    B, D = Q.shape
+    N = X.shape[0]
+    if out is None:
+        out = torch.empty((B, N), dtype=torch.float32, device=Q.device)
+    if Q.is_cuda:
+        if out.stride(1) != 1:
+            raise ValueError("score_gemm output must have unit column stride")
+        lib = N_.require()
+        N_.check(lib.fps_score_gemm(_c(Q).data_ptr(), _c(X).data_ptr(), out.data_ptr(), B, N, D, out.stride(0),
+                                    N_.stream_ptr(Q.device)), "score_gemm")
+        return out
+    out.copy_(Q.float() @ X.float().T)
+    return out
+
+
+N_ = N
 PA_VARIANTS = {"PA": 0, "PA-I": 1, "PA-II": 2}
 PA_MODES = {"ova": 0, "pb": 1, "ml": 2}
 
