@@ -81,6 +81,8 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
         dst[j] = g;
       } else if (OP == 2) {
         atomic_add_noret(dst + j, -lr * g);
+      } else if (OP == 4) {
+        dst[j] += g;  // keys unique within the launch: plain read-modify-write
       } else {
         float* acc = state + row * D + j;
         float a = *acc + g * g;
@@ -272,6 +274,7 @@ static void launch_apply(float* table, float* state, const int32_t* idx, int64_t
       case 0: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 0>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 4: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 4>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       default: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
     }
   } else {
@@ -279,6 +282,7 @@ static void launch_apply(float* table, float* state, const int32_t* idx, int64_t
       case 0: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 0>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 4: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 4>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       default: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
     }
   }

@@ -12,7 +12,7 @@ import torch
 from . import _native as N
 from . import reference as R
 
-_OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3}
+_OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3, "add_unique": 4}
 
 
 def native_available() -> bool:

@@ -59,7 +59,7 @@ def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touch
     idx, delta = idx[keep], delta[keep].to(torch.float32)
     if touched is not None:
         touched[idx] = 1
-    if op == "add":
+    if op in ("add", "add_unique"):
         table.index_add_(0, idx, delta)
     elif op == "set":
         table[idx] = delta

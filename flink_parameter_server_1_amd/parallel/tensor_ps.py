@@ -93,7 +93,17 @@ class TensorPS:
         """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply."""
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
         recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
-        self.table.apply(plan.recv_keys, recv, lr=lr)
+        if self.table.optimizer == "add" and self.table.dim < 32 and len(plan.recv_splits) <= 16:
+            # narrow rows: one float atomic per lane hits a different row (the
+            # slow atomic shape).  Keys are unique within each source's segment,
+            # so apply segment by segment with plain read-modify-write.
+            off = 0
+            for n in plan.recv_splits:
+                if n:
+                    self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], op="add_unique")
+                off += n
+        else:
+            self.table.apply(plan.recv_keys, recv, lr=lr)
 
     def pull_values(self, keys: torch.Tensor) -> torch.Tensor:
         """Convenience: fp32 ``[B, D]`` values for every request (expanded)."""
