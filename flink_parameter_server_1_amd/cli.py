@@ -1,0 +1,323 @@
+"""Command line front-end: ``python -m flink_parameter_server_1_amd <command> ...``.
+
+The reference has no CLI (only two ``main()`` test drivers,
+``T/matrix/factorization/PSOnlineMatrixFactorizationImplicitTest.scala:31-97``);
+every knob is a method parameter.  Here the same knobs are dataclass
+configs (``MFConfig``, ``SGNSConfig``, ``PAConfig``) that can come from flags
+or a YAML file (``--config``, safe-loaded).
+
+Commands
+  mf-online   per-record online MF on a rating log (``ts user item [rating]``),
+              writes user / item factors as ``id;value`` files (the driver's output)
+  mf-offline  per-record multi-epoch MF, same IO
+  mf-gpu      MF on the tensor engine (GPU / CPU), synthetic or from a log; optional
+              checkpoints; one process per GPU under torch.distributed.run
+  topk        top-K recommendation from factor files + nDCG / hit-rate per period
+  pa-train    PA classifier on a libsvm-style file (``label idx:val ...``)
+  w2v         word2vec SGNS on a token file (whitespace separated ints) or synthetic
+  bench       the headline benchmark (bench.py)
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+import os
+import sys
+import time
+
+
+def _load_yaml(path):
+    import yaml
+
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def _apply_config(cfg_cls, args, extra=None):
+    vals = {}
+    if getattr(args, "config", None):
+        vals.update(_load_yaml(args.config))
+    for f in dataclasses.fields(cfg_cls):
+        v = getattr(args, f.name, None)
+        if v is not None:
+            vals[f.name] = v
+    if extra:
+        vals.update(extra)
+    return cfg_cls(**{k: v for k, v in vals.items() if k in {f.name for f in dataclasses.fields(cfg_cls)}})
+
+
+def _ratings_from_log(path):
+    from .models.mf.core import Rating
+    from .utils.io import read_ratings
+
+    ts, u, i, r = read_ratings(path)
+    return [Rating(int(a), int(b), float(c), int(t)) for t, a, b, c in zip(ts, u, i, r)]
+
+
+def _write_factors(stream, users_out, items_out):
+    import numpy as np
+
+    from .utils.io import fold_model, write_factors_text
+
+    for side, path in (("left", users_out), ("right", items_out)):
+        if path:
+            m = fold_model(stream, side)
+            ids = np.array(sorted(m), dtype=np.int64)
+            vals = np.stack([np.asarray(m[i], dtype=np.float32) for i in ids]) if len(ids) else np.zeros((0, 1))
+            write_factors_text(path, ids, vals)
+
+
+def cmd_mf(args, offline: bool):
+    from .models.mf import apps
+
+    ratings = _ratings_from_log(args.input)
+    kw = dict(num_factors=args.num_factors, range_min=args.range_min, range_max=args.range_max,
+              learning_rate=args.learning_rate, negative_sample_rate=args.negative_sample_rate,
+              user_memory=args.user_memory, pull_limit=args.pull_limit, worker_parallelism=args.workers,
+              ps_parallelism=args.ps, seed=args.seed)
+    t0 = time.time()
+    out = apps.ps_offline_mf(ratings, iterations=args.iterations, **kw) if offline else apps.ps_online_mf(ratings, **kw)
+    _write_factors(out, args.users_out, args.items_out)
+    print(json.dumps({"ratings": len(ratings), "seconds": time.time() - t0, "outputs": len(out)}))
+
+
+def cmd_mf_gpu(args):
+    import torch
+
+    from .models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from .parallel.comm import Comm
+    from .utils.io import Checkpointer, read_ratings
+
+    comm = Comm.init_from_env()
+    cfg = _apply_config(MFConfig, args)
+    m = DistributedMF(cfg, comm)
+    if args.input:
+        ts, u, i, r = read_ratings(args.input)
+        mine = (u % comm.world) == comm.rank
+        dev = comm.device
+        uid = torch.from_numpy(u[mine] // comm.world).to(dev)
+        iid = torch.from_numpy(i[mine]).to(dev)
+        rat = torch.from_numpy(r[mine]).to(dev)
+        n = uid.numel()
+
+        def batch(s):
+            a = (s * args.batch) % max(n, 1)
+            return uid[a:a + args.batch], iid[a:a + args.batch], rat[a:a + args.batch]
+    else:
+        data = SyntheticRatings(cfg.num_users, cfg.num_items, args.batch * 4, comm.rank, comm.world,
+                                device=comm.device, truth_dim=args.truth_dim)
+        batch = lambda s: data.batch(s, args.batch)  # noqa: E731
+    ck = Checkpointer(args.checkpoint_dir, {"users": m.users, "items": m.items}, comm,
+                      every_steps=args.checkpoint_every) if args.checkpoint_dir else None
+    start = 0
+    if ck and args.resume:
+        man = ck.restore_latest()
+        start = man["step"] if man else 0
+    t0 = time.time()
+    for s in range(start, start + args.steps):
+        m.step(*batch(s))
+        if ck:
+            m.flush()
+            ck.maybe_save(s + 1)
+    m.flush()
+    rmse = m.rmse(*batch(0))
+    if comm.rank == 0:
+        print(json.dumps({"steps": args.steps, "seconds": time.time() - t0, "updates": m.updates * comm.world,
+                          "rmse_first_batch": rmse}))
+    if args.items_out:
+        from .utils.io import write_factors_text
+
+        ids, vals = m.item_vectors()
+        write_factors_text(f"{args.items_out}.{comm.rank}", ids.cpu().numpy(), vals.cpu().numpy())
+
+
+def cmd_topk(args):
+    import numpy as np
+    import torch
+
+    from .models.mf.topk_fast import LempTopK
+    from .utils.io import read_factors_text, read_ratings
+    from .utils.metrics import NDCGAggregator
+
+    users = read_factors_text(args.users)
+    items = read_factors_text(args.items)
+    iid = torch.tensor(sorted(items))
+    X = torch.tensor(np.stack([items[int(i)] for i in iid]), dtype=torch.float32)
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    lemp = LempTopK(iid.to(dev), X.to(dev))
+    ts, u, i, r = read_ratings(args.test)
+    agg = NDCGAggregator(args.period)
+    known = [k for k in range(len(u)) if int(u[k]) in users]
+    for a in range(0, len(known), 4096):
+        idx = known[a:a + 4096]
+        Q = torch.tensor(np.stack([users[int(u[k])] for k in idx]), dtype=torch.float32, device=dev)
+        _, top = lemp.query(Q, args.k)
+        for row, k in zip(top.cpu().tolist(), idx):
+            agg.add(int(ts[k]), row, int(i[k]))
+    if args.csv:
+        agg.to_csv(args.csv)
+    print(json.dumps({"periods": agg.periods()[:10], "n": len(known)}))
+
+
+def _read_libsvm(path):
+    labels, rows = [], []
+    for ln in open(path):
+        p = ln.split()
+        if not p:
+            continue
+        labels.append(float(p[0]))
+        rows.append([(int(t.split(":")[0]), float(t.split(":")[1])) for t in p[1:]])
+    return labels, rows
+
+
+def cmd_pa(args):
+    import torch
+
+    from .models.pa.fast import DistributedPA, PAConfig
+    from .parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    cfg = _apply_config(PAConfig, args)
+    m = DistributedPA(cfg, comm)
+    labels, rows = _read_libsvm(args.input)
+    dev = comm.device
+    correct = total = 0
+    for e in range(args.epochs):
+        for a in range(comm.rank * args.batch, len(rows), args.batch * comm.world):
+            chunk = rows[a:a + args.batch]
+            lab = labels[a:a + args.batch]
+            indptr = torch.tensor([0] + [len(r) for r in chunk]).cumsum(0).to(dev)
+            idx = torch.tensor([k for r in chunk for k, _ in r], dtype=torch.int32, device=dev)
+            val = torch.tensor([v for r in chunk for _, v in r], dtype=torch.float32, device=dev)
+            if cfg.kind == "binary":
+                y = torch.tensor([1 if x > 0 else -1 for x in lab], dtype=torch.int8, device=dev)
+            else:
+                y = torch.tensor([int(x) for x in lab], dtype=torch.int32, device=dev)
+            pred, _ = m.train_step(indptr, idx, val, y)
+            if e == args.epochs - 1:
+                correct += int((pred.to(y.dtype) == y).sum())
+                total += len(chunk)
+    print(json.dumps({"examples": total, "online_accuracy_last_epoch": correct / max(total, 1)}))
+
+
+def cmd_w2v(args):
+    import torch
+
+    from .models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, synthetic_corpus
+    from .parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    cfg = _apply_config(SGNSConfig, args)
+    m = DistributedSGNS(cfg, comm=comm)
+    if args.input:
+        toks = torch.tensor([int(t) for t in open(args.input).read().split()], dtype=torch.int32)
+    else:
+        toks = synthetic_corpus(args.tokens, cfg.vocab_size, seed=comm.rank)
+    toks = toks.to(comm.device)
+    c, o = skipgram_pairs(toks, cfg.window)
+    losses = []
+    for a in range(0, c.numel(), args.batch):
+        loss = m.step(c[a:a + args.batch], o[a:a + args.batch], with_loss=(a // args.batch) % 50 == 0)
+        if loss is not None:
+            losses.append(loss)
+    print(json.dumps({"pairs": int(c.numel()), "loss_trace": losses[:20]}))
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(prog="flink_parameter_server_1_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def mf_common(p):
+        p.add_argument("--input", required=True)
+        p.add_argument("--users-out")
+        p.add_argument("--items-out")
+        p.add_argument("--num-factors", type=int, default=10)
+        p.add_argument("--range-min", type=float, default=-0.01)
+        p.add_argument("--range-max", type=float, default=0.01)
+        p.add_argument("--learning-rate", type=float, default=0.01)
+        p.add_argument("--negative-sample-rate", type=int, default=0)
+        p.add_argument("--user-memory", type=int, default=128)
+        p.add_argument("--pull-limit", type=int, default=1600)
+        p.add_argument("--workers", type=int, default=4)
+        p.add_argument("--ps", type=int, default=4)
+        p.add_argument("--seed", type=int, default=None)
+
+    p = sub.add_parser("mf-online")
+    mf_common(p)
+    p = sub.add_parser("mf-offline")
+    mf_common(p)
+    p.add_argument("--iterations", type=int, default=10)
+
+    p = sub.add_parser("mf-gpu")
+    p.add_argument("--config")
+    p.add_argument("--input")
+    p.add_argument("--num-users", type=int)
+    p.add_argument("--num-items", type=int)
+    p.add_argument("--dim", type=int)
+    p.add_argument("--learning-rate", type=float)
+    p.add_argument("--wire-dtype")
+    p.add_argument("--batch", type=int, default=1 << 20)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--truth-dim", type=int, default=8)
+    p.add_argument("--checkpoint-dir")
+    p.add_argument("--checkpoint-every", type=int, default=0)
+    p.add_argument("--resume", action="store_true")
+    p.add_argument("--items-out")
+
+    p = sub.add_parser("topk")
+    p.add_argument("--users", required=True)
+    p.add_argument("--items", required=True)
+    p.add_argument("--test", required=True)
+    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--period", type=int, default=86400)
+    p.add_argument("--csv")
+
+    p = sub.add_parser("pa-train")
+    p.add_argument("--config")
+    p.add_argument("--input", required=True)
+    p.add_argument("--feature-count", type=int, required=False)
+    p.add_argument("--kind")
+    p.add_argument("--label-count", type=int)
+    p.add_argument("--variant")
+    p.add_argument("--aggressiveness", type=float)
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--epochs", type=int, default=1)
+
+    p = sub.add_parser("w2v")
+    p.add_argument("--config")
+    p.add_argument("--input")
+    p.add_argument("--vocab-size", type=int)
+    p.add_argument("--dim", type=int)
+    p.add_argument("--window", type=int)
+    p.add_argument("--learning-rate", type=float)
+    p.add_argument("--tokens", type=int, default=1 << 20)
+    p.add_argument("--batch", type=int, default=1 << 16)
+
+    p = sub.add_parser("bench")
+    p.add_argument("rest", nargs=argparse.REMAINDER)
+    return ap
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    if args.cmd in ("mf-online", "mf-offline"):
+        return cmd_mf(args, offline=args.cmd == "mf-offline")
+    if args.cmd == "mf-gpu":
+        return cmd_mf_gpu(args)
+    if args.cmd == "topk":
+        return cmd_topk(args)
+    if args.cmd == "pa-train":
+        return cmd_pa(args)
+    if args.cmd == "w2v":
+        return cmd_w2v(args)
+    if args.cmd == "bench":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+
+        return bench.main(args.rest)
+    return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

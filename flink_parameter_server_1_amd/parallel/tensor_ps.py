@@ -31,6 +31,7 @@ from typing import List
 import torch
 
 from .. import ops
+from ..utils.tracing import trace_range
 from .comm import Comm
 from .table import ShardedTable
 
@@ -57,7 +58,8 @@ class TensorPS:
         request->row map out of the reusable dedup workspace, so the plan
         survives the next ``plan`` call (pipelined steps)."""
         keys = keys.to(torch.int32).contiguous()
-        counts, prefix, uniq, pos = self.dedup.run(keys)
+        with trace_range("ps.dedup"):
+            counts, prefix, uniq, pos = self.dedup.run(keys)
         recv_counts = self.comm.exchange_counts(counts)
         both = torch.cat([counts, recv_counts]).cpu().tolist()  # host sync (split sizes)
         W = self.comm.world
@@ -76,8 +78,10 @@ class TensorPS:
     def pull(self, keys: torch.Tensor):
         """Returns ``(rows[U, D] in wire dtype, plan)``; request b's row is ``rows[plan.pos[b]]``."""
         plan = self.plan(keys)
-        served = self.table.serve(plan.recv_keys, self.wire_dtype)
-        rows = self.comm.all_to_all(served, plan.recv_splits, plan.send_splits)
+        with trace_range("ps.serve"):
+            served = self.table.serve(plan.recv_keys, self.wire_dtype)
+        with trace_range("ps.answer-a2a"):
+            rows = self.comm.all_to_all(served, plan.recv_splits, plan.send_splits)
         return rows, plan
 
     def pull_async(self, keys: torch.Tensor):
@@ -92,7 +96,8 @@ class TensorPS:
     def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0):
         """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply."""
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
-        recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
+        with trace_range("ps.push-a2a"):
+            recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
         if self.table.optimizer == "add" and self.table.dim < 32 and len(plan.recv_splits) <= 16:
             # narrow rows: one float atomic per lane hits a different row (the
             # slow atomic shape).  Keys are unique within each source's segment,

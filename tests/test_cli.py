@@ -1,0 +1,60 @@
+"""CLI end-to-end on small files (CPU)."""
+import json
+import subprocess
+import sys
+
+import numpy as np
+
+
+def _run(args, tmp_path):
+    r = subprocess.run([sys.executable, "-m", "flink_parameter_server_1_amd"] + args, capture_output=True, text=True,
+                       cwd=str(tmp_path.parent.parent) if False else None, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+def _log(tmp_path, n=400):
+    rng = np.random.default_rng(0)
+    p = tmp_path / "ratings.txt"
+    with open(p, "w") as f:
+        for t in range(n):
+            f.write(f"{t} {rng.integers(20)} {rng.integers(15)} {rng.random():.3f}\n")
+    return str(p)
+
+
+def test_cli_mf_offline_writes_factor_files(tmp_path):
+    log = _log(tmp_path)
+    out = _run(["mf-offline", "--input", log, "--users-out", str(tmp_path / "U.map"), "--items-out",
+                str(tmp_path / "I.map"), "--iterations", "2", "--workers", "2", "--ps", "2", "--num-factors", "4"],
+               tmp_path)
+    assert json.loads(out.strip().splitlines()[-1])["ratings"] == 400
+    lines = open(tmp_path / "I.map").read().splitlines()
+    assert len(lines) % 4 == 0 and ";" in lines[0]
+
+
+def test_cli_mf_gpu_path_with_checkpoint(tmp_path):
+    out = _run(["mf-gpu", "--num-users", "300", "--num-items", "100", "--dim", "8", "--batch", "500", "--steps", "6",
+                "--checkpoint-dir", str(tmp_path / "ck"), "--checkpoint-every", "3"], tmp_path)
+    assert json.loads(out.strip().splitlines()[-1])["updates"] == 3000
+    out = _run(["mf-gpu", "--num-users", "300", "--num-items", "100", "--dim", "8", "--batch", "500", "--steps", "2",
+                "--checkpoint-dir", str(tmp_path / "ck"), "--resume"], tmp_path)
+    assert (tmp_path / "ck").exists()
+
+
+def test_cli_topk_and_pa(tmp_path):
+    log = _log(tmp_path)
+    _run(["mf-online", "--input", log, "--users-out", str(tmp_path / "U.map"), "--items-out", str(tmp_path / "I.map"),
+          "--workers", "2", "--ps", "2", "--num-factors", "4"], tmp_path)
+    out = _run(["topk", "--users", str(tmp_path / "U.map"), "--items", str(tmp_path / "I.map"), "--test", log,
+                "--k", "5", "--period", "100", "--csv", str(tmp_path / "ndcg.csv")], tmp_path)
+    assert json.loads(out.strip().splitlines()[-1])["n"] > 0
+    assert open(tmp_path / "ndcg.csv").readline().startswith("period")
+    svm = tmp_path / "d.svm"
+    rng = np.random.default_rng(1)
+    with open(svm, "w") as f:
+        for _ in range(300):
+            idx = sorted(rng.choice(50, 5, replace=False))
+            lab = 1 if sum(idx) > 120 else -1
+            f.write(f"{lab} " + " ".join(f"{i}:1.0" for i in idx) + "\n")
+    out = _run(["pa-train", "--input", str(svm), "--feature-count", "50", "--epochs", "3", "--batch", "16"], tmp_path)
+    assert json.loads(out.strip().splitlines()[-1])["examples"] == 300
