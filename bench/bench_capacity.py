@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""BASELINE config #5: 100B-parameter embedding table sharded over 8 x 288 GB HBM
+(PS capacity / bounded-staleness stress).
+
+    python bench/bench_capacity.py [--params-per-gpu 12.5e9] [--dim 64] [--batch 1048576]
+                                   [--staleness 2] [--optimizer add|adagrad] [--steps K]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bench_capacity.py --gpus 8
+
+Weak scaling of the table: every GPU holds ``--params-per-gpu`` fp32 parameters
+(default 12.5e9 = 50 GB; at 8 GPUs the table is 100e9 parameters = 1.5625e9
+rows of dim 64, range-partitioned).  Each step every rank trains on ``--batch``
+(a, b, label) id pairs with power-law id popularity: dedup (hashed claim map) ->
+key/row all-to-all -> fused ``pair_sgd_pulled`` -> delta all-to-all -> PS apply,
+with up to ``--staleness`` later pulls in flight before a push lands.
+
+Reports the whole-job rate of applied parameter updates (unique rows pushed x
+dim per second) plus pairs/s; random-init weights, synthetic pairs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--params-per-gpu", type=float, default=12.5e9)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="pairs per GPU per step")
+    ap.add_argument("--staleness", type=int, default=2)
+    ap.add_argument("--optimizer", default="add", choices=["add", "adagrad"])
+    ap.add_argument("--zipf", type=float, default=3.0)
+    ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"])
+    ap.add_argument("--pool", type=int, default=4, help="pre-generated batches cycled through")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from flink_parameter_server_1_amd.models.emb import DistributedPairEmbedding, PairEmbeddingConfig, synthetic_pairs
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm.init_from_env()
+    dev = comm.device
+    num_ids = int(a.params_per_gpu * comm.world) // a.dim
+    wire = a.wire if a.wire != "auto" else ("bf16" if comm.world > 1 else "fp32")
+    cfg = PairEmbeddingConfig(num_ids=num_ids, dim=a.dim, staleness=a.staleness, optimizer=a.optimizer,
+                              wire_dtype=wire)
+    t_init = time.perf_counter()
+    m = DistributedPairEmbedding(cfg, comm)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_init = time.perf_counter() - t_init
+    pool = [synthetic_pairs(num_ids, a.batch, seed=comm.rank + 1, step=s, device=dev, zipf=a.zipf)
+            for s in range(a.pool)]
+    eval_batch = synthetic_pairs(num_ids, 1 << 16, seed=12345, step=0, device=dev, zipf=a.zipf)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    loss0 = m.mean_loss(*eval_batch)
+    for s in range(a.warmup):
+        m.step(*pool[s % a.pool])
+    m.flush()
+    comm.barrier()
+    sync()
+    rows0, t0 = m.rows_pushed, time.perf_counter()
+    for s in range(a.steps):
+        m.step(*pool[s % a.pool])
+    m.flush()  # the timed region includes every push of the timed batches
+    sync()
+    comm.barrier()
+    dt = comm.max_over_ranks(time.perf_counter() - t0)
+    rows = comm.sum_over_ranks(float(m.rows_pushed - rows0))
+    loss1 = m.mean_loss(*eval_batch)
+    mem = torch.cuda.max_memory_allocated(dev) / 2**30 if dev.type == "cuda" else 0.0
+    if comm.rank == 0:
+        pairs = a.batch * a.steps * comm.world
+        print(json.dumps({
+            "metric": "param updates/sec (whole node), 100B-param sharded embedding table",
+            "value": rows * a.dim / dt, "unit": "param updates/s",
+            "pairs_per_s": pairs / dt, "unique_rows_per_step_per_gpu": rows / a.steps / comm.world,
+            "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic power-law id pairs (cluster labels), random-init table",
+            "table_params": cfg.num_params, "table_gb_per_gpu": m.table.nbytes() / 2**30,
+            "peak_hbm_gib_rank0": mem, "init_s": t_init, "eval_loss_before": loss0, "eval_loss_after": loss1,
+            "config": {"model": f"pair-embedding ids={num_ids} dim={a.dim}", "global_batch": a.batch * comm.world,
+                       "seq_len": None, "parallelism": f"ps{comm.world}", "staleness": a.staleness,
+                       "optimizer": a.optimizer, "wire_dtype": wire, "partition": "range", "zipf": a.zipf},
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -97,12 +97,51 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
 // ---- de-duplication of request keys (one step, epoch-tagged map, no spins)
 // map[key] = epoch << 32 | (0xffffffff - owner_request_index); atomicMax makes
 // the newest epoch win and, inside it, the smallest request index.
-__global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, int64_t n, unsigned long long* __restrict__ map,
-                                   uint32_t epoch) {
+//
+// Two addressings of the claim map:
+//  * dense  (HASHED = false): map has one entry per id of the table (MF items:
+//    1M ids -> 8 MB), map index = key;
+//  * hashed (HASHED = true): for id spaces of 1e9+ (PA 1B features, the
+//    100B-parameter table) a per-batch open-addressing hash table
+//    (dedup_hash_insert_kernel) first gives every request the slot of its key,
+//    and the claim map is indexed by that slot (capacity ~2x the batch).
+template <bool HASHED>
+__device__ __forceinline__ int64_t map_index(const int32_t* __restrict__ keys, const int32_t* __restrict__ hslot,
+                                             int64_t b) {
+  return HASHED ? (int64_t)hslot[b] : (int64_t)keys[b];
+}
+
+// Epoch-tagged linear-probing insert: tab[h] = epoch << 32 | key.  Entries of
+// older epochs count as empty, so nothing is cleared between steps.  The
+// capacity (power of two, >= 2n) bounds every probe sequence.
+__global__ void dedup_hash_insert_kernel(const int32_t* __restrict__ keys, int64_t n,
+                                         unsigned long long* __restrict__ tab, uint32_t mask, uint32_t epoch,
+                                         int32_t* __restrict__ hslot) {
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = keys[b];
+    const uint32_t k = (uint32_t)keys[b];
+    const unsigned long long mine = ((unsigned long long)epoch << 32) | k;
+    uint32_t h = fmix32(k ^ 0x5bd1e995u) & mask;
+    for (;;) {
+      unsigned long long cur = tab[h];
+      if ((uint32_t)(cur >> 32) != epoch) {
+        const unsigned long long old = atomicCAS(tab + h, cur, mine);
+        if (old == cur) break;   // claimed the empty slot
+        cur = old;               // somebody else wrote it first: re-examine
+        if ((uint32_t)(cur >> 32) != epoch) continue;
+      }
+      if (cur == mine) break;    // our key already lives here
+      h = (h + 1) & mask;
+    }
+    hslot[b] = (int32_t)h;
+  }
+}
+
+template <bool HASHED>
+__global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, const int32_t* __restrict__ hslot, int64_t n,
+                                   unsigned long long* __restrict__ map, uint32_t epoch) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long v = ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (uint32_t)b);
-    atomicMax(map + k, v);
+    atomicMax(map + map_index<HASHED>(keys, hslot, b), v);
   }
 }
 
@@ -141,7 +180,9 @@ __device__ __forceinline__ int32_t wave_alloc(bool want, int d, int32_t* __restr
 constexpr int DEDUP_ITEMS = 16;
 constexpr int DEDUP_MAX_W = 64;
 
-__global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __restrict__ keys, int64_t n,
+template <bool HASHED>
+__global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __restrict__ keys,
+                                                           const int32_t* __restrict__ hslot, int64_t n,
                                                            const unsigned long long* __restrict__ map, int W,
                                                            int part_kind, int64_t block, int32_t* __restrict__ counts,
                                                            int32_t* __restrict__ owner_slot) {
@@ -159,7 +200,7 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
     int d = 0;
     if (b < n) {
       const int32_t k = keys[b];
-      const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+      const uint32_t owner = 0xffffffffu - (uint32_t)(map[map_index<HASHED>(keys, hslot, b)] & 0xffffffffull);
       int32_t local;
       key_dest(k, W, part_kind, block, d, local);
       own = owner == (uint32_t)b;
@@ -188,13 +229,15 @@ __global__ void dedup_scan_kernel(const int32_t* __restrict__ counts, int W, int
 
 // compact position of every request; owners also write their unique local
 // key, so uniq[0:total] is grouped by destination shard in ascending order
-__global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, int64_t n, const unsigned long long* __restrict__ map,
+template <bool HASHED>
+__global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, const int32_t* __restrict__ hslot, int64_t n,
+                                     const unsigned long long* __restrict__ map,
                                      int W, int part_kind, int64_t block, const int32_t* __restrict__ prefix,
                                      const int32_t* __restrict__ owner_slot, int32_t* __restrict__ uniq,
                                      int32_t* __restrict__ pos) {
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
     const int32_t k = keys[b];
-    const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+    const uint32_t owner = 0xffffffffu - (uint32_t)(map[map_index<HASHED>(keys, hslot, b)] & 0xffffffffull);
     int d; int32_t local;
     key_dest(k, W, part_kind, block, d, local);
     const int32_t p = prefix[d] + owner_slot[owner];
@@ -297,26 +340,51 @@ FPS_API int fps_apply_rows(float* table, float* state, const int32_t* idx, int64
   return 0;
 }
 
+template <bool HASHED>
+static int launch_dedup(const int32_t* keys, const int32_t* hslot, int64_t n, unsigned long long* map,
+                        uint32_t epoch, int W, int part_kind, int64_t block, int32_t* counts, int32_t* prefix,
+                        int32_t* owner_slot, int32_t* uniq, int32_t* pos, hipStream_t s) {
+  if (W > DEDUP_MAX_W) return (int)hipErrorInvalidValue;
+  const int g = grid_for(n > 0 ? n : 1, 256, 256 * 16);
+  if (n > 0) {
+    hipLaunchKernelGGL(dedup_claim_kernel<HASHED>, dim3(g), dim3(256), 0, s, keys, hslot, n, map, epoch);
+    const int64_t ga = (n + 256 * DEDUP_ITEMS - 1) / (256 * DEDUP_ITEMS);
+    hipLaunchKernelGGL(dedup_assign_kernel<HASHED>, dim3((unsigned)ga), dim3(256), 0, s, keys, hslot, n,
+                       (const unsigned long long*)map, W, part_kind, block, counts, owner_slot);
+  }
+  hipLaunchKernelGGL(dedup_scan_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)counts, W, prefix);
+  if (n > 0)
+    hipLaunchKernelGGL(dedup_resolve_kernel<HASHED>, dim3(g), dim3(256), 0, s, keys, hslot, n,
+                       (const unsigned long long*)map, W, part_kind, block, (const int32_t*)prefix,
+                       (const int32_t*)owner_slot, uniq, pos);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 // counts[W] must be zeroed by the caller; prefix has W+1 entries
 // (prefix[W] = number of unique keys); uniq/pos/owner_slot have n entries.
 FPS_API int fps_dedup(const int32_t* keys, int64_t n, unsigned long long* map, uint32_t epoch, int W, int part_kind,
                       int64_t block, int32_t* counts, int32_t* prefix, int32_t* owner_slot, int32_t* uniq,
                       int32_t* pos, void* stream) {
+  return launch_dedup<false>(keys, nullptr, n, map, epoch, W, part_kind, block, counts, prefix, owner_slot, uniq,
+                             pos, (hipStream_t)stream);
+}
+
+// Hashed variant for huge id spaces: tab and map both hold cap (power of two,
+// >= 2n) uint64 entries; hslot has n entries.  Keys must be >= 0.
+FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long* tab, unsigned long long* map,
+                             int64_t cap, uint32_t epoch, int W, int part_kind, int64_t block, int32_t* counts,
+                             int32_t* prefix, int32_t* hslot, int32_t* owner_slot, int32_t* uniq, int32_t* pos,
+                             void* stream) {
+  if (cap < 2 * n || (cap & (cap - 1)) != 0 || cap > (1ll << 31)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int g = grid_for(n > 0 ? n : 1, 256, 256 * 16);
   if (n > 0) {
-    hipLaunchKernelGGL(dedup_claim_kernel, dim3(g), dim3(256), 0, s, keys, n, map, epoch);
-    if (W > DEDUP_MAX_W) return (int)hipErrorInvalidValue;
-    const int64_t ga = (n + 256 * DEDUP_ITEMS - 1) / (256 * DEDUP_ITEMS);
-    hipLaunchKernelGGL(dedup_assign_kernel, dim3((unsigned)ga), dim3(256), 0, s, keys, n,
-                       (const unsigned long long*)map, W, part_kind, block, counts, owner_slot);
+    const int g = grid_for(n, 256, 256 * 16);
+    hipLaunchKernelGGL(dedup_hash_insert_kernel, dim3(g), dim3(256), 0, s, keys, n, tab, (uint32_t)(cap - 1), epoch,
+                       hslot);
   }
-  hipLaunchKernelGGL(dedup_scan_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)counts, W, prefix);
-  if (n > 0)
-    hipLaunchKernelGGL(dedup_resolve_kernel, dim3(g), dim3(256), 0, s, keys, n, (const unsigned long long*)map, W,
-                       part_kind, block, (const int32_t*)prefix, (const int32_t*)owner_slot, uniq, pos);
-  FPS_CHECK_LAUNCH();
-  return 0;
+  return launch_dedup<true>(keys, hslot, n, map, epoch, W, part_kind, block, counts, prefix, owner_slot, uniq, pos,
+                            s);
 }
 
 FPS_API int fps_bucketize(const int32_t* keys, int64_t n, int W, int part_kind, int64_t block, int32_t* shard,

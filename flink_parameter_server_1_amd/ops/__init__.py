@@ -7,6 +7,8 @@ fallback on a GPU box).
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from . import _native as N
@@ -85,18 +87,22 @@ class DedupWorkspace:
     send buffer with splits ``counts``) and each request's row in it.
     """
 
-    #: id spaces above this use a sort-based dedup instead of a dense claim map
+    #: id spaces above this use the hashed claim map (per-batch open-addressing
+    #: table, ~32 B per request) instead of a dense ``uint64[num_ids]`` map
     #: (1B-feature PA tables would otherwise need an 8 GB map per worker)
     DENSE_MAP_MAX_IDS = 1 << 28
 
-    def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu"):
+    def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu",
+                 hashed: Optional[bool] = None):
         self.num_ids, self.W, self.part_kind, self.block = num_ids, W, part_kind, block
         self.device = torch.device(device)
         self.epoch = 0
         self.cap = 0
-        self.sort_based = num_ids > self.DENSE_MAP_MAX_IDS
-        if self.device.type == "cuda" and not self.sort_based:
-            self.map = torch.zeros(num_ids, dtype=torch.int64, device=device)
+        self.hash_cap = 0
+        self.hashed = num_ids > self.DENSE_MAP_MAX_IDS if hashed is None else bool(hashed)
+        if self.device.type == "cuda":
+            if not self.hashed:
+                self.map = torch.zeros(num_ids, dtype=torch.int64, device=device)
             self.counts = torch.zeros(W, dtype=torch.int32, device=device)
             self.prefix = torch.zeros(W + 1, dtype=torch.int32, device=device)
 
@@ -106,37 +112,39 @@ class DedupWorkspace:
             self.owner_slot = torch.empty(self.cap, dtype=torch.int32, device=self.device)
             self.uniq = torch.empty(self.cap, dtype=torch.int32, device=self.device)
             self.pos = torch.empty(self.cap, dtype=torch.int32, device=self.device)
-
-    def _run_sorted(self, keys: torch.Tensor):
-        """Radix-sort dedup (torch.unique on device) for huge id spaces."""
-        uniq_g, inv = torch.unique(keys.long(), sorted=True, return_inverse=True)
-        d, local = R.shard_of(uniq_g, self.W, self.part_kind, self.block)
-        if self.part_kind == 0 and self.W > 1:
-            order = torch.argsort(d, stable=True)
-            slot_of = torch.empty_like(order)
-            slot_of[order] = torch.arange(order.numel(), device=order.device)
-            uniq, pos = local[order], slot_of[inv]
-        else:  # range partitioning: sorted keys are already grouped by shard
-            uniq, pos = local, inv
-        counts = torch.bincount(d, minlength=self.W).to(torch.int32)
-        prefix = torch.zeros(self.W + 1, dtype=torch.int32, device=keys.device)
-        prefix[1:] = torch.cumsum(counts, 0)
-        return counts, prefix, uniq.to(torch.int32), pos.to(torch.int32)
+            if self.hashed:
+                self.hslot = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+        if self.hashed and 2 * n > self.hash_cap:
+            self.hash_cap = 1 << max(10, (2 * n - 1).bit_length())
+            # fresh zeroed tables: epoch 0 entries count as empty, epochs restart at 1
+            self.tab = torch.zeros(self.hash_cap, dtype=torch.int64, device=self.device)
+            self.map = torch.zeros(self.hash_cap, dtype=torch.int64, device=self.device)
+            self.epoch = 0
 
     def run(self, keys: torch.Tensor):
         if self.device.type != "cuda":
             return R.dedup(keys, self.W, self.part_kind, self.block)
-        if self.sort_based:
-            return self._run_sorted(keys)
         n = keys.numel()
         self._grow(max(n, 1))
         self.epoch += 1
+        if self.epoch >= 0xFFFFFFFF:  # wrap: clear the tags once every 4e9 steps
+            self.epoch = 1
+            self.map.zero_()
+            if self.hashed:
+                self.tab.zero_()
         self.counts.zero_()
         lib = N.require()
-        N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch & 0xFFFFFFFF, self.W,
-                              self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
-                              self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(),
-                              N.stream_ptr(self.device)), "dedup")
+        s = N.stream_ptr(self.device)
+        if self.hashed:
+            N.check(lib.fps_dedup_hashed(_c(keys).data_ptr(), n, self.tab.data_ptr(), self.map.data_ptr(),
+                                         self.hash_cap, self.epoch, self.W, self.part_kind, self.block,
+                                         self.counts.data_ptr(), self.prefix.data_ptr(), self.hslot.data_ptr(),
+                                         self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s),
+                    "dedup_hashed")
+        else:
+            N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch, self.W,
+                                  self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
+                                  self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup")
         return self.counts, self.prefix, self.uniq, self.pos[:n]
 
 
@@ -173,6 +181,26 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr: float, lam: float = 0.0, user
                 "mf_sgd_pulled")
         return
     R.mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam, user_atomic)
+
+
+PAIR_LOSSES = {"logistic": 0, "squared": 1}
+
+
+def pair_sgd_pulled(rows, pa, pb, label, delta, lr: float, loss: str = "logistic", with_loss: bool = False):
+    """Pairwise embedding SGD on pulled rows (both sides from one PS table):
+    ``delta[pa] += lr*g*rows[pb]``, ``delta[pb] += lr*g*rows[pa]`` (config #5 compute).
+    Returns the loss sum as a device/host scalar tensor when ``with_loss``."""
+    kind = PAIR_LOSSES[loss]
+    if _on_gpu(delta):
+        out = torch.zeros(1, dtype=torch.float64, device=delta.device) if with_loss else None
+        lib = N.require()
+        N.check(lib.fps_pair_sgd_pulled(_c(rows).data_ptr(), int(rows.dtype == torch.bfloat16), _c(pa).data_ptr(),
+                                        _c(pb).data_ptr(), _c(label).data_ptr(), _c(delta).data_ptr(), pa.numel(),
+                                        delta.shape[1], lr, kind, out.data_ptr() if out is not None else None,
+                                        N.stream_ptr(delta.device)), "pair_sgd_pulled")
+        return out
+    loss_v = R.pair_sgd_pulled(rows, pa, pb, label, delta, lr, kind)
+    return torch.tensor([loss_v], dtype=torch.float64) if with_loss else None
 
 
 class CSRGrouper:

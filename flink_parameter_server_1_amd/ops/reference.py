@@ -142,6 +142,24 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
     delta.index_add_(0, pos, di)
 
 
+def pair_sgd_pulled(rows, pa, pb, label, delta, lr, loss_kind=0):
+    """Pairwise embedding SGD on pulled rows; returns the loss sum (see ``pair.hip``)."""
+    pa, pb = pa.long(), pb.long()
+    a, b = rows[pa].to(torch.float32), rows[pb].to(torch.float32)
+    s = (a * b).sum(1)
+    if loss_kind == 0:
+        g = label - torch.sigmoid(s)
+        z = torch.where(label > 0.5, s, -s)
+        loss = torch.nn.functional.softplus(-z).sum()
+    else:
+        g = label - s
+        loss = 0.5 * (g * g).sum()
+    c = (lr * g)[:, None]
+    delta.index_add_(0, pa, c * b)
+    delta.index_add_(0, pb, c * a)
+    return float(loss)
+
+
 def csr_group(keys: torch.Tensor, n_groups: int):
     """Counting sort: ``ptr[G+1]`` offsets and ``order`` = request indices grouped by key."""
     k = keys.long()

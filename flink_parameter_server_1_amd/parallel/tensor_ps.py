@@ -98,14 +98,19 @@ class TensorPS:
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
         with trace_range("ps.push-a2a"):
             recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
-        if self.table.optimizer == "add" and self.table.dim < 32 and len(plan.recv_splits) <= 16:
-            # narrow rows: one float atomic per lane hits a different row (the
-            # slow atomic shape).  Keys are unique within each source's segment,
-            # so apply segment by segment with plain read-modify-write.
+        opt = self.table.optimizer
+        narrow_add = opt == "add" and self.table.dim < 32 and len(plan.recv_splits) <= 16
+        if narrow_add or opt in ("adagrad", "set"):
+            # Keys are unique within each source's segment but may repeat across
+            # sources; non-atomic rules (adagrad's accumulator RMW, set) must
+            # therefore apply segment by segment.  Narrow ``add`` rows do the
+            # same with plain read-modify-write: one float atomic per lane on a
+            # different row each is the slow atomic shape.
             off = 0
             for n in plan.recv_splits:
                 if n:
-                    self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], op="add_unique")
+                    self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], lr=lr,
+                                     op="add_unique" if narrow_add else None)
                 off += n
         else:
             self.table.apply(plan.recv_keys, recv, lr=lr)
