@@ -3,12 +3,12 @@
 (PS capacity / bounded-staleness stress).
 
     python bench/bench_capacity.py [--params-per-gpu 12.5e9] [--dim 64] [--batch 1048576]
-                                   [--staleness 2] [--optimizer add|adagrad] [--steps K]
+                                   [--staleness 2] [--optimizer adagrad|add] [--steps K]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bench_capacity.py --gpus 8
 
 Weak scaling of the table: every GPU holds ``--params-per-gpu`` fp32 parameters
-(default 12.5e9 = 50 GB; at 8 GPUs the table is 100e9 parameters = 1.5625e9
-rows of dim 64, range-partitioned).  Each step every rank trains on ``--batch``
+(default 12.5e9 = 50 GB, plus 50 GB of Adagrad state; at 8 GPUs the table is
+100e9 parameters = 1.5625e9 rows of dim 64, range-partitioned).  Each step every rank trains on ``--batch``
 (a, b, label) id pairs with power-law id popularity: dedup (hashed claim map) ->
 key/row all-to-all -> fused ``pair_sgd_pulled`` -> delta all-to-all -> PS apply,
 with up to ``--staleness`` later pulls in flight before a push lands.
@@ -36,7 +36,10 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--batch", type=int, default=1 << 20, help="pairs per GPU per step")
     ap.add_argument("--staleness", type=int, default=2)
-    ap.add_argument("--optimizer", default="add", choices=["add", "adagrad"])
+    ap.add_argument("--optimizer", default="adagrad", choices=["add", "adagrad"],
+                    help="PS apply rule; adagrad keeps a per-parameter accumulator (2x table memory) and is "
+                         "robust to the summed deltas of hot ids")
+    ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--zipf", type=float, default=3.0)
     ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"])
     ap.add_argument("--pool", type=int, default=4, help="pre-generated batches cycled through")
@@ -52,7 +55,7 @@ def main(argv=None):
     num_ids = int(a.params_per_gpu * comm.world) // a.dim
     wire = a.wire if a.wire != "auto" else ("bf16" if comm.world > 1 else "fp32")
     cfg = PairEmbeddingConfig(num_ids=num_ids, dim=a.dim, staleness=a.staleness, optimizer=a.optimizer,
-                              wire_dtype=wire)
+                              learning_rate=a.lr, wire_dtype=wire)
     t_init = time.perf_counter()
     m = DistributedPairEmbedding(cfg, comm)
     if dev.type == "cuda":
@@ -60,7 +63,7 @@ def main(argv=None):
     t_init = time.perf_counter() - t_init
     pool = [synthetic_pairs(num_ids, a.batch, seed=comm.rank + 1, step=s, device=dev, zipf=a.zipf)
             for s in range(a.pool)]
-    eval_batch = synthetic_pairs(num_ids, 1 << 16, seed=12345, step=0, device=dev, zipf=a.zipf)
+    eval_batch = tuple(t[: 1 << 16] for t in pool[0])  # loss on (a slice of) a trained batch
 
     def sync():
         if dev.type == "cuda":

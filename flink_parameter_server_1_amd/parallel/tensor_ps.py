@@ -99,18 +99,19 @@ class TensorPS:
         with trace_range("ps.push-a2a"):
             recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
         opt = self.table.optimizer
-        narrow_add = opt == "add" and self.table.dim < 32 and len(plan.recv_splits) <= 16
-        if narrow_add or opt in ("adagrad", "set"):
+        seg_add = opt == "add" and len(plan.recv_splits) <= 16
+        if seg_add or opt in ("adagrad", "set"):
             # Keys are unique within each source's segment but may repeat across
             # sources; non-atomic rules (adagrad's accumulator RMW, set) must
-            # therefore apply segment by segment.  Narrow ``add`` rows do the
-            # same with plain read-modify-write: one float atomic per lane on a
-            # different row each is the slow atomic shape.
+            # therefore apply segment by segment.  ``add`` does the same with a
+            # plain read-modify-write (add_unique) instead of one float atomic per
+            # element (the atomic apply ran at ~1 TB/s: 480 us for 2M dim-64
+            # rows, profiles/r1_capacity_kernel_stats.csv; narrow rows are worse).
             off = 0
             for n in plan.recv_splits:
                 if n:
                     self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], lr=lr,
-                                     op="add_unique" if narrow_add else None)
+                                     op="add_unique" if seg_add else None)
                 off += n
         else:
             self.table.apply(plan.recv_keys, recv, lr=lr)

@@ -151,12 +151,14 @@ def test_pair_kernel_matches_reference_gpu(D, wire, loss):
 def test_pair_embedding_gpu_hashed_dedup_learns():
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    cfg = PairEmbeddingConfig(num_ids=300_000_000, dim=64, learning_rate=0.3, staleness=2, init_scale=0.5)
+    cfg = PairEmbeddingConfig(num_ids=300_000_000, dim=32, learning_rate=0.05, staleness=2, init_scale=0.5,
+                              optimizer="adagrad")
     m = DistributedPairEmbedding(cfg, Comm(device=torch.device("cuda")))
     assert m.ps.dedup.hashed  # 3e8 ids > dense-map limit (2^28)
-    batches = [synthetic_pairs(cfg.num_ids, 65536, seed=5, step=s, device="cuda", zipf=6.0) for s in range(4)]
+    batches = [synthetic_pairs(cfg.num_ids, 65536, seed=5, step=s, device="cuda", zipf=3.0) for s in range(4)]
     before = m.mean_loss(*batches[0])
     for s in range(40):
         m.step(*batches[s % 4])
     m.flush()
-    assert m.mean_loss(*batches[0]) < before - 0.05
+    after = m.mean_loss(*batches[0])
+    assert after < before - 0.2, (before, after)  # (CPU simulation at dim 16: 0.69 -> 0.20)
