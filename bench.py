@@ -4,10 +4,17 @@
 Metric and config from BASELINE.json: "param updates/sec (whole node), MF-SGD
 10M x 1M rank-64 at 1/2/4/8 MI355X".  One update = one rating-SGD step
 (one user row + one item row of 64 fp32 each).  Synthetic ratings, random
-init, fp32 parameters and compute.  At N > 1 the pulled item rows and pushed
-deltas cross xGMI as bf16 by default (``--wire``; tables and arithmetic stay
-fp32), and the pull of micro-batch k+1 overlaps the SGD of micro-batch k
-(``--no-pipeline`` disables it).
+init, fp32 parameters and compute.
+
+At N > 1 the default exchange is the item-block ring rotation
+(``--exchange rotate``, ``parallel/rotation.py``): the 1M x 64 item table
+travels around the xGMI ring in 2N blocks while every GPU updates the block it
+holds with its users' ratings -- each item block is owned by one GPU at a time,
+so the updates are exact (no staleness) and the 32 MB block transfers hide
+behind the compute of the previous block.  ``--exchange ps`` runs the
+reference's pull/push protocol instead (dedup -> all-to-all pull -> SGD ->
+all-to-all push; rows cross xGMI as bf16 by default, ``--wire``; the pull of
+micro-batch k+1 overlaps the SGD of k, ``--no-pipeline`` disables it).
 
     python bench.py --gpus N --steps K --warmup W
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -31,14 +38,18 @@ sys.path.insert(0, ROOT)
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1 << 22, help="ratings per GPU per step")
+    ap.add_argument("--batch", type=int, default=1 << 25,
+                    help="ratings per GPU per step (32M: each of the 2N rotation sub-steps computes longer than "
+                         "its block transfer)")
     ap.add_argument("--users", type=int, default=10_000_000)
     ap.add_argument("--items", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--pool", type=int, default=8, help="data pool = pool * batch ratings per GPU")
+    ap.add_argument("--pool", type=int, default=4, help="data pool = pool * batch ratings per GPU")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "rotate", "ps", "local"],
+                    help="auto = local at N=1, rotate at N>1")
     ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"],
                     help="all-to-all row dtype; auto = bf16 at N>1")
     ap.add_argument("--no-pipeline", action="store_true")
@@ -64,7 +75,7 @@ def main(argv=None):
         a.wire = "bf16" if n > 1 else "fp32"
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
-                   pipeline=not a.no_pipeline)
+                   pipeline=not a.no_pipeline, exchange=a.exchange)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -110,13 +121,16 @@ def main(argv=None):
                 "model": f"mf-sgd users={a.users} items={a.items} rank={a.dim}",
                 "global_batch": a.batch * n,
                 "seq_len": None,
-                "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded)",
-                "wire_dtype": a.wire if (n > 1 or a.force_ps_path) else "none (local PS shard)",
+                "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded, exchange={model.exchange})",
+                "exchange": model.exchange,
+                "wire_dtype": a.wire if model.exchange == "ps" else "none (fp32 parameters stay resident or travel "
+                                                                     "whole)",
                 "sgd_mode": model.sgd_mode,
                 "pipelined": model.pipeline,
                 "scalar_params_per_s": value * 2 * a.dim,
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
-                if n > 1 else None,
+                if model.exchange == "ps" else None,
+                "rotation_bytes_sent_rank0": model.rot.bytes_sent if model.exchange == "rotate" else None,
             },
         }
         print(json.dumps(out), flush=True)

@@ -37,12 +37,20 @@ __device__ __forceinline__ void group_coords(int64_t& first, int64_t& step, int&
   j0 = lane % TPR;
 }
 
+// seg != nullptr: the batch is the segment [seg[0], seg[1]) of uid/iid/rating,
+// read on the device (item-block rotation: segment sizes never visit the host)
 template <int TPR, int NV, int UNR, bool USER_ATOMIC>
 __global__ void __launch_bounds__(256) mf_sgd_local_kernel(float* __restrict__ U, float* __restrict__ I,
                                                            const int32_t* __restrict__ uid,
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating, int64_t B, int D,
-                                                           float lr, float lambda) {
+                                                           float lr, float lambda,
+                                                           const int32_t* __restrict__ seg) {
+  if (seg != nullptr) {
+    const int32_t beg = seg[0];
+    B = seg[1] - beg;
+    uid += beg; iid += beg; rating += beg;
+  }
   int64_t first, step; int j0;
   group_coords<TPR>(first, step, j0);
   for (int64_t base = first; base < B; base += step * UNR) {
@@ -198,8 +206,25 @@ FPS_API int fps_mf_sgd_local(float* U, float* I, const int32_t* uid, const int32
   constexpr int UNR = 4;
   NV_TPR_SWITCH(D, {
     const int g = sgd_grid(B, TPR, UNR);
-    if (user_atomic) hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, true>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, B, D, lr, lambda);
-    else hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, false>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, B, D, lr, lambda);
+    if (user_atomic) hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, true>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, B, D, lr, lambda, (const int32_t*)nullptr);
+    else hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, false>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, B, D, lr, lambda, (const int32_t*)nullptr);
+  });
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// Segment form: ratings [seg[0], seg[1]) with seg a DEVICE pointer; max_B only
+// sizes the grid (grid-stride loop, any segment length is handled).
+FPS_API int fps_mf_sgd_local_seg(float* U, float* I, const int32_t* uid, const int32_t* iid, const float* r,
+                                 const int32_t* seg, int64_t max_B, int D, float lr, float lambda, int user_atomic,
+                                 void* stream) {
+  if (max_B <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  constexpr int UNR = 4;
+  NV_TPR_SWITCH(D, {
+    const int g = sgd_grid(max_B, TPR, UNR);
+    if (user_atomic) hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, true>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, (int64_t)0, D, lr, lambda, seg);
+    else hipLaunchKernelGGL((mf_sgd_local_kernel<TPR, NV, UNR, false>), dim3(g), dim3(256), 0, s, U, I, uid, iid, r, (int64_t)0, D, lr, lambda, seg);
   });
   FPS_CHECK_LAUNCH();
   return 0;

@@ -109,7 +109,7 @@ def cmd_mf_gpu(args):
                                 device=comm.device, truth_dim=args.truth_dim)
         batch = lambda s: data.batch(s, args.batch)  # noqa: E731
     ck = Checkpointer(args.checkpoint_dir, {"users": m.users, "items": m.items}, comm,
-                      every_steps=args.checkpoint_every) if args.checkpoint_dir else None
+                      every_steps=args.checkpoint_every, before_save=m.flush) if args.checkpoint_dir else None
     start = 0
     if ck and args.resume:
         man = ck.restore_latest()
@@ -118,7 +118,6 @@ def cmd_mf_gpu(args):
     for s in range(start, start + args.steps):
         m.step(*batch(s))
         if ck:
-            m.flush()
             ck.maybe_save(s + 1)
     m.flush()
     rmse = m.rmse(*batch(0))

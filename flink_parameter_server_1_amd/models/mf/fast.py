@@ -15,9 +15,17 @@ Execution per micro-batch of B ratings on each GPU:
 * ``W == 1`` — the item shard is local: one fused kernel reads u and i,
   stores u (Hogwild inside the batch; optional atomics) and atomically adds
   di into the item row (``ops.mf_sgd_local``).  No wire buffers at all.
-* ``W > 1`` — ``TensorPS.pull`` (dedup + 2 all-to-alls), fused SGD on the
-  pulled rows accumulating per-unique-item deltas (``ops.mf_sgd_pulled``),
-  ``TensorPS.push`` (all-to-all + atomic apply).
+* ``W > 1``, ``exchange="rotate"`` (default) — the item shards travel around
+  the xGMI ring instead of rows travelling to the ratings
+  (``parallel.rotation.RingRotation``, stratified SGD): the micro-batch is
+  partitioned by item block on the GPU (``ops.RotationPartitioner``), then 2W
+  sub-steps each run the fused local kernel on the resident block while the
+  next block arrives from the neighbour.  No dedup, no pulls, no staleness.
+* ``W > 1``, ``exchange="ps"`` — ``TensorPS.pull`` (dedup + 2 all-to-alls),
+  fused SGD on the pulled rows accumulating per-unique-item deltas
+  (``ops.mf_sgd_pulled``), ``TensorPS.push`` (all-to-all + apply); the pull of
+  batch k+1 overlaps the SGD of batch k.  The reference's protocol, for
+  workloads whose model does not fit the rotation (and the parity tests).
 
 Throughput unit: rating-SGD updates/s (each updates one user row and one item
 row of ``dim`` floats), see BASELINE.md.
@@ -28,9 +36,11 @@ from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
+import torch.distributed
 
 from ... import ops
 from ...parallel.comm import Comm
+from ...parallel.rotation import RingRotation, shard_halves
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
 
@@ -50,6 +60,8 @@ class MFConfig:
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "grouped" | "flat"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
+    exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
+                                      # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
 
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
@@ -76,7 +88,19 @@ class DistributedMF:
             mode = "flat"
         self.sgd_mode = mode
         self.grouper = ops.CSRGrouper(dev)
-        self.pipeline = cfg.pipeline and (W > 1 or cfg.force_ps_path)
+        exchange = cfg.exchange
+        if exchange == "auto":
+            exchange = "ps" if cfg.force_ps_path else ("rotate" if W > 1 else "local")
+        if exchange not in ("rotate", "ps", "local") or (exchange == "local" and W > 1):
+            raise ValueError(f"exchange {cfg.exchange!r} invalid at world size {W}")
+        self.exchange = exchange
+        if self.exchange == "rotate":
+            self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
+            self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
+            # rows are updated in rotating buffers: remember which items were rated
+            # so the close-time dump still covers exactly the touched parameters
+            self._seen = torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev)
+        self.pipeline = cfg.pipeline and self.exchange == "ps"
         self._pending = None
         self.updates = 0
 
@@ -94,12 +118,22 @@ class DistributedMF:
         c = self.cfg
         grouped = self.sgd_mode == "grouped"
         uid_local, iid, rating = uid_local.contiguous(), iid.contiguous(), rating.contiguous()
-        if self.comm.world == 1 and not c.force_ps_path:
+        if self.exchange == "local":
             if grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
             else:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
+        elif self.exchange == "rotate":
+            if self.items.touched is not None:
+                self._seen[iid.long()] = 1
+            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating)
+            n = uid_local.numel()
+            for _ in range(self.rot.K):
+                self.rot.begin()  # transfer of the next block overlaps this sub-step
+                ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
+                                     c.learning_rate, c.lam, self.user_atomic)
+                self.rot.end()
         elif self.pipeline:
             # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD
             # of batch k; k's push follows.  Staleness bound: one micro-batch.
@@ -131,7 +165,14 @@ class DistributedMF:
         self.ps.push(plan, delta)
 
     def flush(self):
-        """Complete the in-flight micro-batch of the pipelined path."""
+        """Complete the in-flight micro-batch of the pipelined path / bring the
+        rotating item blocks back to their PS shards."""
+        if self.exchange == "rotate" and not self.rot.at_rest:
+            self.rot.home()
+            if self.items.touched is not None:
+                seen = self.comm.all_reduce(self._seen.clone(), op=torch.distributed.ReduceOp.MAX)
+                loc = torch.arange(self.items.n_local, device=seen.device)
+                self.items.touched |= seen[self.items.global_ids(loc)]
         if self._pending is not None:
             p, self._pending = self._pending, None
             self._finish(p)
@@ -156,6 +197,7 @@ class DistributedMF:
         return ids, self.U
 
     def item_vectors(self, only_touched=True):
+        self.flush()
         return self.items.dump(only_touched)
 
 

@@ -183,6 +183,56 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr: float, lam: float = 0.0, user
     R.mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam, user_atomic)
 
 
+def mf_sgd_local_seg(U, I, uid, iid, r, seg_ptr, seg: int, max_b: int, lr: float, lam: float = 0.0,
+                     user_atomic: bool = False):
+    """``mf_sgd_local`` on the ratings ``[ptr[seg], ptr[seg+1])``; on the GPU the
+    bounds are read on the device (no host sync), ``max_b`` only sizes the grid."""
+    if _on_gpu(U):
+        lib = N.require()
+        sp = _c(seg_ptr)
+        N.check(lib.fps_mf_sgd_local_seg(_c(U).data_ptr(), _c(I).data_ptr(), _c(uid).data_ptr(), _c(iid).data_ptr(),
+                                         _c(r).data_ptr(), sp.data_ptr() + 4 * seg, max(int(max_b), 1), U.shape[1],
+                                         lr, lam, int(user_atomic), N.stream_ptr(U.device)), "mf_sgd_local_seg")
+        return
+    a, b = int(seg_ptr[seg]), int(seg_ptr[seg + 1])
+    R.mf_sgd_local(U, I, uid[a:b], iid[a:b], r[a:b], lr, lam, user_atomic)
+
+
+class RotationPartitioner:
+    """Groups a worker's ratings by rotation item block (``rotate.hip``) with
+    reusable device buffers; ``run`` returns ``(ptr[K+1], uid, row, rating)``
+    (device tensors; nothing is synchronised to the host)."""
+
+    def __init__(self, W: int, half: torch.Tensor, device):
+        self.W, self.K = W, 2 * W
+        self.device = torch.device(device)
+        self.half = half.to(device=self.device, dtype=torch.int32).contiguous()
+        self.cap = 0
+        if self.device.type == "cuda":
+            self.counts = torch.zeros(self.K, dtype=torch.int32, device=self.device)
+            self.cursor = torch.zeros(self.K, dtype=torch.int32, device=self.device)
+            self.ptr = torch.zeros(self.K + 1, dtype=torch.int32, device=self.device)
+
+    def run(self, uid, iid, rating):
+        if self.device.type != "cuda":
+            _, ptr, u, row, r = R.rot_partition(uid, iid, rating, self.W, self.half)
+            return ptr, u, row, r
+        n = uid.numel()
+        if n > self.cap:
+            self.cap = max(n, int(self.cap * 1.25))
+            self.u_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.row_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.r_out = torch.empty(self.cap, dtype=torch.float32, device=self.device)
+        self.counts.zero_()
+        self.cursor.zero_()
+        lib = N.require()
+        N.check(lib.fps_rot_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
+                                      self.half.data_ptr(), self.counts.data_ptr(), self.ptr.data_ptr(),
+                                      self.cursor.data_ptr(), self.u_out.data_ptr(), self.row_out.data_ptr(),
+                                      self.r_out.data_ptr(), N.stream_ptr(self.device)), "rot_partition")
+        return self.ptr, self.u_out[:n], self.row_out[:n], self.r_out[:n]
+
+
 PAIR_LOSSES = {"logistic": 0, "squared": 1}
 
 

@@ -142,6 +142,27 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
     delta.index_add_(0, pos, di)
 
 
+def rot_block_of(iid, W, half):
+    """Item -> (block 2q+h, row inside the block) of the rotation layout (``rotate.hip``)."""
+    i = iid.long()
+    q = i % W
+    loc = i // W
+    hq = half.long()[q]
+    h = (loc >= hq).long()
+    return 2 * q + h, loc - h * hq
+
+
+def rot_partition(uid, iid, rating, W, half):
+    """Ratings grouped by item block: ``(counts[K], ptr[K+1], uid, row, rating)`` (stable order)."""
+    K = 2 * W
+    b, row = rot_block_of(iid, W, half)
+    order = torch.argsort(b, stable=True)
+    counts = torch.bincount(b, minlength=K).to(torch.int32)
+    ptr = torch.zeros(K + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(counts, 0)
+    return counts, ptr, uid[order].to(torch.int32), row[order].to(torch.int32), rating[order]
+
+
 def pair_sgd_pulled(rows, pa, pb, label, delta, lr, loss_kind=0):
     """Pairwise embedding SGD on pulled rows; returns the loss sum (see ``pair.hip``)."""
     pa, pb = pa.long(), pb.long()

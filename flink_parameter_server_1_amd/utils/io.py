@@ -194,9 +194,13 @@ class Checkpointer:
     Layout: ``<dir>/step_<k>/<name>.shard<rank>-of-<world>.bin`` + ``manifest.json``
     written by rank 0 after a barrier (the snapshot is complete when the
     manifest exists).  ``restore_latest`` re-shards to the current world size.
+    ``before_save`` (e.g. ``DistributedMF.flush``) runs first, so in-flight
+    pushes land and rotating item blocks are back in their shards.
     """
 
-    def __init__(self, directory: str, tables: Dict[str, object], comm=None, every_steps: int = 0, keep: int = 2):
+    def __init__(self, directory: str, tables: Dict[str, object], comm=None, every_steps: int = 0, keep: int = 2,
+                 before_save=None):
+        self.before_save = before_save
         self.dir = directory
         self.tables = tables
         self.comm = comm
@@ -216,6 +220,8 @@ class Checkpointer:
         return False
 
     def save(self, step: int, extra: Optional[dict] = None) -> str:
+        if self.before_save is not None:
+            self.before_save()
         rank, world = self._rank_world()
         d = os.path.join(self.dir, f"step_{step:09d}")
         os.makedirs(d, exist_ok=True)

@@ -70,11 +70,11 @@ def _ckpt(rank, world, d):
     comm = Comm()
     m = DistributedMF(MFConfig(num_users=200, num_items=100, dim=4), comm)
     data = SyntheticRatings(200, 100, 4000, rank, world)
-    ck = io.Checkpointer(d, {"users": m.users, "items": m.items}, comm, every_steps=5)
+    ck = io.Checkpointer(d, {"users": m.users, "items": m.items}, comm, every_steps=5, before_save=m.flush)
     for s in range(1, 11):
         m.step(*data.batch(s, 200))
         ck.maybe_save(s)
-    ids, w = m.items.dump(False)
+    ids, w = m.item_vectors(False)  # flushes (rotating blocks home)
     # fresh model, restore
     m2 = DistributedMF(MFConfig(num_users=200, num_items=100, dim=4, seed=9), comm)
     man = io.Checkpointer(d, {"users": m2.users, "items": m2.items}, comm).restore_latest()

@@ -1,0 +1,140 @@
+"""Item-block ring rotation (stratified MF-SGD over the ring) on gloo, W = 2..4."""
+import pytest
+import torch
+
+from dist_utils import run_ranks
+from flink_parameter_server_1_amd.ops import reference as R
+from flink_parameter_server_1_amd.parallel.rotation import block_rows, shard_halves
+
+NU, NI, D, B, STEPS = 700, 301, 8, 500, 3
+
+
+def test_block_layout_covers_every_item_once():
+    for W in (1, 2, 3, 5, 8):
+        half = torch.tensor(shard_halves(NI, W))
+        rows = block_rows(NI, W)
+        b, row = R.rot_block_of(torch.arange(NI), W, half)
+        assert sum(rows) == NI
+        for k in range(2 * W):
+            sel = row[b == k]
+            assert sorted(sel.tolist()) == list(range(rows[k]))
+
+
+def test_rot_partition_reference_groups_by_block():
+    W = 3
+    half = torch.tensor(shard_halves(NI, W))
+    uid = torch.randint(0, 50, (400,), dtype=torch.int32)
+    iid = torch.randint(0, NI, (400,), dtype=torch.int32)
+    r = torch.rand(400)
+    counts, ptr, u, row, rr = R.rot_partition(uid, iid, r, W, half)
+    b, rowg = R.rot_block_of(iid, W, half)
+    for k in range(2 * W):
+        a, e = int(ptr[k]), int(ptr[k + 1])
+        m = b == k
+        assert torch.equal(u[a:e], uid[m]) and torch.equal(row[a:e], rowg[m].int()) and torch.equal(rr[a:e], r[m])
+
+
+def _rot_train(rank, world, steps):
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm()
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3)
+    m = DistributedMF(cfg, comm)
+    assert m.exchange == "rotate"
+    data = SyntheticRatings(NU, NI, B * steps, rank, world, seed=3)
+    for s in range(steps):
+        m.step(*data.batch(s, B))
+    se = m.sq_err(*data.batch(0, B))  # flushes: blocks return home
+    assert m.rot.at_rest
+    ids, vals = m.item_vectors(only_touched=True)
+    uids, uv = m.user_vectors()
+    return ids, vals, uids, uv.clone(), se, m.rot.bytes_sent
+
+
+def _emulate(world, steps):
+    """Single-process replay of the same schedule (sub-step t: rank r on block (2r+t) % 2W)."""
+    from flink_parameter_server_1_amd.models.mf.fast import MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.table import ShardedTable
+
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3)
+    init = ("uniform", cfg.range_min, cfg.range_max)
+    users = [ShardedTable(NU, D, r, world, "hash", init, cfg.seed, track_touched=False) for r in range(world)]
+    items = ShardedTable(NI, D, 0, 1, "hash", init, cfg.seed + 7919, track_touched=False).weight
+    half = torch.tensor(shard_halves(NI, world))
+    data = [SyntheticRatings(NU, NI, B * steps, r, world, seed=3) for r in range(world)]
+    K = 2 * world
+    seen = torch.zeros(NI, dtype=torch.bool)
+    for s in range(steps):
+        parts = []
+        for r in range(world):
+            uid, iid, rating = data[r].batch(s, B)
+            seen[iid.long()] = True
+            parts.append(R.rot_partition(uid, iid, rating, world, half))
+        for t in range(K):
+            for r in range(world):
+                b = (2 * r + t) % K
+                q, h = b // 2, b % 2
+                _, ptr, u, row, rr = parts[r]
+                n_local = (NI - q + world - 1) // world
+                lo = 0 if h == 0 else int(half[q])
+                hi = int(half[q]) if h == 0 else n_local
+                gid = q + world * torch.arange(lo, hi)
+                blk = items[gid].clone()
+                a, e = int(ptr[b]), int(ptr[b + 1])
+                R.mf_sgd_local(users[r].weight, blk, u[a:e], row[a:e], rr[a:e], cfg.learning_rate)
+                items[gid] = blk
+    return users, items, seen
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_rotation_equals_sequential_schedule(world):
+    res = run_ranks(_rot_train, world, STEPS)
+    users, items, seen = _emulate(world, STEPS)
+    ids = torch.cat([x[0] for x in res])
+    vals = torch.cat([x[1] for x in res])
+    # dump covers exactly the rated items
+    assert torch.equal(torch.sort(ids).values, torch.nonzero(seen).flatten())
+    torch.testing.assert_close(vals, items[ids], rtol=1e-6, atol=1e-7)
+    for r in range(world):
+        torch.testing.assert_close(res[r][3], users[r].weight, rtol=1e-6, atol=1e-7)
+    # every sub-step after the first moved one block per rank
+    assert all(x[5] > 0 for x in res)
+
+
+def _rot_vs_ps(rank, world, exchange):
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm()
+    cfg = MFConfig(num_users=600, num_items=300, dim=8, learning_rate=0.2, range_min=0.0, range_max=0.3,
+                   exchange=exchange)
+    m = DistributedMF(cfg, comm)
+    data = SyntheticRatings(600, 300, 20000, rank, world, seed=11, truth_dim=4)
+    first = m.rmse(*data.batch(0, 4000))
+    for s in range(25):
+        m.step(*data.batch(s % 5, 4000))
+    return first, m.rmse(*data.batch(0, 4000))
+
+
+def test_rotation_learns_like_ps_path():
+    rot = run_ranks(_rot_vs_ps, 2, "rotate")
+    ps = run_ranks(_rot_vs_ps, 2, "ps")
+    assert rot[0][1] < 0.6 * rot[0][0]
+    assert rot[0][1] < 1.2 * ps[0][1]
+
+
+def test_rotation_single_rank_matches_local_block_order():
+    """W = 1 rotate: the two half-blocks alternate in place; equals the emulation."""
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3,
+                   exchange="rotate")
+    m = DistributedMF(cfg)
+    data = SyntheticRatings(NU, NI, B * STEPS, 0, 1, seed=3)
+    for s in range(STEPS):
+        m.step(*data.batch(s, B))
+    m.flush()
+    users, items, _ = _emulate(1, STEPS)
+    torch.testing.assert_close(m.I, items, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(m.U, users[0].weight, rtol=1e-6, atol=1e-7)

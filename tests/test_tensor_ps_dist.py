@@ -41,12 +41,13 @@ def test_tensor_ps_pull_push(world, partition):
     torch.testing.assert_close(w, expect, rtol=1e-5, atol=1e-5)
 
 
-def _train(rank, world, steps):
+def _train(rank, world, steps, exchange="auto"):
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     comm = Comm()
-    cfg = MFConfig(num_users=600, num_items=300, dim=8, learning_rate=0.2, range_min=0.0, range_max=0.3)
+    cfg = MFConfig(num_users=600, num_items=300, dim=8, learning_rate=0.2, range_min=0.0, range_max=0.3,
+                   exchange=exchange)
     m = DistributedMF(cfg, comm)
     data = SyntheticRatings(600, 300, 20000 // world, rank, world, truth_dim=4)
     uid, iid, r = data.batch(0, 20000 // world)
@@ -56,9 +57,9 @@ def _train(rank, world, steps):
     return before, m.rmse(uid, iid, r)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_mf_training_converges_distributed(world):
-    res = run_ranks(_train, world, 150)
+@pytest.mark.parametrize("world,exchange", [(1, "auto"), (2, "ps"), (3, "ps"), (2, "rotate"), (3, "rotate")])
+def test_mf_training_converges_distributed(world, exchange):
+    res = run_ranks(_train, world, 150, exchange)
     before, after = res[0]
     assert after < 0.6 * before, (before, after)
     assert all(abs(r[1] - after) < 1e-9 for r in res)  # rmse is a global reduction
