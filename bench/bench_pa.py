@@ -27,7 +27,7 @@ def main(argv=None):
     ap.add_argument("--features", type=int, default=1_000_000_000)
     ap.add_argument("--batch", type=int, default=1 << 16, help="examples per GPU per step")
     ap.add_argument("--nnz", type=int, default=64)
-    ap.add_argument("--zipf", type=float, default=2.0)
+    ap.add_argument("--zipf", type=float, default=1.0)
     ap.add_argument("--kind", default="binary", choices=["binary", "ova", "pb", "ml"])
     ap.add_argument("--labels", type=int, default=1)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])

@@ -32,15 +32,18 @@ __device__ __forceinline__ void item_block(int32_t i, int W, const int32_t* __re
 }
 
 __global__ void __launch_bounds__(256) rot_count_kernel(const int32_t* __restrict__ iid, int64_t n, int W,
-                                                        const int32_t* __restrict__ half, int32_t* __restrict__ counts) {
+                                                        const int32_t* __restrict__ half, int32_t* __restrict__ counts,
+                                                        uint8_t* __restrict__ seen) {
   __shared__ int32_t h[ROT_MAX_K];
   const int K = 2 * W;
   for (int k = threadIdx.x; k < K; k += blockDim.x) h[k] = 0;
   __syncthreads();
   for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
     int b; int32_t row;
-    item_block(iid[x], W, half, b, row);
+    const int32_t i = iid[x];
+    item_block(i, W, half, b, row);
     atomicAdd(h + b, 1);
+    if (seen != nullptr) seen[i] = 1;  // touched-item marks for the close-time dump
   }
   __syncthreads();
   for (int k = threadIdx.x; k < K; k += blockDim.x)
@@ -97,14 +100,15 @@ __global__ void rot_scan_kernel(const int32_t* __restrict__ counts, int K, int32
 
 }  // namespace
 
-// counts[K] and cursor[K] must be zeroed by the caller; ptr has K+1 entries.
+// counts[K] and cursor[K] must be zeroed by the caller; ptr has K+1 entries;
+// seen (optional, num_items bytes) gets seen[i] = 1 for every rated item.
 FPS_API int fps_rot_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                               const int32_t* half, int32_t* counts, int32_t* ptr, int32_t* cursor, int32_t* uid_out,
-                              int32_t* row_out, float* r_out, void* stream) {
+                              int32_t* row_out, float* r_out, uint8_t* seen, void* stream) {
   if (2 * W > ROT_MAX_K) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   if (n > 0) hipLaunchKernelGGL(rot_count_kernel, dim3(grid_for(n, 256 * 8, 256 * 8)), dim3(256), 0, s, iid, n, W,
-                                half, counts);
+                                half, counts, seen);
   hipLaunchKernelGGL(rot_scan_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)counts, 2 * W, ptr);
   if (n > 0) {
     const int64_t g = (n + 256 * ROT_ITEMS - 1) / (256 * ROT_ITEMS);

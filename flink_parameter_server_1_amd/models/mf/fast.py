@@ -125,9 +125,8 @@ class DistributedMF:
             else:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
         elif self.exchange == "rotate":
-            if self.items.touched is not None:
-                self._seen[iid.long()] = 1
-            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating)
+            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating,
+                                                  self._seen if self.items.touched is not None else None)
             n = uid_local.numel()
             for _ in range(self.rot.K):
                 self.rot.begin()  # transfer of the next block overlaps this sub-step

@@ -213,8 +213,11 @@ class RotationPartitioner:
             self.cursor = torch.zeros(self.K, dtype=torch.int32, device=self.device)
             self.ptr = torch.zeros(self.K + 1, dtype=torch.int32, device=self.device)
 
-    def run(self, uid, iid, rating):
+    def run(self, uid, iid, rating, seen: Optional[torch.Tensor] = None):
+        """``seen`` (uint8[num_items], optional): set to 1 for every rated item."""
         if self.device.type != "cuda":
+            if seen is not None:
+                seen[iid.long()] = 1
             _, ptr, u, row, r = R.rot_partition(uid, iid, rating, self.W, self.half)
             return ptr, u, row, r
         n = uid.numel()
@@ -229,7 +232,7 @@ class RotationPartitioner:
         N.check(lib.fps_rot_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
                                       self.half.data_ptr(), self.counts.data_ptr(), self.ptr.data_ptr(),
                                       self.cursor.data_ptr(), self.u_out.data_ptr(), self.row_out.data_ptr(),
-                                      self.r_out.data_ptr(), N.stream_ptr(self.device)), "rot_partition")
+                                      self.r_out.data_ptr(), N.ptr(seen), N.stream_ptr(self.device)), "rot_partition")
         return self.ptr, self.u_out[:n], self.row_out[:n], self.r_out[:n]
 
 
