@@ -41,6 +41,7 @@ import torch.distributed
 from ... import ops
 from ...parallel.comm import Comm
 from ...parallel.rotation import RingRotation, shard_halves
+from ...parallel.rotation import block_rows as block_rows_of
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
 
@@ -58,7 +59,7 @@ class MFConfig:
     user_update: str = "store"        # "store" (Hogwild) | "atomic"
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
-    sgd_mode: str = "auto"            # "auto" | "grouped" | "flat"
+    sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
@@ -79,21 +80,38 @@ class DistributedMF:
         self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.seed + 7919, dev, optimizer="add")
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
         self.user_atomic = cfg.user_update == "atomic"
-        # "flat": one rating per lane group, item deltas by float atomics (measured
-        # fastest: 3.89e9 vs 2.84e9 updates/s for "grouped" at 4M ratings/step on
-        # one MI355X, profiles/README.md); "grouped": ratings sorted by item, each
-        # item row updated in registers (exact per-item order, no item atomics).
-        mode = cfg.sgd_mode
-        if mode == "auto":
-            mode = "flat"
-        self.sgd_mode = mode
-        self.grouper = ops.CSRGrouper(dev)
         exchange = cfg.exchange
         if exchange == "auto":
             exchange = "ps" if cfg.force_ps_path else ("rotate" if W > 1 else "local")
         if exchange not in ("rotate", "ps", "local") or (exchange == "local" and W > 1):
             raise ValueError(f"exchange {cfg.exchange!r} invalid at world size {W}")
         self.exchange = exchange
+        # SGD kernel:
+        #  "tiled"   item rows staged in LDS per tile of R rows, ratings bucketed
+        #            by tile, item deltas by LDS atomics -- no global item atomics
+        #            (mf_tiled.hip; default where the dim/table size fit);
+        #  "flat"    one rating per lane group, item deltas by 256-B global float
+        #            atomics (atomic-rate bound: 3.9e9 ratings/s, profiles/README.md);
+        #  "grouped" ratings sorted by item, each item row updated in registers
+        #            (exact per-item order; latency bound, 2.8e9/s).
+        block_rows = cfg.num_items if exchange == "local" else max(block_rows_of(cfg.num_items, W))
+        tile_w = 1 if exchange == "local" else W
+        tile_R = ops.tile_rows_for(cfg.dim, block_rows, tile_w)
+        mode = cfg.sgd_mode
+        if mode == "auto":
+            mode = "tiled" if (exchange != "ps" and tile_R is not None and not self.user_atomic) else "flat"
+        if mode == "tiled" and (exchange == "ps" or tile_R is None or self.user_atomic):
+            raise ValueError("sgd_mode 'tiled' needs exchange local/rotate, dim in ops.TILED_DIMS, "
+                             "a table small enough for the LDS bucket counters and user_update='store'")
+        if mode == "grouped" and exchange == "rotate":
+            raise ValueError("sgd_mode 'grouped' is not available with the rotation exchange")
+        self.sgd_mode = mode
+        self.grouper = ops.CSRGrouper(dev)
+        if mode == "tiled":
+            self.tile_R = tile_R
+            self.tile_T = -(-block_rows // tile_R)
+            half = [cfg.num_items] if exchange == "local" else shard_halves(cfg.num_items, W)
+            self.tiler = ops.TilePartitioner(tile_w, half, tile_R, self.tile_T, dev)
         if self.exchange == "rotate":
             self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
             self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
@@ -118,20 +136,30 @@ class DistributedMF:
         c = self.cfg
         grouped = self.sgd_mode == "grouped"
         uid_local, iid, rating = uid_local.contiguous(), iid.contiguous(), rating.contiguous()
+        tiled = self.sgd_mode == "tiled"
         if self.exchange == "local":
-            if grouped:
+            if tiled:
+                ptr, u, row, r = self.tiler.run(uid_local, iid, rating)
+                ops.mf_sgd_tiled(self.U, self.I, u, row, r, ptr, 0, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+            elif grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
             else:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
         elif self.exchange == "rotate":
-            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating,
-                                                  self._seen if self.items.touched is not None else None)
+            seen = self._seen if self.items.touched is not None else None
+            part = self.tiler if tiled else self.partitioner
+            ptr, u, row, r = part.run(uid_local, iid, rating, seen)
             n = uid_local.numel()
             for _ in range(self.rot.K):
                 self.rot.begin()  # transfer of the next block overlaps this sub-step
-                ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
-                                     c.learning_rate, c.lam, self.user_atomic)
+                b = self.rot.active_block()
+                if tiled:
+                    ops.mf_sgd_tiled(self.U, self.rot.active(), u, row, r, ptr, b, self.tile_T, self.tile_R,
+                                     c.learning_rate, c.lam)
+                else:
+                    ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, b, n, c.learning_rate, c.lam,
+                                         self.user_atomic)
                 self.rot.end()
         elif self.pipeline:
             # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD

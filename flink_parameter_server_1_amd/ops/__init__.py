@@ -236,6 +236,87 @@ class RotationPartitioner:
         return self.ptr, self.u_out[:n], self.row_out[:n], self.r_out[:n]
 
 
+#: dims the LDS-tiled MF kernel is instantiated for
+TILED_DIMS = (16, 32, 64, 128, 256)
+
+
+#: bucket counters a tile partition keeps in LDS (``TP_MAX_BUCKETS`` in mf_tiled.hip)
+TILE_MAX_BUCKETS = 16384
+
+
+def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
+    """Rows per LDS tile for blocks of ``block_rows``: 32 KiB tiles (R = 128 at
+    D = 64), halved while a block gives fewer than ~1k workgroups (small
+    rotation blocks at N = 8), grown while the 2W*T buckets exceed the LDS
+    counters.  None if no tile size fits (then use the flat kernel)."""
+    if dim not in TILED_DIMS:
+        return None
+    r_max = min(256, 65536 // (4 * dim))
+    r = min(r_max, max(16, 32768 // (4 * dim)))
+
+    def kt(rr):
+        return 2 * W * -(-block_rows // rr)
+
+    while r > 32 and -(-block_rows // r) < 1024 and kt(r // 2) <= TILE_MAX_BUCKETS:
+        r //= 2
+    while kt(r) > TILE_MAX_BUCKETS and r < r_max:
+        r *= 2
+    return r if kt(r) <= TILE_MAX_BUCKETS else None
+
+
+class TilePartitioner:
+    """Buckets a micro-batch's ratings by (item block, tile of ``R`` rows) for
+    ``mf_sgd_tiled`` (``mf_tiled.hip``): 4 kernels, no global atomics, nothing
+    synchronised to the host.  ``run`` returns ``(ptr[2W*T+1], uid, row, rating)``."""
+
+    def __init__(self, W: int, half, R: int, T: int, device):
+        self.W, self.R, self.T = W, int(R), int(T)
+        self.KT = 2 * W * self.T
+        self.device = torch.device(device)
+        self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
+        self.cap = 0
+        self.g_cap = 0
+        if self.device.type == "cuda":
+            self.totals = torch.empty(self.KT, dtype=torch.int32, device=self.device)
+            self.ptr = torch.empty(self.KT + 1, dtype=torch.int32, device=self.device)
+
+    def run(self, uid, iid, rating, seen: Optional[torch.Tensor] = None):
+        if self.device.type != "cuda":
+            if seen is not None:
+                seen[iid.long()] = 1
+            return R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T)
+        lib = N.require()
+        n = uid.numel()
+        G = lib.fps_tile_partition_groups(n)
+        if G * self.KT > self.g_cap:
+            self.g_cap = G * self.KT
+            self.H = torch.empty(self.g_cap, dtype=torch.int32, device=self.device)
+        if n > self.cap:
+            self.cap = max(n, int(self.cap * 1.25))
+            self.u_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.row_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+            self.r_out = torch.empty(self.cap, dtype=torch.float32, device=self.device)
+        N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
+                                       self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),
+                                       self.totals.data_ptr(), self.ptr.data_ptr(), self.u_out.data_ptr(),
+                                       self.row_out.data_ptr(), self.r_out.data_ptr(), N.ptr(seen),
+                                       N.stream_ptr(self.device)), "tile_partition")
+        return self.ptr, self.u_out[:n], self.row_out[:n], self.r_out[:n]
+
+
+def mf_sgd_tiled(U, I_block, uid, row, r, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
+    """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``)
+    with the block's rows staged in LDS per tile (no global item atomics)."""
+    if _on_gpu(U):
+        lib = N.require()
+        N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(uid).data_ptr(),
+                                     _c(row).data_ptr(), _c(r).data_ptr(), _c(ptr).data_ptr() + 4 * block * T, T,
+                                     tile_rows, I_block.shape[0], U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
+        return
+    a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
+    R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
+
+
 PAIR_LOSSES = {"logistic": 0, "squared": 1}
 
 

@@ -163,6 +163,17 @@ def rot_partition(uid, iid, rating, W, half):
     return counts, ptr, uid[order].to(torch.int32), row[order].to(torch.int32), rating[order]
 
 
+def tile_partition(uid, iid, rating, W, half, R, T):
+    """Ratings grouped by (item block, tile of R rows): ``(ptr[2W*T+1], uid, row_in_block, rating)``."""
+    b, row = rot_block_of(iid, W, half)
+    bucket = b * T + row // R
+    order = torch.argsort(bucket, stable=True)
+    counts = torch.bincount(bucket, minlength=2 * W * T)
+    ptr = torch.zeros(2 * W * T + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(counts, 0)
+    return ptr, uid[order].to(torch.int32), row[order].to(torch.int32), rating[order]
+
+
 def pair_sgd_pulled(rows, pa, pb, label, delta, lr, loss_kind=0):
     """Pairwise embedding SGD on pulled rows; returns the loss sum (see ``pair.hip``)."""
     pa, pb = pa.long(), pb.long()

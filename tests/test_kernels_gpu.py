@@ -179,3 +179,74 @@ def test_mf_sgd_local_seg_matches_slice():
     ops.mf_sgd_local_seg(U, I, uid, iid, r, ptr, 1, B, 0.05, 0.01)
     torch.testing.assert_close(U.cpu(), Ur, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(I.cpu(), Ir, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("W,R", [(1, 128), (2, 64), (8, 64)])
+def test_tile_partition_matches_reference(W, R):
+    from flink_parameter_server_1_amd.parallel.rotation import block_rows, shard_halves
+
+    NI, n = 200_003, 500_000
+    half = [NI] if W == 1 else shard_halves(NI, W)
+    rows_max = NI if W == 1 else max(block_rows(NI, W))
+    T = -(-rows_max // R)
+    half_t = torch.tensor(half, dtype=torch.int32)
+    uid = torch.randint(0, 10_000, (n,), dtype=torch.int32)
+    iid = torch.randint(0, NI, (n,), dtype=torch.int32)
+    r = torch.rand(n)
+    p_ref, u_ref, row_ref, r_ref = R_tile(uid, iid, r, W, half_t, R, T)
+    part = ops.TilePartitioner(W, half, R, T, DEV)
+    seen = torch.zeros(NI, dtype=torch.uint8, device=DEV)
+    for _ in range(2):
+        ptr, u, row, rr = part.run(uid.to(DEV), iid.to(DEV), r.to(DEV), seen)
+        assert torch.equal(ptr.cpu(), p_ref)
+        # same multiset of (bucket, uid, row, rating): sort both by (bucket, uid, row)
+        for t_ in (u, row, rr):
+            assert t_.numel() == n
+        bucket = torch.repeat_interleave(torch.arange(p_ref.numel() - 1), (p_ref[1:] - p_ref[:-1]).long())
+        key = lambda U_, Rw, Rt: sorted(zip(bucket.tolist(), U_.tolist(), Rw.tolist(), Rt.tolist()))  # noqa: E731
+        assert key(u.cpu(), row.cpu(), rr.cpu()) == key(u_ref, row_ref, r_ref)
+    assert torch.equal(seen.cpu().bool(), torch.bincount(iid.long(), minlength=NI) > 0)
+
+
+def R_tile(*a):
+    return R.tile_partition(*a)
+
+
+@pytest.mark.parametrize("D", [16, 32, 64, 128, 256])
+def test_mf_sgd_tiled_unique_rows(D):
+    """Unique users and items: the tiled kernel equals the batch reference."""
+    nu, ni, B = 6000, 5000, 3000
+    U = torch.rand(nu, D, device=DEV) * 0.1
+    I = torch.rand(ni, D, device=DEV) * 0.1
+    uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
+    iid = torch.randperm(ni, device=DEV)[:B].to(torch.int32)
+    r = torch.rand(B, device=DEV)
+    Rt = ops.tile_rows_for(D, ni, 1)
+    T = -(-ni // Rt)
+    part = ops.TilePartitioner(1, [ni], Rt, T, DEV)
+    ptr, u, row, rr = part.run(uid, iid, r)
+    Ur, Ir = U.cpu().clone(), I.cpu().clone()
+    R.mf_sgd_local(Ur, Ir, uid.cpu(), iid.cpu(), r.cpu(), 0.05, 0.01)
+    ops.mf_sgd_tiled(U, I, u, row, rr, ptr, 0, T, Rt, 0.05, 0.01)
+    torch.testing.assert_close(U.cpu(), Ur, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(I.cpu(), Ir, rtol=1e-5, atol=1e-6)
+
+
+def test_mf_sgd_tiled_duplicate_items_accumulate():
+    """Many ratings per item: LDS atomics must keep every item delta (no lost update)."""
+    D, B, ni = 64, 20000, 300
+    nu = B
+    U = torch.full((nu, D), 1e-3, device=DEV)
+    I = torch.rand(ni, D, device=DEV) * 0.1
+    uid = torch.arange(B, device=DEV, dtype=torch.int32)
+    iid = torch.randint(0, ni, (B,), device=DEV, dtype=torch.int32)
+    r = torch.rand(B, device=DEV)
+    Rt = 128
+    T = -(-ni // Rt)
+    ptr, u, row, rr = ops.TilePartitioner(1, [ni], Rt, T, DEV).run(uid, iid, r)
+    Ur, Ir = U.cpu().clone(), I.cpu().clone()
+    R.mf_sgd_local(Ur, Ir, uid.cpu(), iid.cpu(), r.cpu(), 0.01)
+    ops.mf_sgd_tiled(U, I, u, row, rr, ptr, 0, T, Rt, 0.01)
+    # users tiny -> item drift within the batch is second order; sums must match
+    torch.testing.assert_close(I.cpu(), Ir, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(U.cpu(), Ur, rtol=1e-3, atol=1e-6)

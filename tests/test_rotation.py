@@ -34,14 +34,15 @@ def test_rot_partition_reference_groups_by_block():
         assert torch.equal(u[a:e], uid[m]) and torch.equal(row[a:e], rowg[m].int()) and torch.equal(rr[a:e], r[m])
 
 
-def _rot_train(rank, world, steps):
+def _rot_train(rank, world, steps, dim=D):
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     comm = Comm()
-    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3)
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=dim, learning_rate=0.1, range_min=0.0, range_max=0.3)
     m = DistributedMF(cfg, comm)
     assert m.exchange == "rotate"
+    assert m.sgd_mode == ("tiled" if dim in (16, 32, 64) else "flat")
     data = SyntheticRatings(NU, NI, B * steps, rank, world, seed=3)
     for s in range(steps):
         m.step(*data.batch(s, B))
@@ -52,15 +53,21 @@ def _rot_train(rank, world, steps):
     return ids, vals, uids, uv.clone(), se, m.rot.bytes_sent
 
 
-def _emulate(world, steps):
+def _emulate(world, steps, dim=D):
     """Single-process replay of the same schedule (sub-step t: rank r on block (2r+t) % 2W)."""
+    from flink_parameter_server_1_amd import ops
     from flink_parameter_server_1_amd.models.mf.fast import MFConfig, SyntheticRatings
     from flink_parameter_server_1_amd.parallel.table import ShardedTable
 
-    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3)
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=dim, learning_rate=0.1, range_min=0.0, range_max=0.3)
     init = ("uniform", cfg.range_min, cfg.range_max)
-    users = [ShardedTable(NU, D, r, world, "hash", init, cfg.seed, track_touched=False) for r in range(world)]
-    items = ShardedTable(NI, D, 0, 1, "hash", init, cfg.seed + 7919, track_touched=False).weight
+    users = [ShardedTable(NU, dim, r, world, "hash", init, cfg.seed, track_touched=False) for r in range(world)]
+    items = ShardedTable(NI, dim, 0, 1, "hash", init, cfg.seed + 7919, track_touched=False).weight
+    tiled = dim in ops.TILED_DIMS
+    if tiled:  # same tile geometry as DistributedMF
+        rows_max = max(block_rows(NI, world))
+        Rt = ops.tile_rows_for(dim, rows_max, world)
+        Tt = -(-rows_max // Rt)
     half = torch.tensor(shard_halves(NI, world))
     data = [SyntheticRatings(NU, NI, B * steps, r, world, seed=3) for r in range(world)]
     K = 2 * world
@@ -70,7 +77,11 @@ def _emulate(world, steps):
         for r in range(world):
             uid, iid, rating = data[r].batch(s, B)
             seen[iid.long()] = True
-            parts.append(R.rot_partition(uid, iid, rating, world, half))
+            if tiled:
+                ptr, u_, row_, r_ = R.tile_partition(uid, iid, rating, world, half, Rt, Tt)
+                parts.append((None, ptr[:: Tt], u_, row_, r_))  # block b's segment: ptr[b*T] .. ptr[(b+1)*T]
+            else:
+                parts.append(R.rot_partition(uid, iid, rating, world, half))
         for t in range(K):
             for r in range(world):
                 b = (2 * r + t) % K
@@ -87,10 +98,17 @@ def _emulate(world, steps):
     return users, items, seen
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_rotation_equals_sequential_schedule(world):
-    res = run_ranks(_rot_train, world, STEPS)
-    users, items, seen = _emulate(world, STEPS)
+@pytest.mark.parametrize("world,dim", [(2, D), (3, D), (4, D), (2, 16), (3, 32)])
+def test_rotation_equals_sequential_schedule(world, dim):
+    res = run_ranks(_rot_train, world, STEPS, dim)
+    # single thread like the ranks: index_put with duplicate users is last-writer-wins,
+    # and which write is last depends on the thread split
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        users, items, seen = _emulate(world, STEPS, dim)
+    finally:
+        torch.set_num_threads(nt)
     ids = torch.cat([x[0] for x in res])
     vals = torch.cat([x[1] for x in res])
     # dump covers exactly the rated items
