@@ -101,15 +101,16 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restri
   if (threadIdx.x == 1023) ptr[KT] = part[1023];
 }
 
-// K4: scatter (uid, row-in-block, rating) to ptr[bucket] + H[w][bucket] + LDS slot
+// K4: scatter packed 16-B records {uid, row-in-block, rating bits, 0} to
+// ptr[bucket] + H[w][bucket] + LDS slot (one 16-B store per rating instead of
+// three scattered 4-B stores)
 __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __restrict__ uid,
                                                             const int32_t* __restrict__ iid,
                                                             const float* __restrict__ rating, int64_t n,
                                                             int64_t chunk, int W, const int32_t* __restrict__ half,
                                                             int R, int T, int KT, const int32_t* __restrict__ H,
                                                             const int32_t* __restrict__ ptr,
-                                                            int32_t* __restrict__ uid_out,
-                                                            int32_t* __restrict__ row_out, float* __restrict__ r_out) {
+                                                            int4* __restrict__ rec) {
   __shared__ int32_t cur[TP_MAX_BUCKETS];
   const int32_t* Hw = H + (int64_t)blockIdx.x * KT;
   for (int k = threadIdx.x; k < KT; k += blockDim.x) cur[k] = ptr[k] + Hw[k];
@@ -119,18 +120,14 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
     int bk; int32_t row;
     tile_bucket(iid[x], W, half, R, T, bk, row);
     const int32_t o = atomicAdd(cur + bk, 1);
-    uid_out[o] = uid[x];
-    row_out[o] = row;
-    r_out[o] = rating[x];
+    rec[o] = make_int4(uid[x], row, __float_as_int(rating[x]), 0);
   }
 }
 
 // ---------------------------------------------------------------- SGD
 template <int TPR, int V, int UNR>
 __global__ void __launch_bounds__(512) mf_sgd_tiled_kernel(float* __restrict__ U, float* __restrict__ I,
-                                                           const int32_t* __restrict__ uid,
-                                                           const int32_t* __restrict__ row,
-                                                           const float* __restrict__ rating,
+                                                           const int4* __restrict__ rec,
                                                            const int32_t* __restrict__ ptr, int R,
                                                            int64_t block_rows, float lr, float lambda) {
   extern __shared__ float4 tile[];
@@ -140,33 +137,52 @@ __global__ void __launch_bounds__(512) mf_sgd_tiled_kernel(float* __restrict__ U
   const int64_t r0 = (int64_t)t * R;
   const int nr = (int)min((int64_t)R, block_rows - r0);
   float4* Ig = reinterpret_cast<float4*>(I) + r0 * D4;
-  for (int x = threadIdx.x; x < nr * D4; x += blockDim.x) tile[x] = Ig[x];
+  {  // tile load: all of a thread's loads in flight before its LDS writes
+    constexpr int LPT = 8;  // float4 per thread per round (<= 64 KiB tiles at 512 threads)
+    const int tot = nr * D4;
+    for (int x0 = threadIdx.x; x0 < tot; x0 += blockDim.x * LPT) {
+      float4 v[LPT];
+#pragma unroll
+      for (int k = 0; k < LPT; ++k) {
+        const int x = x0 + k * blockDim.x;
+        if (x < tot) v[k] = Ig[x];
+      }
+#pragma unroll
+      for (int k = 0; k < LPT; ++k) {
+        const int x = x0 + k * blockDim.x;
+        if (x < tot) tile[x] = v[k];
+      }
+    }
+  }
   __syncthreads();
   const int32_t beg = ptr[t], end = ptr[t + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int g = lane / TPR, j = lane % TPR;
   const int stride = nw * RPW;
   const float4* Ug = reinterpret_cast<const float4*>(U);
-  for (int32_t base = beg + wave * RPW + g; base < end; base += stride * UNR) {
+  // records of the first round; every load is unconditional (index clamped to
+  // the segment) so the UNR loads issue back to back
+  int4 cur[UNR];
+  int32_t base = beg + wave * RPW + g;
+  const int32_t last = end - 1;  // records are only read when the tile has ratings (beg < end)
+  if (beg < end) {
+#pragma unroll
+    for (int q = 0; q < UNR; ++q) cur[q] = rec[min(base + q * stride, last)];
+  }
+  for (; base < end; base += stride * UNR) {
+    int4 nxt[UNR];
+#pragma unroll
+    for (int q = 0; q < UNR; ++q)  // prefetch the next round's records
+      nxt[q] = rec[min(base + (UNR + q) * stride, last)];
     float4 uv[UNR][V], iv[UNR][V];
-    int64_t ur[UNR];
-    int tr[UNR];
-    float rv[UNR];
-    bool ok[UNR];
 #pragma unroll
     for (int q = 0; q < UNR; ++q) {
-      const int32_t x = base + q * stride;
-      ok[q] = x < end;
-      ur[q] = ok[q] ? (int64_t)uid[x] * D4 : 0;
-      tr[q] = ok[q] ? (int)(row[x] - r0) * D4 : 0;
-      rv[q] = ok[q] ? rating[x] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < UNR; ++q) {
+      const int64_t ur = (int64_t)cur[q].x * D4;
+      const int tr = (int)(cur[q].y - r0) * D4;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        uv[q][v] = ok[q] ? Ug[ur[q] + j + v * TPR] : make_float4(0.f, 0.f, 0.f, 0.f);
-        iv[q][v] = tile[tr[q] + j + v * TPR];
+        uv[q][v] = Ug[ur + j + v * TPR];
+        iv[q][v] = tile[tr + j + v * TPR];
       }
     }
 #pragma unroll
@@ -175,8 +191,10 @@ __global__ void __launch_bounds__(512) mf_sgd_tiled_kernel(float* __restrict__ U
 #pragma unroll
       for (int v = 0; v < V; ++v)
         p += uv[q][v].x * iv[q][v].x + uv[q][v].y * iv[q][v].y + uv[q][v].z * iv[q][v].z + uv[q][v].w * iv[q][v].w;
-      const float e = rv[q] - group_sum<TPR>(p);
-      if (!ok[q]) continue;
+      const float e = __int_as_float(cur[q].z) - group_sum<TPR>(p);
+      if (base + q * stride >= end) continue;  // uniform in the lane group
+      const int64_t ur = (int64_t)cur[q].x * D4;
+      const int tr = (int)(cur[q].y - r0) * D4;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float4 u = uv[q][v], i = iv[q][v];
@@ -185,14 +203,16 @@ __global__ void __launch_bounds__(512) mf_sgd_tiled_kernel(float* __restrict__ U
         nu.y = u.y + lr * (e * i.y - lambda * u.y);
         nu.z = u.z + lr * (e * i.z - lambda * u.z);
         nu.w = u.w + lr * (e * i.w - lambda * u.w);
-        reinterpret_cast<float4*>(U)[ur[q] + j + v * TPR] = nu;
-        float* ti = reinterpret_cast<float*>(tile + tr[q] + j + v * TPR);
+        reinterpret_cast<float4*>(U)[ur + j + v * TPR] = nu;
+        float* ti = reinterpret_cast<float*>(tile + tr + j + v * TPR);
         atomicAdd(ti + 0, lr * (e * u.x - lambda * i.x));
         atomicAdd(ti + 1, lr * (e * u.y - lambda * i.y));
         atomicAdd(ti + 2, lr * (e * u.z - lambda * i.z));
         atomicAdd(ti + 3, lr * (e * u.w - lambda * i.w));
       }
     }
+#pragma unroll
+    for (int q = 0; q < UNR; ++q) cur[q] = nxt[q];
   }
   __syncthreads();
   for (int x = threadIdx.x; x < nr * D4; x += blockDim.x) Ig[x] = tile[x];
@@ -208,9 +228,10 @@ FPS_API int fps_tile_partition_groups(int64_t n) {
   return (int)g;
 }
 
+// rec: n packed records {uid, row-in-block, rating bits, 0} grouped by bucket
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                                const int32_t* half, int R, int T, int32_t* H, int32_t* totals, int32_t* ptr,
-                               int32_t* uid_out, int32_t* row_out, float* r_out, uint8_t* seen, void* stream) {
+                               int4* rec, uint8_t* seen, void* stream) {
   const int KT = 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -221,23 +242,22 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)totals, KT, ptr);
   if (n > 0)
     hipLaunchKernelGGL(tile_scatter_kernel, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half, R, T,
-                       KT, (const int32_t*)H, (const int32_t*)ptr, uid_out, row_out, r_out);
+                       KT, (const int32_t*)H, (const int32_t*)ptr, rec);
   FPS_CHECK_LAUNCH();
   return 0;
 }
 
 // One launch per block: T tiles of R rows of I[block_rows, D]; ptr = the
 // block's T+1 tile offsets (device).  D must be 16, 32, 64, 128 or 256.
-FPS_API int fps_mf_sgd_tiled(float* U, float* I, const int32_t* uid, const int32_t* row, const float* r,
-                             const int32_t* ptr, int T, int R, int64_t block_rows, int D, float lr, float lambda,
-                             void* stream) {
+FPS_API int fps_mf_sgd_tiled(float* U, float* I, const int4* rec, const int32_t* ptr, int T, int R,
+                             int64_t block_rows, int D, float lr, float lambda, void* stream) {
   if (T <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = (size_t)R * D * sizeof(float);
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
   constexpr int UNR = 4;
 #define FPS_TILED(TPR_, V_)                                                                                      \
-  hipLaunchKernelGGL((mf_sgd_tiled_kernel<TPR_, V_, UNR>), dim3(T), dim3(512), lds, s, U, I, uid, row, r, ptr, R, \
+  hipLaunchKernelGGL((mf_sgd_tiled_kernel<TPR_, V_, UNR>), dim3(T), dim3(512), lds, s, U, I, rec, ptr, R,      \
                      block_rows, lr, lambda)
   switch (D) {
     case 16: FPS_TILED(4, 1); break;

@@ -139,8 +139,8 @@ class DistributedMF:
         tiled = self.sgd_mode == "tiled"
         if self.exchange == "local":
             if tiled:
-                ptr, u, row, r = self.tiler.run(uid_local, iid, rating)
-                ops.mf_sgd_tiled(self.U, self.I, u, row, r, ptr, 0, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+                ptr, rec = self.tiler.run(uid_local, iid, rating)
+                ops.mf_sgd_tiled(self.U, self.I, rec, ptr, 0, self.tile_T, self.tile_R, c.learning_rate, c.lam)
             elif grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
@@ -148,14 +148,16 @@ class DistributedMF:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
         elif self.exchange == "rotate":
             seen = self._seen if self.items.touched is not None else None
-            part = self.tiler if tiled else self.partitioner
-            ptr, u, row, r = part.run(uid_local, iid, rating, seen)
+            if tiled:
+                ptr, rec = self.tiler.run(uid_local, iid, rating, seen)
+            else:
+                ptr, u, row, r = self.partitioner.run(uid_local, iid, rating, seen)
             n = uid_local.numel()
             for _ in range(self.rot.K):
                 self.rot.begin()  # transfer of the next block overlaps this sub-step
                 b = self.rot.active_block()
                 if tiled:
-                    ops.mf_sgd_tiled(self.U, self.rot.active(), u, row, r, ptr, b, self.tile_T, self.tile_R,
+                    ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, b, self.tile_T, self.tile_R,
                                      c.learning_rate, c.lam)
                 else:
                     ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, b, n, c.learning_rate, c.lam,

@@ -267,7 +267,9 @@ def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
 class TilePartitioner:
     """Buckets a micro-batch's ratings by (item block, tile of ``R`` rows) for
     ``mf_sgd_tiled`` (``mf_tiled.hip``): 4 kernels, no global atomics, nothing
-    synchronised to the host.  ``run`` returns ``(ptr[2W*T+1], uid, row, rating)``."""
+    synchronised to the host.  ``run`` returns ``(ptr[2W*T+1], rec)`` with
+    ``rec`` an int32 ``[n, 4]`` array of packed records {uid, row-in-block,
+    rating bits, 0} grouped by bucket (on CPU: the three columns as tensors)."""
 
     def __init__(self, W: int, half, R: int, T: int, device):
         self.W, self.R, self.T = W, int(R), int(T)
@@ -284,7 +286,8 @@ class TilePartitioner:
         if self.device.type != "cuda":
             if seen is not None:
                 seen[iid.long()] = 1
-            return R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T)
+            ptr, u, row, r = R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T)
+            return ptr, (u, row, r)
         lib = N.require()
         n = uid.numel()
         G = lib.fps_tile_partition_groups(n)
@@ -293,26 +296,32 @@ class TilePartitioner:
             self.H = torch.empty(self.g_cap, dtype=torch.int32, device=self.device)
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
-            self.u_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
-            self.row_out = torch.empty(self.cap, dtype=torch.int32, device=self.device)
-            self.r_out = torch.empty(self.cap, dtype=torch.float32, device=self.device)
+            self.rec = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
                                        self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),
-                                       self.totals.data_ptr(), self.ptr.data_ptr(), self.u_out.data_ptr(),
-                                       self.row_out.data_ptr(), self.r_out.data_ptr(), N.ptr(seen),
-                                       N.stream_ptr(self.device)), "tile_partition")
-        return self.ptr, self.u_out[:n], self.row_out[:n], self.r_out[:n]
+                                       self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
+                                       N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
+        return self.ptr, self.rec[:n]
+
+    @staticmethod
+    def unpack(rec):
+        """(uid, row, rating) columns of packed records (tests / CPU)."""
+        if isinstance(rec, tuple):
+            return rec
+        return rec[:, 0], rec[:, 1], rec[:, 2].contiguous().view(torch.float32)
 
 
-def mf_sgd_tiled(U, I_block, uid, row, r, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
-    """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``)
-    with the block's rows staged in LDS per tile (no global item atomics)."""
+def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
+    """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
+    records from ``TilePartitioner``) with the block's rows staged in LDS per tile
+    (no global item atomics)."""
     if _on_gpu(U):
         lib = N.require()
-        N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(uid).data_ptr(),
-                                     _c(row).data_ptr(), _c(r).data_ptr(), _c(ptr).data_ptr() + 4 * block * T, T,
-                                     tile_rows, I_block.shape[0], U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
+        N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
+                                     _c(ptr).data_ptr() + 4 * block * T, T, tile_rows, I_block.shape[0], U.shape[1],
+                                     lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
         return
+    uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
     R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
 
