@@ -1,30 +1,33 @@
-// LDS-tiled MF SGD (gfx950): item rows live in LDS, no global item atomics.
+// Tile-grouped MF SGD (gfx950): no global item atomics, no LDS float atomics.
 //
 // Why: the flat kernel (mf.hip) pushes every rating's item delta with a
 // 256-B global float-atomic wave-instruction; those execute at the memory
 // side at ~1.3 TB/s chip-wide (MI355X_MICROARCH.md "Global float atomics"),
-// so a rating costs >= 256 B / 1.3 TB/s of atomic time on top of its 768 B
-// of plain traffic -- the measured 3.9e9 ratings/s sits on that ceiling
-// (profiles/README.md).  Here the item table (or the rotating item block,
-// parallel/rotation.py) is cut into tiles of R rows; the ratings of a
-// micro-batch are bucketed by tile (tile_partition below); one workgroup loads
-// its tile into LDS (R x D fp32, 32 KiB at R = 128, D = 64), runs the SGD of
-// every rating of the tile with the item row read from LDS and the item delta
-// added with LDS float atomics (ds_add_f32, exact), and writes the tile back
-// once.  Global traffic per rating: user row read + write (512 B) + 12 B of
-// rating; the item table moves twice per micro-batch.
+// so the measured 3.9e9 ratings/s sits on that ceiling (profiles/README.md).
+// Staging the item rows in LDS and adding with ds_add_f32 instead was slower
+// still: SQ_LDS_IDX_ACTIVE showed the LDS busy for the whole kernel, ~3 LDS
+// cycles per float atomic lane (profiles/r1_tiled_lds_atomics.md).
 //
-// Semantics are those of the flat kernel: every rating reads the item row as
-// it is at that moment and its delta is added atomically; user rows are
-// updated Hogwild (plain store) -- M/matrix/factorization/workers/
-// PSOnlineMatrixFactorizationWorker.scala:41-55 with the PS add of
-// M/matrix/factorization/PSOnlineMatrixFactorization.scala:58-60.
+// This kernel: the ratings of a micro-batch are bucketed by tile of R item rows
+// (tile_partition below, no global atomics); one workgroup takes one tile,
+// stages up to CAP of its rating records in LDS, counting-sorts them by row
+// (one LDS int atomic per rating), and gives every row to ONE lane group.  The
+// lane group reads the item row once into registers, streams the row's ratings
+// with PF user rows in flight, updates each user row (plain store) against the
+// row's value at the start of the chunk, sums the item deltas in registers and
+// writes the row back once with a plain store.  Global traffic per rating:
+// user row read + write (512 B) + 16 B record; per item row and chunk: 512 B.
 //
-// Lane layout: TPR lanes per rating, each holding V float4 of the rows
-// (D = 4 * TPR * V; D = 64 -> 16 lanes x 1 float4, 4 ratings per wave
-// instruction, UNR = 4 in flight per lane group = 16 user rows per wave).
-// LDS row stride = D floats (no padding): a ds_read_b128 lane group then
-// covers each row's 64 banks exactly once (MI355X_MICROARCH.md "LDS").
+// Semantics: inside one chunk (<= CAP ratings of a tile) an item's ratings see
+// the item as of the chunk start and their deltas are summed -- the per-item
+// mini-batch the PS path has (rows pulled once per micro-batch, deltas summed
+// and pushed: M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-55,
+// PS add M/matrix/factorization/PSOnlineMatrixFactorization.scala:58-60).
+// User rows are Hogwild across workgroups, as in the flat kernel.
+//
+// Lane layout: TPR lanes per rating / row, each holding V float4 (D = 4*TPR*V;
+// D = 64 -> 16 lanes x 1 float4: every row access is one 256-B coalesced
+// wave-quarter).
 #include "common.h"
 
 using namespace fps;
@@ -125,97 +128,101 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
 }
 
 // ---------------------------------------------------------------- SGD
-template <int TPR, int V, int UNR>
-__global__ void __launch_bounds__(512) mf_sgd_tiled_kernel(float* __restrict__ U, float* __restrict__ I,
-                                                           const int4* __restrict__ rec,
-                                                           const int32_t* __restrict__ ptr, int R,
-                                                           int64_t block_rows, float lr, float lambda) {
-  extern __shared__ float4 tile[];
-  constexpr int D4 = TPR * V;  // float4 per row
-  constexpr int RPW = 64 / TPR;
+constexpr int TG_CAP = 4096;    // records staged per chunk (64 KiB of LDS)
+constexpr int TG_MAX_R = 256;   // rows per tile
+
+template <int TPR, int V, int PF>
+__global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
+                                                               const int4* __restrict__ rec,
+                                                               const int32_t* __restrict__ ptr, int R,
+                                                               int64_t block_rows, float lr, float lambda) {
+  __shared__ int4 srec[TG_CAP];
+  __shared__ int16_t order[TG_CAP];
+  __shared__ int32_t cnt[TG_MAX_R + 1];
+  __shared__ int32_t start[TG_MAX_R + 1];
+  constexpr int D4 = TPR * V;
+  constexpr int GPW = 64 / TPR;  // lane groups per wave
   const int t = blockIdx.x;
   const int64_t r0 = (int64_t)t * R;
   const int nr = (int)min((int64_t)R, block_rows - r0);
-  float4* Ig = reinterpret_cast<float4*>(I) + r0 * D4;
-  {  // tile load: all of a thread's loads in flight before its LDS writes
-    constexpr int LPT = 8;  // float4 per thread per round (<= 64 KiB tiles at 512 threads)
-    const int tot = nr * D4;
-    for (int x0 = threadIdx.x; x0 < tot; x0 += blockDim.x * LPT) {
-      float4 v[LPT];
-#pragma unroll
-      for (int k = 0; k < LPT; ++k) {
-        const int x = x0 + k * blockDim.x;
-        if (x < tot) v[k] = Ig[x];
-      }
-#pragma unroll
-      for (int k = 0; k < LPT; ++k) {
-        const int x = x0 + k * blockDim.x;
-        if (x < tot) tile[x] = v[k];
-      }
-    }
-  }
-  __syncthreads();
   const int32_t beg = ptr[t], end = ptr[t + 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int g = lane / TPR, j = lane % TPR;
-  const int stride = nw * RPW;
-  const float4* Ug = reinterpret_cast<const float4*>(U);
-  // records of the first round; every load is unconditional (index clamped to
-  // the segment) so the UNR loads issue back to back
-  int4 cur[UNR];
-  int32_t base = beg + wave * RPW + g;
-  const int32_t last = end - 1;  // records are only read when the tile has ratings (beg < end)
-  if (beg < end) {
-#pragma unroll
-    for (int q = 0; q < UNR; ++q) cur[q] = rec[min(base + q * stride, last)];
-  }
-  for (; base < end; base += stride * UNR) {
-    int4 nxt[UNR];
-#pragma unroll
-    for (int q = 0; q < UNR; ++q)  // prefetch the next round's records
-      nxt[q] = rec[min(base + (UNR + q) * stride, last)];
-    float4 uv[UNR][V], iv[UNR][V];
-#pragma unroll
-    for (int q = 0; q < UNR; ++q) {
-      const int64_t ur = (int64_t)cur[q].x * D4;
-      const int tr = (int)(cur[q].y - r0) * D4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ngroups = (blockDim.x >> 6) * GPW;
+  const int grp = wave * GPW + lane / TPR, j = lane % TPR;
+  float4* Ig = reinterpret_cast<float4*>(I) + r0 * D4;
+  float4* Ug = reinterpret_cast<float4*>(U);
+  for (int32_t c0 = beg; c0 < end; c0 += TG_CAP) {
+    const int nc = min(TG_CAP, end - c0);
+    for (int k = threadIdx.x; k <= nr; k += blockDim.x) cnt[k] = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < nc; k += blockDim.x) {
+      const int4 x = rec[c0 + k];
+      srec[k] = x;
+      atomicAdd(cnt + (x.y - (int32_t)r0), 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan of <= 256 counters
+      int32_t run = 0;
+      for (int k = 0; k < nr; ++k) { start[k] = run; run += cnt[k]; cnt[k] = start[k]; }
+      start[nr] = run;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nc; k += blockDim.x) order[atomicAdd(cnt + (srec[k].y - (int32_t)r0), 1)] = (int16_t)k;
+    __syncthreads();
+    for (int row = grp; row < nr; row += ngroups) {
+      const int a = start[row], b = start[row + 1];
+      if (a == b) continue;  // uniform in the lane group
+      float4 iv[V], acc[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        uv[q][v] = Ug[ur + j + v * TPR];
-        iv[q][v] = tile[tr + j + v * TPR];
+        iv[v] = Ig[(int64_t)row * D4 + j + v * TPR];
+        acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-    }
+      for (int k0 = a; k0 < b; k0 += PF) {
+        float4 uv[PF][V];
+        int64_t ur[PF];
+        float rv[PF];
 #pragma unroll
-    for (int q = 0; q < UNR; ++q) {
-      float p = 0.f;
+        for (int q = 0; q < PF; ++q) {  // all PF user rows in flight (index clamped, result masked)
+          const int4 x = srec[order[min(k0 + q, b - 1)]];
+          ur[q] = (int64_t)x.x * D4;
+          rv[q] = __int_as_float(x.z);
 #pragma unroll
-      for (int v = 0; v < V; ++v)
-        p += uv[q][v].x * iv[q][v].x + uv[q][v].y * iv[q][v].y + uv[q][v].z * iv[q][v].z + uv[q][v].w * iv[q][v].w;
-      const float e = __int_as_float(cur[q].z) - group_sum<TPR>(p);
-      if (base + q * stride >= end) continue;  // uniform in the lane group
-      const int64_t ur = (int64_t)cur[q].x * D4;
-      const int tr = (int)(cur[q].y - r0) * D4;
+          for (int v = 0; v < V; ++v) uv[q][v] = Ug[ur[q] + j + v * TPR];
+        }
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          float p = 0.f;
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+            p += uv[q][v].x * iv[v].x + uv[q][v].y * iv[v].y + uv[q][v].z * iv[v].z + uv[q][v].w * iv[v].w;
+          const float e = rv[q] - group_sum<TPR>(p);
+          if (k0 + q >= b) continue;  // uniform in the lane group
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            const float4 u = uv[q][v], i = iv[v];
+            float4 nu;
+            nu.x = u.x + lr * (e * i.x - lambda * u.x);
+            nu.y = u.y + lr * (e * i.y - lambda * u.y);
+            nu.z = u.z + lr * (e * i.z - lambda * u.z);
+            nu.w = u.w + lr * (e * i.w - lambda * u.w);
+            Ug[ur[q] + j + v * TPR] = nu;
+            acc[v].x += lr * (e * u.x - lambda * i.x);
+            acc[v].y += lr * (e * u.y - lambda * i.y);
+            acc[v].z += lr * (e * u.z - lambda * i.z);
+            acc[v].w += lr * (e * u.w - lambda * i.w);
+          }
+        }
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        const float4 u = uv[q][v], i = iv[q][v];
-        float4 nu;
-        nu.x = u.x + lr * (e * i.x - lambda * u.x);
-        nu.y = u.y + lr * (e * i.y - lambda * u.y);
-        nu.z = u.z + lr * (e * i.z - lambda * u.z);
-        nu.w = u.w + lr * (e * i.w - lambda * u.w);
-        reinterpret_cast<float4*>(U)[ur + j + v * TPR] = nu;
-        float* ti = reinterpret_cast<float*>(tile + tr + j + v * TPR);
-        atomicAdd(ti + 0, lr * (e * u.x - lambda * i.x));
-        atomicAdd(ti + 1, lr * (e * u.y - lambda * i.y));
-        atomicAdd(ti + 2, lr * (e * u.z - lambda * i.z));
-        atomicAdd(ti + 3, lr * (e * u.w - lambda * i.w));
+        float4 o = iv[v];
+        o.x += acc[v].x; o.y += acc[v].y; o.z += acc[v].z; o.w += acc[v].w;
+        Ig[(int64_t)row * D4 + j + v * TPR] = o;
       }
     }
-#pragma unroll
-    for (int q = 0; q < UNR; ++q) cur[q] = nxt[q];
+    __syncthreads();  // LDS reused by the next chunk
   }
-  __syncthreads();
-  for (int x = threadIdx.x; x < nr * D4; x += blockDim.x) Ig[x] = tile[x];
 }
 
 }  // namespace
@@ -247,17 +254,16 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   return 0;
 }
 
-// One launch per block: T tiles of R rows of I[block_rows, D]; ptr = the
-// block's T+1 tile offsets (device).  D must be 16, 32, 64, 128 or 256.
+// One launch per item block: T tiles of R (<= 256) rows of I[block_rows, D];
+// ptr = the block's T+1 tile offsets (device).  D must be 16, 32, 64, 128 or 256.
 FPS_API int fps_mf_sgd_tiled(float* U, float* I, const int4* rec, const int32_t* ptr, int T, int R,
                              int64_t block_rows, int D, float lr, float lambda, void* stream) {
   if (T <= 0) return 0;
+  if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const size_t lds = (size_t)R * D * sizeof(float);
-  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  constexpr int UNR = 4;
-#define FPS_TILED(TPR_, V_)                                                                                      \
-  hipLaunchKernelGGL((mf_sgd_tiled_kernel<TPR_, V_, UNR>), dim3(T), dim3(512), lds, s, U, I, rec, ptr, R,      \
+  constexpr int PF = 8;
+#define FPS_TILED(TPR_, V_)                                                                                    \
+  hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF>), dim3(T), dim3(512), 0, s, U, I, rec, ptr, R,   \
                      block_rows, lr, lambda)
   switch (D) {
     case 16: FPS_TILED(4, 1); break;

@@ -94,8 +94,9 @@ class DistributedMF:
         #            atomics (atomic-rate bound: 3.9e9 ratings/s, profiles/README.md);
         #  "grouped" ratings sorted by item, each item row updated in registers
         #            (exact per-item order; latency bound, 2.8e9/s).
-        block_rows = cfg.num_items if exchange == "local" else max(block_rows_of(cfg.num_items, W))
+        # local: the table as 2 blocks (halves) of one shard; rotate: 2W blocks
         tile_w = 1 if exchange == "local" else W
+        block_rows = max(block_rows_of(cfg.num_items, tile_w))
         tile_R = ops.tile_rows_for(cfg.dim, block_rows, tile_w)
         mode = cfg.sgd_mode
         if mode == "auto":
@@ -110,8 +111,9 @@ class DistributedMF:
         if mode == "tiled":
             self.tile_R = tile_R
             self.tile_T = -(-block_rows // tile_R)
-            half = [cfg.num_items] if exchange == "local" else shard_halves(cfg.num_items, W)
-            self.tiler = ops.TilePartitioner(tile_w, half, tile_R, self.tile_T, dev)
+            self.tiler = ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T, dev)
+            h0 = shard_halves(cfg.num_items, 1)[0]
+            self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
         if self.exchange == "rotate":
             self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
             self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
@@ -140,7 +142,8 @@ class DistributedMF:
         if self.exchange == "local":
             if tiled:
                 ptr, rec = self.tiler.run(uid_local, iid, rating)
-                ops.mf_sgd_tiled(self.U, self.I, rec, ptr, 0, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+                for b, blk in enumerate(self._local_blocks):
+                    ops.mf_sgd_tiled(self.U, blk, rec, ptr, b, self.tile_T, self.tile_R, c.learning_rate, c.lam)
             elif grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)

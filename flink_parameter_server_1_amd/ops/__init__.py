@@ -245,21 +245,19 @@ TILE_MAX_BUCKETS = 16384
 
 
 def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
-    """Rows per LDS tile for blocks of ``block_rows``: 32 KiB tiles (R = 128 at
-    D = 64), halved while a block gives fewer than ~1k workgroups (small
-    rotation blocks at N = 8), grown while the 2W*T buckets exceed the LDS
-    counters.  None if no tile size fits (then use the flat kernel)."""
+    """Rows per tile for blocks of ``block_rows``: the smallest power of two
+    >= 32 whose 2W*T tile buckets fit the partition's LDS counters (R = 64 for
+    1M items at W = 1..8: ~2k ratings per tile at 32M ratings per step, inside
+    one 4096-record LDS chunk).  None if no tile size <= 256 fits (then use the
+    flat kernel)."""
     if dim not in TILED_DIMS:
         return None
-    r_max = min(256, 65536 // (4 * dim))
-    r = min(r_max, max(16, 32768 // (4 * dim)))
 
     def kt(rr):
         return 2 * W * -(-block_rows // rr)
 
-    while r > 32 and -(-block_rows // r) < 1024 and kt(r // 2) <= TILE_MAX_BUCKETS:
-        r //= 2
-    while kt(r) > TILE_MAX_BUCKETS and r < r_max:
+    r = 32
+    while kt(r) > TILE_MAX_BUCKETS and r < 256:
         r *= 2
     return r if kt(r) <= TILE_MAX_BUCKETS else None
 
@@ -313,8 +311,8 @@ class TilePartitioner:
 
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
-    records from ``TilePartitioner``) with the block's rows staged in LDS per tile
-    (no global item atomics)."""
+    records from ``TilePartitioner``): one workgroup per tile, every item row owned
+    by one lane group (registers), item deltas summed per row -- no item atomics."""
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
