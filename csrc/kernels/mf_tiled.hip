@@ -227,11 +227,17 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
 
 }  // namespace
 
+// Ratings per partition workgroup: longer chunks give longer runs per bucket in
+// the scatter (chunk / KT records land contiguously), fewer give more parallelism.
+static int64_t g_tp_chunk = 65536;
+
+FPS_API void fps_tile_partition_set_chunk(int64_t chunk) { g_tp_chunk = chunk > 1024 ? chunk : 1024; }
+
 // Workspace: H holds G * KT int32 (G = fps_tile_partition_groups(n)), totals KT.
 FPS_API int fps_tile_partition_groups(int64_t n) {
-  int64_t g = (n + 65535) / 65536;  // >= 64 Ki ratings per workgroup
+  int64_t g = (n + g_tp_chunk - 1) / g_tp_chunk;
   if (g < 1) g = 1;
-  if (g > 512) g = 512;
+  if (g > 1024) g = 1024;
   return (int)g;
 }
 

@@ -7,6 +7,7 @@ fallback on a GPU box).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -272,6 +273,9 @@ class TilePartitioner:
     def __init__(self, W: int, half, R: int, T: int, device):
         self.W, self.R, self.T = W, int(R), int(T)
         self.KT = 2 * W * self.T
+        chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
+        if chunk and self.device_is_cuda(device):
+            N.require().fps_tile_partition_set_chunk(int(chunk))
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
@@ -300,6 +304,10 @@ class TilePartitioner:
                                        self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
                                        N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]
+
+    @staticmethod
+    def device_is_cuda(device) -> bool:
+        return torch.device(device).type == "cuda"
 
     @staticmethod
     def unpack(rec):
