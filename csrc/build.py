@@ -96,11 +96,31 @@ def build_host(force: bool = False, verbose: bool = True) -> str:
     return target
 
 
+def asan_selftest(workdir: str = "/tmp", verbose: bool = True) -> int:
+    """Build the host runtime + ``csrc/tests/host_selftest.cpp`` with ASan/UBSan
+    (host code only -- GPU sanitizers are not available) and run it; returns its
+    exit code."""
+    cxx = os.environ.get("CXX", "g++")
+    exe = os.path.join(workdir, "fps_host_selftest_asan")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))) + [os.path.join(CSRC, "tests", "host_selftest.cpp")]
+    cmd = [cxx, "-O1", "-g", "-std=c++17", "-pthread", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+           "-fno-sanitize-recover=undefined", "-I", os.path.join(CSRC, "host")] + srcs + ["-o", exe]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    return subprocess.run([exe, workdir], env=env).returncode
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["kernels", "host"])
+    ap.add_argument("--asan-selftest", action="store_true",
+                    help="build + run the host runtime self-test under ASan/UBSan, then exit")
     a = ap.parse_args(argv)
+    if a.asan_selftest:
+        return asan_selftest()
     if a.only in (None, "kernels"):
         print(build_kernels(a.force))
     if a.only in (None, "host"):

@@ -19,6 +19,7 @@
 #include <cerrno>
 #include <charconv>
 #include <cmath>
+#include <climits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -271,7 +272,11 @@ struct HashStore {
   float lo, hi;
   uint32_t seed;
   int64_t size = 0;
-  std::vector<int64_t> keys;   // -1 empty
+  // empty slot marker: INT64_MIN (ids are any other int64, negative ones
+  // included -- the reference's Int ids may be negative, only the
+  // partitioner takes |id|, M/FlinkParameterServer.scala:355-366)
+  static constexpr int64_t kEmpty = INT64_MIN;
+  std::vector<int64_t> keys;
   std::vector<float> vals;
   std::mutex mu;
 
@@ -282,11 +287,11 @@ struct HashStore {
     while (c < cap * 2) c <<= 1;
     std::vector<int64_t> ok = std::move(keys);
     std::vector<float> ov = std::move(vals);
-    keys.assign((size_t)c, -1);
+    keys.assign((size_t)c, kEmpty);
     vals.assign((size_t)c * dim, 0.f);
     size = 0;
     for (size_t i = 0; i < ok.size(); ++i)
-      if (ok[i] >= 0) std::memcpy(&vals[(size_t)slot_insert(ok[i]) * dim], &ov[i * dim], sizeof(float) * dim);
+      if (ok[i] != kEmpty) std::memcpy(&vals[(size_t)slot_insert(ok[i]) * dim], &ov[i * dim], sizeof(float) * dim);
   }
 
   int64_t mask() const { return (int64_t)keys.size() - 1; }
@@ -295,7 +300,7 @@ struct HashStore {
     int64_t i = (int64_t)(fmix32((uint32_t)k ^ fmix32((uint32_t)((uint64_t)k >> 32))) & mask());
     while (true) {
       if (keys[i] == k) return i;
-      if (keys[i] < 0) return -1;
+      if (keys[i] == kEmpty) return -1;
       i = (i + 1) & mask();
     }
   }
@@ -303,8 +308,8 @@ struct HashStore {
   int64_t slot_insert(int64_t k) {
     if ((size + 1) * 2 > (int64_t)keys.size()) rehash(size + 1);
     int64_t i = (int64_t)(fmix32((uint32_t)k ^ fmix32((uint32_t)((uint64_t)k >> 32))) & mask());
-    while (keys[i] >= 0 && keys[i] != k) i = (i + 1) & mask();
-    if (keys[i] < 0) { keys[i] = k; ++size; }
+    while (keys[i] != kEmpty && keys[i] != k) i = (i + 1) & mask();
+    if (keys[i] == kEmpty) { keys[i] = k; ++size; }
     return i;
   }
 
@@ -357,7 +362,7 @@ FPS_HOST_API int64_t fps_hs_dump(void* h, int64_t* keys, float* vals, int64_t ca
   std::lock_guard<std::mutex> g(s->mu);
   int64_t n = 0;
   for (size_t i = 0; i < s->keys.size() && n < cap; ++i) {
-    if (s->keys[i] < 0) continue;
+    if (s->keys[i] == HashStore::kEmpty) continue;
     keys[n] = s->keys[i];
     std::memcpy(vals + n * s->dim, &s->vals[i * s->dim], sizeof(float) * s->dim);
     ++n;

@@ -293,13 +293,52 @@ def build_parser():
     p.add_argument("--tokens", type=int, default=1 << 20)
     p.add_argument("--batch", type=int, default=1 << 16)
 
+    p = sub.add_parser("split-log", help="31-day train / 14-day test split (Data_Manipulation notebook)")
+    p.add_argument("--input", required=True)
+    p.add_argument("--train-out", required=True)
+    p.add_argument("--test-out", required=True)
+    p.add_argument("--train-days", type=float, default=31)
+    p.add_argument("--test-days", type=float, default=14)
+
+    p = sub.add_parser("eval-factors", help="top-k recall/precision of dumped factors (Tester notebook)")
+    p.add_argument("--users", required=True)
+    p.add_argument("--items", required=True)
+    p.add_argument("--test", required=True)
+    p.add_argument("--train")
+    p.add_argument("--k", type=int, default=5)
+
     p = sub.add_parser("bench")
     p.add_argument("rest", nargs=argparse.REMAINDER)
+    ap.add_argument("--log-level", default=None, help="package log level (default FPS_LOG_LEVEL or WARNING)")
+    ap.add_argument("--log-messages", action="store_true",
+                    help="DEBUG line per record / pull answer / PS message (the reference main-jar logging)")
     return ap
+
+
+def cmd_split_log(args):
+    from .utils.eval_tools import split_log_file
+
+    n_tr, n_te = split_log_file(args.input, args.train_out, args.test_out, args.train_days, args.test_days)
+    print(json.dumps({"train": n_tr, "test": n_te}))
+    return 0
+
+
+def cmd_eval_factors(args):
+    from .utils.eval_tools import evaluate_factor_files
+
+    print(json.dumps(evaluate_factor_files(args.users, args.items, args.test, args.k, args.train)))
+    return 0
 
 
 def main(argv=None):
     args = build_parser().parse_args(argv)
+    from .utils import logs
+
+    logs.configure(args.log_level, True if args.log_messages else None)
+    if args.cmd == "split-log":
+        return cmd_split_log(args)
+    if args.cmd == "eval-factors":
+        return cmd_eval_factors(args)
     if args.cmd in ("mf-online", "mf-offline"):
         return cmd_mf(args, offline=args.cmd == "mf-offline")
     if args.cmd == "mf-gpu":

@@ -36,6 +36,7 @@ from typing import Any, Callable, Iterable, List, Optional, Sequence
 
 from ..api.logic import ParameterServer, ParameterServerClient, ParameterServerLogic, RuntimeContext, WorkerLogic
 from ..ps.logics import SimplePSLogic
+from ..utils.logs import message_tracing, trace_message
 from .adapters import SimplePSReceiver, SimplePSSender, SimpleWorkerReceiver, SimpleWorkerSender
 from .messages import Left, PSToWorker, Right, WorkerToPS
 from .partitioners import hash_partition
@@ -93,12 +94,16 @@ class WorkerTask:
         self.engine.route_to_ps(msg)
 
     def handle_answer(self, wire_msg):
+        if message_tracing():  # M/FlinkParameterServer.scala:247 (debug per pull answer)
+            trace_message("worker <- ps", self.index, wire_msg)
         if self._on_answer is None:
             logic, client = self.logic, self.client
             self._on_answer = lambda pa: logic.on_pull_recv(pa.param_id, pa.param, client)
         self.receiver.on_pull_answer_recv(wire_msg, self._on_answer)
 
     def handle_data(self, rec):
+        if message_tracing():  # M/FlinkParameterServer.scala:237 (debug per data record)
+            trace_message("worker <- data", self.index, rec)
         self.logic.on_recv(rec, self.client)
 
 
@@ -119,6 +124,8 @@ class PSTask:
         self.engine.route_to_worker(msg)
 
     def handle_msg(self, wire_msg):
+        if message_tracing():  # M/FlinkParameterServer.scala:284 (debug per PS message)
+            trace_message("ps <- worker", self.index, wire_msg)
         self.receiver.on_worker_msg(wire_msg, self._on_pull, self._on_push)
 
 
@@ -332,6 +339,9 @@ class LocalRuntime:
             t.logic.close(t.handle)
         for t in list(self.workers.values()) + list(self.servers.values()):
             t.sender.close()
+        close = getattr(self.output_sink, "close", None)
+        if callable(close):  # a Flink sink's close(): may end the job (utils.testing.SuccessException)
+            close()
 
 
 # ---------------------------------------------------------------------------

@@ -138,6 +138,9 @@ class DistributedMF:
         c = self.cfg
         grouped = self.sgd_mode == "grouped"
         uid_local, iid, rating = uid_local.contiguous(), iid.contiguous(), rating.contiguous()
+        if ops.DEBUG:  # FPS_DEBUG=1: range checks before any kernel sees the batch
+            ops.check_index(uid_local, self.users.n_local, "MF step uid_local")
+            ops.check_index(iid, c.num_items, "MF step iid")
         tiled = self.sgd_mode == "tiled"
         if self.exchange == "local":
             if tiled:
@@ -177,6 +180,12 @@ class DistributedMF:
             rows, plan = self.ps.pull(iid)
             self._compute_push(rows, plan, uid_local, rating)
         self.updates += uid_local.numel()
+        if ops.DEBUG:  # FactorIsNotANumberException, M/matrix/factorization/utils/Vector.scala:78-80
+            from .core import FactorIsNotANumberException
+
+            ops.check_finite(self.U, "user factors", FactorIsNotANumberException)
+            if self.exchange != "rotate":
+                ops.check_finite(self.I, "item factors", FactorIsNotANumberException)
 
     def _finish(self, pending):
         (rows, work, plan), uid_local, rating = pending

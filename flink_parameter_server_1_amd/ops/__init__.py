@@ -26,6 +26,28 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+#: debug mode: ``FPS_DEBUG=1`` range-checks every index tensor on
+#: the host before a kernel launch (a device fault becomes a Python exception
+#: naming the op) and lets models check their tables for NaN/inf after a step.
+#: Costs a device sync per check; pair with ``HIP_LAUNCH_BLOCKING=1`` to pin a
+#: fault to its launch.
+DEBUG = os.environ.get("FPS_DEBUG", "0") == "1"
+
+
+def check_index(idx: torch.Tensor, upper: int, what: str, allow_negative: bool = False) -> None:
+    """Raise IndexError unless every entry lies in ``[0, upper)`` (negative allowed as padding)."""
+    if idx.numel() == 0:
+        return
+    lo, hi = int(idx.min()), int(idx.max())
+    if hi >= upper or (lo < 0 and not allow_negative):
+        raise IndexError(f"{what}: index range [{lo}, {hi}] outside [0, {upper})")
+
+
+def check_finite(t: torch.Tensor, what: str, exc=FloatingPointError) -> None:
+    if not bool(torch.isfinite(t).all()):
+        raise exc(f"{what}: non-finite values")
+
+
 def _c(t):
     if not t.is_contiguous():
         raise ValueError("kernel inputs must be contiguous")
@@ -48,6 +70,8 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None
                 touched: torch.Tensor = None) -> torch.Tensor:
     """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2)."""
     n = idx.numel()
+    if DEBUG:
+        check_index(idx, table.shape[0], "gather_rows")
     d = table.shape[1]
     if out is None:
         out = torch.empty((n, d), dtype=out_dtype, device=table.device)
@@ -65,6 +89,9 @@ def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: 
                eps: float = 1e-10, state: torch.Tensor = None, touched: torch.Tensor = None) -> torch.Tensor:
     """Push apply (K3): ``add`` (atomic), ``set``, ``sgd`` (w -= lr*g, atomic),
     ``adagrad`` (unique idx).  ``idx < 0`` marks padding rows."""
+    if DEBUG:
+        check_index(idx, table.shape[0], "apply_rows", allow_negative=True)
+        check_finite(delta.float(), "apply_rows delta")
     n = idx.numel()
     d = table.shape[1]
     if _on_gpu(table):
@@ -163,6 +190,9 @@ def bucketize(keys: torch.Tensor, W: int, part_kind: int = 0, block: int = 1):
 
 def mf_sgd_local(U, I, uid, iid, r, lr: float, lam: float = 0.0, user_atomic: bool = False):
     """Fused MF SGD step with the item shard local (pull = read, push = atomic add) (K4)."""
+    if DEBUG:
+        check_index(uid, U.shape[0], "mf_sgd_local uid")
+        check_index(iid, I.shape[0], "mf_sgd_local iid")
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_local(_c(U).data_ptr(), _c(I).data_ptr(), _c(uid).data_ptr(), _c(iid).data_ptr(),
@@ -174,6 +204,9 @@ def mf_sgd_local(U, I, uid, iid, r, lr: float, lam: float = 0.0, user_atomic: bo
 
 def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr: float, lam: float = 0.0, user_atomic: bool = False):
     """MF SGD on pulled item rows; item deltas accumulate into ``delta[pos]`` (K4)."""
+    if DEBUG:
+        check_index(uid, U.shape[0], "mf_sgd_pulled uid")
+        check_index(pos, rows.shape[0], "mf_sgd_pulled pos")
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_pulled(_c(U).data_ptr(), _c(uid).data_ptr(), _c(r).data_ptr(), _c(rows).data_ptr(),

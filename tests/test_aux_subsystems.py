@@ -1,0 +1,149 @@
+"""Aux subsystems: success harness (C50), logging (C57), notebook tools (C55), debug mode (§5.2)."""
+import io
+import logging
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from flink_parameter_server_1_amd import LocalRuntime, transform
+from flink_parameter_server_1_amd.api.logic import WorkerLogic
+from flink_parameter_server_1_amd.utils import eval_tools, logs
+from flink_parameter_server_1_amd.utils.io import write_factors_text
+from flink_parameter_server_1_amd.utils.testing import (CollectingSuccessSink, SuccessException,
+                                                        execute_with_success_check)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _PullEach(WorkerLogic):
+    def on_recv(self, data, ps):
+        ps.pull(data)
+
+    def on_pull_recv(self, param_id, value, ps):
+        ps.output((param_id, value))
+
+
+def _job(sink):
+    return lambda: transform(list(range(20)), _PullEach(), param_init=lambda i: float(i) * 2,
+                             param_update=lambda a, b: a + b, worker_parallelism=2, ps_parallelism=2,
+                             runtime=LocalRuntime(output_sink=sink))
+
+
+def test_success_exception_harness_unwraps_and_checks():
+    seen = {}
+
+    def check(result):
+        left = sorted(e.value for e in result if e.is_left)
+        seen["n"] = len(left)
+        assert left == [(i, 2.0 * i) for i in range(20)]
+
+    res = execute_with_success_check(_job(CollectingSuccessSink()), check)
+    assert seen["n"] == 20 and len(res) >= 20
+
+
+def test_success_harness_wrapped_cause_and_failure_modes():
+    def wrapped():
+        try:
+            raise SuccessException(42)
+        except SuccessException as e:
+            raise RuntimeError("job execution failed") from e
+
+    assert execute_with_success_check(wrapped) == 42
+    with pytest.raises(AssertionError):
+        execute_with_success_check(lambda: None)
+    with pytest.raises(ValueError):
+        execute_with_success_check(lambda: (_ for _ in ()).throw(ValueError("boom")))
+
+
+def test_per_message_debug_logging():
+    buf = io.StringIO()
+    logs.configure("DEBUG", messages=True, stream=buf)
+    try:
+        for h in logging.getLogger(logs.ROOT).handlers:
+            if getattr(h, "_fps", False):
+                h.stream = buf
+        transform(list(range(3)), _PullEach(), param_init=lambda i: 0.0, param_update=lambda a, b: a + b,
+                  worker_parallelism=1, ps_parallelism=1)
+    finally:
+        logs.configure("WARNING", messages=False)
+    text = buf.getvalue()
+    assert "worker <- data" in text and "ps <- worker" in text and "worker <- ps" in text
+
+
+def test_split_and_evaluate_factor_files(tmp_path):
+    # 60 days of a log: users like item (user % 7); train = first 31 days, test = next 14
+    rng = np.random.default_rng(0)
+    lines = []
+    for d in range(60):
+        for u in range(30):
+            lines.append(f"{d * 86400 + int(rng.integers(0, 86400))} {u} {u % 7} 1")
+    log = tmp_path / "log.txt"
+    log.write_text("\n".join(lines) + "\n")
+    n_tr, n_te = eval_tools.split_log_file(str(log), str(tmp_path / "tr"), str(tmp_path / "te"))
+    assert n_tr == 31 * 30 and n_te == 14 * 30
+    # factors that rank item u % 7 first for user u
+    users = np.eye(7)[np.arange(30) % 7].astype(np.float32)
+    items = np.eye(7).astype(np.float32)
+    write_factors_text(str(tmp_path / "U.map"), np.arange(30), users)
+    write_factors_text(str(tmp_path / "I.map"), np.arange(7), items)
+    m = eval_tools.evaluate_factor_files(str(tmp_path / "U.map"), str(tmp_path / "I.map"), str(tmp_path / "te"), k=5)
+    assert m["recall"] == 1.0 and abs(m["precision"] - 0.2) < 1e-9 and m["users"] == 30
+
+
+def test_cli_split_and_eval(tmp_path):
+    log = tmp_path / "log.txt"
+    log.write_text("\n".join(f"{d * 86400} {d % 3} {d % 5} 1" for d in range(50)) + "\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "flink_parameter_server_1_amd", "split-log", "--input", str(log),
+                          "--train-out", str(tmp_path / "a"), "--test-out", str(tmp_path / "b")],
+                         capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert '"train": 31' in out.stdout and '"test": 14' in out.stdout
+
+
+def test_debug_mode_catches_bad_index_and_nan():
+    code = r"""
+import torch
+from flink_parameter_server_1_amd import ops
+from flink_parameter_server_1_amd.models.mf.core import FactorIsNotANumberException
+from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig
+assert ops.DEBUG
+m = DistributedMF(MFConfig(num_users=50, num_items=20, dim=4))
+try:
+    m.step(torch.tensor([0], dtype=torch.int32), torch.tensor([25], dtype=torch.int32), torch.tensor([1.0]))
+    raise SystemExit("no IndexError")
+except IndexError as e:
+    assert "iid" in str(e)
+try:
+    m.step(torch.tensor([0], dtype=torch.int32), torch.tensor([3], dtype=torch.int32), torch.tensor([float("nan")]))
+    raise SystemExit("no FactorIsNotANumberException")
+except FactorIsNotANumberException:
+    pass
+print("OK")
+"""
+    env = dict(os.environ, PYTHONPATH=ROOT, FPS_DEBUG="1")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0 and "OK" in out.stdout, out.stderr + out.stdout
+
+
+def test_host_runtime_asan_ubsan_selftest(tmp_path):
+    """Host C++ runtime under AddressSanitizer + UBSan (GPU sanitizers are unavailable)."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc"))
+    import build as native_build
+
+    assert native_build.asan_selftest(str(tmp_path), verbose=False) == 0
+
+
+def test_hash_store_negative_ids():
+    from flink_parameter_server_1_amd.utils import native_host
+
+    hs = native_host.HashStore(2, -1.0, 1.0, seed=1)
+    v = hs.pull([-5, 5, -5])
+    assert len(hs) == 2 and np.array_equal(v[0], v[2])
+    hs.push([-7], [[1.0, 2.0]])
+    ids, vals = hs.dump()
+    assert sorted(ids.tolist()) == [-7, -5, 5]
