@@ -61,6 +61,7 @@ class MFConfig:
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
+    prefetch_partition: bool = True   # tiled: bucket batch k+1 on a side stream during the SGD of k
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
 
@@ -111,7 +112,15 @@ class DistributedMF:
         if mode == "tiled":
             self.tile_R = tile_R
             self.tile_T = -(-block_rows // tile_R)
-            self.tiler = ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T, dev)
+            # two partition buffers: with prefetch the partition of batch k+1 runs on a
+            # side stream while batch k's SGD runs (one micro-batch of latency, flush()
+            # completes it; same SGD order)
+            self._tilers = [ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T,
+                                                dev) for _ in range(2)]
+            self._tiler_i = 0
+            self._prefetch = cfg.prefetch_partition and dev.type == "cuda"
+            self._side = torch.cuda.Stream(dev) if self._prefetch else None
+            self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
         if self.exchange == "rotate":
@@ -142,32 +151,31 @@ class DistributedMF:
             ops.check_index(uid_local, self.users.n_local, "MF step uid_local")
             ops.check_index(iid, c.num_items, "MF step iid")
         tiled = self.sgd_mode == "tiled"
-        if self.exchange == "local":
-            if tiled:
-                ptr, rec = self.tiler.run(uid_local, iid, rating)
-                for b, blk in enumerate(self._local_blocks):
-                    ops.mf_sgd_tiled(self.U, blk, rec, ptr, b, self.tile_T, self.tile_R, c.learning_rate, c.lam)
-            elif grouped:
+        if tiled:
+            # bucket this batch (side stream when prefetching) and run the SGD of
+            # the batch staged by the previous call: the partition of k+1 overlaps
+            # the SGD of k; the order of the SGD steps is unchanged
+            staged = self._stage_partition(uid_local, iid, rating)
+            if self._prefetch:
+                prev, self._staged = self._staged, staged
+                if prev is not None:
+                    self._tiled_sgd(prev)
+            else:
+                self._tiled_sgd(staged)
+        elif self.exchange == "local":
+            if grouped:
                 ptr, order = self.grouper.run(iid, self.items.n_local)
                 ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
             else:
                 ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
         elif self.exchange == "rotate":
             seen = self._seen if self.items.touched is not None else None
-            if tiled:
-                ptr, rec = self.tiler.run(uid_local, iid, rating, seen)
-            else:
-                ptr, u, row, r = self.partitioner.run(uid_local, iid, rating, seen)
+            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating, seen)
             n = uid_local.numel()
             for _ in range(self.rot.K):
                 self.rot.begin()  # transfer of the next block overlaps this sub-step
-                b = self.rot.active_block()
-                if tiled:
-                    ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, b, self.tile_T, self.tile_R,
-                                     c.learning_rate, c.lam)
-                else:
-                    ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, b, n, c.learning_rate, c.lam,
-                                         self.user_atomic)
+                ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
+                                     c.learning_rate, c.lam, self.user_atomic)
                 self.rot.end()
         elif self.pipeline:
             # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD
@@ -186,6 +194,40 @@ class DistributedMF:
             ops.check_finite(self.U, "user factors", FactorIsNotANumberException)
             if self.exchange != "rotate":
                 ops.check_finite(self.I, "item factors", FactorIsNotANumberException)
+
+    def _stage_partition(self, uid_local, iid, rating):
+        """Tile partition of one batch into the next of the two partition buffers;
+        returns ``(ptr, rec, ready_event)``."""
+        seen = self._seen if (self.exchange == "rotate" and self.items.touched is not None) else None
+        tiler = self._tilers[self._tiler_i]
+        self._tiler_i ^= 1
+        if self._side is None:
+            ptr, rec = tiler.run(uid_local, iid, rating, seen)
+            return ptr, rec, None
+        main = torch.cuda.current_stream(self.U.device)
+        self._side.wait_stream(main)  # inputs written, and this buffer's previous SGD done
+        with torch.cuda.stream(self._side):
+            ptr, rec = tiler.run(uid_local, iid, rating, seen)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        for t in (uid_local, iid, rating):
+            t.record_stream(self._side)
+        return ptr, rec, ev
+
+    def _tiled_sgd(self, staged):
+        c = self.cfg
+        ptr, rec, ev = staged
+        if ev is not None:
+            torch.cuda.current_stream(self.U.device).wait_event(ev)
+        if self.exchange == "local":
+            for b, blk in enumerate(self._local_blocks):
+                ops.mf_sgd_tiled(self.U, blk, rec, ptr, b, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+            return
+        for _ in range(self.rot.K):
+            self.rot.begin()  # transfer of the next block overlaps this sub-step
+            ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, self.rot.active_block(), self.tile_T,
+                             self.tile_R, c.learning_rate, c.lam)
+            self.rot.end()
 
     def _finish(self, pending):
         (rows, work, plan), uid_local, rating = pending
@@ -208,6 +250,9 @@ class DistributedMF:
     def flush(self):
         """Complete the in-flight micro-batch of the pipelined path / bring the
         rotating item blocks back to their PS shards."""
+        if self.sgd_mode == "tiled" and self._staged is not None:
+            staged, self._staged = self._staged, None
+            self._tiled_sgd(staged)
         if self.exchange == "rotate" and not self.rot.at_rest:
             self.rot.home()
             if self.items.touched is not None:
