@@ -279,21 +279,29 @@ TILE_MAX_BUCKETS = 16384
 
 
 def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
-    """Rows per tile for blocks of ``block_rows``: the smallest power of two
-    >= 32 whose 2W*T tile buckets fit the partition's LDS counters (R = 64 for
-    1M items at W = 1..8: ~2k ratings per tile at 32M ratings per step, inside
-    one 4096-record LDS chunk).  None if no tile size <= 256 fits (then use the
-    flat kernel)."""
+    """Rows per tile for blocks of ``block_rows``: the largest power of two <= 256
+    that still gives >= ~1k tiles (workgroups) per block, grown if the 2W*T tile
+    buckets exceed the partition's LDS counters.  Large tiles shorten the
+    partition (fewer buckets: longer scatter runs, smaller histograms; R = 256
+    beat 128 and 64 at N = 1, 64M ratings per step); small blocks (rotation at
+    N = 8) need small tiles to fill the GPU.  ``FPS_TILE_ROWS`` overrides.
+    None if no tile size fits (then use the flat kernel)."""
     if dim not in TILED_DIMS:
         return None
 
     def kt(rr):
         return 2 * W * -(-block_rows // rr)
 
-    r = 32
+    env = os.environ.get("FPS_TILE_ROWS")
+    if env:
+        r = max(32, int(env))
+    else:
+        r = 256
+        while r > 32 and -(-block_rows // r) < 960:
+            r //= 2
     while kt(r) > TILE_MAX_BUCKETS and r < 256:
         r *= 2
-    return r if kt(r) <= TILE_MAX_BUCKETS else None
+    return r if kt(r) <= TILE_MAX_BUCKETS and r <= 256 else None
 
 
 class TilePartitioner:
