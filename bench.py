@@ -10,8 +10,10 @@ At N > 1 the default exchange is the item-block ring rotation
 (``--exchange rotate``, ``parallel/rotation.py``): the 1M x 64 item table
 travels around the xGMI ring in 2N blocks while every GPU updates the block it
 holds with its users' ratings -- each item block is owned by one GPU at a time,
-so the updates are exact (no staleness) and the 32 MB block transfers hide
-behind the compute of the previous block.  ``--exchange ps`` runs the
+so the updates are exact (no staleness) and each block transfer (256 MB / 2N)
+hides behind the compute of the resident block.  The SGD kernel is the
+tile-grouped one (``csrc/kernels/mf_tiled.hip``: ratings bucketed by item
+tile, one lane group per item row, no item atomics).  ``--exchange ps`` runs the
 reference's pull/push protocol instead (dedup -> all-to-all pull -> SGD ->
 all-to-all push; rows cross xGMI as bf16 by default, ``--wire``; the pull of
 micro-batch k+1 overlaps the SGD of k, ``--no-pipeline`` disables it).
@@ -54,8 +56,11 @@ def main(argv=None):
     ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"],
                     help="all-to-all row dtype; auto = bf16 at N>1")
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="tiled SGD: partition each batch on the main stream instead of prefetching it")
     ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
-    ap.add_argument("--sgd-mode", default="auto", choices=["auto", "grouped", "flat"])
+    ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
+                    help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     a = ap.parse_args(argv)
@@ -76,7 +81,7 @@ def main(argv=None):
         a.wire = "bf16" if n > 1 else "fp32"
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
-                   pipeline=not a.no_pipeline, exchange=a.exchange)
+                   pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
