@@ -127,6 +127,85 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
   }
 }
 
+// ---- two-level partition (default): coarse key (bucket >> cshift, ~128
+// keys) then the full bucket, each level with few open output runs per
+// workgroup so the scattered 16-B stores combine in L2 (the single-level
+// scatter above keeps ~16k runs open per workgroup: ~4 records each).
+// Reservations use one global atomic per (workgroup, key); no histograms
+// matrix, no column scan.  Order inside a bucket is arbitrary.
+constexpr int TP2_MAX_COARSE = 1024;
+
+// both histograms in one pass over iid: coarse counts and per-bucket counts
+__global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                                                         int W, const int32_t* __restrict__ half, int R, int T,
+                                                         int cshift, int NC, int KT, int32_t* __restrict__ ccount,
+                                                         int32_t* __restrict__ bcount, uint8_t* __restrict__ seen) {
+  __shared__ int32_t hb[TP_MAX_BUCKETS];
+  __shared__ int32_t hc[TP2_MAX_COARSE];
+  for (int k = threadIdx.x; k < KT; k += blockDim.x) hb[k] = 0;
+  for (int k = threadIdx.x; k < NC; k += blockDim.x) hc[k] = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
+  for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+    const int32_t i = iid[x];
+    int bk; int32_t row;
+    tile_bucket(i, W, half, R, T, bk, row);
+    atomicAdd(hb + bk, 1);
+    atomicAdd(hc + (bk >> cshift), 1);
+    if (seen != nullptr) seen[i] = 1;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < KT; k += blockDim.x)
+    if (hb[k]) atomicAdd(bcount + k, hb[k]);
+  for (int k = threadIdx.x; k < NC; k += blockDim.x)
+    if (hc[k]) atomicAdd(ccount + k, hc[k]);
+}
+
+// LEVEL 1: records from (uid, iid, rating), key = coarse; out = {uid, row, rating, bucket}
+// LEVEL 2: records from tmp, key = bucket (tmp.w); out = the same record
+template <int LEVEL>
+__global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __restrict__ uid,
+                                                           const int32_t* __restrict__ iid,
+                                                           const float* __restrict__ rating,
+                                                           const int4* __restrict__ tmp, int64_t n, int64_t chunk,
+                                                           int W, const int32_t* __restrict__ half, int R, int T,
+                                                           int cshift, int nkeys, const int32_t* __restrict__ ptr,
+                                                           int32_t* __restrict__ cursor, int4* __restrict__ out) {
+  __shared__ int32_t h[TP_MAX_BUCKETS];
+  for (int k = threadIdx.x; k < nkeys; k += blockDim.x) h[k] = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
+  for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+    int key;
+    if (LEVEL == 1) {
+      int bk; int32_t row;
+      tile_bucket(iid[x], W, half, R, T, bk, row);
+      key = bk >> cshift;
+    } else {
+      key = tmp[x].w;
+    }
+    atomicAdd(h + key, 1);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nkeys; k += blockDim.x)
+    if (h[k]) h[k] = ptr[k] + atomicAdd(cursor + k, h[k]);  // this workgroup's range of key k
+  __syncthreads();
+  for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
+    int4 r;
+    int key;
+    if (LEVEL == 1) {
+      int bk; int32_t row;
+      tile_bucket(iid[x], W, half, R, T, bk, row);
+      r = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
+      key = bk >> cshift;
+    } else {
+      r = tmp[x];
+      key = r.w;
+    }
+    out[atomicAdd(h + key, 1)] = r;
+  }
+}
+
 // ---------------------------------------------------------------- SGD
 constexpr int TG_CAP = 4096;    // records staged per chunk (64 KiB of LDS)
 constexpr int TG_MAX_R = 256;   // rows per tile
@@ -258,6 +337,49 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
                        KT, (const int32_t*)H, (const int32_t*)ptr, rec);
   FPS_CHECK_LAUNCH();
   return 0;
+}
+
+// Two-level partition.  Workspace (int32): ccount[NC], ccursor[NC], cptr[NC+1],
+// bcount[KT], bcursor[KT] (all zeroed here), tmp: n int4.  ptr[KT+1] = tile
+// offsets, rec: n records {uid, row-in-block, rating bits, bucket}.
+FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
+                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, int4* rec,
+                                uint8_t* seen, void* stream) {
+  const int KT = 2 * W * T;
+  if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
+  int cshift = 0;
+  while (((KT - 1) >> cshift) + 1 > 128) ++cshift;  // ~128 coarse keys
+  const int NC = ((KT - 1) >> cshift) + 1;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* ccount = ws;
+  int32_t* ccursor = ccount + NC;
+  int32_t* cptr = ccursor + NC;
+  int32_t* bcount = cptr + NC + 1;
+  int32_t* bcursor = bcount + KT;
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(int32_t) * (size_t)(3 * NC + 1 + 2 * KT), s);
+  if (e != hipSuccess) return (int)e;
+  const int G = fps_tile_partition_groups(n);
+  const int64_t chunk = (n + G - 1) / G;
+  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, cshift, NC, KT,
+                     ccount, bcount, seen);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
+  if (n > 0) {
+    hipLaunchKernelGGL(tp2_scatter_kernel<1>, dim3(G), dim3(1024), 0, s, uid, iid, rating, (const int4*)nullptr, n,
+                       chunk, W, half, R, T, cshift, NC, (const int32_t*)cptr, ccursor, tmp);
+    hipLaunchKernelGGL(tp2_scatter_kernel<2>, dim3(G), dim3(1024), 0, s, uid, iid, rating, (const int4*)tmp, n,
+                       chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+  }
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int64_t fps_tile_partition2_ws_ints(int W, int T) {
+  const int KT = 2 * W * T;
+  int cshift = 0;
+  while (((KT - 1) >> cshift) + 1 > 128) ++cshift;
+  const int NC = ((KT - 1) >> cshift) + 1;
+  return 3 * (int64_t)NC + 1 + 2 * (int64_t)KT;
 }
 
 // One launch per item block: T tiles of R (<= 256) rows of I[block_rows, D];

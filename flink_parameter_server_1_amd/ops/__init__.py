@@ -311,12 +311,15 @@ class TilePartitioner:
     ``rec`` an int32 ``[n, 4]`` array of packed records {uid, row-in-block,
     rating bits, 0} grouped by bucket (on CPU: the three columns as tensors)."""
 
-    def __init__(self, W: int, half, R: int, T: int, device):
+    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None):
         self.W, self.R, self.T = W, int(R), int(T)
         self.KT = 2 * W * self.T
         chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
         if chunk and self.device_is_cuda(device):
             N.require().fps_tile_partition_set_chunk(int(chunk))
+        # 2 = two-level (coarse key, then bucket: few open output runs per
+        # workgroup); 1 = single level (per-workgroup histograms of every bucket)
+        self.levels = int(levels or os.environ.get("FPS_TILE_PARTITION_LEVELS", "2"))
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
@@ -334,12 +337,23 @@ class TilePartitioner:
         lib = N.require()
         n = uid.numel()
         G = lib.fps_tile_partition_groups(n)
-        if G * self.KT > self.g_cap:
+        if self.levels == 1 and G * self.KT > self.g_cap:
             self.g_cap = G * self.KT
             self.H = torch.empty(self.g_cap, dtype=torch.int32, device=self.device)
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
             self.rec = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
+            if self.levels == 2:
+                self.tmp = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
+        if self.levels == 2:
+            if not hasattr(self, "ws"):
+                self.ws = torch.empty(lib.fps_tile_partition2_ws_ints(self.W, self.T), dtype=torch.int32,
+                                      device=self.device)
+            N.check(lib.fps_tile_partition2(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n,
+                                            self.W, self.half.data_ptr(), self.R, self.T, self.ws.data_ptr(),
+                                            self.tmp.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
+                                            N.ptr(seen), N.stream_ptr(self.device)), "tile_partition2")
+            return self.ptr, self.rec[:n]
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
                                        self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),
                                        self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
