@@ -317,9 +317,13 @@ class TilePartitioner:
         chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
         if chunk and self.device_is_cuda(device):
             N.require().fps_tile_partition_set_chunk(int(chunk))
-        # 2 = two-level (coarse key, then bucket: few open output runs per
-        # workgroup); 1 = single level (per-workgroup histograms of every bucket)
-        self.levels = int(levels or os.environ.get("FPS_TILE_PARTITION_LEVELS", "2"))
+        # 1 = single level (per-workgroup histograms of every bucket + column scan);
+        # 2 = two-level (coarse key, then bucket; atomic range reservations, no
+        # histogram matrix).  Measured at 64M ratings, KT = 3.9k buckets: 1.66 vs
+        # 1.83 ms (profiles/r1_mf_partition_levels.md); the single level's
+        # G x KT histogram grows with KT, so larger bucket counts use 2 levels.
+        env = os.environ.get("FPS_TILE_PARTITION_LEVELS")
+        self.levels = int(levels or env or (1 if self.KT <= 4096 else 2))
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
