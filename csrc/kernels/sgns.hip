@@ -15,10 +15,13 @@
 // fp32 in / fp32 accumulate: v_mfma_f32_32x32x2_f32 (exact f32 FMA chain,
 // cdna_hip_programming.md §3).  H and N are staged in LDS with rows padded
 // to an odd dword stride (conflict-free row-strided operand reads, §2 bank
-// rule), one wave per row with 16-B loads (a 1 KiB coalesced transaction
-// per wave-instruction).  The context rows O are not staged: they are read
-// once, coalesced, for h.o and again in the dH epilogue.  512-thread blocks
-// (8 waves) keep enough loads in flight at one block per CU.
+// rule), 16-B loads, every load of a wave's 4 rows issued before its first
+// LDS store (v1 staged one row per wave at a time: latency-bound at one
+// block per CU).  S = H N^T is four 16x16x4 MFMA tiles, one per wave, over
+// the full K (no cross-wave partial-score buffer) while the other 12 waves
+// compute the positive scores.  The context rows O are not staged: they are
+// read once, coalesced, for h.o and again in the dH epilogue.  1024-thread
+// blocks (16 waves) at one block per CU (87 KB of LDS at D = 300).
 // Gradients are accumulated with no-return float atomics straight from the
 // MFMA accumulator layout: one register = two rows x 32 consecutive floats,
 // the full-rate atomic shape (MI355X_MICROARCH.md "Global float atomics").
@@ -34,9 +37,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int M = 32;   // pairs per block
-constexpr int K = 32;   // shared negatives per block
-constexpr int NT = 512; // threads per block
+constexpr int M = 32;    // pairs per block
+constexpr int K = 32;    // shared negatives per block
+constexpr int NT = 1024; // threads per block (16 waves: one block per CU holds 87 KB of LDS)
 constexpr int NW = NT / 64;
 
 template <bool BF16>
@@ -47,27 +50,28 @@ __device__ __forceinline__ float ld1(const void* rows, int64_t idx) {
 
 // 4 consecutive elements of a row (c..c+3), zero beyond D
 template <bool BF16>
-__device__ __forceinline__ void ld4(const void* rows, int64_t row, int D, int c, float (&v)[4]) {
+__device__ __forceinline__ float4 ld4(const void* rows, int64_t row, int D, int c) {
   const int64_t o = row * D + c;
+  float v[4];
   if (c + 3 < D && ((o & 3) == 0)) {
     if (BF16) {
       const uint2 u = *(const uint2*)((const uint16_t*)rows + o);
-      v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
-      v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
-    } else {
-      const float4 f = *(const float4*)((const float*)rows + o);
-      v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+      return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                         __uint_as_float(u.y & 0xffff0000u));
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (c + j < D) ? ld1<BF16>(rows, o + j) : 0.f;
+    return *(const float4*)((const float*)rows + o);
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (c + j < D) ? ld1<BF16>(rows, o + j) : 0.f;
+  return make_float4(v[0], v[1], v[2], v[3]);
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // C/D map of the 32x32 MFMA: lane l, reg r -> row (col = l & 31)
 __device__ __forceinline__ int acc_row(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 template <bool BF16>
 __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__ rows_in,
@@ -84,14 +88,14 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
   float* Hs = smem;                // [M][LD]
   float* Ns = Hs + M * LD;         // [K][LD]
   float* Gs = Ns + K * LD;         // [M][K+1]
-  float* Sred = Gs + M * (K + 1);  // [NW][M][K] per-wave partial scores
-  float* gpos = Sred + NW * M * K; // [M]
+  float* gpos = Gs + M * (K + 1);  // [M]
   int32_t* pc = (int32_t*)(gpos + M);  // [M]
   int32_t* po = pc + M;                // [M]
   int32_t* pn = po + M;                // [K]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n_blocks = (n_pairs + M - 1) / M;
+  constexpr int RPW = (M + K) / NW;  // staged rows per wave (4)
 
   for (int64_t blk = blockIdx.x; blk < n_blocks; blk += gridDim.x) {
     const int64_t p0 = blk * M;
@@ -103,55 +107,71 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
       pn[tid - M] = pos_neg[blk * K + (tid - M)];
     }
     __syncthreads();
-    // ---- stage H and N: one wave per row, 16-B loads, zero padded
-    for (int r = wave; r < M + K; r += NW) {
-      const bool is_h = r < M;
-      const int32_t rr = is_h ? pc[r] : pn[r - M];
-      float* dst = is_h ? Hs + r * LD : Ns + (r - M) * LD;
-      for (int c = lane * 4; c < Dp; c += 256) {
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        if (rr >= 0) ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[c + j] = v[j];
-      }
-    }
-    __syncthreads();
-    // ---- S = H N^T: each wave 1/NW of the k range (k-steps of 2)
+    // ---- stage H and N: RPW rows per wave, every 16-B load of the wave's rows
+    // issued before the first LDS store (latency paid once per block, not per row)
     {
-      floatx16 acc = {0};
-      const int ksteps = Dp / 2;
-      const int per = (ksteps + NW - 1) / NW;
-      const int k_beg = wave * per, k_end = min(ksteps, k_beg + per);
-      const int i = lane & 31, kh = lane >> 5;
-      for (int ks = k_beg; ks < k_end; ++ks) {
-        const int k = 2 * ks + kh;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Hs[i * LD + k], Ns[i * LD + k], acc, 0, 0, 0);
+      float4 v[RPW][2];
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int r = wave + NW * j;
+        const bool is_h = r < M;
+        const int32_t rr = is_h ? pc[r] : pn[r - M];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = lane * 4 + 256 * h;
+          v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) Sred[(wave * M + acc_row(lane, r)) * K + (lane & 31)] = acc[r];
-    }
-    // ---- positive scores h.o, O read straight from global (coalesced)
-    for (int m = wave; m < M; m += NW) {
-      float p = 0.f;
-      if (m < npairs) {
-        for (int c = lane; c < D; c += 64) p = fmaf(Hs[m * LD + c], ld1<BF16>(rows_out, (int64_t)po[m] * D + c), p);
-      }
-      p = group_sum<64>(p);
-      if (lane == 0) {
-        const bool ok = m < npairs;
-        gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
-        if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
+      for (int j = 0; j < RPW; ++j) {
+        const int r = wave + NW * j;
+        float* dst = r < M ? Hs + r * LD : Ns + (r - M) * LD;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = lane * 4 + 256 * h;
+          if (c < Dp) { dst[c] = v[j][h].x; dst[c + 1] = v[j][h].y; dst[c + 2] = v[j][h].z; dst[c + 3] = v[j][h].w; }
+        }
       }
     }
     __syncthreads();
-    for (int e = tid; e < M * K; e += NT) {
-      const int m = e / K;
-      float s = 0.f;
+    if (wave < 4) {
+      // ---- S = H N^T: four 16x16 tiles, one per wave, full K (no cross-wave reduction)
+      const int ti = wave >> 1, tj = wave & 1;
+      const int i = lane & 15, kq = lane >> 4;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* hrow = Hs + (16 * ti + i) * LD + kq;
+      const float* nrow = Ns + (16 * tj + i) * LD + kq;
+      for (int k = 0; k < Dp; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc, 0, 0, 0);
+      // C/D: col = lane & 15, row = 4 * (lane >> 4) + r
+      float lsum = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) s += Sred[w * M * K + e];
-      const bool ok = m < npairs;
-      Gs[m * (K + 1) + (e % K)] = ok ? -lr * neg_weight * sigmoidf_(s) : 0.f;
-      if (ok && loss_out) atomicAdd(loss_out, -neg_weight * __logf(1.f - sigmoidf_(s) + 1e-12f));
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * ti + 4 * kq + r, kk = 16 * tj + i;
+        const bool ok = m < npairs;
+        const float sg = sigmoidf_(acc[r]);
+        Gs[m * (K + 1) + kk] = ok ? -lr * neg_weight * sg : 0.f;
+        if (ok) lsum += -neg_weight * __logf(1.f - sg + 1e-12f);
+      }
+      if (loss_out) {
+        lsum = group_sum<64>(lsum);
+        if (lane == 0) atomicAdd(loss_out, lsum);
+      }
+    } else {
+      // ---- positive scores h.o (O read from global, coalesced), waves 4..15
+      for (int m = wave - 4; m < M; m += NW - 4) {
+        float p = 0.f;
+        if (m < npairs) {
+#pragma unroll 5
+          for (int c = lane; c < D; c += 64) p = fmaf(Hs[m * LD + c], ld1<BF16>(rows_out, (int64_t)po[m] * D + c), p);
+        }
+        p = group_sum<64>(p);
+        if (lane == 0) {
+          const bool ok = m < npairs;
+          gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
+          if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
+        }
+      }
     }
     __syncthreads();
     // ---- dH = G N (+ g+ O) and dN = G^T H: 2 * Dp/32 output tiles over NW waves
@@ -198,7 +218,7 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
 
 FPS_API size_t fps_sgns_smem_bytes(int D) {
   const int Dp = (D + 31) & ~31, LD = Dp + 1;
-  return sizeof(float) * ((size_t)2 * 32 * LD + 32 * 33 + NW * 32 * 32 + 32) + sizeof(int32_t) * 96;
+  return sizeof(float) * ((size_t)2 * 32 * LD + 32 * 33 + 32) + sizeof(int32_t) * 96;
 }
 
 // pos_neg holds K = 32 negative rows per block of 32 pairs (ceil(n_pairs/32) blocks)
@@ -206,6 +226,7 @@ FPS_API int fps_sgns_step(const void* rows_in, const void* rows_out, int rows_bf
                           const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
                           float neg_weight, float* d_in, float* d_out, float* loss_out, void* stream) {
   if (n_pairs <= 0) return 0;
+  if (((D + 31) & ~31) > 512) return (int)hipErrorInvalidValue;  // staging covers 2 x 256 columns
   const size_t smem = fps_sgns_smem_bytes(D);
   if (smem > 160 * 1024) return (int)hipErrorInvalidValue;
   const int64_t nb = (n_pairs + 31) / 32;
