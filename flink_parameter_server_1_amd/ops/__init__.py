@@ -49,6 +49,10 @@ def check_finite(t: torch.Tensor, what: str, exc=FloatingPointError) -> None:
 
 
 def _c(t):
+    """Kernel operand check: every pointer handed to a gfx950 kernel must be a
+    contiguous DEVICE tensor (a host pointer in a kernel faults the GPU)."""
+    if not t.is_cuda:
+        raise ValueError(f"kernel operand on {t.device}: expected a GPU tensor")
     if not t.is_contiguous():
         raise ValueError("kernel inputs must be contiguous")
     return t

@@ -114,4 +114,9 @@ def stream_ptr(device=None) -> int:
 
 
 def ptr(t):
-    return None if t is None else t.data_ptr()
+    """Optional kernel operand (None -> nullptr); must be a GPU tensor."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"kernel operand on {t.device}: expected a GPU tensor")
+    return t.data_ptr()

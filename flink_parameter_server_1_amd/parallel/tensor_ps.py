@@ -57,7 +57,7 @@ class TensorPS:
         """Dedup + split exchange + key all-to-all.  ``persistent`` copies the
         request->row map out of the reusable dedup workspace, so the plan
         survives the next ``plan`` call (pipelined steps)."""
-        keys = keys.to(torch.int32).contiguous()
+        keys = keys.to(device=self.table.device, dtype=torch.int32).contiguous()
         with trace_range("ps.dedup"):
             counts, prefix, uniq, pos = self.dedup.run(keys)
         recv_counts = self.comm.exchange_counts(counts)

@@ -147,3 +147,15 @@ def test_hash_store_negative_ids():
     hs.push([-7], [[1.0, 2.0]])
     ids, vals = hs.dump()
     assert sorted(ids.tolist()) == [-7, -5, 5]
+
+
+def test_kernel_operands_must_be_device_tensors():
+    """A host pointer handed to a GPU kernel faults the device: the launch wrappers refuse it."""
+    from flink_parameter_server_1_amd import ops
+    from flink_parameter_server_1_amd.ops import _native
+
+    with pytest.raises(ValueError, match="expected a GPU tensor"):
+        ops._c(torch.zeros(4))
+    with pytest.raises(ValueError, match="expected a GPU tensor"):
+        _native.ptr(torch.zeros(4))
+    assert _native.ptr(None) is None
