@@ -103,17 +103,13 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
 //    1M ids -> 8 MB), map index = key;
 //  * hashed (HASHED = true): for id spaces of 1e9+ (PA 1B features, the
 //    100B-parameter table) a per-batch open-addressing hash table
-//    (dedup_hash_insert_kernel) first gives every request the slot of its key,
-//    and the claim map is indexed by that slot (capacity ~2x the batch).
-template <bool HASHED>
-__device__ __forceinline__ int64_t map_index(const int32_t* __restrict__ keys, const int32_t* __restrict__ hslot,
-                                             int64_t b) {
-  return HASHED ? (int64_t)hslot[b] : (int64_t)keys[b];
-}
-
+//    (dedup_hash_insert_kernel, capacity ~2x the batch) gives every request
+//    the slot of its key and marks the one request whose CAS inserted it as
+//    the owner -- no claim map, no claim pass.
 // Epoch-tagged linear-probing insert: tab[h] = epoch << 32 | key.  Entries of
 // older epochs count as empty, so nothing is cleared between steps.  The
-// capacity (power of two, >= 2n) bounds every probe sequence.
+// capacity (power of two, >= 2n) bounds every probe sequence.  The request
+// whose CAS writes the key owns it; owner_slot is then indexed by hash slot.
 __global__ void dedup_hash_insert_kernel(const int32_t* __restrict__ keys, int64_t n,
                                          unsigned long long* __restrict__ tab, uint32_t mask, uint32_t epoch,
                                          int32_t* __restrict__ hslot) {
@@ -121,27 +117,30 @@ __global__ void dedup_hash_insert_kernel(const int32_t* __restrict__ keys, int64
     const uint32_t k = (uint32_t)keys[b];
     const unsigned long long mine = ((unsigned long long)epoch << 32) | k;
     uint32_t h = fmix32(k ^ 0x5bd1e995u) & mask;
+    bool own = false;
     for (;;) {
       unsigned long long cur = tab[h];
       if ((uint32_t)(cur >> 32) != epoch) {
         const unsigned long long old = atomicCAS(tab + h, cur, mine);
-        if (old == cur) break;   // claimed the empty slot
+        if (old == cur) { own = true; break; }  // claimed the empty slot: this request owns the key
         cur = old;               // somebody else wrote it first: re-examine
         if ((uint32_t)(cur >> 32) != epoch) continue;
       }
       if (cur == mine) break;    // our key already lives here
       h = (h + 1) & mask;
     }
-    hslot[b] = (int32_t)h;
+    // bit 31 marks the key's owner (the CAS winner: exactly one per key), so no
+    // separate claim pass is needed on the hashed path; cap <= 2^31 keeps h < 2^31
+    hslot[b] = (int32_t)(h | (own ? 0x80000000u : 0u));
   }
 }
 
-template <bool HASHED>
-__global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, const int32_t* __restrict__ hslot, int64_t n,
-                                   unsigned long long* __restrict__ map, uint32_t epoch) {
+// dense path only (the hashed path takes ownership from the insert's CAS)
+__global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, int64_t n, unsigned long long* __restrict__ map,
+                                   uint32_t epoch) {
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long v = ((unsigned long long)epoch << 32) | (unsigned long long)(0xffffffffu - (uint32_t)b);
-    atomicMax(map + map_index<HASHED>(keys, hslot, b), v);
+    atomicMax(map + keys[b], v);
   }
 }
 
@@ -200,10 +199,14 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
     int d = 0;
     if (b < n) {
       const int32_t k = keys[b];
-      const uint32_t owner = 0xffffffffu - (uint32_t)(map[map_index<HASHED>(keys, hslot, b)] & 0xffffffffull);
       int32_t local;
       key_dest(k, W, part_kind, block, d, local);
-      own = owner == (uint32_t)b;
+      if (HASHED) {
+        own = hslot[b] < 0;
+      } else {
+        const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+        own = owner == (uint32_t)b;
+      }
     }
     dd[it] = own ? d : -1;
     slot_l[it] = wave_alloc(own, d, lds_cnt);  // LDS atomics: cheap
@@ -214,7 +217,10 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < DEDUP_ITEMS; ++it) {
-    if (dd[it] >= 0) owner_slot[base + (int64_t)it * blockDim.x + threadIdx.x] = lds_base[dd[it]] + slot_l[it];
+    if (dd[it] < 0) continue;
+    const int64_t b = base + (int64_t)it * blockDim.x + threadIdx.x;
+    // dense: indexed by the owner's request index; hashed: by the key's hash slot
+    owner_slot[HASHED ? (int64_t)(hslot[b] & 0x7fffffff) : b] = lds_base[dd[it]] + slot_l[it];
   }
 }
 
@@ -237,12 +243,22 @@ __global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, const int
                                      int32_t* __restrict__ pos) {
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
     const int32_t k = keys[b];
-    const uint32_t owner = 0xffffffffu - (uint32_t)(map[map_index<HASHED>(keys, hslot, b)] & 0xffffffffull);
     int d; int32_t local;
     key_dest(k, W, part_kind, block, d, local);
-    const int32_t p = prefix[d] + owner_slot[owner];
+    int64_t at;
+    bool own;
+    if (HASHED) {
+      const int32_t hs = hslot[b];
+      at = hs & 0x7fffffff;
+      own = hs < 0;
+    } else {
+      const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
+      at = owner;
+      own = owner == (uint32_t)b;
+    }
+    const int32_t p = prefix[d] + owner_slot[at];
     pos[b] = p;
-    if (owner == (uint32_t)b) uniq[p] = local;
+    if (own) uniq[p] = local;
   }
 }
 
@@ -347,7 +363,7 @@ static int launch_dedup(const int32_t* keys, const int32_t* hslot, int64_t n, un
   if (W > DEDUP_MAX_W) return (int)hipErrorInvalidValue;
   const int g = grid_for(n > 0 ? n : 1, 256, 256 * 16);
   if (n > 0) {
-    hipLaunchKernelGGL(dedup_claim_kernel<HASHED>, dim3(g), dim3(256), 0, s, keys, hslot, n, map, epoch);
+    if (!HASHED) hipLaunchKernelGGL(dedup_claim_kernel, dim3(g), dim3(256), 0, s, keys, n, map, epoch);
     const int64_t ga = (n + 256 * DEDUP_ITEMS - 1) / (256 * DEDUP_ITEMS);
     hipLaunchKernelGGL(dedup_assign_kernel<HASHED>, dim3((unsigned)ga), dim3(256), 0, s, keys, hslot, n,
                        (const unsigned long long*)map, W, part_kind, block, counts, owner_slot);
@@ -370,12 +386,11 @@ FPS_API int fps_dedup(const int32_t* keys, int64_t n, unsigned long long* map, u
                              pos, (hipStream_t)stream);
 }
 
-// Hashed variant for huge id spaces: tab and map both hold cap (power of two,
-// >= 2n) uint64 entries; hslot has n entries.  Keys must be >= 0.
-FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long* tab, unsigned long long* map,
-                             int64_t cap, uint32_t epoch, int W, int part_kind, int64_t block, int32_t* counts,
-                             int32_t* prefix, int32_t* hslot, int32_t* owner_slot, int32_t* uniq, int32_t* pos,
-                             void* stream) {
+// Hashed variant for huge id spaces: tab (uint64) and owner_slot (int32) hold
+// cap entries (power of two, >= 2n, <= 2^31); hslot has n entries.  Keys >= 0.
+FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long* tab, int64_t cap, uint32_t epoch,
+                             int W, int part_kind, int64_t block, int32_t* counts, int32_t* prefix, int32_t* hslot,
+                             int32_t* owner_slot, int32_t* uniq, int32_t* pos, void* stream) {
   if (cap < 2 * n || (cap & (cap - 1)) != 0 || cap > (1ll << 31)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   if (n > 0) {
@@ -383,8 +398,8 @@ FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long*
     hipLaunchKernelGGL(dedup_hash_insert_kernel, dim3(g), dim3(256), 0, s, keys, n, tab, (uint32_t)(cap - 1), epoch,
                        hslot);
   }
-  return launch_dedup<true>(keys, hslot, n, map, epoch, W, part_kind, block, counts, prefix, owner_slot, uniq, pos,
-                            s);
+  return launch_dedup<true>(keys, hslot, n, nullptr, epoch, W, part_kind, block, counts, prefix, owner_slot, uniq,
+                            pos, s);
 }
 
 FPS_API int fps_bucketize(const int32_t* keys, int64_t n, int W, int part_kind, int64_t block, int32_t* shard,

@@ -112,8 +112,10 @@ def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: 
 class DedupWorkspace:
     """Per-step key de-duplication + shard grouping for one worker (K1).
 
-    ``map`` is an epoch-tagged ``uint64[num_ids]`` claim table (nothing is
-    cleared between steps).  ``run(keys)`` returns device tensors
+    Dense path: ``map`` is an epoch-tagged ``uint64[num_ids]`` claim table
+    (nothing is cleared between steps).  Hashed path (id spaces above
+    ``DENSE_MAP_MAX_IDS``): a per-batch epoch-tagged open-addressing table of
+    ~2x the batch whose inserting CAS also elects each key's owner.  ``run(keys)`` returns device tensors
     ``counts[W], prefix[W+1], uniq[U], pos[B]``: the unique *local* keys
     grouped by owning shard (contiguous, so they are directly the all-to-all
     send buffer with splits ``counts``) and each request's row in it.
@@ -148,9 +150,10 @@ class DedupWorkspace:
                 self.hslot = torch.empty(self.cap, dtype=torch.int32, device=self.device)
         if self.hashed and 2 * n > self.hash_cap:
             self.hash_cap = 1 << max(10, (2 * n - 1).bit_length())
-            # fresh zeroed tables: epoch 0 entries count as empty, epochs restart at 1
+            # fresh zeroed table: epoch 0 entries count as empty, epochs restart at 1;
+            # owner slots are indexed by hash slot on this path
             self.tab = torch.zeros(self.hash_cap, dtype=torch.int64, device=self.device)
-            self.map = torch.zeros(self.hash_cap, dtype=torch.int64, device=self.device)
+            self.owner_slot_h = torch.empty(self.hash_cap, dtype=torch.int32, device=self.device)
             self.epoch = 0
 
     def run(self, keys: torch.Tensor):
@@ -161,18 +164,15 @@ class DedupWorkspace:
         self.epoch += 1
         if self.epoch >= 0xFFFFFFFF:  # wrap: clear the tags once every 4e9 steps
             self.epoch = 1
-            self.map.zero_()
-            if self.hashed:
-                self.tab.zero_()
+            (self.tab if self.hashed else self.map).zero_()
         self.counts.zero_()
         lib = N.require()
         s = N.stream_ptr(self.device)
         if self.hashed:
-            N.check(lib.fps_dedup_hashed(_c(keys).data_ptr(), n, self.tab.data_ptr(), self.map.data_ptr(),
-                                         self.hash_cap, self.epoch, self.W, self.part_kind, self.block,
-                                         self.counts.data_ptr(), self.prefix.data_ptr(), self.hslot.data_ptr(),
-                                         self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s),
-                    "dedup_hashed")
+            N.check(lib.fps_dedup_hashed(_c(keys).data_ptr(), n, self.tab.data_ptr(), self.hash_cap, self.epoch,
+                                         self.W, self.part_kind, self.block, self.counts.data_ptr(),
+                                         self.prefix.data_ptr(), self.hslot.data_ptr(), self.owner_slot_h.data_ptr(),
+                                         self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup_hashed")
         else:
             N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch, self.W,
                                   self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),

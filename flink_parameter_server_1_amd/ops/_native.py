@@ -32,8 +32,8 @@ _SIGNATURES = {
     "fps_gather_rows": [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_int, c_vp, c_vp],
     "fps_apply_rows": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_f32, c_f32, c_vp, c_vp],
     "fps_dedup": [c_vp, c_i64, c_vp, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "fps_dedup_hashed": [c_vp, c_i64, c_vp, c_vp, c_i64, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                         c_vp, c_vp],
+    "fps_dedup_hashed": [c_vp, c_i64, c_vp, c_i64, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                         c_vp],
     "fps_pair_sgd_pulled": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_int, c_vp, c_vp],
     "fps_mf_sgd_local_seg": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
     "fps_rot_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],

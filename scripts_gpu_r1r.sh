@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
-timeout -k 10 600 python -m pytest tests/test_sgns_sampling.py -q -x > gpurun_out/gpu_sgns.log 2>&1; rc=$?
+timeout -k 10 300 python -m pytest tests/test_sgns_sampling.py -q -x -m gpu > gpurun_out/gpu_sgns.log 2>&1; rc=$?
 echo "sgns tests rc=$rc" >> gpurun_out/gpu_sgns.log
 tail -4 gpurun_out/gpu_sgns.log
 case $rc in 0) ;; *) echo "stopping after test rc=$rc"; exit 1;; esac
