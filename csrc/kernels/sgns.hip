@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
   int32_t* pn = po + M;                // [K]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* scr = (float*)(pn + K) + (size_t)wave * 32 * 33;  // [NW][32][33] wave-private dH tile scratch
   const int64_t n_blocks = (n_pairs + M - 1) / M;
   constexpr int RPW = (M + K) / NW;  // staged rows per wave (4)
 
@@ -189,19 +190,35 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
       }
       const int col = c0 + (lane & 31);
-      if (col < D) {
+      if (is_h) {
+        // dH rows of pairs that share a center (center-major pair order:
+        // skipgram_pairs) are summed through LDS first -- one atomic row per
+        // run of equal centers instead of one per pair
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = acc_row(lane, r);
-          if (is_h) {
-            if (row < npairs) {
-              const float v = acc[r] + gpos[row] * ld1<BF16>(rows_out, (int64_t)po[row] * D + col);
-              atomic_add_noret(d_in + (int64_t)pc[row] * D + col, v);
+          float v = acc[r];
+          if (row < npairs && col < D) v += gpos[row] * ld1<BF16>(rows_out, (int64_t)po[row] * D + col);
+          scr[row * 33 + (lane & 31)] = v;
+        }
+        // wave-private scratch: the wave's own LDS writes are visible to it after
+        // the LDS counter drains (no block barrier needed)
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        if (col < D) {
+          const int r0 = 16 * (lane >> 5), r1 = min(r0 + 16, npairs);
+          float run = 0.f;
+          for (int row = r0; row < r1; ++row) {
+            run += scr[row * 33 + (lane & 31)];
+            if (row + 1 == r1 || pc[row + 1] != pc[row]) {
+              atomic_add_noret(d_in + (int64_t)pc[row] * D + col, run);
+              run = 0.f;
             }
-          } else {
-            atomic_add_noret(d_out + (int64_t)pn[row] * D + col, acc[r]);
           }
         }
+      } else if (col < D) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) atomic_add_noret(d_out + (int64_t)pn[acc_row(lane, r)] * D + col, acc[r]);
       }
     }
     // ---- dO = g+ H: one wave per row, 256-B atomic wave-instructions
@@ -218,7 +235,7 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
 
 FPS_API size_t fps_sgns_smem_bytes(int D) {
   const int Dp = (D + 31) & ~31, LD = Dp + 1;
-  return sizeof(float) * ((size_t)2 * 32 * LD + 32 * 33 + 32) + sizeof(int32_t) * 96;
+  return sizeof(float) * ((size_t)2 * 32 * LD + 32 * 33 + 32 + (size_t)NW * 32 * 33) + sizeof(int32_t) * 96;
 }
 
 // pos_neg holds K = 32 negative rows per block of 32 pairs (ceil(n_pairs/32) blocks)

@@ -90,18 +90,29 @@ class DistributedSGNS:
         return self.w_in.dump(only_touched)
 
 
-def skipgram_pairs(tokens: torch.Tensor, window: int, generator: Optional[torch.Generator] = None):
-    """(center, context) pairs with word2vec's random reduced window b ~ U{1..window}."""
+def skipgram_pairs(tokens: torch.Tensor, window: int, generator: Optional[torch.Generator] = None,
+                   center_major: bool = True):
+    """(center, context) pairs with word2vec's random reduced window b ~ U{1..window}.
+
+    ``center_major`` orders the pairs by center position (word2vec's own order:
+    a center's whole window, then the next center), so the pairs of one
+    32-pair kernel block share few centers and the kernel sums their center
+    gradients before the atomics (``sgns.hip``)."""
     T = tokens.numel()
     b = torch.randint(1, window + 1, (T,), generator=generator, device=tokens.device)
-    cs, os_ = [], []
+    cs, os_, ps = [], [], []
     for o in range(1, window + 1):
         idx = torch.arange(T - o, device=tokens.device)
         fwd = b[idx] >= o           # context t+o of center t
         bwd = b[idx + o] >= o       # context t of center t+o
         cs += [tokens[idx][fwd], tokens[idx + o][bwd]]
         os_ += [tokens[idx + o][fwd], tokens[idx][bwd]]
-    return torch.cat(cs).to(torch.int32), torch.cat(os_).to(torch.int32)
+        ps += [idx[fwd], (idx + o)[bwd]]
+    c, o_ = torch.cat(cs).to(torch.int32), torch.cat(os_).to(torch.int32)
+    if center_major:
+        order = torch.argsort(torch.cat(ps), stable=True)
+        c, o_ = c[order], o_[order]
+    return c, o_
 
 
 def synthetic_corpus(n_tokens: int, vocab_size: int, n_topics: int = 64, topic_len: int = 50, seed: int = 0,
