@@ -64,12 +64,15 @@ def test_sgns_distributed_gloo():
 @pytest.mark.gpu
 @pytest.mark.parametrize("D", [16, 64, 100, 300])
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
-def test_sgns_kernel_matches_reference(D, wire):
+@pytest.mark.parametrize("runs", [False, True])
+def test_sgns_kernel_matches_reference(D, wire, runs):
     torch.manual_seed(D)
     Uin, Uout, P = 300, 400, 200
     rows_in = (torch.randn(Uin, D) * 0.3).to(wire)
     rows_out = (torch.randn(Uout, D) * 0.3).to(wire)
     pos_c = torch.randint(0, Uin, (P,), dtype=torch.int32)
+    if runs:  # center-major order: runs of equal centers (summed in LDS before the atomics)
+        pos_c = torch.sort(torch.randint(0, 40, (P,), dtype=torch.int32)).values
     pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
     pos_neg = torch.randint(0, Uout, (((P + 31) // 32) * 32,), dtype=torch.int32)
     d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
