@@ -283,9 +283,13 @@ __global__ void bucketize_kernel(const int32_t* __restrict__ keys, int64_t n, in
 
 }  // namespace
 
+// D = 1 (PA weights, LEMP norms): one lane per row, 64 independent rows per
+// wave instruction (scattered 4-B rows are transaction-bound, not byte-bound)
 #define TPR_SWITCH(D, ...)                                   \
   do {                                                       \
-    if ((D) <= 4) { constexpr int TPR = 4; __VA_ARGS__; }     \
+    if ((D) <= 1) { constexpr int TPR = 1; __VA_ARGS__; }     \
+    else if ((D) <= 2) { constexpr int TPR = 2; __VA_ARGS__; } \
+    else if ((D) <= 4) { constexpr int TPR = 4; __VA_ARGS__; } \
     else if ((D) <= 8) { constexpr int TPR = 8; __VA_ARGS__; } \
     else if ((D) <= 16) { constexpr int TPR = 16; __VA_ARGS__; } \
     else if ((D) <= 32) { constexpr int TPR = 32; __VA_ARGS__; } \
