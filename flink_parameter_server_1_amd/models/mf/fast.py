@@ -62,6 +62,8 @@ class MFConfig:
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
     prefetch_partition: bool = True   # tiled: bucket batch k+1 on a side stream during the SGD of k
+    graph_capture: bool = False       # tiled, W = 1: replay each batch size's step as one hipGraph
+                                      # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
 
@@ -118,7 +120,8 @@ class DistributedMF:
             self._tilers = [ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T,
                                                 dev) for _ in range(2)]
             self._tiler_i = 0
-            self._prefetch = cfg.prefetch_partition and dev.type == "cuda"
+            self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
+            self._prefetch = cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
             self._side = torch.cuda.Stream(dev) if self._prefetch else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
@@ -151,7 +154,9 @@ class DistributedMF:
             ops.check_index(uid_local, self.users.n_local, "MF step uid_local")
             ops.check_index(iid, c.num_items, "MF step iid")
         tiled = self.sgd_mode == "tiled"
-        if tiled:
+        if tiled and self._graphs is not None:
+            self._graph_step(uid_local, iid, rating)
+        elif tiled:
             # bucket this batch (side stream when prefetching) and run the SGD of
             # the batch staged by the previous call: the partition of k+1 overlaps
             # the SGD of k; the order of the SGD steps is unchanged
@@ -194,6 +199,30 @@ class DistributedMF:
             ops.check_finite(self.U, "user factors", FactorIsNotANumberException)
             if self.exchange != "rotate":
                 ops.check_finite(self.I, "item factors", FactorIsNotANumberException)
+
+    def _graph_step(self, uid_local, iid, rating):
+        """One local tiled step as a captured hipGraph (partition + SGD kernels,
+        no host sync inside), one graph per batch size.  The first batch of a
+        size runs eagerly (warm-up: buffers allocated) and is captured after."""
+        n = uid_local.numel()
+        entry = self._graphs.get(n)
+        if entry is not None:
+            graph, static = entry
+            for dst, src in zip(static, (uid_local, iid, rating)):
+                dst.copy_(src)
+            graph.replay()
+            return
+        dev = self.U.device
+        static = [uid_local.clone(), iid.clone(), rating.clone()]
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # eager warm-up = this batch's real step
+            self._tiled_sgd(self._stage_partition(*static))
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):  # capture only: nothing executes here
+            self._tiled_sgd(self._stage_partition(*static))
+        self._graphs[n] = (graph, static)
 
     def _stage_partition(self, uid_local, iid, rating):
         """Tile partition of one batch into the next of the two partition buffers;
