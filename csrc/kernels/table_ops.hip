@@ -406,6 +406,47 @@ FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long*
                             pos, s);
 }
 
+namespace {
+
+// ---- parameter locks (device-mode LockPSLogicA/B, M/server/LockPSLogicA.scala,
+// M/server/LockPSLogicB.scala): lock[row] = owner worker or -1.  A request is
+// granted when it takes a free lock or already holds it (a worker's duplicate
+// requests share its lock, the LockPSLogicB de-duplication).  Launched once
+// per source worker segment in rank order, so the lowest rank wins a contended
+// row deterministically; denied requests are retried by their worker.
+__global__ void lock_acquire_kernel(int32_t* __restrict__ lock, const int32_t* __restrict__ rows, int64_t n,
+                                    int32_t src, uint8_t* __restrict__ granted) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t old = atomicCAS(lock + rows[b], -1, src);
+    granted[b] = (old == -1 || old == src) ? 1 : 0;
+  }
+}
+
+__global__ void lock_release_kernel(int32_t* __restrict__ lock, const int32_t* __restrict__ rows, int64_t n,
+                                    const uint8_t* __restrict__ granted) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x)
+    if (granted[b]) lock[rows[b]] = -1;
+}
+
+}  // namespace
+
+FPS_API int fps_lock_acquire(int32_t* lock, const int32_t* rows, int64_t n, int32_t src, uint8_t* granted,
+                             void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(lock_acquire_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, lock, rows, n,
+                     src, granted);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int fps_lock_release(int32_t* lock, const int32_t* rows, int64_t n, const uint8_t* granted, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(lock_release_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, lock, rows, n,
+                     granted);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_bucketize(const int32_t* keys, int64_t n, int W, int part_kind, int64_t block, int32_t* shard,
                           int32_t* counts, void* stream) {
   if (n <= 0) return 0;

@@ -180,6 +180,26 @@ class DedupWorkspace:
         return self.counts, self.prefix, self.uniq, self.pos[:n]
 
 
+def lock_acquire(lock: torch.Tensor, rows: torch.Tensor, src: int) -> torch.Tensor:
+    """Device-mode LockPS: try to lock ``rows`` for worker ``src``; uint8 granted flags."""
+    if _on_gpu(lock):
+        granted = torch.empty(rows.numel(), dtype=torch.uint8, device=lock.device)
+        if DEBUG:
+            check_index(rows, lock.numel(), "lock_acquire")
+        N.check(N.require().fps_lock_acquire(_c(lock).data_ptr(), _c(rows).data_ptr(), rows.numel(), int(src),
+                                             granted.data_ptr(), N.stream_ptr(lock.device)), "lock_acquire")
+        return granted
+    return R.lock_acquire(lock, rows, src)
+
+
+def lock_release(lock: torch.Tensor, rows: torch.Tensor, granted: torch.Tensor) -> None:
+    if _on_gpu(lock):
+        N.check(N.require().fps_lock_release(_c(lock).data_ptr(), _c(rows).data_ptr(), rows.numel(),
+                                             _c(granted).data_ptr(), N.stream_ptr(lock.device)), "lock_release")
+        return
+    R.lock_release(lock, rows, granted)
+
+
 def bucketize(keys: torch.Tensor, W: int, part_kind: int = 0, block: int = 1):
     """Shard id per key and per-shard counts."""
     if _on_gpu(keys):

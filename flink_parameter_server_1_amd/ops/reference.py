@@ -142,6 +142,22 @@ def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
     delta.index_add_(0, pos, di)
 
 
+def lock_acquire(lock, rows, src: int):
+    """Sequential semantics of ``lock_acquire_kernel``: take free locks, keep own."""
+    rows = rows.long()
+    granted = torch.zeros(rows.numel(), dtype=torch.uint8)
+    for b, r in enumerate(rows.tolist()):
+        if int(lock[r]) in (-1, src):
+            lock[r] = src
+            granted[b] = 1
+    return granted
+
+
+def lock_release(lock, rows, granted):
+    rows = rows.long()
+    lock[rows[granted.bool()]] = -1
+
+
 def rot_block_of(iid, W, half):
     """Item -> (block 2q+h, row inside the block) of the rotation layout (``rotate.hip``)."""
     i = iid.long()
