@@ -62,6 +62,8 @@ class MFConfig:
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
     prefetch_partition: bool = True   # tiled: bucket batch k+1 on a side stream during the SGD of k
+    negative_sample_rate: int = 0     # implicit feedback: negatives (rating 0) per rating
+    user_memory: int = 128            # per-user ring of recent items excluded from the negatives
     graph_capture: bool = False       # tiled, W = 1: replay each batch size's step as one hipGraph
                                       # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
@@ -133,6 +135,18 @@ class DistributedMF:
             # so the close-time dump still covers exactly the touched parameters
             self._seen = torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev)
         self.pipeline = cfg.pipeline and self.exchange == "ps"
+        if cfg.negative_sample_rate > 0:
+            # PSOnlineMatrixFactorizationWorker.scala:70-79: per rating, negativeSampleRate
+            # items (rating 0) drawn among the items this worker has seen, not among the
+            # user's last userMemory items.  Device state: per-user ring + cursor, the
+            # worker's known-item list; the negatives join the batch as extra ratings.
+            n_u = self.users.n_local
+            self._ring = torch.full((n_u * cfg.user_memory,), -1, dtype=torch.int32, device=dev)
+            self._ring_cursor = torch.zeros(n_u, dtype=torch.int32, device=dev)
+            self._known_flag = torch.zeros(cfg.num_items, dtype=torch.int32, device=dev)
+            self._known = torch.zeros(cfg.num_items, dtype=torch.int32, device=dev)
+            self._known_count = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._neg_counter = 0
         self._pending = None
         self.updates = 0
 
@@ -153,6 +167,8 @@ class DistributedMF:
         if ops.DEBUG:  # FPS_DEBUG=1: range checks before any kernel sees the batch
             ops.check_index(uid_local, self.users.n_local, "MF step uid_local")
             ops.check_index(iid, c.num_items, "MF step iid")
+        if c.negative_sample_rate > 0:
+            uid_local, iid, rating = self._with_negatives(uid_local, iid, rating)
         tiled = self.sgd_mode == "tiled"
         if tiled and self._graphs is not None:
             self._graph_step(uid_local, iid, rating)
@@ -199,6 +215,19 @@ class DistributedMF:
             ops.check_finite(self.U, "user factors", FactorIsNotANumberException)
             if self.exchange != "rotate":
                 ops.check_finite(self.I, "item factors", FactorIsNotANumberException)
+
+    def _with_negatives(self, uid, iid, rating):
+        """Append ``negative_sample_rate`` implicit negatives (rating 0) per rating."""
+        c = self.cfg
+        k = c.negative_sample_rate
+        ops.ring_push(self._ring, self._ring_cursor, uid, iid, c.user_memory)
+        ops.known_append(self._known_flag, self._known, self._known_count, iid)
+        negs = ops.sample_uniform_reject(uid.numel(), k, c.num_items, iid, uid, self._ring, c.user_memory,
+                                         seed=c.seed + 7 * self.comm.rank, counter=self._neg_counter,
+                                         device=uid.device, known=self._known, known_count=self._known_count)
+        self._neg_counter += 1
+        return (torch.cat([uid, uid.repeat_interleave(k)]), torch.cat([iid, negs]),
+                torch.cat([rating, torch.zeros(uid.numel() * k, dtype=rating.dtype, device=rating.device)]))
 
     def _graph_step(self, uid_local, iid, rating):
         """One local tiled step as a captured hipGraph (partition + SGD kernels,

@@ -488,17 +488,40 @@ def mf_sgd_grouped(U, I, uid, r, ptr, order, lr: float, lam: float = 0.0, delta:
 
 
 def sample_uniform_reject(n: int, k: int, n_items: int, positive=None, user=None, ring=None, mem: int = 0,
-                          seed: int = 0, counter: int = 0, device="cpu") -> torch.Tensor:
-    """``k`` uniform negatives per row, avoiding the positive and the user's ring (K5)."""
+                          seed: int = 0, counter: int = 0, device="cpu", known=None, known_count=None) -> torch.Tensor:
+    """``k`` uniform negatives per row, avoiding the positive and the user's ring (K5).
+    With ``known``/``known_count`` (device list + count) candidates come from the
+    worker's known items, as in the reference worker."""
     device = torch.device(device)
     if device.type == "cuda":
         out = torch.empty(n * k, dtype=torch.int32, device=device)
         lib = N.require()
         N.check(lib.fps_sample_uniform_reject(n, k, n_items, N.ptr(positive), N.ptr(user), N.ptr(ring), mem,
-                                              seed & 0xFFFFFFFF, counter, out.data_ptr(), N.stream_ptr(device)),
-                "sample_uniform_reject")
+                                              N.ptr(known), N.ptr(known_count), seed & 0xFFFFFFFF, counter,
+                                              out.data_ptr(), N.stream_ptr(device)), "sample_uniform_reject")
         return out
-    return R.sample_uniform_reject(n, k, n_items, positive, user, ring, mem, seed, counter)
+    kc = int(known_count[0]) if known_count is not None else None
+    return R.sample_uniform_reject(n, k, n_items, positive, user, ring, mem, seed, counter, known, kc)
+
+
+def ring_push(ring, cursor, uid, iid, mem: int) -> None:
+    """Append each rating's item to its user's ring of the last ``mem`` items."""
+    if _on_gpu(ring):
+        N.check(N.require().fps_ring_push(_c(ring).data_ptr(), _c(cursor).data_ptr(), _c(uid).data_ptr(),
+                                          _c(iid).data_ptr(), uid.numel(), mem, N.stream_ptr(ring.device)),
+                "ring_push")
+        return
+    R.ring_push(ring, cursor, uid, iid, mem)
+
+
+def known_append(flag, lst, count, iid) -> None:
+    """Append first-seen items to a known-item list (``count`` is a 1-element device counter)."""
+    if _on_gpu(flag):
+        N.check(N.require().fps_known_append(_c(flag).data_ptr(), _c(lst).data_ptr(), _c(count).data_ptr(),
+                                             _c(iid).data_ptr(), iid.numel(), N.stream_ptr(flag.device)),
+                "known_append")
+        return
+    R.known_append(flag, lst, count, iid)
 
 
 def build_alias_table(weights):

@@ -52,8 +52,10 @@ _SIGNATURES = {
     "fps_csr_count": [c_vp, c_i64, c_vp, c_vp],
     "fps_csr_scatter": [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
     "fps_mf_sgd_grouped": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp],
-    "fps_sample_uniform_reject": [c_i64, c_int, ctypes.c_int32, c_vp, c_vp, c_vp, c_int, c_u32, ctypes.c_uint64,
-                                  c_vp, c_vp],
+    "fps_sample_uniform_reject": [c_i64, c_int, ctypes.c_int32, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_u32,
+                                  ctypes.c_uint64, c_vp, c_vp],
+    "fps_ring_push": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp],
+    "fps_known_append": [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "fps_sample_alias": [c_vp, c_vp, ctypes.c_int32, c_i64, c_u32, ctypes.c_uint64, c_vp, c_vp],
     "fps_sgns_step": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp],

@@ -256,15 +256,19 @@ def rnd(seed: int, counter: int, i: torch.Tensor, salt) -> torch.Tensor:
     return h
 
 
-def sample_uniform_reject(n, k, n_items, positive=None, user=None, ring=None, mem=0, seed=0, counter=0):
+def sample_uniform_reject(n, k, n_items, positive=None, user=None, ring=None, mem=0, seed=0, counter=0,
+                          known=None, known_count=None):
     t = torch.arange(n * k, dtype=torch.int64)
     b = t // k
     pos = positive.long()[b] if positive is not None else torch.full_like(t, -1)
     out = torch.zeros(n * k, dtype=torch.int64)
     done = torch.zeros(n * k, dtype=torch.bool)
     rows = ring.long().view(-1, mem)[user.long()[b]] if (ring is not None and user is not None and mem) else None
+    span = max(int(known_count), 1) if known is not None else n_items
     for tries in range(32):
-        cand = (rnd(seed, counter, t, tries) * n_items) >> 32
+        cand = (rnd(seed, counter, t, tries) * span) >> 32
+        if known is not None:
+            cand = known.long()[cand]
         bad = cand == pos
         if rows is not None:
             bad |= (rows == cand[:, None]).any(1)
@@ -272,6 +276,21 @@ def sample_uniform_reject(n, k, n_items, positive=None, user=None, ring=None, me
         out[take] = cand[take]
         done |= ~bad
     return out.to(torch.int32)
+
+
+def ring_push(ring, cursor, uid, iid, mem):
+    """Sequential ring push (the GPU takes slots in atomic arrival order)."""
+    for u, i in zip(uid.tolist(), iid.tolist()):
+        ring[u * mem + int(cursor[u]) % mem] = i
+        cursor[u] += 1
+
+
+def known_append(flag, lst, count, iid):
+    for i in iid.tolist():
+        if int(flag[i]) == 0:
+            flag[i] = 1
+            lst[int(count[0])] = i
+            count[0] += 1
 
 
 def sample_alias(prob, alias, n, seed=0, counter=0):

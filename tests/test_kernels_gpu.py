@@ -253,3 +253,30 @@ def test_mf_sgd_tiled_duplicate_items_accumulate():
     # start; a tile with > 4096 ratings runs in 2 chunks (second sees the first's sum)
     torch.testing.assert_close(I.cpu(), Ir, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(U.cpu(), Ur, rtol=1e-2, atol=2e-5)
+
+
+def test_ring_known_and_known_list_sampling_match_reference():
+    nu, ni, mem = 500, 3000, 8
+    ring_g = torch.full((nu * mem,), -1, dtype=torch.int32, device=DEV)
+    cur_g = torch.zeros(nu, dtype=torch.int32, device=DEV)
+    ring_r, cur_r = ring_g.cpu().clone(), cur_g.cpu().clone()
+    flag_g = torch.zeros(ni, dtype=torch.int32, device=DEV)
+    lst_g = torch.zeros(ni, dtype=torch.int32, device=DEV)
+    cnt_g = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for step in range(3):  # unique users per push: slot order is deterministic
+        uid = torch.randperm(nu, dtype=torch.int32)[:400]
+        iid = torch.randint(0, ni // 2, (400,), dtype=torch.int32)
+        ops.ring_push(ring_g, cur_g, uid.to(DEV), iid.to(DEV), mem)
+        R.ring_push(ring_r, cur_r, uid, iid, mem)
+        ops.known_append(flag_g, lst_g, cnt_g, iid.to(DEV))
+    assert torch.equal(ring_g.cpu(), ring_r) and torch.equal(cur_g.cpu(), cur_r)
+    n_known = int(cnt_g[0])
+    known_set = set(lst_g[:n_known].cpu().tolist())
+    assert known_set == set(torch.nonzero(flag_g.cpu()).flatten().tolist()) and len(known_set) == n_known
+    uid = torch.randint(0, nu, (1000,), dtype=torch.int32)
+    pos = torch.randint(0, ni, (1000,), dtype=torch.int32)
+    g = ops.sample_uniform_reject(1000, 3, ni, pos.to(DEV), uid.to(DEV), ring_g, mem, seed=4, counter=2,
+                                  device=DEV, known=lst_g, known_count=cnt_g).cpu()
+    r = R.sample_uniform_reject(1000, 3, ni, pos, uid, ring_r, mem, 4, 2, lst_g.cpu(), n_known)
+    assert torch.equal(g, r)  # same known list on both sides
+    assert set(g.tolist()) <= known_set
