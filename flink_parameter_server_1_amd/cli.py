@@ -256,6 +256,10 @@ def build_parser():
     p.add_argument("--dim", type=int)
     p.add_argument("--learning-rate", type=float)
     p.add_argument("--wire-dtype")
+    p.add_argument("--exchange", choices=["auto", "rotate", "ps", "local"])
+    p.add_argument("--sgd-mode", choices=["auto", "tiled", "flat", "grouped"])
+    p.add_argument("--negative-sample-rate", type=int)
+    p.add_argument("--user-memory", type=int)
     p.add_argument("--batch", type=int, default=1 << 20)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--truth-dim", type=int, default=8)
