@@ -1,0 +1,167 @@
+// Running top-K merge for the LEMP bucket scan (gfx950).  Kernel K13.
+//
+// After the MFMA score GEMM of a query batch against one length-sorted item
+// bucket (score_gemm.hip), every query row of S[B, n] must be merged into the
+// query's running top-k (best_s / best_i, sorted descending).  torch.topk over
+// [B, k + n] re-selects from scratch (3.5 ms per 4096 x 65536 bucket,
+// profiles/r1_topk_bench.jsonl).  Here one workgroup per query:
+//
+//   1. tau = current k-th best.  Count the row's scores > tau (after the first
+//      bucket nearly none pass: the reference's own pruning argument,
+//      M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:35-114).
+//   2. If more than CAP pass (first bucket), raise the threshold with a 2-level
+//      radix histogram (11 + 11 bits of the order-preserving float key) to the
+//      largest value that still keeps >= k candidates.
+//   3. Collect the candidates into LDS, append the running top-k, bitonic-sort
+//      (key desc, then item id asc for ties) and keep the first k.
+//
+// Exact whenever fewer than CAP scores share the 22-bit key prefix of the k-th
+// best (ties beyond that are cut at CAP).
+#include "common.h"
+
+using namespace fps;
+
+namespace {
+
+constexpr int TK_NT = 256;
+constexpr int TK_CAP = 2048;          // collected candidates per query
+constexpr int TK_MAXK = 256;          // running top-k capacity
+constexpr int TK_SORT = 4096;         // pow2 >= TK_CAP + TK_MAXK
+constexpr int TK_BINS = 2048;         // 11-bit radix digits
+
+__device__ __forceinline__ uint32_t fkey(float f) {  // order-preserving float -> uint32
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float kfloat(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// among hist[0..TK_BINS), find the highest bin b with (#elements in bins >= b) >= need;
+// returns b and the count of elements in bins > b via *above (one thread scans:
+// at most two calls per query row, 2048 bins)
+__device__ int select_bin(const uint32_t* hist, uint32_t need, uint32_t* above, int* bin_out) {
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    int b = -1;
+    for (int i = TK_BINS - 1; i >= 0; --i) {
+      if (run + hist[i] >= need) { b = i; break; }
+      run += hist[i];
+    }
+    *bin_out = b < 0 ? 0 : b;
+    *above = run;
+  }
+  __syncthreads();
+  return *bin_out;
+}
+
+__global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restrict__ S, int64_t ldS, int n,
+                                                           const int64_t* __restrict__ ids,
+                                                           float* __restrict__ best_s, int64_t* __restrict__ best_i,
+                                                           int k) {
+  __shared__ uint32_t hist[TK_BINS];
+  __shared__ uint32_t skey[TK_SORT];
+  __shared__ int64_t sid[TK_SORT];
+  __shared__ uint32_t cnt, above;
+  __shared__ int bin_sel;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* s = S + (int64_t)row * ldS;
+  float* bs = best_s + (int64_t)row * k;
+  int64_t* bi = best_i + (int64_t)row * k;
+  const float tau = bs[k - 1];
+  const uint32_t ktau = fkey(tau);
+  // 1. count candidates strictly above tau
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  for (int j = tid; j < n; j += TK_NT) c += fkey(s[j]) > ktau;
+  c = (uint32_t)group_sum<64>((float)c);  // exact for counts < 2^24
+  if ((tid & 63) == 0) atomicAdd(&cnt, c);
+  __syncthreads();
+  uint32_t thr = ktau + 1;  // keys >= thr are candidates
+  if (cnt > TK_CAP) {
+    // 2a. histogram of the top 11 key bits over the candidates
+    for (int i = tid; i < TK_BINS; i += TK_NT) hist[i] = 0;
+    __syncthreads();
+    for (int j = tid; j < n; j += TK_NT) {
+      const uint32_t kk = fkey(s[j]);
+      if (kk >= thr) atomicAdd(&hist[kk >> 21], 1u);
+    }
+    __syncthreads();
+    const int b1 = select_bin(hist, (uint32_t)k, &above, &bin_sel);
+    uint32_t total = above + hist[b1];
+    uint32_t t1 = (uint32_t)b1 << 21;
+    thr = t1 > thr ? t1 : thr;
+    __syncthreads();
+    if (total > TK_CAP) {
+      // 2b. refine inside bin b1 with the next 11 bits
+      const uint32_t need2 = (uint32_t)k > above ? (uint32_t)k - above : 1u;
+      for (int i = tid; i < TK_BINS; i += TK_NT) hist[i] = 0;
+      __syncthreads();
+      for (int j = tid; j < n; j += TK_NT) {
+        const uint32_t kk = fkey(s[j]);
+        if ((kk >> 21) == (uint32_t)b1 && kk >= thr) atomicAdd(&hist[(kk >> 10) & (TK_BINS - 1)], 1u);
+      }
+      __syncthreads();
+      const int b2 = select_bin(hist, need2, &above, &bin_sel);
+      const uint32_t t2 = ((uint32_t)b1 << 21) | ((uint32_t)b2 << 10);
+      thr = t2 > thr ? t2 : thr;
+      __syncthreads();
+    }
+  }
+  // 3. collect candidates (key >= thr), cut at TK_CAP
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  for (int j = tid; j < n; j += TK_NT) {
+    const uint32_t kk = fkey(s[j]);
+    if (kk >= thr) {
+      const uint32_t slot = atomicAdd(&cnt, 1u);
+      if (slot < TK_CAP) { skey[slot] = kk; sid[slot] = ids[j]; }
+    }
+  }
+  __syncthreads();
+  const int nc = (int)min(cnt, (uint32_t)TK_CAP);
+  // append the running top-k, pad to a power of two
+  int m = nc + k;
+  int P = 1;
+  while (P < m) P <<= 1;
+  for (int i = tid; i < P; i += TK_NT) {
+    if (i >= nc && i < m) { skey[i] = fkey(bs[i - nc]); sid[i] = bi[i - nc]; }
+    else if (i >= m) { skey[i] = 0u; sid[i] = INT64_MAX; }
+  }
+  __syncthreads();
+  // 4. bitonic sort, descending by key (ties: smaller id first)
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P; i += TK_NT) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const uint32_t ki = skey[i], kj = skey[j];
+          const int64_t ii = sid[i], ij = sid[j];
+          // "i before j" in the final order: larger key, or equal key and smaller id
+          const bool i_first = ki > kj || (ki == kj && ii < ij);
+          if (desc != i_first) { skey[i] = kj; skey[j] = ki; sid[i] = ij; sid[j] = ii; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += TK_NT) {
+    bs[i] = kfloat(skey[i]);
+    bi[i] = skey[i] == 0u ? -1 : sid[i];
+  }
+}
+
+}  // namespace
+
+// best_s / best_i: [B, k] sorted descending (start: -inf / -1); S: [B, n] with row stride ldS
+FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int64_t* ids, float* best_s,
+                           int64_t* best_i, int k, void* stream) {
+  if (B <= 0 || n <= 0) return 0;
+  if (k <= 0 || k > TK_MAXK) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s, best_i,
+                     k);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}

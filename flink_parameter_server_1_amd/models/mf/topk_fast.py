@@ -57,10 +57,13 @@ class LempTopK:
             if S is None or S.shape[1] < n:
                 S = torch.empty((B, self.bucket), device=dev)
             ops.score_gemm(Q, self.vecs[s:e], S[:, :n])
-            cand_s = torch.cat([best_s, S[:, :n]], 1)
-            top_s, top_j = torch.topk(cand_s, min(k, cand_s.shape[1]), dim=1)
-            cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
-            best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
+            if dev.type == "cuda" and k <= ops.TOPK_MAX_K:
+                ops.topk_merge(S[:, :n], self.ids[s:e], best_s, best_i)  # threshold filter + LDS sort
+            else:
+                cand_s = torch.cat([best_s, S[:, :n]], 1)
+                top_s, top_j = torch.topk(cand_s, min(k, cand_s.shape[1]), dim=1)
+                cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
+                best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
             self.buckets_scanned += 1
         return best_s, best_i
 

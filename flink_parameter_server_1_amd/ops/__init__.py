@@ -571,6 +571,30 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
     return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out)])
 
 
+TOPK_MAX_K = 256
+
+
+def topk_merge(S: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, best_i: torch.Tensor) -> None:
+    """Merge each row of ``S[B, n]`` (item ids ``ids[n]``) into the running top-k
+    ``best_s``/``best_i`` ``[B, k]`` (sorted descending; start -inf / -1) in place (K13)."""
+    B, n = S.shape
+    k = best_s.shape[1]
+    if _on_gpu(S):
+        if k > TOPK_MAX_K:
+            raise ValueError(f"topk_merge: k <= {TOPK_MAX_K}")
+        if S.stride(1) != 1:
+            raise ValueError("topk_merge: S needs unit column stride")
+        N.check(N.require().fps_topk_merge(S.data_ptr(), S.stride(0), B, n, _c(ids.long()).data_ptr(),
+                                           _c(best_s).data_ptr(), _c(best_i).data_ptr(), k, N.stream_ptr(S.device)),
+                "topk_merge")
+        return
+    cand_s = torch.cat([best_s, S], 1)
+    cand_i = torch.cat([best_i, ids.long().expand(B, n)], 1)
+    top_s, j = torch.topk(cand_s, k, dim=1)
+    best_s.copy_(top_s)
+    best_i.copy_(torch.gather(cand_i, 1, j))
+
+
 def score_gemm(Q: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """``out[b, i] = <Q[b], X[i]>`` on MFMA (fp32 in/accumulate, K8 scoring).  ``out`` may be
     a column slice of a wider buffer (row stride taken from it)."""

@@ -79,3 +79,30 @@ def test_lemp_topk_gpu_exact():
     bs, bi = torch.topk(Q @ X.T, 100, dim=1)
     torch.testing.assert_close(s, bs, rtol=1e-5, atol=1e-4)
     assert float((i == bi).float().mean()) > 0.999  # ties may reorder
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 10, 100, 256])
+@pytest.mark.parametrize("n", [100, 5000, 65536])
+def test_topk_merge_kernel_exact(k, n):
+    """Running-top-k merge kernel == torch.topk over [best, S] (two rounds: -inf start, then merge)."""
+    torch.manual_seed(k + n)
+    B = 64
+    best_s = torch.full((B, k), float("-inf"), device="cuda")
+    best_i = torch.full((B, k), -1, dtype=torch.long, device="cuda")
+    ref_s, ref_i = best_s.cpu().clone(), best_i.cpu().clone()
+    for rnd in range(2):
+        S = torch.randn(B, n, device="cuda")
+        if rnd == 1:
+            S[:, : n // 3] += 2.0  # many new candidates above the running k-th best
+        ids = torch.arange(n, device="cuda") + rnd * n
+        ops.topk_merge(S, ids, best_s, best_i)
+        cs = torch.cat([ref_s, S.cpu()], 1)
+        ci = torch.cat([ref_i, ids.cpu().expand(B, n)], 1)
+        kk = min(k, cs.shape[1])
+        ts, tj = torch.topk(cs, kk, dim=1)
+        ref_s[:, :kk], ref_i[:, :kk] = ts, torch.gather(ci, 1, tj)
+        torch.testing.assert_close(best_s.cpu()[:, :kk], ref_s[:, :kk])
+        # ids equal wherever the score is not tied with a neighbour
+        same = (best_i.cpu()[:, :kk] == ref_i[:, :kk]) | (ref_s[:, :kk].diff(dim=1, prepend=ref_s[:, :1] + 1) == 0)
+        assert bool(same.all())
