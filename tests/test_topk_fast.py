@@ -103,6 +103,10 @@ def test_topk_merge_kernel_exact(k, n):
         ts, tj = torch.topk(cs, kk, dim=1)
         ref_s[:, :kk], ref_i[:, :kk] = ts, torch.gather(ci, 1, tj)
         torch.testing.assert_close(best_s.cpu()[:, :kk], ref_s[:, :kk])
-        # ids equal wherever the score is not tied with a neighbour
-        same = (best_i.cpu()[:, :kk] == ref_i[:, :kk]) | (ref_s[:, :kk].diff(dim=1, prepend=ref_s[:, :1] + 1) == 0)
+        # ids equal wherever the score is not tied with a neighbour (x + 2.0 rounds: ties happen)
+        rs = ref_s[:, :kk]
+        tie = torch.zeros_like(rs, dtype=torch.bool)
+        tie[:, 1:] |= rs[:, 1:] == rs[:, :-1]
+        tie[:, :-1] |= rs[:, :-1] == rs[:, 1:]
+        same = (best_i.cpu()[:, :kk] == ref_i[:, :kk]) | tie
         assert bool(same.all())
