@@ -70,14 +70,17 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   int64_t* bi = best_i + (int64_t)row * k;
   const float tau = bs[k - 1];
   const uint32_t ktau = fkey(tau);
-  // 1. count candidates strictly above tau
-  if (tid == 0) cnt = 0;
+  // 1. count candidates strictly above tau (an empty running list: all n pass,
+  //    no counting pass needed)
+  if (tid == 0) cnt = tau == -INFINITY ? (uint32_t)n : 0u;
   __syncthreads();
-  uint32_t c = 0;
-  for (int j = tid; j < n; j += TK_NT) c += fkey(s[j]) > ktau;
-  c = (uint32_t)group_sum<64>((float)c);  // exact for counts < 2^24
-  if ((tid & 63) == 0) atomicAdd(&cnt, c);
-  __syncthreads();
+  if (tau != -INFINITY) {
+    uint32_t c = 0;
+    for (int j = tid; j < n; j += TK_NT) c += fkey(s[j]) > ktau;
+    c = (uint32_t)group_sum<64>((float)c);  // exact for counts < 2^24
+    if ((tid & 63) == 0) atomicAdd(&cnt, c);
+    __syncthreads();
+  }
   uint32_t thr = ktau + 1;  // keys >= thr are candidates
   if (cnt > TK_CAP) {
     // 2a. histogram of the top 11 key bits over the candidates
