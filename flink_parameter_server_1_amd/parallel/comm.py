@@ -13,8 +13,11 @@ would be bound by one link.  Three all-to-all phases per micro-batch:
                                        order -- the reference's FIFO property)
   X1' deltas worker -> owner shard    (fp32 or bf16 rows, pre-reduced per key)
 
-Gloo provides the same calls on CPU (multi-process tests).  ``world == 1``
-short-circuits every exchange to a local copy.
+Gloo provides the same calls on CPU (multi-process tests).  With gloo and
+GPU tensors (several ranks sharing one GPU: the full device compute path with
+a host transport -- rehearsal of the multi-GPU code on a one-GPU box) every
+exchange is staged through host memory.  ``world == 1`` short-circuits every
+exchange to a local copy.
 """
 from __future__ import annotations
 
@@ -65,6 +68,11 @@ class Comm:
             dist.init_process_group(**kw)
         return Comm(device=device)
 
+    # ------------------------------------------------------------- staging
+    def _staged(self, t: torch.Tensor) -> bool:
+        """gloo cannot move device tensors: stage them through host memory."""
+        return self.backend == "gloo" and t.is_cuda
+
     # ------------------------------------------------------------- collectives
     def barrier(self):
         if self.world > 1:
@@ -77,6 +85,8 @@ class Comm:
         """Every rank tells every other how many rows it will send it."""
         if self.world == 1:
             return send_counts.clone()
+        if self._staged(send_counts):
+            return self.exchange_counts(send_counts.cpu()).to(send_counts.device)
         recv = torch.empty_like(send_counts)
         dist.all_to_all_single(recv, send_counts, group=self.group)
         return recv
@@ -94,6 +104,12 @@ class Comm:
             out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
         row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
         self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
+        if self._staged(send):
+            host_out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype)
+            dist.all_to_all_single(host_out, send[: int(sum(send_splits))].cpu(), list(map(int, recv_splits)),
+                                   list(map(int, send_splits)), group=self.group)
+            out[:n_out].copy_(host_out)
+            return out
         dist.all_to_all_single(out[:n_out], send[: int(sum(send_splits))], list(map(int, recv_splits)),
                                list(map(int, send_splits)), group=self.group)
         return out
@@ -104,6 +120,8 @@ class Comm:
         n_out = int(sum(recv_splits))
         if self.world == 1:
             return send[:n_out], None
+        if self._staged(send):  # host-staged transport is synchronous
+            return self.all_to_all(send, send_splits, recv_splits), None
         out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
         row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
         self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
@@ -113,15 +131,39 @@ class Comm:
 
     def all_reduce(self, t: torch.Tensor, op=None) -> torch.Tensor:
         if self.world > 1:
-            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
+            if self._staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, op=op or dist.ReduceOp.SUM, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t
 
     def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
         if self.world == 1:
             return [t]
+        if self._staged(t):
+            return [x.to(t.device) for x in self.all_gather(t.cpu())]
         outs = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(outs, t, group=self.group)
         return outs
+
+    def p2p(self, sends: Sequence, recvs: Sequence) -> list:
+        """Batched point-to-point: ``sends`` / ``recvs`` are ``(tensor, peer)`` pairs,
+        posted as one group (no ordering deadlock between pairs of ranks).  Returns
+        the works to wait on (empty when the transfer already completed: staged)."""
+        if self.backend == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs)):
+            host_recvs = [(torch.empty(t.shape, dtype=t.dtype), peer) for t, peer in recvs]
+            ops = [dist.P2POp(dist.isend, t.cpu(), peer, group=self.group) for t, peer in sends]
+            ops += [dist.P2POp(dist.irecv, h, peer, group=self.group) for h, peer in host_recvs]
+            for w in (dist.batch_isend_irecv(ops) if ops else []):
+                w.wait()
+            for (t, _), (h, _) in zip(recvs, host_recvs):
+                t.copy_(h)
+            return []
+        ops = [dist.P2POp(dist.isend, t, peer, group=self.group) for t, peer in sends]
+        ops += [dist.P2POp(dist.irecv, t, peer, group=self.group) for t, peer in recvs]
+        return dist.batch_isend_irecv(ops) if ops else []
 
     def max_over_ranks(self, x: float) -> float:
         if self.world == 1:

@@ -32,7 +32,6 @@ from __future__ import annotations
 from typing import List, Optional
 
 import torch
-import torch.distributed as dist
 
 from .comm import Comm
 
@@ -101,9 +100,8 @@ class RingRotation:
             return
         out_b = (2 * self.r + self.s - 1) % self.K
         in_b = (2 * self.r + self.s + 1) % self.K
-        ops = [dist.P2POp(dist.isend, self.buf[self._P][: self.rows[out_b]], self._peer(-1), group=self.comm.group),
-               dist.P2POp(dist.irecv, self.buf[self._F][: self.rows[in_b]], self._peer(+1), group=self.comm.group)]
-        self._works = dist.batch_isend_irecv(ops)
+        self._works = self.comm.p2p([(self.buf[self._P][: self.rows[out_b]], self._peer(-1))],
+                                    [(self.buf[self._F][: self.rows[in_b]], self._peer(+1))])
         self.bytes_sent += self.buf[self._P][: self.rows[out_b]].numel() * self.buf[0].element_size()
 
     def end(self):
@@ -140,17 +138,17 @@ class RingRotation:
 
         # messages between one pair are matched in posting order: post sends and
         # receives in ascending block id on both sides
-        ops = []
+        sends, recvs = [], []
         for b, bi in sorted(held.items()):
             dst = b // 2
             if dst != self.r:
-                ops.append(dist.P2POp(dist.isend, self.buf[bi][: self.rows[b]], dst, group=self.comm.group))
+                sends.append((self.buf[bi][: self.rows[b]], dst))
         for h in (0, 1):
             b = 2 * self.r + h
             src = holder(b)
             if src != self.r:
-                ops.append(dist.P2POp(dist.irecv, self._home_slice(h), src, group=self.comm.group))
-        works = dist.batch_isend_irecv(ops) if ops else []
+                recvs.append((self._home_slice(h), src))
+        works = self.comm.p2p(sends, recvs)
         for b, bi in held.items():
             if b // 2 == self.r:
                 self._home_slice(b % 2).copy_(self.buf[bi][: self.rows[b]])
