@@ -54,9 +54,14 @@ class Comm:
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         use_gpu = torch.cuda.is_available()
+        # rehearsal of the multi-GPU launch on a one-GPU box: FPS_SHARE_GPU=1 puts
+        # every rank on cuda:0 and defaults the backend to gloo (host-staged)
+        share = os.environ.get("FPS_SHARE_GPU", "0") == "1"
+        backend = backend or os.environ.get("FPS_DIST_BACKEND") or ("gloo" if share else None)
         if use_gpu:
-            torch.cuda.set_device(local_rank)
-            device = torch.device("cuda", local_rank)
+            dev_index = 0 if share else local_rank
+            torch.cuda.set_device(dev_index)
+            device = torch.device("cuda", dev_index)
         else:
             device = torch.device("cpu")
         if world > 1 and not dist.is_initialized():
