@@ -104,16 +104,25 @@ __global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restri
   if (threadIdx.x == 1023) ptr[KT] = part[1023];
 }
 
-// K4: scatter packed 16-B records {uid, row-in-block, rating bits, 0} to
-// ptr[bucket] + H[w][bucket] + LDS slot (one 16-B store per rating instead of
-// three scattered 4-B stores)
+// Packed rating records.  REC8 (users < 2^24, R <= 256): 8 B {uid | row_in_tile << 24,
+// rating bits}; else 16 B {uid, row-in-block, rating bits, bucket}.
+template <bool REC8>
+__device__ __forceinline__ void put_rec(void* rec, int64_t o, int32_t uid, int32_t row, float rating, int bucket,
+                                        int R) {
+  if (REC8) reinterpret_cast<int2*>(rec)[o] = make_int2(uid | ((row & (R - 1)) << 24), __float_as_int(rating));
+  else reinterpret_cast<int4*>(rec)[o] = make_int4(uid, row, __float_as_int(rating), bucket);
+}
+
+// K4: scatter packed records to ptr[bucket] + H[w][bucket] + LDS slot (one
+// store per rating instead of three scattered 4-B stores)
+template <bool REC8>
 __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __restrict__ uid,
                                                             const int32_t* __restrict__ iid,
                                                             const float* __restrict__ rating, int64_t n,
                                                             int64_t chunk, int W, const int32_t* __restrict__ half,
                                                             int R, int T, int KT, const int32_t* __restrict__ H,
                                                             const int32_t* __restrict__ ptr,
-                                                            int4* __restrict__ rec) {
+                                                            void* __restrict__ rec) {
   __shared__ int32_t cur[TP_MAX_BUCKETS];
   const int32_t* Hw = H + (int64_t)blockIdx.x * KT;
   for (int k = threadIdx.x; k < KT; k += blockDim.x) cur[k] = ptr[k] + Hw[k];
@@ -123,7 +132,7 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
     int bk; int32_t row;
     tile_bucket(iid[x], W, half, R, T, bk, row);
     const int32_t o = atomicAdd(cur + bk, 1);
-    rec[o] = make_int4(uid[x], row, __float_as_int(rating[x]), 0);
+    put_rec<REC8>(rec, o, uid[x], row, rating[x], bk, R);
   }
 }
 
@@ -163,14 +172,14 @@ __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restri
 
 // LEVEL 1: records from (uid, iid, rating), key = coarse; out = {uid, row, rating, bucket}
 // LEVEL 2: records from tmp, key = bucket (tmp.w); out = the same record
-template <int LEVEL>
+template <int LEVEL, bool REC8>
 __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __restrict__ uid,
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
                                                            const int4* __restrict__ tmp, int64_t n, int64_t chunk,
                                                            int W, const int32_t* __restrict__ half, int R, int T,
                                                            int cshift, int nkeys, const int32_t* __restrict__ ptr,
-                                                           int32_t* __restrict__ cursor, int4* __restrict__ out) {
+                                                           int32_t* __restrict__ cursor, void* __restrict__ out) {
   __shared__ int32_t h[TP_MAX_BUCKETS];
   for (int k = threadIdx.x; k < nkeys; k += blockDim.x) h[k] = 0;
   __syncthreads();
@@ -202,7 +211,9 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
       r = tmp[x];
       key = r.w;
     }
-    out[atomicAdd(h + key, 1)] = r;
+    const int32_t o = atomicAdd(h + key, 1);
+    if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = r;  // level 1 keeps the bucket for level 2
+    else put_rec<REC8>(out, o, r.x, r.y, __int_as_float(r.z), r.w, R);
   }
 }
 
@@ -210,12 +221,34 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
 constexpr int TG_CAP = 4096;    // records staged per chunk (64 KiB of LDS)
 constexpr int TG_MAX_R = 256;   // rows per tile
 
-template <int TPR, int V, int PF>
+template <bool REC8>
+struct RecT { using type = int4; };
+template <>
+struct RecT<true> { using type = int2; };
+
+// (uid, row in tile, rating) of a staged record
+template <bool REC8>
+__device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int64_t r0, int32_t& uid, int& row,
+                                        float& rating) {
+  if constexpr (REC8) {
+    uid = x.x & 0xffffff;
+    row = (int)((uint32_t)x.x >> 24);
+    rating = __int_as_float(x.y);
+  } else {
+    uid = x.x;
+    row = (int)(x.y - r0);
+    rating = __int_as_float(x.z);
+  }
+}
+
+template <int TPR, int V, int PF, bool REC8>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
-                                                               const int4* __restrict__ rec,
+                                                               const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
                                                                int64_t block_rows, float lr, float lambda) {
-  __shared__ int4 srec[TG_CAP];
+  using Rec = typename RecT<REC8>::type;
+  const Rec* __restrict__ rec = reinterpret_cast<const Rec*>(rec_);
+  __shared__ Rec srec[TG_CAP];
   __shared__ int16_t order[TG_CAP];
   __shared__ int32_t cnt[TG_MAX_R + 1];
   __shared__ int32_t start[TG_MAX_R + 1];
@@ -235,9 +268,11 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
     for (int k = threadIdx.x; k <= nr; k += blockDim.x) cnt[k] = 0;
     __syncthreads();
     for (int k = threadIdx.x; k < nc; k += blockDim.x) {
-      const int4 x = rec[c0 + k];
+      const Rec x = rec[c0 + k];
       srec[k] = x;
-      atomicAdd(cnt + (x.y - (int32_t)r0), 1);
+      int32_t u; int rw; float rt;
+      get_rec<REC8>(x, r0, u, rw, rt);
+      atomicAdd(cnt + rw, 1);
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive scan of <= 256 counters
@@ -246,7 +281,11 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
       start[nr] = run;
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nc; k += blockDim.x) order[atomicAdd(cnt + (srec[k].y - (int32_t)r0), 1)] = (int16_t)k;
+    for (int k = threadIdx.x; k < nc; k += blockDim.x) {
+      int32_t u; int rw; float rt;
+      get_rec<REC8>(srec[k], r0, u, rw, rt);
+      order[atomicAdd(cnt + rw, 1)] = (int16_t)k;
+    }
     __syncthreads();
     for (int row = grp; row < nr; row += ngroups) {
       const int a = start[row], b = start[row + 1];
@@ -263,9 +302,9 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
         float rv[PF];
 #pragma unroll
         for (int q = 0; q < PF; ++q) {  // all PF user rows in flight (index clamped, result masked)
-          const int4 x = srec[order[min(k0 + q, b - 1)]];
-          ur[q] = (int64_t)x.x * D4;
-          rv[q] = __int_as_float(x.z);
+          int32_t u; int rw;
+          get_rec<REC8>(srec[order[min(k0 + q, b - 1)]], r0, u, rw, rv[q]);
+          ur[q] = (int64_t)u * D4;
 #pragma unroll
           for (int v = 0; v < V; ++v) uv[q][v] = Ug[ur[q] + j + v * TPR];
         }
@@ -320,10 +359,10 @@ FPS_API int fps_tile_partition_groups(int64_t n) {
   return (int)g;
 }
 
-// rec: n packed records {uid, row-in-block, rating bits, 0} grouped by bucket
+// rec: n packed records (8 B if rec8, else 16 B; see put_rec) grouped by bucket
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                                const int32_t* half, int R, int T, int32_t* H, int32_t* totals, int32_t* ptr,
-                               int4* rec, uint8_t* seen, void* stream) {
+                               void* rec, int rec8, uint8_t* seen, void* stream) {
   const int KT = 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -332,9 +371,14 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   hipLaunchKernelGGL(tile_hist_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, KT, H, seen);
   hipLaunchKernelGGL(tile_colscan_kernel, dim3((KT + 255) / 256), dim3(256), 0, s, H, G, KT, totals);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)totals, KT, ptr);
-  if (n > 0)
-    hipLaunchKernelGGL(tile_scatter_kernel, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half, R, T,
-                       KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+  if (n > 0) {
+    if (rec8)
+      hipLaunchKernelGGL(tile_scatter_kernel<true>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half, R,
+                         T, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+    else
+      hipLaunchKernelGGL(tile_scatter_kernel<false>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half,
+                         R, T, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+  }
   FPS_CHECK_LAUNCH();
   return 0;
 }
@@ -343,8 +387,8 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // bcount[KT], bcursor[KT] (all zeroed here), tmp: n int4.  ptr[KT+1] = tile
 // offsets, rec: n records {uid, row-in-block, rating bits, bucket}.
 FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
-                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, int4* rec,
-                                uint8_t* seen, void* stream) {
+                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
+                                int rec8, uint8_t* seen, void* stream) {
   const int KT = 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   int cshift = 0;
@@ -365,10 +409,15 @@ FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const fl
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
   if (n > 0) {
-    hipLaunchKernelGGL(tp2_scatter_kernel<1>, dim3(G), dim3(1024), 0, s, uid, iid, rating, (const int4*)nullptr, n,
-                       chunk, W, half, R, T, cshift, NC, (const int32_t*)cptr, ccursor, tmp);
-    hipLaunchKernelGGL(tp2_scatter_kernel<2>, dim3(G), dim3(1024), 0, s, uid, iid, rating, (const int4*)tmp, n,
-                       chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+    hipLaunchKernelGGL((tp2_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                       (const int4*)nullptr, n, chunk, W, half, R, T, cshift, NC, (const int32_t*)cptr, ccursor,
+                       (void*)tmp);
+    if (rec8)
+      hipLaunchKernelGGL((tp2_scatter_kernel<2, true>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+    else
+      hipLaunchKernelGGL((tp2_scatter_kernel<2, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
   }
   FPS_CHECK_LAUNCH();
   return 0;
@@ -384,15 +433,17 @@ FPS_API int64_t fps_tile_partition2_ws_ints(int W, int T) {
 
 // One launch per item block: T tiles of R (<= 256) rows of I[block_rows, D];
 // ptr = the block's T+1 tile offsets (device).  D must be 16, 32, 64, 128 or 256.
-FPS_API int fps_mf_sgd_tiled(float* U, float* I, const int4* rec, const int32_t* ptr, int T, int R,
+FPS_API int fps_mf_sgd_tiled(float* U, float* I, const void* rec, int rec8, const int32_t* ptr, int T, int R,
                              int64_t block_rows, int D, float lr, float lambda, void* stream) {
   if (T <= 0) return 0;
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
 #define FPS_TILED(TPR_, V_)                                                                                    \
-  hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF>), dim3(T), dim3(512), 0, s, U, I, rec, ptr, R,   \
-                     block_rows, lr, lambda)
+  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(T), dim3(512), 0, s, U, I,  \
+                               rec, ptr, R, block_rows, lr, lambda);                                          \
+  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(T), dim3(512), 0, s, U, I, rec, \
+                          ptr, R, block_rows, lr, lambda)
   switch (D) {
     case 16: FPS_TILED(4, 1); break;
     case 32: FPS_TILED(8, 1); break;

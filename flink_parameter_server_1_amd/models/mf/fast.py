@@ -119,8 +119,9 @@ class DistributedMF:
             # two partition buffers: with prefetch the partition of batch k+1 runs on a
             # side stream while batch k's SGD runs (one micro-batch of latency, flush()
             # completes it; same SGD order)
+            rec8 = self.users.n_local < (1 << 24)  # 8-B rating records (user index in 24 bits)
             self._tilers = [ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T,
-                                                dev) for _ in range(2)]
+                                                dev, rec8=rec8) for _ in range(2)]
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
             self._prefetch = cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None

@@ -335,8 +335,11 @@ class TilePartitioner:
     ``rec`` an int32 ``[n, 4]`` array of packed records {uid, row-in-block,
     rating bits, 0} grouped by bucket (on CPU: the three columns as tensors)."""
 
-    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None):
+    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None, rec8: bool = False):
         self.W, self.R, self.T = W, int(R), int(T)
+        # 8-B records {uid | row_in_tile << 24, rating}: users < 2^24, R <= 256
+        self.rec8 = bool(rec8) and self.R <= 256
+        self.rec_cols = 2 if self.rec8 else 4
         self.KT = 2 * W * self.T
         chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
         if chunk and self.device_is_cuda(device):
@@ -370,7 +373,7 @@ class TilePartitioner:
             self.H = torch.empty(self.g_cap, dtype=torch.int32, device=self.device)
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
-            self.rec = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
+            self.rec = torch.empty((self.cap, self.rec_cols), dtype=torch.int32, device=self.device)
             if self.levels == 2:
                 self.tmp = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
         if self.levels == 2:
@@ -380,24 +383,33 @@ class TilePartitioner:
             N.check(lib.fps_tile_partition2(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n,
                                             self.W, self.half.data_ptr(), self.R, self.T, self.ws.data_ptr(),
                                             self.tmp.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
-                                            N.ptr(seen), N.stream_ptr(self.device)), "tile_partition2")
+                                            int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)),
+                    "tile_partition2")
             return self.ptr, self.rec[:n]
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
                                        self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),
                                        self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
-                                       N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
+                                       int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]
 
     @staticmethod
     def device_is_cuda(device) -> bool:
         return torch.device(device).type == "cuda"
 
-    @staticmethod
-    def unpack(rec):
-        """(uid, row, rating) columns of packed records (tests / CPU)."""
+    def unpack(self, rec, ptr=None):
+        """(uid, row-in-block, rating) columns of packed records (tests / CPU);
+        8-B records need ``ptr`` to recover the tile of every record."""
         if isinstance(rec, tuple):
             return rec
-        return rec[:, 0], rec[:, 1], rec[:, 2].contiguous().view(torch.float32)
+        if rec.shape[1] == 4:
+            return rec[:, 0], rec[:, 1], rec[:, 2].contiguous().view(torch.float32)
+        x = rec[:, 0]
+        uid = x & 0xFFFFFF
+        row_in_tile = (x.long() >> 24) & 0xFF
+        counts = (ptr[1:] - ptr[:-1]).long()
+        bucket = torch.repeat_interleave(torch.arange(counts.numel(), device=rec.device), counts)
+        row = (bucket % self.T) * self.R + row_in_tile
+        return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
@@ -407,8 +419,8 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
-                                     _c(ptr).data_ptr() + 4 * block * T, T, tile_rows, I_block.shape[0], U.shape[1],
-                                     lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
+                                     int(rec.shape[1] == 2), _c(ptr).data_ptr() + 4 * block * T, T, tile_rows,
+                                     I_block.shape[0], U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
         return
     uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
