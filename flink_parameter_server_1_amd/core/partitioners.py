@@ -116,6 +116,55 @@ class RangePartitioner(Partitioner):
         return torch.arange(lo, lo + self.shard_size(num_ids, shard), dtype=torch.int64)
 
 
+class LookupPartitioner(Partitioner):
+    """Arbitrary id -> shard assignment given as a table (P2c: the reference's
+    custom ``WorkerToPS => Int`` partitioners, ``M/FlinkParameterServer.scala:198-199``,
+    on the device path).  ``owner[i]`` is the shard of id ``i``; a shard stores its
+    ids densely in id order.  The tensor engine addresses it through *virtual keys*
+    ``vkey = owner * block + local`` (``block`` = largest shard), i.e. as a range
+    partition of the virtual key space, so every dedup / all-to-all / gather kernel
+    is reused unchanged."""
+
+    kind = "lookup"
+
+    def __init__(self, n: int, owner):
+        super().__init__(n)
+        owner = torch.as_tensor(owner, dtype=torch.int64).cpu()
+        if owner.numel() and (int(owner.min()) < 0 or int(owner.max()) >= n):
+            raise ValueError("owner entries must lie in [0, n)")
+        self.owner = owner
+        counts = torch.bincount(owner, minlength=n)
+        self.counts = counts
+        self.block = max(1, int(counts.max())) if owner.numel() else 1
+        order = torch.argsort(owner, stable=True)
+        starts = torch.zeros(n + 1, dtype=torch.int64)
+        starts[1:] = torch.cumsum(counts, 0)
+        local = torch.empty_like(owner)
+        local[order] = torch.arange(owner.numel()) - starts[owner[order]]
+        self.local = local
+        if n * self.block >= (1 << 31):
+            raise ValueError("virtual key space exceeds int32")
+
+    def shard(self, param_id):
+        return int(self.owner[abs(int(param_id))])
+
+    def shard_tensor(self, ids):
+        return self.owner.to(ids.device)[ids.abs()]
+
+    def local_index(self, ids):
+        return self.local.to(ids.device)[ids.abs()]
+
+    def shard_size(self, num_ids: int, shard: int) -> int:
+        return int(self.counts[shard])
+
+    def global_ids(self, shard: int, num_ids: int) -> torch.Tensor:
+        return torch.nonzero(self.owner == shard).flatten()
+
+    def vkeys(self) -> torch.Tensor:
+        """``owner * block + local`` per id (int32)."""
+        return (self.owner * self.block + self.local).to(torch.int32)
+
+
 def range_partitioner_ps(feature_count: int):
     """``rangePartitionerPS(featureCount)(psParallelism)`` as a WorkerToPS partitioner."""
 

@@ -21,24 +21,33 @@ from typing import Optional, Tuple
 import torch
 
 from .. import ops
-from ..core.partitioners import HashPartitioner, RangePartitioner
+from ..core.partitioners import HashPartitioner, LookupPartitioner, RangePartitioner
 
 
 class ShardedTable:
-    PART_KIND = {"hash": 0, "range": 1}
+    PART_KIND = {"hash": 0, "range": 1, "lookup": 1}
 
     def __init__(self, num_ids: int, dim: int, rank: int = 0, world: int = 1, partition: str = "hash",
                  init: Tuple = ("uniform", -0.01, 0.01), seed: int = 0, device="cpu", optimizer: str = "add",
-                 track_touched: bool = True, dtype=torch.float32):
+                 track_touched: bool = True, dtype=torch.float32, owner: Optional[torch.Tensor] = None):
+        """``partition="lookup"`` takes ``owner[num_ids]`` (id -> shard): an arbitrary
+        assignment, addressed through virtual keys (``LookupPartitioner``)."""
         if partition not in self.PART_KIND:
             raise ValueError(partition)
         self.num_ids, self.dim, self.rank, self.world = int(num_ids), int(dim), rank, world
         self.partition = partition
         self.part_kind = self.PART_KIND[partition]
-        self.part = HashPartitioner(world) if partition == "hash" else RangePartitioner(world, num_ids)
+        self.device = torch.device(device)
+        if partition == "lookup":
+            if owner is None or len(owner) != self.num_ids:
+                raise ValueError("partition='lookup' needs owner[num_ids]")
+            self.part = LookupPartitioner(world, owner)
+            self._vkey = self.part.vkeys().to(self.device)
+            self._gids = self.part.global_ids(rank, self.num_ids).to(self.device)
+        else:
+            self.part = HashPartitioner(world) if partition == "hash" else RangePartitioner(world, num_ids)
         self.block = 1 if partition == "hash" else self.part.block
         self.n_local = self.part.shard_size(self.num_ids, rank)
-        self.device = torch.device(device)
         self.optimizer = optimizer
         self.seed = seed
         self.init_spec = init
@@ -56,7 +65,20 @@ class ShardedTable:
     def id_stride(self) -> int:
         return self.world if self.partition == "hash" else 1
 
+    @property
+    def key_space(self) -> int:
+        """Size of the key space the tensor PS dedups / routes (virtual keys for lookup)."""
+        return self.world * self.block if self.partition == "lookup" else self.num_ids
+
+    def route_keys(self, ids: torch.Tensor) -> torch.Tensor:
+        """Global ids -> routing keys (identity, or virtual keys for ``lookup``)."""
+        if self.partition == "lookup":
+            return self._vkey[ids.long()]
+        return ids
+
     def global_ids(self, local: torch.Tensor) -> torch.Tensor:
+        if self.partition == "lookup":
+            return self._gids[local.long()]
         return self.id_base + local.long() * self.id_stride
 
     def local_of(self, ids: torch.Tensor) -> torch.Tensor:
@@ -65,7 +87,14 @@ class ShardedTable:
     # ----------------------------------------------------------- lifecycle
     def reset_parameters(self):
         kind = self.init_spec[0]
-        if kind == "uniform":
+        if kind == "uniform" and self.partition == "lookup":
+            _, lo, hi = self.init_spec  # ids are not an arithmetic progression: init by explicit id
+            from ..ops import reference as R
+
+            j = torch.arange(self.dim, dtype=torch.int64, device=self.device).view(1, -1)
+            vals = float(lo) + (float(hi) - float(lo)) * R.hash_uniform(self.seed, self._gids.view(-1, 1), j)
+            self.weight.copy_(vals)
+        elif kind == "uniform":
             _, lo, hi = self.init_spec
             ops.init_rows(self.weight, self.id_base, self.id_stride, float(lo), float(hi), self.seed)
         elif kind == "zeros":

@@ -50,14 +50,14 @@ class TensorPS:
         self.table = table
         self.comm = comm
         self.wire_dtype = wire_dtype
-        self.dedup = ops.DedupWorkspace(table.num_ids, comm.world, table.part_kind, table.block, table.device)
+        self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device)
         self.stats = {"pulls": 0, "unique": 0, "steps": 0}
 
     def plan(self, keys: torch.Tensor, persistent: bool = False) -> PullPlan:
         """Dedup + split exchange + key all-to-all.  ``persistent`` copies the
         request->row map out of the reusable dedup workspace, so the plan
         survives the next ``plan`` call (pipelined steps)."""
-        keys = keys.to(device=self.table.device, dtype=torch.int32).contiguous()
+        keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
         with trace_range("ps.dedup"):
             counts, prefix, uniq, pos = self.dedup.run(keys)
         recv_counts = self.comm.exchange_counts(counts)

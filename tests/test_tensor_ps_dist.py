@@ -13,7 +13,12 @@ def _pull_push(rank, world, partition):
 
     comm = Comm()
     N, D = 1000, 8
-    tab = ShardedTable(N, D, comm.rank, comm.world, partition, ("uniform", -1.0, 1.0), seed=5)
+    owner = None
+    if partition == "lookup":  # an arbitrary id -> shard table (custom partitioner on the device path)
+        owner = torch.randint(0, comm.world, (N,), generator=torch.Generator().manual_seed(123))
+    tab = ShardedTable(N, D, comm.rank, comm.world, partition, ("uniform", -1.0, 1.0), seed=5, owner=owner)
+    if owner is not None:
+        assert tab.n_local == int((owner == comm.rank).sum())
     ps = TensorPS(tab, comm)
     g = torch.Generator().manual_seed(rank)
     keys = torch.randint(0, N, (300,), generator=g, dtype=torch.int32)
@@ -29,7 +34,7 @@ def _pull_push(rank, world, partition):
     return keys, ids, w
 
 
-@pytest.mark.parametrize("world,partition", [(2, "hash"), (3, "hash"), (2, "range")])
+@pytest.mark.parametrize("world,partition", [(2, "hash"), (3, "hash"), (2, "range"), (3, "lookup")])
 def test_tensor_ps_pull_push(world, partition):
     res = run_ranks(_pull_push, world, partition)
     all_keys = torch.cat([r[0] for r in res]).long()
