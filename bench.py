@@ -15,8 +15,8 @@ hides behind the compute of the resident block.  The SGD kernel is the
 tile-grouped one (``csrc/kernels/mf_tiled.hip``: ratings bucketed by item
 tile, one lane group per item row, no item atomics).  ``--exchange ps`` runs the
 reference's pull/push protocol instead (dedup -> all-to-all pull -> SGD ->
-all-to-all push; rows cross xGMI as bf16 by default, ``--wire``; the pull of
-micro-batch k+1 overlaps the SGD of k, ``--no-pipeline`` disables it).
+all-to-all push; rows cross xGMI as fp32, ``--wire bf16`` halves the bytes; the
+pull of micro-batch k+1 overlaps the SGD of k, ``--no-pipeline`` disables it).
 
     python bench.py --gpus N --steps K --warmup W
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -53,8 +53,8 @@ def main(argv=None):
     ap.add_argument("--pool", type=int, default=4, help="data pool = pool * batch ratings per GPU")
     ap.add_argument("--exchange", default="auto", choices=["auto", "rotate", "ps", "local"],
                     help="auto = local at N=1, rotate at N>1")
-    ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"],
-                    help="all-to-all row dtype; auto = bf16 at N>1")
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"],
+                    help="PS-path all-to-all row dtype (bf16 halves the bytes; opt-in: the headline keeps fp32)")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="tiled SGD: partition each batch on the main stream instead of prefetching it")
@@ -77,8 +77,6 @@ def main(argv=None):
     n = comm.world
     if a.gpus != n:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
-    if a.wire == "auto":
-        a.wire = "bf16" if n > 1 else "fp32"
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch)

@@ -41,7 +41,7 @@ def main(argv=None):
                          "robust to the summed deltas of hot ids")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--zipf", type=float, default=3.0)
-    ap.add_argument("--wire", default="auto", choices=["auto", "fp32", "bf16"])
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pool", type=int, default=4, help="pre-generated batches cycled through")
     a = ap.parse_args(argv)
 
@@ -53,7 +53,7 @@ def main(argv=None):
     comm = Comm.init_from_env()
     dev = comm.device
     num_ids = int(a.params_per_gpu * comm.world) // a.dim
-    wire = a.wire if a.wire != "auto" else ("bf16" if comm.world > 1 else "fp32")
+    wire = a.wire
     cfg = PairEmbeddingConfig(num_ids=num_ids, dim=a.dim, staleness=a.staleness, optimizer=a.optimizer,
                               learning_rate=a.lr, wire_dtype=wire)
     t_init = time.perf_counter()
