@@ -39,6 +39,7 @@ class SGNSConfig:
     unigram_power: float = 0.75
     seed: int = 0
     wire_dtype: str = "fp32"
+    pipeline: bool = True         # W > 1: row all-to-alls of batch k+1 overlap the SGNS step of batch k
 
 
 class DistributedSGNS:
@@ -63,15 +64,56 @@ class DistributedSGNS:
 
     def step(self, centers: torch.Tensor, contexts: torch.Tensor, lr: Optional[float] = None,
              with_loss: bool = False):
+        """One micro-batch of (center, context) pairs.  With ``pipeline`` at W > 1
+        the pulls of this batch are issued and the previously pulled batch is
+        computed and pushed (staleness: one micro-batch); ``flush()`` finishes the
+        last one.  ``with_loss`` computes synchronously and returns the mean loss."""
         c = self.cfg
         lr = c.learning_rate if lr is None else lr
+        if with_loss:
+            self.flush()
+            return self._finish(self._start(centers, contexts), lr, True)
+        pending = self._start(centers, contexts, async_rows=self._pipelined)
+        if self._pipelined:
+            prev, self._pending = self._pending, (pending, lr)
+            if prev is not None:
+                self._finish(prev[0], prev[1], False)
+        else:
+            self._finish(pending, lr, False)
+        return None
+
+    @property
+    def _pipelined(self) -> bool:
+        return self.cfg.pipeline and self.comm.world > 1
+
+    def flush(self):
+        p = getattr(self, "_pending", None)
+        self._pending = None
+        if p is not None:
+            self._finish(p[0], p[1], False)
+
+    def _start(self, centers, contexts, async_rows: bool = False):
+        c = self.cfg
         P = centers.numel()
         nb = (P + self.BLOCK - 1) // self.BLOCK
         negs = ops.sample_alias(self.prob, self.alias, nb * self.BLOCK, seed=c.seed + 17 * self.comm.rank,
                                 counter=self.counter)
         self.counter += 1
-        rows_in, plan_in = self.ps_in.pull(centers)
-        rows_out, plan_out = self.ps_out.pull(torch.cat([contexts.to(torch.int32), negs]))
+        outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
+        if async_rows:
+            rin, win, plan_in = self.ps_in.pull_async(centers)
+            rout, wout, plan_out = self.ps_out.pull_async(outs)
+            return P, (rin, win, plan_in), (rout, wout, plan_out)
+        rin, plan_in = self.ps_in.pull(centers)
+        rout, plan_out = self.ps_out.pull(outs)
+        return P, (rin, None, plan_in), (rout, None, plan_out)
+
+    def _finish(self, pending, lr, with_loss):
+        c = self.cfg
+        P, (rows_in, w_in, plan_in), (rows_out, w_out, plan_out) = pending
+        for w in (w_in, w_out):
+            if w is not None:
+                w.wait()
         dev = rows_in.device
         d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
         d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
@@ -87,6 +129,7 @@ class DistributedSGNS:
         return None
 
     def embeddings(self, only_touched: bool = True):
+        self.flush()
         return self.w_in.dump(only_touched)
 
 

@@ -77,3 +77,25 @@ def test_pair_embedding_and_locks_multirank_on_one_gpu():
     assert res[0][1] < res[0][0] - 0.1
     assert sum(r[2] for r in res) == 64 * 3 * 2  # every locked increment landed once
     assert all(r[3] == 0 for r in res)
+
+
+def _w2v(rank, world):
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    comm = Comm(device=torch.device("cuda", 0))
+    m = DistributedSGNS(SGNSConfig(vocab_size=20000, dim=128, window=4, learning_rate=0.01), comm=comm)
+    assert m._pipelined
+    toks = synthetic_corpus(200000, 20000, n_topics=50, seed=rank, device="cuda")
+    c, o = skipgram_pairs(toks, 4)
+    first = m.step(c[:8192], o[:8192], with_loss=True)
+    for s in range(0, c.numel() - 8192, 8192):
+        m.step(c[s:s + 8192], o[s:s + 8192])
+    return first, m.step(c[:8192], o[:8192], with_loss=True)
+
+
+def test_w2v_pipelined_multirank_on_one_gpu():
+    res = run_ranks(_w2v, 2)
+    for first, last in res:
+        assert last < 0.9 * first, (first, last)
