@@ -90,8 +90,9 @@ def _w2v(rank, world):
     toks = synthetic_corpus(200000, 20000, n_topics=50, seed=rank, device="cuda")
     c, o = skipgram_pairs(toks, 4)
     first = m.step(c[:8192], o[:8192], with_loss=True)
-    for s in range(0, c.numel() - 8192, 8192):
-        m.step(c[s:s + 8192], o[s:s + 8192])
+    for s in range(40):  # same number of collective steps on every rank
+        a = (s * 8192) % (c.numel() - 8192)
+        m.step(c[a:a + 8192], o[a:a + 8192])
     return first, m.step(c[:8192], o[:8192], with_loss=True)
 
 

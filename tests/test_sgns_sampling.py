@@ -49,8 +49,9 @@ def _dist_sgns(rank, world):
     toks = synthetic_corpus(12000, 2000, n_topics=6, seed=rank)
     c, o = skipgram_pairs(toks, 2, torch.Generator().manual_seed(rank))
     first = m.step(c[:1024], o[:1024], with_loss=True)
-    for s in range(0, c.numel() - 512, 512):
-        m.step(c[s:s + 512], o[s:s + 512])
+    for s in range(60):  # every rank runs the same number of (collective) steps
+        a = (s * 512) % (c.numel() - 512)
+        m.step(c[a:a + 512], o[a:a + 512])
     return first, m.step(c[:1024], o[:1024], with_loss=True)
 
 
