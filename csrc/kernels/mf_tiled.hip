@@ -148,7 +148,8 @@ constexpr int TP2_MAX_COARSE = 1024;
 __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
                                                          int W, const int32_t* __restrict__ half, int R, int T,
                                                          int cshift, int NC, int KT, int32_t* __restrict__ ccount,
-                                                         int32_t* __restrict__ bcount, uint8_t* __restrict__ seen) {
+                                                         int32_t* __restrict__ bcount, uint8_t* __restrict__ seen,
+                                                         int32_t* __restrict__ H1 = nullptr) {
   __shared__ int32_t hb[TP_MAX_BUCKETS];
   __shared__ int32_t hc[TP2_MAX_COARSE];
   for (int k = threadIdx.x; k < KT; k += blockDim.x) hb[k] = 0;
@@ -166,8 +167,10 @@ __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restri
   __syncthreads();
   for (int k = threadIdx.x; k < KT; k += blockDim.x)
     if (hb[k]) atomicAdd(bcount + k, hb[k]);
-  for (int k = threadIdx.x; k < NC; k += blockDim.x)
+  for (int k = threadIdx.x; k < NC; k += blockDim.x) {
     if (hc[k]) atomicAdd(ccount + k, hc[k]);
+    if (H1 != nullptr) H1[(int64_t)blockIdx.x * NC + k] = hc[k];  // tp3: per-workgroup coarse counts
+  }
 }
 
 // LEVEL 1: records from (uid, iid, rating), key = coarse; out = {uid, row, rating, bucket}
@@ -214,6 +217,160 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     const int32_t o = atomicAdd(h + key, 1);
     if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = r;  // level 1 keeps the bucket for level 2
     else put_rec<REC8>(out, o, r.x, r.y, __int_as_float(r.z), r.w, R);
+  }
+}
+
+// ---- two-level partition with LDS-sorted batches (default).  Both scatters
+// above leave each lane's store on its own output run, so a wave's 64 stores
+// hit ~64 different lines and the L2 writes lines back half-filled (1.2-2.5
+// TB/s, profiles/r1_mf_partition_levels.md).  Here every workgroup stages a
+// batch of TP3_B records in LDS, counting-sorts it by key (<= TP3_MAXK keys:
+// ~128 coarse keys at level 1, the <= 2^cshift buckets of one coarse key at
+// level 2), reserves one output range per (batch, key) with a global atomic,
+// and writes the sorted batch out so consecutive lanes store consecutive
+// records of one run (32-128 records per run at uniform keys).  Level 2 walks
+// work items (coarse key, sub-range of CH records) so its key span is bounded
+// whatever the key skew.
+constexpr int TP3_B = 4096;      // records per LDS batch (64 KiB of int4)
+constexpr int TP3_MAXK = 256;    // keys per batch sort
+constexpr int TP3_CH = 32768;    // level-2 records per work item
+
+// exclusive scan of cnt[0..nk) (nk <= 256) into off[] by wave 0; 4 keys per lane
+__device__ __forceinline__ void tp3_scan(const int32_t* cnt, int32_t* off, int nk) {
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x;
+  int32_t v[4], s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { const int k = 4 * l + q; v[q] = k < nk ? cnt[k] : 0; s += v[q]; }
+  int32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (l >= o) inc += y;
+  }
+  int32_t run = inc - s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { const int k = 4 * l + q; if (k < nk) off[k] = run; run += v[q]; }
+}
+
+// tp3 level-1 bases: H1[w][k] = cptr[k] + sum over w' < w of H1[w'][k]; one
+// workgroup per coarse key, one thread per partition workgroup (G <= 1024)
+__global__ void __launch_bounds__(1024) tp3_colscan_kernel(int32_t* __restrict__ H1, int G, int NC,
+                                                           const int32_t* __restrict__ cptr) {
+  __shared__ int32_t wsum[16];
+  const int k = blockIdx.x, w = threadIdx.x, l = w & 63, wv = w >> 6;
+  const int32_t v = w < G ? H1[(int64_t)w * NC + k] : 0;
+  int32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (l >= o) inc += y;
+  }
+  if (l == 63) wsum[wv] = inc;
+  __syncthreads();
+  int32_t before = cptr[k];
+  for (int q = 0; q < wv; ++q) before += wsum[q];
+  if (w < G) H1[(int64_t)w * NC + k] = before + inc - v;
+}
+
+// work items of level 2: wptr[c] = sum over c' < c of ceil(ccount[c'] / CH)
+__global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, int32_t* __restrict__ wptr) {
+  if (threadIdx.x != 0) return;
+  int32_t run = 0;
+  for (int c = 0; c < NC; ++c) { wptr[c] = run; run += (ccount[c] + TP3_CH - 1) / TP3_CH; }
+  wptr[NC] = run;
+}
+
+// LEVEL 1: (uid, iid, rating)[chunk of this workgroup] -> tmp {uid, row, rating, bucket}
+//          grouped by coarse key (bucket >> cshift); kptr = cptr, cursor = ccursor
+// LEVEL 2: tmp[work item] -> out (8- or 16-B records) grouped by bucket; kptr = ptr,
+//          cursor = bcursor; work items from wptr / cptr
+template <int LEVEL, bool REC8>
+__global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
+                                                           const int32_t* __restrict__ iid,
+                                                           const float* __restrict__ rating,
+                                                           const int4* __restrict__ tmp, int64_t n, int64_t chunk,
+                                                           int W, const int32_t* __restrict__ half, int R, int T,
+                                                           int cshift, int NC, int KT,
+                                                           const int32_t* __restrict__ kptr,
+                                                           int32_t* __restrict__ cursor,
+                                                           const int32_t* __restrict__ cptr,
+                                                           const int32_t* __restrict__ wptr,
+                                                           const int32_t* __restrict__ H1,
+                                                           void* __restrict__ out) {
+  constexpr int E = TP3_B / 1024;
+  __shared__ int4 srt[TP3_B];
+  __shared__ int32_t cnt[TP3_MAXK], off[TP3_MAXK], base[TP3_MAXK];
+  __shared__ int32_t s_item[3];  // level 2: lo, hi, key base of the current work item
+  const int tid = threadIdx.x;
+  const int nwork = LEVEL == 1 ? 1 : wptr[NC];
+  for (int w = LEVEL == 1 ? 0 : blockIdx.x; w < nwork; w += (LEVEL == 1 ? 1 : gridDim.x)) {
+    int64_t lo, hi;
+    int kb, nk;
+    if (LEVEL == 1) {
+      lo = (int64_t)blockIdx.x * chunk;
+      hi = min(n, lo + chunk);
+      kb = 0;
+      nk = NC;
+      if (tid < nk) base[tid] = H1[(int64_t)blockIdx.x * NC + tid];  // this workgroup's run starts
+    } else {
+      if (tid == 0) {
+        int c = 0;
+        while (wptr[c + 1] <= w) ++c;  // NC <= 256: linear search
+        const int32_t a = cptr[c] + (w - wptr[c]) * TP3_CH;
+        s_item[0] = a;
+        s_item[1] = min(cptr[c + 1], a + TP3_CH);
+        s_item[2] = c << cshift;
+      }
+      __syncthreads();
+      lo = s_item[0];
+      hi = s_item[1];
+      kb = s_item[2];
+      nk = min(1 << cshift, KT - kb);
+      __syncthreads();  // s_item is rewritten for the next work item
+    }
+    for (int64_t b0 = lo; b0 < hi; b0 += TP3_B) {
+      const int nb = (int)min((int64_t)TP3_B, hi - b0);
+      if (tid < nk) cnt[tid] = 0;
+      __syncthreads();
+      int4 r[E];
+      int k[E], slot[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int p = e * 1024 + tid;
+        slot[e] = -1;
+        if (p < nb) {
+          const int64_t x = b0 + p;
+          if (LEVEL == 1) {
+            int bk; int32_t row;
+            tile_bucket(iid[x], W, half, R, T, bk, row);
+            r[e] = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
+            k[e] = bk >> cshift;
+          } else {
+            r[e] = tmp[x];
+            k[e] = r[e].w - kb;
+          }
+          slot[e] = atomicAdd(cnt + k[e], 1);
+        }
+      }
+      __syncthreads();
+      tp3_scan(cnt, off, nk);
+      if (LEVEL == 2 && tid < nk && cnt[tid]) base[tid] = kptr[kb + tid] + atomicAdd(cursor + kb + tid, cnt[tid]);
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (slot[e] >= 0) srt[off[k[e]] + slot[e]] = r[e];
+      __syncthreads();
+      for (int p = tid; p < nb; p += 1024) {
+        const int4 x = srt[p];
+        const int kk = LEVEL == 1 ? (x.w >> cshift) : x.w - kb;
+        const int64_t o = (int64_t)base[kk] + (p - off[kk]);
+        if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = x;
+        else put_rec<REC8>(out, o, x.x, x.y, __int_as_float(x.z), x.w, R);
+      }
+      __syncthreads();  // LDS reused by the next batch
+      if (LEVEL == 1 && tid < nk) base[tid] += cnt[tid];  // same thread zeroes cnt[tid] next
+    }
   }
 }
 
@@ -429,6 +586,66 @@ FPS_API int64_t fps_tile_partition2_ws_ints(int W, int T) {
   while (((KT - 1) >> cshift) + 1 > 128) ++cshift;
   const int NC = ((KT - 1) >> cshift) + 1;
   return 3 * (int64_t)NC + 1 + 2 * (int64_t)KT;
+}
+
+// Two-level partition with LDS-sorted batches (tp3 above).  Workspace (int32,
+// fps_tile_partition3_ws_ints): ccount[NC], ccursor[NC], cptr[NC+1], bcount[KT],
+// bcursor[KT], wptr[NC+1] (zeroed here); tmp: n int4.
+static int tp3_cshift(int KT) {
+  int cshift = 0;
+  while (((KT - 1) >> cshift) + 1 > 128) ++cshift;  // ~128 coarse keys of <= 128 buckets
+  return cshift;
+}
+
+FPS_API int64_t fps_tile_partition3_ws_ints(int W, int T) {
+  const int KT = 2 * W * T;
+  const int NC = ((KT - 1) >> tp3_cshift(KT)) + 1;
+  return 4 * (int64_t)NC + 2 + 2 * (int64_t)KT + 1024 * (int64_t)NC;  // + H1[G <= 1024][NC]
+}
+
+FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
+                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
+                                int rec8, uint8_t* seen, void* stream) {
+  const int KT = 2 * W * T;
+  if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
+  const int cshift = tp3_cshift(KT);
+  const int NC = ((KT - 1) >> cshift) + 1;
+  if (NC > TP3_MAXK || (1 << cshift) > TP3_MAXK) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* ccount = ws;
+  int32_t* ccursor = ccount + NC;
+  int32_t* cptr = ccursor + NC;
+  int32_t* bcount = cptr + NC + 1;
+  int32_t* bcursor = bcount + KT;
+  int32_t* wptr = bcursor + KT;
+  int32_t* H1 = wptr + NC + 1;
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(int32_t) * (size_t)(4 * NC + 2 + 2 * KT), s);
+  if (e != hipSuccess) return (int)e;
+  const int G = fps_tile_partition_groups(n);
+  const int64_t chunk = (n + G - 1) / G;
+  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, cshift, NC, KT,
+                     ccount, bcount, seen, H1);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
+  hipLaunchKernelGGL(tp3_colscan_kernel, dim3(NC), dim3(1024), 0, s, H1, G, NC, (const int32_t*)cptr);
+  hipLaunchKernelGGL(tp3_workptr_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)ccount, NC, wptr);
+  if (n > 0) {
+    int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
+    if (g2 > 1024) g2 = 1024;
+    hipLaunchKernelGGL((tp3_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                       (const int4*)nullptr, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)cptr, ccursor,
+                       (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
+    if (rec8)
+      hipLaunchKernelGGL((tp3_scatter_kernel<2, true>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
+    else
+      hipLaunchKernelGGL((tp3_scatter_kernel<2, false>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
+  }
+  FPS_CHECK_LAUNCH();
+  return 0;
 }
 
 // One launch per item block: T tiles of R (<= 256) rows of I[block_rows, D];

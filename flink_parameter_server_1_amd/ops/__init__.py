@@ -346,11 +346,14 @@ class TilePartitioner:
             N.require().fps_tile_partition_set_chunk(int(chunk))
         # 1 = single level (per-workgroup histograms of every bucket + column scan);
         # 2 = two-level (coarse key, then bucket; atomic range reservations, no
-        # histogram matrix).  Measured at 64M ratings, KT = 3.9k buckets: 1.66 vs
-        # 1.83 ms (profiles/r1_mf_partition_levels.md); the single level's
-        # G x KT histogram grows with KT, so larger bucket counts use 2 levels.
+        # histogram matrix); 3 (default) = two-level with LDS-sorted batches, so
+        # consecutive lanes store consecutive records of one output run.  Levels
+        # 1 / 2 measured 1.66 / 1.83 ms at 64M ratings, KT = 3.9k buckets
+        # (profiles/r1_mf_partition_levels.md).
         env = os.environ.get("FPS_TILE_PARTITION_LEVELS")
-        self.levels = int(levels or env or (1 if self.KT <= 4096 else 2))
+        self.levels = int(levels or env or 3)
+        if self.levels not in (1, 2, 3):
+            raise ValueError(f"tile partition levels must be 1, 2 or 3, not {self.levels}")
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
@@ -374,17 +377,17 @@ class TilePartitioner:
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
             self.rec = torch.empty((self.cap, self.rec_cols), dtype=torch.int32, device=self.device)
-            if self.levels == 2:
+            if self.levels >= 2:
                 self.tmp = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
-        if self.levels == 2:
+        if self.levels >= 2:
+            fn, ws_ints = ((lib.fps_tile_partition2, lib.fps_tile_partition2_ws_ints) if self.levels == 2 else
+                           (lib.fps_tile_partition3, lib.fps_tile_partition3_ws_ints))
             if not hasattr(self, "ws"):
-                self.ws = torch.empty(lib.fps_tile_partition2_ws_ints(self.W, self.T), dtype=torch.int32,
-                                      device=self.device)
-            N.check(lib.fps_tile_partition2(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n,
-                                            self.W, self.half.data_ptr(), self.R, self.T, self.ws.data_ptr(),
-                                            self.tmp.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
-                                            int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)),
-                    "tile_partition2")
+                self.ws = torch.empty(ws_ints(self.W, self.T), dtype=torch.int32, device=self.device)
+            N.check(fn(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
+                       self.half.data_ptr(), self.R, self.T, self.ws.data_ptr(), self.tmp.data_ptr(),
+                       self.ptr.data_ptr(), self.rec.data_ptr(), int(self.rec8), N.ptr(seen),
+                       N.stream_ptr(self.device)), f"tile_partition{self.levels}")
             return self.ptr, self.rec[:n]
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
                                        self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),

@@ -182,9 +182,10 @@ def test_mf_sgd_local_seg_matches_slice():
 
 
 @pytest.mark.parametrize("rec8", [False, True])
-@pytest.mark.parametrize("levels", [1, 2])
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("levels", [1, 2, 3])
 @pytest.mark.parametrize("W,R", [(1, 128), (2, 64), (8, 64), (1, 256)])
-def test_tile_partition_matches_reference(W, R, levels, rec8):
+def test_tile_partition_matches_reference(W, R, levels, rec8, skew):
     from flink_parameter_server_1_amd.parallel.rotation import block_rows, shard_halves
 
     NI, n = 200_003, 500_000
@@ -194,6 +195,9 @@ def test_tile_partition_matches_reference(W, R, levels, rec8):
     half_t = torch.tensor(half, dtype=torch.int32)
     uid = torch.randint(0, 10_000, (n,), dtype=torch.int32)
     iid = torch.randint(0, NI, (n,), dtype=torch.int32)
+    if skew:  # 70% of the ratings on 3 hot items: coarse keys of very different sizes
+        hot = torch.tensor([5, NI // 2, NI - 1], dtype=torch.int32)
+        iid = torch.where(torch.rand(n) < 0.7, hot[torch.randint(0, 3, (n,))], iid)
     r = torch.rand(n)
     p_ref, u_ref, row_ref, r_ref = R_tile(uid, iid, r, W, half_t, R, T)
     part = ops.TilePartitioner(W, half, R, T, DEV, levels=levels, rec8=rec8)
