@@ -61,6 +61,8 @@ def main(argv=None):
     ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
+    ap.add_argument("--user-phases", type=int, default=0,
+                    help="tiled SGD: user-range phases per step (0 = auto, ~2.5M users per phase)")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     a = ap.parse_args(argv)
@@ -79,7 +81,8 @@ def main(argv=None):
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
-                   pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch)
+                   pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
+                   user_phases=a.user_phases)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -130,6 +133,7 @@ def main(argv=None):
                 "wire_dtype": a.wire if model.exchange == "ps" else "none (fp32 parameters stay resident or travel "
                                                                      "whole)",
                 "sgd_mode": model.sgd_mode,
+                "user_phases": getattr(model, "user_phases", None),
                 "pipelined": model.pipeline,
                 "scalar_params_per_s": value * 2 * a.dim,
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))

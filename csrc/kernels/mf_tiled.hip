@@ -35,24 +35,27 @@ using namespace fps;
 namespace {
 
 // ---------------------------------------------------------------- partition
-// bucket of a rating = block * T + row_in_block / R (block layout of rotate.hip:
-// b = 2q + h, q = i % W, h = (i / W >= half[q])); W = 1 with half[0] = num_items
-// gives a single block (the whole local table).
-__device__ __forceinline__ void tile_bucket(int32_t i, int W, const int32_t* __restrict__ half, int R, int T,
-                                            int& bucket, int32_t& row) {
+// bucket of a rating = (phase * 2W + block) * T + row_in_block / R (block layout of
+// rotate.hip: b = 2q + h, q = i % W, h = (i / W >= half[q])); W = 1 with half[0] =
+// num_items gives a single block (the whole local table).  phase = uid / upp: the
+// SGD runs the phases one after another, so the user rows one launch touches
+// (upp of them) mostly stay in the 256 MiB Infinity Cache (P = 1: upp > users).
+__device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, int W, const int32_t* __restrict__ half, int R,
+                                            int T, int upp, int& bucket, int32_t& row) {
   const int q = i % W;
   const int32_t loc = i / W;
   const int32_t hq = half[q];
   const int h = loc >= hq;
   row = loc - (h ? hq : 0);
-  bucket = (2 * q + h) * T + row / R;
+  bucket = ((u / upp) * 2 * W + 2 * q + h) * T + row / R;  // user phase, item block, tile
 }
 
 constexpr int TP_MAX_BUCKETS = 16384;  // 64 KiB of LDS counters
 
 // K1: per-workgroup histogram H[w][KT] (plain stores, no global atomics)
-__global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
-                                                         int W, const int32_t* __restrict__ half, int R, int T,
+__global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restrict__ uid,
+                                                         const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                                                         int W, const int32_t* __restrict__ half, int R, int T, int upp,
                                                          int KT, int32_t* __restrict__ H, uint8_t* __restrict__ seen) {
   __shared__ int32_t cnt[TP_MAX_BUCKETS];
   for (int k = threadIdx.x; k < KT; k += blockDim.x) cnt[k] = 0;
@@ -61,7 +64,7 @@ __global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restri
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     const int32_t i = iid[x];
     int bk; int32_t row;
-    tile_bucket(i, W, half, R, T, bk, row);
+    tile_bucket(i, uid[x], W, half, R, T, upp, bk, row);
     atomicAdd(cnt + bk, 1);
     if (seen != nullptr) seen[i] = 1;
   }
@@ -120,7 +123,8 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
                                                             const int32_t* __restrict__ iid,
                                                             const float* __restrict__ rating, int64_t n,
                                                             int64_t chunk, int W, const int32_t* __restrict__ half,
-                                                            int R, int T, int KT, const int32_t* __restrict__ H,
+                                                            int R, int T, int upp, int KT,
+                                                            const int32_t* __restrict__ H,
                                                             const int32_t* __restrict__ ptr,
                                                             void* __restrict__ rec) {
   __shared__ int32_t cur[TP_MAX_BUCKETS];
@@ -130,7 +134,7 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     int bk; int32_t row;
-    tile_bucket(iid[x], W, half, R, T, bk, row);
+    tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
     const int32_t o = atomicAdd(cur + bk, 1);
     put_rec<REC8>(rec, o, uid[x], row, rating[x], bk, R);
   }
@@ -145,8 +149,9 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
 constexpr int TP2_MAX_COARSE = 1024;
 
 // both histograms in one pass over iid: coarse counts and per-bucket counts
-__global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
-                                                         int W, const int32_t* __restrict__ half, int R, int T,
+__global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restrict__ uid,
+                                                         const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                                                         int W, const int32_t* __restrict__ half, int R, int T, int upp,
                                                          int cshift, int NC, int KT, int32_t* __restrict__ ccount,
                                                          int32_t* __restrict__ bcount, uint8_t* __restrict__ seen,
                                                          int32_t* __restrict__ H1 = nullptr) {
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restri
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     const int32_t i = iid[x];
     int bk; int32_t row;
-    tile_bucket(i, W, half, R, T, bk, row);
+    tile_bucket(i, uid[x], W, half, R, T, upp, bk, row);
     atomicAdd(hb + bk, 1);
     atomicAdd(hc + (bk >> cshift), 1);
     if (seen != nullptr) seen[i] = 1;
@@ -180,7 +185,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
                                                            const int4* __restrict__ tmp, int64_t n, int64_t chunk,
-                                                           int W, const int32_t* __restrict__ half, int R, int T,
+                                                           int W, const int32_t* __restrict__ half, int R, int T, int upp,
                                                            int cshift, int nkeys, const int32_t* __restrict__ ptr,
                                                            int32_t* __restrict__ cursor, void* __restrict__ out) {
   __shared__ int32_t h[TP_MAX_BUCKETS];
@@ -191,7 +196,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     int key;
     if (LEVEL == 1) {
       int bk; int32_t row;
-      tile_bucket(iid[x], W, half, R, T, bk, row);
+      tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
       key = bk >> cshift;
     } else {
       key = tmp[x].w;
@@ -207,7 +212,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     int key;
     if (LEVEL == 1) {
       int bk; int32_t row;
-      tile_bucket(iid[x], W, half, R, T, bk, row);
+      tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
       r = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
       key = bk >> cshift;
     } else {
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
                                                            const int4* __restrict__ tmp, int64_t n, int64_t chunk,
-                                                           int W, const int32_t* __restrict__ half, int R, int T,
+                                                           int W, const int32_t* __restrict__ half, int R, int T, int upp,
                                                            int cshift, int NC, int KT,
                                                            const int32_t* __restrict__ kptr,
                                                            int32_t* __restrict__ cursor,
@@ -343,7 +348,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
           const int64_t x = b0 + p;
           if (LEVEL == 1) {
             int bk; int32_t row;
-            tile_bucket(iid[x], W, half, R, T, bk, row);
+            tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
             r[e] = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
             k[e] = bk >> cshift;
           } else {
@@ -518,23 +523,23 @@ FPS_API int fps_tile_partition_groups(int64_t n) {
 
 // rec: n packed records (8 B if rec8, else 16 B; see put_rec) grouped by bucket
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
-                               const int32_t* half, int R, int T, int32_t* H, int32_t* totals, int32_t* ptr,
+                               const int32_t* half, int R, int T, int P, int upp, int32_t* H, int32_t* totals, int32_t* ptr,
                                void* rec, int rec8, uint8_t* seen, void* stream) {
-  const int KT = 2 * W * T;
+  const int KT = P * 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tile_hist_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, KT, H, seen);
+  hipLaunchKernelGGL(tile_hist_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, KT, H, seen);
   hipLaunchKernelGGL(tile_colscan_kernel, dim3((KT + 255) / 256), dim3(256), 0, s, H, G, KT, totals);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)totals, KT, ptr);
   if (n > 0) {
     if (rec8)
       hipLaunchKernelGGL(tile_scatter_kernel<true>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half, R,
-                         T, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+                         T, upp, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
     else
       hipLaunchKernelGGL(tile_scatter_kernel<false>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half,
-                         R, T, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+                         R, T, upp, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
   }
   FPS_CHECK_LAUNCH();
   return 0;
@@ -544,9 +549,9 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // bcount[KT], bcursor[KT] (all zeroed here), tmp: n int4.  ptr[KT+1] = tile
 // offsets, rec: n records {uid, row-in-block, rating bits, bucket}.
 FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
-                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
+                                const int32_t* half, int R, int T, int P, int upp, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
                                 int rec8, uint8_t* seen, void* stream) {
-  const int KT = 2 * W * T;
+  const int KT = P * 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   int cshift = 0;
   while (((KT - 1) >> cshift) + 1 > 128) ++cshift;  // ~128 coarse keys
@@ -561,27 +566,27 @@ FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const fl
   if (e != hipSuccess) return (int)e;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, cshift, NC, KT,
+  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, cshift, NC, KT,
                      ccount, bcount, seen);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
   if (n > 0) {
     hipLaunchKernelGGL((tp2_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                       (const int4*)nullptr, n, chunk, W, half, R, T, cshift, NC, (const int32_t*)cptr, ccursor,
+                       (const int4*)nullptr, n, chunk, W, half, R, T, upp, cshift, NC, (const int32_t*)cptr, ccursor,
                        (void*)tmp);
     if (rec8)
       hipLaunchKernelGGL((tp2_scatter_kernel<2, true>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, KT, (const int32_t*)ptr, bcursor, rec);
     else
       hipLaunchKernelGGL((tp2_scatter_kernel<2, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, KT, (const int32_t*)ptr, bcursor, rec);
   }
   FPS_CHECK_LAUNCH();
   return 0;
 }
 
-FPS_API int64_t fps_tile_partition2_ws_ints(int W, int T) {
-  const int KT = 2 * W * T;
+FPS_API int64_t fps_tile_partition2_ws_ints(int W, int T, int P) {
+  const int KT = P * 2 * W * T;
   int cshift = 0;
   while (((KT - 1) >> cshift) + 1 > 128) ++cshift;
   const int NC = ((KT - 1) >> cshift) + 1;
@@ -597,16 +602,16 @@ static int tp3_cshift(int KT) {
   return cshift;
 }
 
-FPS_API int64_t fps_tile_partition3_ws_ints(int W, int T) {
-  const int KT = 2 * W * T;
+FPS_API int64_t fps_tile_partition3_ws_ints(int W, int T, int P) {
+  const int KT = P * 2 * W * T;
   const int NC = ((KT - 1) >> tp3_cshift(KT)) + 1;
   return 4 * (int64_t)NC + 2 + 2 * (int64_t)KT + 1024 * (int64_t)NC;  // + H1[G <= 1024][NC]
 }
 
 FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
-                                const int32_t* half, int R, int T, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
+                                const int32_t* half, int R, int T, int P, int upp, int32_t* ws, int4* tmp, int32_t* ptr, void* rec,
                                 int rec8, uint8_t* seen, void* stream) {
-  const int KT = 2 * W * T;
+  const int KT = P * 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   const int cshift = tp3_cshift(KT);
   const int NC = ((KT - 1) >> cshift) + 1;
@@ -623,7 +628,7 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   if (e != hipSuccess) return (int)e;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, iid, n, chunk, W, half, R, T, cshift, NC, KT,
+  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, cshift, NC, KT,
                      ccount, bcount, seen, H1);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
@@ -633,15 +638,15 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
     if (g2 > 1024) g2 = 1024;
     hipLaunchKernelGGL((tp3_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                       (const int4*)nullptr, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)cptr, ccursor,
+                       (const int4*)nullptr, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)cptr, ccursor,
                        (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
     if (rec8)
       hipLaunchKernelGGL((tp3_scatter_kernel<2, true>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)ptr, bcursor,
                          (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
     else
       hipLaunchKernelGGL((tp3_scatter_kernel<2, false>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)ptr, bcursor,
                          (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
   }
   FPS_CHECK_LAUNCH();

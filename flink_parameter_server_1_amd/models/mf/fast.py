@@ -64,6 +64,8 @@ class MFConfig:
     prefetch_partition: bool = True   # tiled: bucket batch k+1 on a side stream during the SGD of k
     negative_sample_rate: int = 0     # implicit feedback: negatives (rating 0) per rating
     user_memory: int = 128            # per-user ring of recent items excluded from the negatives
+    user_phases: int = 0              # tiled: run the SGD in P user-range phases (0 = auto: ~2.5M users
+                                      # per phase, so a launch's user rows mostly hit the Infinity Cache)
     graph_capture: bool = False       # tiled, W = 1: replay each batch size's step as one hipGraph
                                       # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
@@ -71,6 +73,9 @@ class MFConfig:
 
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+#: user rows per SGD phase (auto ``user_phases``): 2.5M x 64 fp32 = 640 MB
+PHASE_USERS = 2_500_000
 
 
 class DistributedMF:
@@ -120,8 +125,18 @@ class DistributedMF:
             # side stream while batch k's SGD runs (one micro-batch of latency, flush()
             # completes it; same SGD order)
             rec8 = self.users.n_local < (1 << 24)  # 8-B rating records (user index in 24 bits)
+            # user phases: ratings also bucketed by local user range, each phase's
+            # launches touch ~2.5M user rows (640 MB) instead of all of them --
+            # measured 1.67 ms x 4 vs 7.34 ms of SGD per 64M ratings at 10M users
+            # (profiles/r1_mf_user_phases.md)
+            P = cfg.user_phases or -(-self.users.n_local // PHASE_USERS)
+            while P > 1 and P * 2 * tile_w * self.tile_T > ops.TILE_MAX_BUCKETS:
+                P -= 1
+            self.user_phases = max(1, P)
+            upp = -(-self.users.n_local // self.user_phases)
             self._tilers = [ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T,
-                                                dev, rec8=rec8) for _ in range(2)]
+                                                dev, rec8=rec8, phases=self.user_phases, users_per_phase=upp)
+                            for _ in range(2)]
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
             self._prefetch = cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
@@ -279,13 +294,16 @@ class DistributedMF:
         if ev is not None:
             torch.cuda.current_stream(self.U.device).wait_event(ev)
         if self.exchange == "local":
-            for b, blk in enumerate(self._local_blocks):
-                ops.mf_sgd_tiled(self.U, blk, rec, ptr, b, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+            for p in range(self.user_phases):
+                for b, blk in enumerate(self._local_blocks):
+                    ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R, c.learning_rate,
+                                     c.lam)
             return
         for _ in range(self.rot.K):
             self.rot.begin()  # transfer of the next block overlaps this sub-step
-            ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, self.rot.active_block(), self.tile_T,
-                             self.tile_R, c.learning_rate, c.lam)
+            for p in range(self.user_phases):
+                ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, p * self.rot.K + self.rot.active_block(),
+                                 self.tile_T, self.tile_R, c.learning_rate, c.lam)
             self.rot.end()
 
     def _finish(self, pending):

@@ -329,18 +329,25 @@ def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
 
 
 class TilePartitioner:
-    """Buckets a micro-batch's ratings by (item block, tile of ``R`` rows) for
-    ``mf_sgd_tiled`` (``mf_tiled.hip``): 4 kernels, no global atomics, nothing
-    synchronised to the host.  ``run`` returns ``(ptr[2W*T+1], rec)`` with
+    """Buckets a micro-batch's ratings by (user phase, item block, tile of ``R``
+    rows) for ``mf_sgd_tiled`` (``mf_tiled.hip``): a few kernels, nothing
+    synchronised to the host.  ``run`` returns ``(ptr[P*2W*T+1], rec)`` with
     ``rec`` an int32 ``[n, 4]`` array of packed records {uid, row-in-block,
-    rating bits, 0} grouped by bucket (on CPU: the three columns as tensors)."""
+    rating bits, bucket} (``[n, 2]`` with ``rec8``) grouped by bucket (on CPU:
+    the three columns as tensors).  Phase ``p`` = local users
+    ``[p*upp, (p+1)*upp)``; bucket ``(p*2W + b)*T + t``."""
 
-    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None, rec8: bool = False):
+    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None, rec8: bool = False,
+                 phases: int = 1, users_per_phase: Optional[int] = None):
         self.W, self.R, self.T = W, int(R), int(T)
+        self.P = max(1, int(phases))
+        self.upp = int(users_per_phase) if (self.P > 1 and users_per_phase) else (1 << 30)
+        if self.P > 1 and not users_per_phase:
+            raise ValueError("phases > 1 needs users_per_phase")
         # 8-B records {uid | row_in_tile << 24, rating}: users < 2^24, R <= 256
         self.rec8 = bool(rec8) and self.R <= 256
         self.rec_cols = 2 if self.rec8 else 4
-        self.KT = 2 * W * self.T
+        self.KT = self.P * 2 * W * self.T
         chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
         if chunk and self.device_is_cuda(device):
             N.require().fps_tile_partition_set_chunk(int(chunk))
@@ -366,7 +373,8 @@ class TilePartitioner:
         if self.device.type != "cuda":
             if seen is not None:
                 seen[iid.long()] = 1
-            ptr, u, row, r = R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T)
+            ptr, u, row, r = R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T, self.P,
+                                              self.upp)
             return ptr, (u, row, r)
         lib = N.require()
         n = uid.numel()
@@ -383,14 +391,14 @@ class TilePartitioner:
             fn, ws_ints = ((lib.fps_tile_partition2, lib.fps_tile_partition2_ws_ints) if self.levels == 2 else
                            (lib.fps_tile_partition3, lib.fps_tile_partition3_ws_ints))
             if not hasattr(self, "ws"):
-                self.ws = torch.empty(ws_ints(self.W, self.T), dtype=torch.int32, device=self.device)
+                self.ws = torch.empty(ws_ints(self.W, self.T, self.P), dtype=torch.int32, device=self.device)
             N.check(fn(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
-                       self.half.data_ptr(), self.R, self.T, self.ws.data_ptr(), self.tmp.data_ptr(),
+                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.ws.data_ptr(), self.tmp.data_ptr(),
                        self.ptr.data_ptr(), self.rec.data_ptr(), int(self.rec8), N.ptr(seen),
                        N.stream_ptr(self.device)), f"tile_partition{self.levels}")
             return self.ptr, self.rec[:n]
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
-                                       self.half.data_ptr(), self.R, self.T, self.H.data_ptr(),
+                                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.H.data_ptr(),
                                        self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
                                        int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]

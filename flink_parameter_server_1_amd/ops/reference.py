@@ -179,13 +179,16 @@ def rot_partition(uid, iid, rating, W, half):
     return counts, ptr, uid[order].to(torch.int32), row[order].to(torch.int32), rating[order]
 
 
-def tile_partition(uid, iid, rating, W, half, R, T):
-    """Ratings grouped by (item block, tile of R rows): ``(ptr[2W*T+1], uid, row_in_block, rating)``."""
+def tile_partition(uid, iid, rating, W, half, R, T, P=1, upp=None):
+    """Ratings grouped by (user phase ``uid // upp``, item block, tile of R rows):
+    ``(ptr[P*2W*T+1], uid, row_in_block, rating)``."""
     b, row = rot_block_of(iid, W, half)
-    bucket = b * T + row // R
+    phase = uid.long() // upp if (P > 1 and upp) else torch.zeros_like(b)
+    bucket = (phase * 2 * W + b) * T + row // R
+    KT = P * 2 * W * T
     order = torch.argsort(bucket, stable=True)
-    counts = torch.bincount(bucket, minlength=2 * W * T)
-    ptr = torch.zeros(2 * W * T + 1, dtype=torch.int32)
+    counts = torch.bincount(bucket, minlength=KT)
+    ptr = torch.zeros(KT + 1, dtype=torch.int32)
     ptr[1:] = torch.cumsum(counts, 0)
     return ptr, uid[order].to(torch.int32), row[order].to(torch.int32), rating[order]
 
