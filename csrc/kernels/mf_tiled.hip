@@ -40,14 +40,39 @@ namespace {
 // num_items gives a single block (the whole local table).  phase = uid / upp: the
 // SGD runs the phases one after another, so the user rows one launch touches
 // (upp of them) mostly stay in the 256 MiB Infinity Cache (P = 1: upp > users).
-__device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, int W, const int32_t* __restrict__ half, int R,
-                                            int T, int upp, int& bucket, int32_t& row) {
-  const int q = i % W;
-  const int32_t loc = i / W;
-  const int32_t hq = half[q];
+//
+// The divisions by W, R and upp use multiply-shift reciprocals: with four
+// hardware integer divisions per rating the count kernel was VALU-bound.
+struct FastDiv {  // n / d for 0 <= n < 2^31: (n * M) >> k, k = 31 + ceil(log2 d), M = ceil(2^k / d)
+  uint64_t M;
+  int k;
+  __device__ __forceinline__ int32_t div(int32_t n) const { return (int32_t)(((uint64_t)(uint32_t)n * M) >> k); }
+};
+
+static FastDiv make_fastdiv(int d) {
+  int l = 0;
+  while ((1ll << l) < d) ++l;
+  const int k = 31 + l;
+  return FastDiv{((1ull << k) + (uint64_t)d - 1) / (uint64_t)d, k};
+}
+
+struct TileGeo {
+  int W, R, T;
+  FastDiv dW, dR, dU;
+  const int32_t* half;
+};
+
+static TileGeo make_geo(int W, const int32_t* half, int R, int T, int upp) {
+  return TileGeo{W, R, T, make_fastdiv(W), make_fastdiv(R), make_fastdiv(upp), half};
+}
+
+__device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, const TileGeo& g, int& bucket, int32_t& row) {
+  const int32_t loc = g.dW.div(i);
+  const int q = i - loc * g.W;
+  const int32_t hq = g.half[q];
   const int h = loc >= hq;
   row = loc - (h ? hq : 0);
-  bucket = ((u / upp) * 2 * W + 2 * q + h) * T + row / R;  // user phase, item block, tile
+  bucket = (g.dU.div(u) * 2 * g.W + 2 * q + h) * g.T + g.dR.div(row);  // user phase, item block, tile
 }
 
 constexpr int TP_MAX_BUCKETS = 16384;  // 64 KiB of LDS counters
@@ -55,7 +80,7 @@ constexpr int TP_MAX_BUCKETS = 16384;  // 64 KiB of LDS counters
 // K1: per-workgroup histogram H[w][KT] (plain stores, no global atomics)
 __global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restrict__ uid,
                                                          const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
-                                                         int W, const int32_t* __restrict__ half, int R, int T, int upp,
+                                                         TileGeo g,
                                                          int KT, int32_t* __restrict__ H, uint8_t* __restrict__ seen) {
   __shared__ int32_t cnt[TP_MAX_BUCKETS];
   for (int k = threadIdx.x; k < KT; k += blockDim.x) cnt[k] = 0;
@@ -64,7 +89,7 @@ __global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restri
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     const int32_t i = iid[x];
     int bk; int32_t row;
-    tile_bucket(i, uid[x], W, half, R, T, upp, bk, row);
+    tile_bucket(i, uid[x], g, bk, row);
     atomicAdd(cnt + bk, 1);
     if (seen != nullptr) seen[i] = 1;
   }
@@ -87,9 +112,12 @@ __global__ void tile_colscan_kernel(int32_t* __restrict__ H, int G, int KT, int3
 }
 
 // K3: exclusive scan of KT totals into ptr[KT+1] (one 1024-thread workgroup)
-__global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restrict__ totals, int KT,
+__global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restrict__ totals_g, int KT,
                                                          int32_t* __restrict__ ptr) {
   __shared__ int32_t part[1024];
+  __shared__ int32_t totals[16384];  // KT <= TP_MAX_BUCKETS: staged by coalesced loads
+  for (int k = threadIdx.x; k < KT; k += 1024) totals[k] = totals_g[k];
+  __syncthreads();
   const int per = (KT + 1023) / 1024;
   const int k0 = threadIdx.x * per;
   int32_t s = 0;
@@ -122,8 +150,7 @@ template <bool REC8>
 __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __restrict__ uid,
                                                             const int32_t* __restrict__ iid,
                                                             const float* __restrict__ rating, int64_t n,
-                                                            int64_t chunk, int W, const int32_t* __restrict__ half,
-                                                            int R, int T, int upp, int KT,
+                                                            int64_t chunk, TileGeo g, int KT,
                                                             const int32_t* __restrict__ H,
                                                             const int32_t* __restrict__ ptr,
                                                             void* __restrict__ rec) {
@@ -134,9 +161,9 @@ __global__ void __launch_bounds__(1024) tile_scatter_kernel(const int32_t* __res
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     int bk; int32_t row;
-    tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
+    tile_bucket(iid[x], uid[x], g, bk, row);
     const int32_t o = atomicAdd(cur + bk, 1);
-    put_rec<REC8>(rec, o, uid[x], row, rating[x], bk, R);
+    put_rec<REC8>(rec, o, uid[x], row, rating[x], bk, g.R);
   }
 }
 
@@ -151,7 +178,7 @@ constexpr int TP2_MAX_COARSE = 1024;
 // both histograms in one pass over iid: coarse counts and per-bucket counts
 __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restrict__ uid,
                                                          const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
-                                                         int W, const int32_t* __restrict__ half, int R, int T, int upp,
+                                                         TileGeo g,
                                                          int cshift, int NC, int KT, int32_t* __restrict__ ccount,
                                                          int32_t* __restrict__ bcount, uint8_t* __restrict__ seen,
                                                          int32_t* __restrict__ H1 = nullptr) {
@@ -164,7 +191,7 @@ __global__ void __launch_bounds__(1024) tp2_count_kernel(const int32_t* __restri
   for (int64_t x = lo + threadIdx.x; x < hi; x += blockDim.x) {
     const int32_t i = iid[x];
     int bk; int32_t row;
-    tile_bucket(i, uid[x], W, half, R, T, upp, bk, row);
+    tile_bucket(i, uid[x], g, bk, row);
     atomicAdd(hb + bk, 1);
     atomicAdd(hc + (bk >> cshift), 1);
     if (seen != nullptr) seen[i] = 1;
@@ -185,7 +212,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
                                                            const int4* __restrict__ tmp, int64_t n, int64_t chunk,
-                                                           int W, const int32_t* __restrict__ half, int R, int T, int upp,
+                                                           TileGeo g,
                                                            int cshift, int nkeys, const int32_t* __restrict__ ptr,
                                                            int32_t* __restrict__ cursor, void* __restrict__ out) {
   __shared__ int32_t h[TP_MAX_BUCKETS];
@@ -196,7 +223,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     int key;
     if (LEVEL == 1) {
       int bk; int32_t row;
-      tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
+      tile_bucket(iid[x], uid[x], g, bk, row);
       key = bk >> cshift;
     } else {
       key = tmp[x].w;
@@ -212,7 +239,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     int key;
     if (LEVEL == 1) {
       int bk; int32_t row;
-      tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
+      tile_bucket(iid[x], uid[x], g, bk, row);
       r = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
       key = bk >> cshift;
     } else {
@@ -221,7 +248,7 @@ __global__ void __launch_bounds__(1024) tp2_scatter_kernel(const int32_t* __rest
     }
     const int32_t o = atomicAdd(h + key, 1);
     if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = r;  // level 1 keeps the bucket for level 2
-    else put_rec<REC8>(out, o, r.x, r.y, __int_as_float(r.z), r.w, R);
+    else put_rec<REC8>(out, o, r.x, r.y, __int_as_float(r.z), r.w, g.R);
   }
 }
 
@@ -258,6 +285,90 @@ __device__ __forceinline__ void tp3_scan(const int32_t* cnt, int32_t* off, int n
   for (int q = 0; q < 4; ++q) { const int k = 4 * l + q; if (k < nk) off[k] = run; run += v[q]; }
 }
 
+// tp3 counts: fine-bucket histogram per count workgroup (row 1 + g of bcount,
+// plain stores, summed by tp3_colsum_kernel) and coarse counts per level-1 chunk
+// (H1[chunk][NC]).  Each workgroup covers `sub` consecutive level-1 chunks, so
+// <= 512 fine histograms are written however many level-1 chunks there are.
+// (Flushing the fine histogram with global atomics cost 16M atomics per step
+// at KT = 15.6k buckets and 65k-rating chunks, 4M with 256 workgroups.)
+__global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restrict__ uid,
+                                                         const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                                                         int G, int sub, TileGeo g, int cshift, int NC, int KT,
+                                                         int32_t* __restrict__ ccount, int32_t* __restrict__ bcount,
+                                                         uint8_t* __restrict__ seen, int32_t* __restrict__ H1) {
+  // One LDS atomic per rating (LDS atomics run at ~1 lane per CU cycle and
+  // bound this kernel); the coarse counts of a chunk are read off the fine
+  // histogram afterwards: 8 lanes per coarse key sum its 2^cshift buckets.
+  __shared__ int32_t hb[TP_MAX_BUCKETS];
+  __shared__ int32_t hc_prev[TP3_MAXK];
+  for (int k = threadIdx.x; k < KT; k += blockDim.x) hb[k] = 0;
+  if (threadIdx.x < NC) hc_prev[threadIdx.x] = 0;
+  __syncthreads();
+  const int span = 1 << cshift;
+  const int per = (span + 7) / 8;
+  const int ck = threadIdx.x >> 3, cl = threadIdx.x & 7;  // coarse key, lane in its group of 8
+  const int c0 = blockIdx.x * sub, c1 = min(G, c0 + sub);
+  for (int c = c0; c < c1; ++c) {
+    const int64_t lo = (int64_t)c * chunk, hi = min(n, lo + chunk);
+    constexpr int U4 = 8;  // loads in flight per thread (a lone dependent load pair per
+                           // iteration left the kernel latency-bound at ~1.7 TB/s)
+    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += U4 * blockDim.x) {
+      int32_t iv[U4], uv[U4];
+#pragma unroll
+      for (int j = 0; j < U4; ++j) {
+        const int64_t x = x0 + (int64_t)j * blockDim.x;
+        iv[j] = x < hi ? iid[x] : -1;
+        uv[j] = x < hi ? uid[x] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < U4; ++j) {
+        if (iv[j] < 0) continue;
+        int bk; int32_t row;
+        tile_bucket(iv[j], uv[j], g, bk, row);
+        atomicAdd(hb + bk, 1);
+        if (seen != nullptr) seen[iv[j]] = 1;
+      }
+    }
+    __syncthreads();
+    int32_t tot = 0;
+    if (ck < NC)
+      for (int q = 0; q < per; ++q) {
+        const int b = (ck << cshift) + cl * per + q;
+        if (cl * per + q < span && b < KT) tot += hb[b];
+      }
+    tot += __shfl_xor(tot, 1, 64);
+    tot += __shfl_xor(tot, 2, 64);
+    tot += __shfl_xor(tot, 4, 64);
+    if (ck < NC && cl == 0) {
+      const int32_t v = tot - hc_prev[ck];
+      hc_prev[ck] = tot;
+      if (v) atomicAdd(ccount + ck, v);
+      H1[(int64_t)c * NC + ck] = v;
+    }
+    __syncthreads();  // hb is read above before the next chunk adds to it
+  }
+  int32_t* Hf = bcount + (int64_t)(blockIdx.x + 1) * KT;  // row 0 = the totals (tp3_colsum_kernel)
+  for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = hb[k];
+}
+
+// bcount[k] = sum of the count workgroups' rows bcount[1 + g][k]: 64 columns x 16
+// row groups per workgroup, independent loads, LDS reduction
+__global__ void __launch_bounds__(1024) tp3_colsum_kernel(int32_t* __restrict__ bcount, int G, int KT) {
+  __shared__ int32_t part[16][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  int32_t s = 0;
+  if (col < KT)
+    for (int g = rg; g < G; g += 16) s += bcount[(int64_t)(g + 1) * KT + col];
+  part[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && col < KT) {
+    int32_t t = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += part[q][threadIdx.x];
+    bcount[col] = t;
+  }
+}
+
 // tp3 level-1 bases: H1[w][k] = cptr[k] + sum over w' < w of H1[w'][k]; one
 // workgroup per coarse key, one thread per partition workgroup (G <= 1024)
 __global__ void __launch_bounds__(1024) tp3_colscan_kernel(int32_t* __restrict__ H1, int G, int NC,
@@ -286,8 +397,10 @@ __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, i
   wptr[NC] = run;
 }
 
-// LEVEL 1: (uid, iid, rating)[chunk of this workgroup] -> tmp {uid, row, rating, bucket}
-//          grouped by coarse key (bucket >> cshift); kptr = cptr, cursor = ccursor
+// LEVEL 1: (uid, iid, rating)[chunk of this workgroup] -> tmp grouped by coarse key
+//          (bucket >> cshift); kptr = cptr, cursor = ccursor.  tmp records: REC8
+//          12 B {uid | row_in_tile << 24, rating bits, bucket}, else 16 B {uid, row,
+//          rating bits, bucket}
 // LEVEL 2: tmp[work item] -> out (8- or 16-B records) grouped by bucket; kptr = ptr,
 //          cursor = bcursor; work items from wptr / cptr
 template <int LEVEL, bool REC8>
@@ -295,7 +408,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
                                                            const int4* __restrict__ tmp, int64_t n, int64_t chunk,
-                                                           int W, const int32_t* __restrict__ half, int R, int T, int upp,
+                                                           TileGeo g,
                                                            int cshift, int NC, int KT,
                                                            const int32_t* __restrict__ kptr,
                                                            int32_t* __restrict__ cursor,
@@ -348,9 +461,14 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
           const int64_t x = b0 + p;
           if (LEVEL == 1) {
             int bk; int32_t row;
-            tile_bucket(iid[x], uid[x], W, half, R, T, upp, bk, row);
-            r[e] = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
+            tile_bucket(iid[x], uid[x], g, bk, row);
+            if (REC8) r[e] = make_int4(uid[x] | ((row & (g.R - 1)) << 24), __float_as_int(rating[x]), bk, 0);
+            else r[e] = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
             k[e] = bk >> cshift;
+          } else if (REC8) {
+            const int3 t = reinterpret_cast<const int3*>(tmp)[x];
+            r[e] = make_int4(t.x, t.y, t.z, 0);
+            k[e] = t.z - kb;
           } else {
             r[e] = tmp[x];
             k[e] = r[e].w - kb;
@@ -368,10 +486,13 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       __syncthreads();
       for (int p = tid; p < nb; p += 1024) {
         const int4 x = srt[p];
-        const int kk = LEVEL == 1 ? (x.w >> cshift) : x.w - kb;
+        const int bk = REC8 ? x.z : x.w;
+        const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
         const int64_t o = (int64_t)base[kk] + (p - off[kk]);
-        if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = x;
-        else put_rec<REC8>(out, o, x.x, x.y, __int_as_float(x.z), x.w, R);
+        if (LEVEL == 1 && REC8) reinterpret_cast<int3*>(out)[o] = make_int3(x.x, x.y, x.z);
+        else if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = x;
+        else if (REC8) reinterpret_cast<int2*>(out)[o] = make_int2(x.x, x.y);
+        else put_rec<false>(out, o, x.x, x.y, __int_as_float(x.z), x.w, g.R);
       }
       __syncthreads();  // LDS reused by the next batch
       if (LEVEL == 1 && tid < nk) base[tid] += cnt[tid];  // same thread zeroes cnt[tid] next
@@ -527,19 +648,20 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
                                void* rec, int rec8, uint8_t* seen, void* stream) {
   const int KT = P * 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
+  const TileGeo g = make_geo(W, half, R, T, upp);
   hipStream_t s = (hipStream_t)stream;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tile_hist_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, KT, H, seen);
+  hipLaunchKernelGGL(tile_hist_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, g,  KT, H, seen);
   hipLaunchKernelGGL(tile_colscan_kernel, dim3((KT + 255) / 256), dim3(256), 0, s, H, G, KT, totals);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)totals, KT, ptr);
   if (n > 0) {
     if (rec8)
-      hipLaunchKernelGGL(tile_scatter_kernel<true>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half, R,
-                         T, upp, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+      hipLaunchKernelGGL(tile_scatter_kernel<true>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, g,
+                          KT, (const int32_t*)H, (const int32_t*)ptr, rec);
     else
-      hipLaunchKernelGGL(tile_scatter_kernel<false>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, W, half,
-                         R, T, upp, KT, (const int32_t*)H, (const int32_t*)ptr, rec);
+      hipLaunchKernelGGL(tile_scatter_kernel<false>, dim3(G), dim3(1024), 0, s, uid, iid, rating, n, chunk, g,
+                          KT, (const int32_t*)H, (const int32_t*)ptr, rec);
   }
   FPS_CHECK_LAUNCH();
   return 0;
@@ -556,6 +678,7 @@ FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const fl
   int cshift = 0;
   while (((KT - 1) >> cshift) + 1 > 128) ++cshift;  // ~128 coarse keys
   const int NC = ((KT - 1) >> cshift) + 1;
+  const TileGeo g = make_geo(W, half, R, T, upp);
   hipStream_t s = (hipStream_t)stream;
   int32_t* ccount = ws;
   int32_t* ccursor = ccount + NC;
@@ -566,20 +689,20 @@ FPS_API int fps_tile_partition2(const int32_t* uid, const int32_t* iid, const fl
   if (e != hipSuccess) return (int)e;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, cshift, NC, KT,
+  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, g,  cshift, NC, KT,
                      ccount, bcount, seen);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
   if (n > 0) {
     hipLaunchKernelGGL((tp2_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                       (const int4*)nullptr, n, chunk, W, half, R, T, upp, cshift, NC, (const int32_t*)cptr, ccursor,
+                       (const int4*)nullptr, n, chunk, g,  cshift, NC, (const int32_t*)cptr, ccursor,
                        (void*)tmp);
     if (rec8)
       hipLaunchKernelGGL((tp2_scatter_kernel<2, true>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+                         (const int4*)tmp, n, chunk, g,  cshift, KT, (const int32_t*)ptr, bcursor, rec);
     else
       hipLaunchKernelGGL((tp2_scatter_kernel<2, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, KT, (const int32_t*)ptr, bcursor, rec);
+                         (const int4*)tmp, n, chunk, g,  cshift, KT, (const int32_t*)ptr, bcursor, rec);
   }
   FPS_CHECK_LAUNCH();
   return 0;
@@ -605,7 +728,8 @@ static int tp3_cshift(int KT) {
 FPS_API int64_t fps_tile_partition3_ws_ints(int W, int T, int P) {
   const int KT = P * 2 * W * T;
   const int NC = ((KT - 1) >> tp3_cshift(KT)) + 1;
-  return 4 * (int64_t)NC + 2 + 2 * (int64_t)KT + 1024 * (int64_t)NC;  // + H1[G <= 1024][NC]
+  // + H1[G <= 1024][NC] + fine histograms [1 + 512][KT]
+  return 4 * (int64_t)NC + 2 + 2 * (int64_t)KT + 1024 * (int64_t)NC + 513 * (int64_t)KT;
 }
 
 FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
@@ -616,6 +740,7 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   const int cshift = tp3_cshift(KT);
   const int NC = ((KT - 1) >> cshift) + 1;
   if (NC > TP3_MAXK || (1 << cshift) > TP3_MAXK) return (int)hipErrorInvalidValue;
+  const TileGeo g = make_geo(W, half, R, T, upp);
   hipStream_t s = (hipStream_t)stream;
   int32_t* ccount = ws;
   int32_t* ccursor = ccount + NC;
@@ -628,8 +753,12 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   if (e != hipSuccess) return (int)e;
   const int G = fps_tile_partition_groups(n);
   const int64_t chunk = (n + G - 1) / G;
-  hipLaunchKernelGGL(tp2_count_kernel, dim3(G), dim3(1024), 0, s, uid, iid, n, chunk, W, half, R, T, upp, cshift, NC, KT,
-                     ccount, bcount, seen, H1);
+  const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
+  const int Gc = (G + sub - 1) / sub;
+  int32_t* bhist = H1 + 1024 * (int64_t)NC;  // [1 + Gc][KT]: totals, then one row per count workgroup
+  hipLaunchKernelGGL(tp3_count_kernel, dim3(Gc), dim3(1024), 0, s, uid, iid, n, chunk, G, sub, g, cshift, NC, KT, ccount, bhist, seen, H1);
+  hipLaunchKernelGGL(tp3_colsum_kernel, dim3((KT + 63) / 64), dim3(1024), 0, s, bhist, Gc, KT);
+  bcount = bhist;
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcount, KT, ptr);
   hipLaunchKernelGGL(tp3_colscan_kernel, dim3(NC), dim3(1024), 0, s, H1, G, NC, (const int32_t*)cptr);
@@ -637,16 +766,21 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   if (n > 0) {
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
     if (g2 > 1024) g2 = 1024;
-    hipLaunchKernelGGL((tp3_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                       (const int4*)nullptr, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)cptr, ccursor,
-                       (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
+    if (rec8)
+      hipLaunchKernelGGL((tp3_scatter_kernel<1, true>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)nullptr, n, chunk, g,  cshift, NC, KT, (const int32_t*)cptr,
+                         ccursor, (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
+    else
+      hipLaunchKernelGGL((tp3_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
+                         (const int4*)nullptr, n, chunk, g,  cshift, NC, KT, (const int32_t*)cptr,
+                         ccursor, (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
     if (rec8)
       hipLaunchKernelGGL((tp3_scatter_kernel<2, true>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int4*)tmp, n, chunk, g,  cshift, NC, KT, (const int32_t*)ptr, bcursor,
                          (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
     else
       hipLaunchKernelGGL((tp3_scatter_kernel<2, false>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, W, half, R, T, upp, cshift, NC, KT, (const int32_t*)ptr, bcursor,
+                         (const int4*)tmp, n, chunk, g,  cshift, NC, KT, (const int32_t*)ptr, bcursor,
                          (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
   }
   FPS_CHECK_LAUNCH();
