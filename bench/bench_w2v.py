@@ -30,6 +30,8 @@ def main(argv=None):
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--lr", type=float, default=0.005)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--shared-negatives", type=int, default=16, choices=[16, 32],
+                    help="negatives shared by each block of 32 pairs (16: kernel v4, 32: kernel v3)")
     a = ap.parse_args(argv)
 
     import torch
@@ -41,7 +43,7 @@ def main(argv=None):
     comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
-                                   wire_dtype=a.wire), comm=comm)
+                                   wire_dtype=a.wire, shared_negatives=a.shared_negatives), comm=comm)
     toks = synthetic_corpus(max(a.pairs // a.window, 1 << 16) * 2, a.vocab, seed=comm.rank, device=dev)
     c, o = skipgram_pairs(toks, a.window)
     n = c.numel()
@@ -75,7 +77,7 @@ def main(argv=None):
             "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
-            "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared 32/block)",
+            "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared {a.shared_negatives}/block)",
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)
 

@@ -231,11 +231,237 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- v4
+// M = 32 pairs x K4 = 16 shared negatives per block, 512-thread blocks, ~64 KB
+// of LDS: two blocks per CU, so one block's float atomics drain while the
+// other stages rows and runs its MFMAs (v3 held one 1024-thread block per CU at
+// 154 KB: its waves waited ~81 % of their cycles, SQ_WAIT_ANY / SQ_WAVE_CYCLES,
+// profiles/r1_w2v_v4.md).  The dH run reduction gathers a tile column's 32
+// rows in registers with one half-wave swap instead of a wave-private LDS tile,
+// and dN = G^T H is a 32x32x2 MFMA whose rows 16-31 are zero.
+constexpr int K4 = 16;
+constexpr int NT4 = 512;
+constexpr int NW4 = NT4 / 64;
+
+template <bool BF16>
+__global__ void __launch_bounds__(NT4) sgns_v4_kernel(const void* __restrict__ rows_in,
+                                                      const void* __restrict__ rows_out,
+                                                      const int32_t* __restrict__ pos_c,
+                                                      const int32_t* __restrict__ pos_o,
+                                                      const int32_t* __restrict__ pos_neg, int64_t n_pairs, int D,
+                                                      float lr, float neg_weight, float* __restrict__ d_in,
+                                                      float* __restrict__ d_out, float* __restrict__ loss_out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Dp = (D + 31) & ~31;
+  const int LD = Dp + 1;
+  float* Hs = smem;                 // [M][LD]
+  float* Ns = Hs + M * LD;          // [K4][LD]
+  float* Gs = Ns + K4 * LD;         // [M][K4+1]
+  float* gpos = Gs + M * (K4 + 1);  // [M]
+  int32_t* pc = (int32_t*)(gpos + M);
+  int32_t* po = pc + M;
+  int32_t* pn = po + M;             // [K4]
+  int32_t* lead = pn + K4;          // [M] first pair of the block with the same context
+  int32_t* nxt = lead + M;          // [M] next pair with the same context (-1: none)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n_blocks = (n_pairs + M - 1) / M;
+  constexpr int RPW = (M + K4) / NW4;  // staged rows per wave (6)
+
+  for (int64_t blk = blockIdx.x; blk < n_blocks; blk += gridDim.x) {
+    const int64_t p0 = blk * M;
+    const int npairs = (int)((n_pairs - p0) < M ? (n_pairs - p0) : M);
+    if (tid < M) {
+      pc[tid] = tid < npairs ? pos_c[p0 + tid] : -1;
+      po[tid] = tid < npairs ? pos_o[p0 + tid] : -1;
+    } else if (tid < M + K4) {
+      pn[tid - M] = pos_neg[blk * K4 + (tid - M)];
+    }
+    __syncthreads();
+    if (tid < M) {  // adjacent centers share most of their window: one dO row per distinct
+                    // context (12.9 distinct contexts per 32 pairs on the bench corpus)
+      int l = tid, nx = -1;
+      for (int j = 0; j < tid; ++j)
+        if (po[j] == po[tid]) { l = j; break; }
+      for (int j = tid + 1; j < M; ++j)
+        if (po[j] == po[tid]) { nx = j; break; }
+      lead[tid] = l;
+      nxt[tid] = nx;
+    }
+    {
+      float4 v[RPW][2];
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int r = wave + NW4 * j;
+        const bool is_h = r < M;
+        const int32_t rr = is_h ? pc[r] : pn[r - M];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = lane * 4 + 256 * h;
+          v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int r = wave + NW4 * j;
+        float* dst = r < M ? Hs + r * LD : Ns + (r - M) * LD;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = lane * 4 + 256 * h;
+          if (c < Dp) { dst[c] = v[j][h].x; dst[c + 1] = v[j][h].y; dst[c + 2] = v[j][h].z; dst[c + 3] = v[j][h].w; }
+        }
+      }
+    }
+    __syncthreads();
+    if (wave < 2) {
+      // ---- S = H N^T [32 x 16]: one 16x16 tile per wave over the full D
+      const int i = lane & 15, kq = lane >> 4;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* hrow = Hs + (16 * wave + i) * LD + kq;
+      const float* nrow = Ns + i * LD + kq;
+      for (int k = 0; k < Dp; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc, 0, 0, 0);
+      float lsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * wave + 4 * kq + r;
+        const bool ok = m < npairs;
+        const float sg = sigmoidf_(acc[r]);
+        Gs[m * (K4 + 1) + i] = ok ? -lr * neg_weight * sg : 0.f;
+        if (ok) lsum += -neg_weight * __logf(1.f - sg + 1e-12f);
+      }
+      if (loss_out) {
+        lsum = group_sum<64>(lsum);
+        if (lane == 0) atomicAdd(loss_out, lsum);
+      }
+    } else {
+      // ---- positive scores h.o (O read from global, coalesced), waves 2..7
+      for (int m = wave - 2; m < M; m += NW4 - 2) {
+        float p = 0.f;
+        if (m < npairs) {
+#pragma unroll 5
+          for (int c = lane; c < D; c += 64) p = fmaf(Hs[m * LD + c], ld1<BF16>(rows_out, (int64_t)po[m] * D + c), p);
+        }
+        p = group_sum<64>(p);
+        if (lane == 0) {
+          const bool ok = m < npairs;
+          gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
+          if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
+        }
+      }
+    }
+    __syncthreads();
+    // ---- dH = G N + g+ O [32 x 32 cols] and dN = G^T H [16 (of 32) x 32 cols]
+    const int ntile = Dp / 32;
+    const int i = lane & 31, kh = lane >> 5;
+    for (int t = wave; t < 2 * ntile; t += NW4) {
+      const bool is_h = t < ntile;
+      const int c0 = (is_h ? t : t - ntile) * 32;
+      const int col = c0 + i;
+      floatx16 acc = {0};
+      if (is_h) {
+#pragma unroll
+        for (int kk = 0; kk < K4; kk += 2) {
+          const int k = kk + kh;
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[i * (K4 + 1) + k], Ns[k * LD + c0 + i], acc, 0, 0, 0);
+        }
+        float v[16], o[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = acc_row(lane, r);
+          v[r] = acc[r];
+          if (row < npairs && col < D) v[r] += gpos[row] * ld1<BF16>(rows_out, (int64_t)po[row] * D + col);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
+        // this half-wave (kh) owns rows 16*kh .. 16*kh+15 of column col; row q sits in
+        // register (q&3) + 4*(q>>3) of the lane half whose (q>>2)&1 matches
+        const int r1 = min(16, npairs - 16 * kh);
+        float run = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int ri0 = (j & 3) + 4 * (j >> 3);         // q = j      (kh = 0)
+          const int ri1 = (j & 3) + 4 * (2 + (j >> 3));   // q = 16 + j (kh = 1)
+          const float a0 = (j & 4) ? o[ri0] : v[ri0];
+          const float a1 = (j & 4) ? v[ri1] : o[ri1];
+          const float val = kh ? a1 : a0;
+          if (j < r1) {
+            const int q = 16 * kh + j;
+            run += val;
+            if (j + 1 == r1 || pc[q + 1] != pc[q]) {
+              if (col < D) atomic_add_noret(d_in + (int64_t)pc[q] * D + col, run);
+              run = 0.f;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < M; kk += 2) {
+          const int k = kk + kh;
+          const float a = i < K4 ? Gs[k * (K4 + 1) + i] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Hs[k * LD + c0 + i], acc, 0, 0, 0);
+        }
+        if (col < D) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) atomic_add_noret(d_out + (int64_t)pn[acc_row(lane, r)] * D + col, acc[r]);
+        }
+      }
+    }
+    // ---- dO = g+ H summed over the pairs of one context: one wave per distinct
+    // context, 256-B atomic wave-instructions
+    for (int m = wave; m < npairs; m += NW4) {
+      if (lead[m] != m) continue;  // uniform in the wave
+      float a[(512 + 63) / 64];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = 0.f;
+      for (int q = m; q >= 0 && q < npairs; q = nxt[q]) {
+        const float g = gpos[q];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (lane + 64 * u < D) a[u] += g * Hs[q * LD + lane + 64 * u];
+      }
+      float* dst = d_out + (int64_t)po[m] * D;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (lane + 64 * u < D) atomic_add_noret(dst + lane + 64 * u, a[u]);
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 FPS_API size_t fps_sgns_smem_bytes(int D) {
   const int Dp = (D + 31) & ~31, LD = Dp + 1;
   return sizeof(float) * ((size_t)2 * 32 * LD + 32 * 33 + 32 + (size_t)NW * 32 * 33) + sizeof(int32_t) * 96;
+}
+
+FPS_API size_t fps_sgns_v4_smem_bytes(int D) {
+  const int Dp = (D + 31) & ~31, LD = Dp + 1;
+  return sizeof(float) * ((size_t)(32 + K4) * LD + 32 * (K4 + 1) + 32) + sizeof(int32_t) * (128 + K4);
+}
+
+// v4: pos_neg holds 16 negative rows per block of 32 pairs
+FPS_API int fps_sgns_step_v4(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
+                             const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
+                             float neg_weight, float* d_in, float* d_out, float* loss_out, void* stream) {
+  if (n_pairs <= 0) return 0;
+  if (((D + 31) & ~31) > 512) return (int)hipErrorInvalidValue;
+  const size_t smem = fps_sgns_v4_smem_bytes(D);
+  if (smem > 80 * 1024) return (int)hipErrorInvalidValue;  // two blocks per CU
+  const int64_t nb = (n_pairs + 31) / 32;
+  const int grid = (int)(nb < 256 * 2 * 4 ? nb : 256 * 2 * 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (rows_bf16) {
+    (void)hipFuncSetAttribute((const void*)sgns_v4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(sgns_v4_kernel<true>, dim3(grid), dim3(NT4), smem, s, rows_in, rows_out, pos_c, pos_o,
+                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
+  } else {
+    (void)hipFuncSetAttribute((const void*)sgns_v4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(sgns_v4_kernel<false>, dim3(grid), dim3(NT4), smem, s, rows_in, rows_out, pos_c, pos_o,
+                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
+  }
+  FPS_CHECK_LAUNCH();
+  return 0;
 }
 
 // pos_neg holds K = 32 negative rows per block of 32 pairs (ceil(n_pairs/32) blocks)

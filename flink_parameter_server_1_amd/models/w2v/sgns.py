@@ -40,10 +40,11 @@ class SGNSConfig:
     seed: int = 0
     wire_dtype: str = "fp32"
     pipeline: bool = True         # W > 1: row all-to-alls of batch k+1 overlap the SGNS step of batch k
+    shared_negatives: int = 16    # negatives shared by each block of 32 pairs (16: kernel v4, 32: v3)
 
 
 class DistributedSGNS:
-    BLOCK = 32  # pairs per block == shared negatives per block (kernel constant)
+    BLOCK = 32  # pairs per block (kernel constant); cfg.shared_negatives negatives per block
 
     def __init__(self, cfg: SGNSConfig, counts: Optional[torch.Tensor] = None, comm: Optional[Comm] = None):
         self.cfg = cfg
@@ -96,7 +97,7 @@ class DistributedSGNS:
         c = self.cfg
         P = centers.numel()
         nb = (P + self.BLOCK - 1) // self.BLOCK
-        negs = ops.sample_alias(self.prob, self.alias, nb * self.BLOCK, seed=c.seed + 17 * self.comm.rank,
+        negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives, seed=c.seed + 17 * self.comm.rank,
                                 counter=self.counter)
         self.counter += 1
         outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
@@ -120,7 +121,8 @@ class DistributedSGNS:
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
         loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
-                             c.negatives / self.BLOCK, d_in, d_out, with_loss=with_loss)
+                             c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
+                             neg_k=c.shared_negatives)
         self.ps_in.push(plan_in, d_in)
         self.ps_out.push(plan_out, d_out)
         self.pairs_seen += P

@@ -578,20 +578,30 @@ def sample_alias(prob: torch.Tensor, alias: torch.Tensor, n: int, seed: int = 0,
     return R.sample_alias(prob, alias, n, seed, counter)
 
 
+#: shared negatives per block of 32 pairs the SGNS kernels take (v4: 16, v3: 32)
+SGNS_NEG_K = (16, 32)
+
+
 def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: float, d_in, d_out,
-              with_loss: bool = False):
+              with_loss: bool = False, neg_k: int = 16):
     """Block-shared-negative skip-gram step on MFMA (K6); deltas accumulate into
-    ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has 32 rows per 32 pairs."""
+    ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has ``neg_k`` rows per 32
+    pairs: 16 runs kernel v4 (two 512-thread blocks per CU), 32 kernel v3."""
     D = rows_in.shape[1]
+    if neg_k not in SGNS_NEG_K:
+        raise ValueError(f"sgns_step: neg_k must be one of {SGNS_NEG_K}")
+    if pos_neg.numel() < neg_k * ((pos_c.numel() + 31) // 32):
+        raise ValueError("sgns_step: pos_neg needs neg_k rows per block of 32 pairs")
     if rows_in.is_cuda:
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
         lib = N.require()
-        N.check(lib.fps_sgns_step(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
+        fn = lib.fps_sgns_step_v4 if neg_k == 16 else lib.fps_sgns_step
+        N.check(fn(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
                                   int(rows_in.dtype == torch.bfloat16), _c(pos_c).data_ptr(), _c(pos_o).data_ptr(),
                                   _c(pos_neg).data_ptr(), pos_c.numel(), D, lr, neg_weight, _c(d_in).data_ptr(),
                                   _c(d_out).data_ptr(), N.ptr(loss), N.stream_ptr(rows_in.device)), "sgns_step")
         return loss
-    return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out)])
+    return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out, neg_k)])
 
 
 TOPK_MAX_K = 256

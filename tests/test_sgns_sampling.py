@@ -66,7 +66,8 @@ def test_sgns_distributed_gloo():
 @pytest.mark.parametrize("D", [16, 64, 100, 300])
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("runs", [False, True])
-def test_sgns_kernel_matches_reference(D, wire, runs):
+@pytest.mark.parametrize("neg_k", [16, 32])
+def test_sgns_kernel_matches_reference(D, wire, runs, neg_k):
     torch.manual_seed(D)
     Uin, Uout, P = 300, 400, 200
     rows_in = (torch.randn(Uin, D) * 0.3).to(wire)
@@ -75,13 +76,13 @@ def test_sgns_kernel_matches_reference(D, wire, runs):
     if runs:  # center-major order: runs of equal centers (summed in LDS before the atomics)
         pos_c = torch.sort(torch.randint(0, 40, (P,), dtype=torch.int32)).values
     pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
-    pos_neg = torch.randint(0, Uout, (((P + 31) // 32) * 32,), dtype=torch.int32)
+    pos_neg = torch.randint(0, Uout, (((P + 31) // 32) * neg_k,), dtype=torch.int32)
     d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
-    loss_r = R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, 0.05, 5 / 32, d_in_r, d_out_r)
+    loss_r = R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, 0.05, 5 / neg_k, d_in_r, d_out_r, neg_k)
     dev = "cuda"
     d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
     loss = ops.sgns_step(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), 0.05,
-                         5 / 32, d_in, d_out, with_loss=True)
+                         5 / neg_k, d_in, d_out, with_loss=True, neg_k=neg_k)
     torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=2e-6)
     torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=2e-6)
     assert abs(float(loss) - loss_r) / loss_r < 1e-4
