@@ -7,6 +7,9 @@
   exactly like the reference job (``M/matrix/factorization/PSOnlineMatrixFactorization.scala``),
   one worker + one PS subtask, every rating a pull + a push through the
   mailboxes -- measures the protocol overhead per record.
+* ``native``: the same per-record job (same messages, schedule and semantics,
+  tested equal to ``record`` on the folded model) in the C++ record engine
+  (``csrc/host/record_engine.cpp``, ``models.mf.native.ps_online_mf_native``).
 * ``tensor``: the same model on the tensor engine on CPU (``DistributedMF`` with
   the PyTorch reference ops), micro-batches of ``--batch`` ratings.
 
@@ -60,6 +63,25 @@ def run_record(n, users, items, rank, lr):
             "rmse": float(np.sqrt(np.mean(np.square(err)))) if err else None}
 
 
+def run_native(n, users, items, rank, lr, reps=5):
+    import numpy as np
+
+    from flink_parameter_server_1_amd.models.mf.native import ps_online_mf_native
+
+    _, (u, i, r) = _ratings(n, users, items, rank, 1)
+    best = None
+    for _ in range(reps):  # best of a few runs (sub-second job)
+        t0 = time.perf_counter()
+        res = ps_online_mf_native(u, i, r, num_factors=rank, range_min=0.0, range_max=0.3, learning_rate=lr,
+                                  worker_parallelism=1, ps_parallelism=1, pull_limit=1600, seed=7)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    U, V = res.users(), res.items()
+    err = [r[k] - float(np.dot(U[u[k]], V[i[k]])) for k in range(n)]
+    return {"engine": "native-record", "updates_per_s": n / best, "seconds": best,
+            "rmse": float(np.sqrt(np.mean(np.square(err)))), "messages": res.stats}
+
+
 def run_tensor(n, users, items, rank, lr, batch):
     import torch
 
@@ -89,17 +111,19 @@ def main(argv=None):
     ap.add_argument("--rank", type=int, default=8)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--batch", type=int, default=1000)
-    ap.add_argument("--engine", default="both", choices=["record", "tensor", "both"])
+    ap.add_argument("--engine", default="all", choices=["record", "native", "tensor", "all"])
     a = ap.parse_args(argv)
     res = []
-    if a.engine in ("record", "both"):
+    if a.engine in ("record", "all"):
         res.append(run_record(a.ratings, a.users, a.items, a.rank, a.lr))
-    if a.engine in ("tensor", "both"):
+    if a.engine in ("native", "all"):
+        res.append(run_native(a.ratings, a.users, a.items, a.rank, a.lr))
+    if a.engine in ("tensor", "all"):
         res.append(run_tensor(a.ratings, a.users, a.items, a.rank, a.lr, a.batch))
     for x in res:
         print(json.dumps({"metric": "MF-SGD rating updates/sec, 1k x 1k rank-8, 1 worker + 1 PS (CPU plumbing)",
                           "value": x["updates_per_s"], "unit": "updates/s", "n_gpus": 0, "higher_is_better": True,
-                          "dtype": "fp64" if x["engine"] == "record" else "fp32", "data": "synthetic rank-8 ratings",
+                          "dtype": "fp32" if x["engine"] == "tensor-cpu" else "fp64", "data": "synthetic rank-8 ratings",
                           **x}), flush=True)
 
 

@@ -31,7 +31,8 @@ from ...core.engine import PartitionedInput, transform, transform_with_double_mo
 from ...core.messages import Left, Right
 from ...ps.logics import SimplePSLogic
 from ...utils.eof import with_eof
-from .core import (IDGenerator, RangedRandomFactorInitializerDescriptor, SGDUpdater, attach_length, vector_sum)
+from .core import (USER_SEED_XOR, HashFactorInitializerDescriptor, IDGenerator, RangedRandomFactorInitializerDescriptor,
+                   SGDUpdater, attach_length, vector_sum)
 from .pruning import COORD, LI
 from .workers import (CollectTopKFromEachWorker, PSOfflineMatrixFactorizationWorker,
                       PSOnlineMatrixFactorizationAndTopKGeneratorWorker, PSOnlineMatrixFactorizationWorker,
@@ -41,11 +42,21 @@ from .workers import (CollectTopKFromEachWorker, PSOfflineMatrixFactorizationWor
 def ps_online_mf(src: Iterable, num_factors: int = 10, range_min: float = -0.01, range_max: float = 0.01,
                  learning_rate: float = 0.01, negative_sample_rate: int = 0, user_memory: int = 128,
                  pull_limit: int = 1600, worker_parallelism: int = 4, ps_parallelism: int = 4,
-                 iteration_wait_time: Optional[float] = None, seed: Optional[int] = None, runtime=None):
-    init = RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed).open()
+                 iteration_wait_time: Optional[float] = None, seed: Optional[int] = None, runtime=None,
+                 init: str = "ranged", lam: float = 0.0):
+    """``init="hash"``: per-id hash init (items: seed, users: seed ^ USER_SEED_XOR), the
+    init of ``ps_online_mf_native`` and the GPU tables (exact parity runs)."""
+    user_init = None
+    if init == "hash":
+        init = HashFactorInitializerDescriptor(num_factors, range_min, range_max, seed or 0).open()
+        user_init = HashFactorInitializerDescriptor(num_factors, range_min, range_max, (seed or 0) ^ USER_SEED_XOR)
+    elif init == "ranged":
+        init = RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed).open()
+    else:
+        raise ValueError(f"init must be 'ranged' or 'hash', not {init!r}")
     worker = PSOnlineMatrixFactorizationWorker(num_factors, range_min, range_max, learning_rate,
                                                user_memory=user_memory, negative_sample_rate=negative_sample_rate,
-                                               seed=seed)
+                                               seed=seed, lam=lam, factor_init=user_init)
     ps_logic = SimplePSLogic(lambda i: init.next_factor(i), vector_sum)
     return transform(src, add_pull_limiter(worker, pull_limit), ps_logic,
                      worker_parallelism=worker_parallelism, ps_parallelism=ps_parallelism,

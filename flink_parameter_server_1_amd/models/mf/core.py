@@ -211,6 +211,52 @@ class PseudoRandomFactorInitializerDescriptor(FactorInitializerDescriptor):
         return PseudoRandomFactorInitializer(self.num_factors)
 
 
+def _fmix32(x: int) -> int:
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+
+
+def hash_uniform01(seed: int, pid: int, j: int) -> float:
+    """The stateless U[0,1) of the device tables and the native engines
+    (``hash_uniform`` in csrc/kernels/common.h / csrc/host)."""
+    h = _fmix32((seed ^ 0x9E3779B9) & 0xFFFFFFFF)
+    h = _fmix32(h ^ (pid & 0xFFFFFFFF))
+    h = _fmix32(h ^ ((pid >> 32) & 0xFFFFFFFF) ^ 0x27D4EB2F)
+    h = _fmix32((h + j * 0x9E3779B9) & 0xFFFFFFFF)
+    return (h >> 8) * (1.0 / 16777216.0)
+
+
+class HashFactorInitializer(FactorInitializer):
+    """U[lo, hi) per coordinate from a hash of (seed, id, coordinate): deterministic
+    per id whatever the order of first touch (like ``PseudoRandomFactorInitializer``)
+    and identical to the native record engine / GPU table init."""
+
+    def __init__(self, num_factors, range_min, range_max, seed):
+        self.num_factors, self.lo, self.hi, self.seed = num_factors, range_min, range_max, seed & 0xFFFFFFFF
+
+    def next_factor(self, param_id):
+        return np.array([self.lo + (self.hi - self.lo) * hash_uniform01(self.seed, int(param_id), j)
+                         for j in range(self.num_factors)])
+
+
+@dataclass
+class HashFactorInitializerDescriptor(FactorInitializerDescriptor):
+    num_factors: int
+    range_min: float
+    range_max: float
+    seed: int = 0
+
+    def open(self):
+        return HashFactorInitializer(self.num_factors, self.range_min, self.range_max, self.seed)
+
+
+#: seed offset of the user-side hash init (the item side uses the job seed)
+USER_SEED_XOR = 0x5BD1E995
+
+
 # ------------------------------------------------------------------ updaters
 class FactorUpdater:
     def delta(self, rating: float, user, item) -> Tuple[np.ndarray, np.ndarray]:

@@ -64,8 +64,9 @@ class _SeenMemory:
 class PSOnlineMatrixFactorizationWorker(WorkerLogic):
     def __init__(self, num_factors: int, range_min: float, range_max: float, learning_rate: float,
                  user_memory: int = 128, negative_sample_rate: int = 0, seed: Optional[int] = None,
-                 lam: float = 0.0):
-        self.factor_init = RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed).open()
+                 lam: float = 0.0, factor_init=None):
+        self.factor_init = (factor_init.open() if factor_init is not None else
+                            RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed).open())
         self.factor_update = SGDUpdater(learning_rate, lam)
         self.negative_sample_rate = negative_sample_rate
         self.user_vectors: Dict[int, np.ndarray] = {}

@@ -32,6 +32,9 @@ _SIG = {
     "fps_hs_pull": ([c_vp, c_vp, c_i64, c_vp], None),
     "fps_hs_push": ([c_vp, c_vp, c_i64, c_vp, c_int], None),
     "fps_hs_dump": ([c_vp, c_vp, c_vp, c_i64], c_i64),
+    "fps_mf_online_record": ([c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_double, ctypes.c_double, c_u32, c_i64, c_int, c_int, c_vp, c_vp, c_i64, c_vp,
+                              c_vp, c_i64, c_vp, c_vp], c_int),
 }
 
 
