@@ -71,6 +71,8 @@ def _write_factors(stream, users_out, items_out):
 def cmd_mf(args, offline: bool):
     from .models.mf import apps
 
+    if not offline and getattr(args, "engine", "python") == "native":
+        return cmd_mf_native(args)
     ratings = _ratings_from_log(args.input)
     kw = dict(num_factors=args.num_factors, range_min=args.range_min, range_max=args.range_max,
               learning_rate=args.learning_rate, negative_sample_rate=args.negative_sample_rate,
@@ -80,6 +82,32 @@ def cmd_mf(args, offline: bool):
     out = apps.ps_offline_mf(ratings, iterations=args.iterations, **kw) if offline else apps.ps_online_mf(ratings, **kw)
     _write_factors(out, args.users_out, args.items_out)
     print(json.dumps({"ratings": len(ratings), "seconds": time.time() - t0, "outputs": len(out)}))
+
+
+def cmd_mf_native(args):
+    """Online MF through the C++ record engine (same job, same output files)."""
+    import numpy as np
+
+    from .models.mf.native import ps_online_mf_native
+    from .utils.io import write_factors_text
+
+    ratings = _ratings_from_log(args.input)
+    u = np.array([r.user for r in ratings], dtype=np.int64)
+    it = np.array([r.item for r in ratings], dtype=np.int64)
+    rt = np.array([r.rating for r in ratings], dtype=np.float64)
+    t0 = time.time()
+    res = ps_online_mf_native(u, it, rt, num_factors=args.num_factors, range_min=args.range_min,
+                              range_max=args.range_max, learning_rate=args.learning_rate,
+                              negative_sample_rate=args.negative_sample_rate, user_memory=args.user_memory,
+                              pull_limit=args.pull_limit, worker_parallelism=args.workers, ps_parallelism=args.ps,
+                              seed=args.seed or 0)
+    dt = time.time() - t0
+    for path, ids, vals in ((args.users_out, res.user_ids, res.user_vectors),
+                            (args.items_out, res.item_ids, res.item_vectors)):
+        if path:
+            o = np.argsort(ids)
+            write_factors_text(path, ids[o], vals[o].astype(np.float32))
+    print(json.dumps({"ratings": len(ratings), "seconds": dt, "engine": "native", **res.stats}))
 
 
 def cmd_mf_gpu(args):
@@ -244,6 +272,8 @@ def build_parser():
 
     p = sub.add_parser("mf-online")
     mf_common(p)
+    p.add_argument("--engine", choices=["python", "native"], default="python",
+                   help="native: the C++ record engine (csrc/host/record_engine.cpp)")
     p = sub.add_parser("mf-offline")
     mf_common(p)
     p.add_argument("--iterations", type=int, default=10)

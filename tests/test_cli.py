@@ -41,6 +41,19 @@ def test_cli_mf_gpu_path_with_checkpoint(tmp_path):
     assert (tmp_path / "ck").exists()
 
 
+def test_cli_mf_online_native_engine(tmp_path):
+    log = _log(tmp_path)
+    args = ["mf-online", "--input", log, "--workers", "2", "--ps", "2", "--num-factors", "4", "--seed", "3"]
+    out = _run(args + ["--engine", "native", "--users-out", str(tmp_path / "Un.map"), "--items-out",
+                       str(tmp_path / "In.map")], tmp_path)
+    stats = json.loads(out.strip().splitlines()[-1])
+    assert stats["engine"] == "native" and stats["pulls"] == stats["pushes"] == stats["ratings"]
+    from flink_parameter_server_1_amd.utils.io import read_factors_text
+
+    U, V = read_factors_text(str(tmp_path / "Un.map")), read_factors_text(str(tmp_path / "In.map"))
+    assert len(U) > 0 and len(V) > 0 and len(next(iter(U.values()))) == 4
+
+
 def test_cli_topk_and_pa(tmp_path):
     log = _log(tmp_path)
     _run(["mf-online", "--input", log, "--users-out", str(tmp_path / "U.map"), "--items-out", str(tmp_path / "I.map"),
