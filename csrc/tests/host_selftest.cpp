@@ -26,6 +26,9 @@ int64_t fps_hs_size(void*);
 void fps_hs_pull(void*, const int64_t*, int64_t, float*);
 void fps_hs_push(void*, const int64_t*, int64_t, const float*, int);
 int64_t fps_hs_dump(void*, int64_t*, float*, int64_t);
+int fps_mf_online_record(const int64_t*, const int64_t*, const double*, int64_t, int, int, int, double, double,
+                         double, double, uint32_t, int64_t, int, int, int64_t*, double*, int64_t, int64_t*, double*,
+                         int64_t, int64_t*, int64_t*);
 }
 
 static int failures = 0;
@@ -110,6 +113,24 @@ int main(int argc, char** argv) {
   CHECK(fps_hs_dump(h, dk.data(), dv.data(), 6000) == 5001);
   CHECK(fps_hs_dump(h, dk.data(), dv.data(), 10) == 10);  // cap respected
   fps_hs_destroy(h);
+
+  // native record engine: negatives + limiter + negative ids, exact message counts
+  {
+    const int64_t n = 4000;
+    std::vector<int64_t> u(n), it(n);
+    std::vector<double> r(n);
+    for (int64_t k = 0; k < n; ++k) { u[k] = (k * 7) % 97; it[k] = (k * 13) % 61 - 30; r[k] = (k % 5) * 0.2; }
+    std::vector<int64_t> uid(97), iid(61), counts(2), stats(7);
+    std::vector<double> uv(97 * 6), iv(61 * 6);
+    CHECK(fps_mf_online_record(u.data(), it.data(), r.data(), n, 3, 2, 6, 0.05, 0.01, -0.1, 0.1, 5, 4, 2, 16,
+                               uid.data(), uv.data(), 97, iid.data(), iv.data(), 61, counts.data(),
+                               stats.data()) == 0);
+    CHECK(counts[0] == 97);
+    CHECK(stats[0] == stats[1] && stats[0] == n + stats[6]);
+    CHECK(fps_mf_online_record(u.data(), it.data(), r.data(), n, 3, 2, 300, 0.05, 0.0, -0.1, 0.1, 5, 4, 0, 16,
+                               uid.data(), uv.data(), 97, iid.data(), iv.data(), 61, counts.data(),
+                               stats.data()) == -3);  // D > 256 rejected
+  }
 
   std::remove(rp.c_str());
   std::remove(fp.c_str());
