@@ -583,10 +583,12 @@ SGNS_NEG_K = (16, 32)
 
 
 def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: float, d_in, d_out,
-              with_loss: bool = False, neg_k: int = 16):
+              with_loss: bool = False, neg_k: int = 16, kernel: Optional[str] = None):
     """Block-shared-negative skip-gram step on MFMA (K6); deltas accumulate into
     ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has ``neg_k`` rows per 32
-    pairs: 16 runs kernel v4 (two 512-thread blocks per CU), 32 kernel v3."""
+    pairs: 16 runs kernel v4 (two 512-thread blocks per CU), 32 kernel v3.
+    ``kernel`` (or ``FPS_SGNS_KERNEL``) = "v5" runs the loader / atomic wave split
+    variant (D <= 320; measured slower than v4, profiles/r1_w2v_v4.md)."""
     D = rows_in.shape[1]
     if neg_k not in SGNS_NEG_K:
         raise ValueError(f"sgns_step: neg_k must be one of {SGNS_NEG_K}")
@@ -595,7 +597,13 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
     if rows_in.is_cuda:
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
         lib = N.require()
-        fn = lib.fps_sgns_step_v4 if neg_k == 16 else lib.fps_sgns_step
+        if neg_k == 32:
+            fn = lib.fps_sgns_step
+        else:
+            kern = kernel or os.environ.get("FPS_SGNS_KERNEL") or "v4"
+            if kern not in ("v4", "v5"):
+                raise ValueError(f"sgns_step: kernel must be 'v4' or 'v5', not {kern!r}")
+            fn = lib.fps_sgns_step_v5 if kern == "v5" else lib.fps_sgns_step_v4
         N.check(fn(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
                                   int(rows_in.dtype == torch.bfloat16), _c(pos_c).data_ptr(), _c(pos_o).data_ptr(),
                                   _c(pos_neg).data_ptr(), pos_c.numel(), D, lr, neg_weight, _c(d_in).data_ptr(),
