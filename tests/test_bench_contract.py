@@ -1,0 +1,49 @@
+"""bench.py driver contract on CPU: one JSON line with the required keys, at world
+size 1 and under torch.distributed.run at world size 2 (gloo), tiny shapes."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+TINY = ["--users", "3000", "--items", "700", "--batch", "4096", "--pool", "2", "--steps", "2", "--warmup", "1"]
+
+
+def _env():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    env.pop("FPS_SHARE_GPU", None)
+    return env
+
+
+def _json_lines(out: str):
+    return [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+
+
+def test_bench_single_rank_json_line():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + TINY, capture_output=True, text=True,
+                       timeout=300, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    assert d["config"]["global_batch"] == 4096
+
+
+@pytest.mark.parametrize("exchange", ["rotate", "ps"])
+def test_bench_two_ranks_gloo(exchange):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29671" if exchange == "rotate" else "29672",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--exchange", exchange] + TINY
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1  # rank 0 only
+    d = lines[0]
+    assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 4096
+    assert d["config"]["exchange"] == exchange
