@@ -78,6 +78,7 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
             "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared {a.shared_negatives}/block)",
+                       "exchange": "local-direct" if m._direct else "ps",
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)
 

@@ -13,6 +13,11 @@ micro-batch of (center, context) pairs:
    ``W_out`` (deduplicated all-to-all, ``TensorPS``);
 3. ``ops.sgns_step`` (MFMA, K6) computes per-row deltas;
 4. push both delta sets; the PS adds them.
+
+With one rank (``local_direct``, default) steps 2 and 4 collapse: the kernel
+reads the rows straight from the local tables and adds its deltas into them
+with its float atomics -- no dedup, gather, delta buffers or apply pass (the
+Hogwild update of the reference word2vec; the PS add is the same sum).
 """
 from __future__ import annotations
 
@@ -41,6 +46,7 @@ class SGNSConfig:
     wire_dtype: str = "fp32"
     pipeline: bool = True         # W > 1: row all-to-alls of batch k+1 overlap the SGNS step of batch k
     shared_negatives: int = 16    # negatives shared by each block of 32 pairs (16: kernel v4, 32: v3)
+    local_direct: bool = True     # W = 1: kernel reads / atomically updates the local tables in place
 
 
 class DistributedSGNS:
@@ -71,6 +77,8 @@ class DistributedSGNS:
         last one.  ``with_loss`` computes synchronously and returns the mean loss."""
         c = self.cfg
         lr = c.learning_rate if lr is None else lr
+        if self._direct:
+            return self._direct_step(centers, contexts, lr, with_loss)
         if with_loss:
             self.flush()
             return self._finish(self._start(centers, contexts), lr, True)
@@ -81,6 +89,37 @@ class DistributedSGNS:
                 self._finish(prev[0], prev[1], False)
         else:
             self._finish(pending, lr, False)
+        return None
+
+    @property
+    def _direct(self) -> bool:
+        return (self.cfg.local_direct and self.comm.world == 1 and self.w_in.optimizer == "add"
+                and self.w_out.optimizer == "add")
+
+    def _direct_step(self, centers, contexts, lr, with_loss):
+        """W = 1: rows of the local tables addressed by id (local row = id), deltas
+        added in place by the kernel's atomics."""
+        c = self.cfg
+        P = centers.numel()
+        nb = (P + self.BLOCK - 1) // self.BLOCK
+        dev = self.w_in.weight.device
+        negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives, seed=c.seed + 17 * self.comm.rank,
+                                counter=self.counter)
+        self.counter += 1
+        cen = centers.to(device=dev, dtype=torch.int32).contiguous()
+        ctx = contexts.to(device=dev, dtype=torch.int32).contiguous()
+        negs = negs.to(device=dev, dtype=torch.int32).contiguous()
+        if self.w_in.touched is not None:  # close-time dumps cover exactly the touched rows
+            self.w_in.touched[cen.long()] = 1
+        if self.w_out.touched is not None:
+            self.w_out.touched[ctx.long()] = 1
+            self.w_out.touched[negs.long()] = 1
+        loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
+                             c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
+                             with_loss=with_loss, neg_k=c.shared_negatives)
+        self.pairs_seen += P
+        if with_loss:
+            return float(loss.item()) / max(P, 1)
         return None
 
     @property

@@ -118,3 +118,26 @@ def test_sgns_gpu_training_reduces_loss():
         m.step(c[s:s + 8192], o[s:s + 8192])
     last = m.step(c[:8192], o[:8192], with_loss=True)
     assert last < 0.8 * first, (first, last)
+
+
+def test_sgns_local_direct_matches_ps_path_on_one_rank():
+    """W = 1 direct path (kernel updates the tables in place) trains like the PS
+    path and its close-time dump covers the same touched rows."""
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    res = {}
+    for direct in (True, False):
+        m = DistributedSGNS(SGNSConfig(vocab_size=2000, dim=32, learning_rate=0.005, local_direct=direct))
+        assert m._direct == direct
+        c, o = skipgram_pairs(synthetic_corpus(40000, 2000, seed=0), 5)
+        l0 = m.step(c[:4096], o[:4096], with_loss=True)
+        for i in range(30):
+            s = (i * 4096) % (c.numel() - 4096)
+            m.step(c[s:s + 4096], o[s:s + 4096])
+        l1 = m.step(c[:4096], o[:4096], with_loss=True)
+        ids, _ = m.embeddings()
+        res[direct] = (l0, l1, set(ids.tolist()))
+    assert res[True][1] < res[True][0] and res[False][1] < res[False][0]
+    assert abs(res[True][1] - res[False][1]) < 0.05 * res[False][1]
+    assert res[True][2] == res[False][2]
