@@ -70,7 +70,8 @@ def main(argv=None):
             "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic sparse CSR (hidden linear model labels)", "train_batch_accuracy": acc,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
-                       "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire},
+                       "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire,
+                       "exchange": "local-direct" if m._direct else "ps"},
         }), flush=True)
 
 

@@ -34,6 +34,7 @@ class PAConfig:
     aggressiveness: float = 1.0   # C
     partition: str = "range"      # range | hash
     wire_dtype: str = "fp32"
+    local_direct: bool = True     # W = 1: the PA kernel reads / atomically updates the table in place
 
 
 class DistributedPA:
@@ -55,8 +56,31 @@ class DistributedPA:
             self.cost = None
         self.examples = 0
 
+    @property
+    def _direct(self) -> bool:
+        return (self.cfg.local_direct and self.comm.world == 1 and self.table.optimizer == "add"
+                and self.table.partition in ("range", "hash"))
+
     def _run(self, indptr, indices, values, labels, train: bool, with_loss=False):
         c = self.cfg
+        if self._direct:
+            # one shard holding every feature (local row = feature id): the kernel reads
+            # the weights of each example's features and adds its deltas in place -- no
+            # dedup, gather, delta buffer or apply pass (asynchronous like the
+            # reference's per-feature pull / push interleaving)
+            w = self.table.weight
+            idx = indices.to(device=w.device, dtype=torch.int32).contiguous()
+            if train and self.table.touched is not None:
+                self.table.touched[idx.long()] = 1
+            if c.kind == "binary":
+                pred, loss = ops.pa_binary(indptr, values, idx, w.view(-1), labels, c.variant, c.aggressiveness,
+                                           w.view(-1), with_loss)
+            else:
+                pred, loss = ops.pa_multi(indptr, values, idx, w, labels, c.kind, c.variant, c.aggressiveness,
+                                          self.cost, w, with_loss)
+            if train:
+                self.examples += indptr.numel() - 1
+            return pred, loss
         rows, plan = self.ps.pull(indices)
         w = rows.float().contiguous()
         delta = torch.zeros((plan.n_unique, self.L), dtype=torch.float32, device=w.device)

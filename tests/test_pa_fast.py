@@ -118,12 +118,13 @@ def test_pa_multi_kernel_matches_reference(mode, L):
 
 
 @pytest.mark.gpu
-def test_pa_fast_gpu_learns_and_hashed_dedup():
+@pytest.mark.parametrize("direct", [False, True])
+def test_pa_fast_gpu_learns_and_hashed_dedup(direct):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    F = 1 << 29  # above the dense-map limit: exercises the hashed dedup
-    m = DistributedPA(PAConfig(feature_count=F, kind="binary"), Comm(device=torch.device("cuda")))
-    assert m.ps.dedup.hashed
+    F = 1 << 29  # above the dense-map limit: exercises the hashed dedup (PS path)
+    m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=direct), Comm(device=torch.device("cuda")))
+    assert m.ps.dedup.hashed and m._direct == direct
     # zipf 1: at heavier skew one batch sums thousands of PA steps on the hot features
     # and overshoots (the same happens on the CPU path: batch-synchronous PA semantics)
     batches = [synthetic_sparse_batch(4096, 32, F, seed=1, step=s, device="cuda", zipf=1.0) for s in range(4)]
