@@ -301,6 +301,22 @@ static inline int rows_grid(int64_t n, int TPR) {
   return grid_for(n, (int)rows_per_block, 256 * 32);
 }
 
+namespace {
+// touched[rows[i]] = 1 (close-time dump bookkeeping of the in-place update paths)
+__global__ void mark_rows_kernel(uint8_t* __restrict__ touched, const int32_t* __restrict__ rows, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    touched[rows[i]] = 1;
+}
+}  // namespace
+
+FPS_API int fps_mark_rows(uint8_t* touched, const int32_t* rows, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(mark_rows_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, touched,
+                     rows, n);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_init_rows(float* table, int64_t n_rows, int D, int64_t id_base, int64_t id_stride, float lo, float hi,
                           uint32_t seed, void* stream) {
   if (n_rows <= 0) return 0;

@@ -71,7 +71,7 @@ class DistributedPA:
             w = self.table.weight
             idx = indices.to(device=w.device, dtype=torch.int32).contiguous()
             if train and self.table.touched is not None:
-                self.table.touched[idx.long()] = 1
+                ops.mark_rows(self.table.touched, idx)
             if c.kind == "binary":
                 pred, loss = ops.pa_binary(indptr, values, idx, w.view(-1), labels, c.variant, c.aggressiveness,
                                            w.view(-1), with_loss)

@@ -110,10 +110,10 @@ class DistributedSGNS:
         ctx = contexts.to(device=dev, dtype=torch.int32).contiguous()
         negs = negs.to(device=dev, dtype=torch.int32).contiguous()
         if self.w_in.touched is not None:  # close-time dumps cover exactly the touched rows
-            self.w_in.touched[cen.long()] = 1
+            ops.mark_rows(self.w_in.touched, cen)
         if self.w_out.touched is not None:
-            self.w_out.touched[ctx.long()] = 1
-            self.w_out.touched[negs.long()] = 1
+            ops.mark_rows(self.w_out.touched, ctx)
+            ops.mark_rows(self.w_out.touched, negs)
         loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
                              c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
                              with_loss=with_loss, neg_k=c.shared_negatives)

@@ -70,6 +70,16 @@ def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: flo
     return R.init_rows(table, id_base, id_stride, lo, hi, seed)
 
 
+def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
+    """``touched[rows] = 1`` (uint8 flags, int32 rows): the dump bookkeeping of the
+    in-place (``local_direct``) update paths, one byte store per request."""
+    if _on_gpu(touched):
+        N.check(N.require().fps_mark_rows(touched.data_ptr(), _c(rows.to(torch.int32)).data_ptr(), rows.numel(),
+                                          N.stream_ptr(touched.device)), "mark_rows")
+        return
+    touched[rows.long()] = 1
+
+
 def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
                 touched: torch.Tensor = None) -> torch.Tensor:
     """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2)."""

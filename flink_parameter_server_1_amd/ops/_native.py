@@ -29,6 +29,7 @@ c_int, c_i64, c_f32, c_u32, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float,
 _SIGNATURES = {
     "fps_abi_version": [],
     "fps_init_rows": [c_vp, c_i64, c_int, c_i64, c_i64, c_f32, c_f32, c_u32, c_vp],
+    "fps_mark_rows": [c_vp, c_vp, c_i64, c_vp],
     "fps_gather_rows": [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_int, c_vp, c_vp],
     "fps_apply_rows": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_f32, c_f32, c_vp, c_vp],
     "fps_dedup": [c_vp, c_i64, c_vp, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
