@@ -117,10 +117,49 @@ struct RowStore {
   }
 };
 
-struct PSMsg {  // PS inbox: pulls (kind 0) and pushes (kind 1)
-  int64_t id;
-  int32_t worker;
-  int32_t kind;
+// FIFO ring of messages (id, worker, kind, D doubles of payload) grown by doubling:
+// one contiguous payload slot per message instead of per-double deque operations
+struct MsgRing {
+  int D;
+  std::vector<int64_t> id;
+  std::vector<int32_t> worker, kind;
+  std::vector<double> val;
+  size_t head = 0, count = 0;
+  explicit MsgRing(int d) : D(d) { grow(256); }
+  bool empty() const { return count == 0; }
+  size_t cap() const { return id.size(); }
+  void grow(size_t c) {
+    std::vector<int64_t> i2(c);
+    std::vector<int32_t> w2(c), k2(c);
+    std::vector<double> v2(c * (size_t)D);
+    for (size_t q = 0; q < count; ++q) {
+      const size_t s = (head + q) % cap();
+      i2[q] = id[s];
+      w2[q] = worker[s];
+      k2[q] = kind[s];
+      std::memcpy(&v2[q * D], &val[s * D], sizeof(double) * D);
+    }
+    id.swap(i2);
+    worker.swap(w2);
+    kind.swap(k2);
+    val.swap(v2);
+    head = 0;
+  }
+  void push(int64_t i, int32_t w, int32_t k, const double* v) {
+    if (count == cap()) grow(cap() * 2);
+    const size_t s = (head + count) % cap();
+    id[s] = i;
+    worker[s] = w;
+    kind[s] = k;
+    if (v != nullptr) std::memcpy(&val[s * D], v, sizeof(double) * D);
+    ++count;
+  }
+  size_t front() const { return head; }  // slot of the oldest message
+  const double* payload(size_t slot) const { return &val[slot * D]; }
+  void pop() {
+    head = (head + 1) % cap();
+    --count;
+  }
 };
 
 struct Worker {
@@ -141,15 +180,14 @@ struct Worker {
   std::vector<int64_t> input;  // rating indices of this partition, in order
   size_t cursor = 0;
   // pull answers: (item, value[D])
-  std::deque<int64_t> ans_id;
-  std::deque<double> ans_val;
+  MsgRing answers;
   // per-user memory of seen items (negative sampling)
   IndexMap user_slot;
   std::vector<std::deque<int64_t>> seen_fifo;  // may hold repeats (FIFO of every rated item)
   std::vector<std::vector<int64_t>> seen_set;   // distinct items (a repeat evicted from the FIFO
                                                 // leaves the set, as in the reference)
   uint64_t rng;
-  explicit Worker(int d, uint64_t seed) : D(d), users(d), rng(seed * 0x9e3779b97f4a7c15ull + 1) {}
+  explicit Worker(int d, uint64_t seed) : D(d), users(d), answers(d), rng(seed * 0x9e3779b97f4a7c15ull + 1) {}
 
   uint64_t next_rand() {  // splitmix64
     uint64_t z = (rng += 0x9e3779b97f4a7c15ull);
@@ -222,14 +260,15 @@ FPS_HOST_API int fps_mf_online_record(const int64_t* user, const int64_t* item, 
   std::vector<RowStore> ps;
   ps.reserve(P);
   for (int p = 0; p < P; ++p) ps.emplace_back(D);
-  std::vector<std::deque<PSMsg>> ps_inbox(P);
-  std::vector<std::deque<double>> ps_payload(P);  // push deltas, D per push, in inbox order
+  std::vector<MsgRing> ps_inbox;  // pulls (kind 0) and pushes with their delta (kind 1)
+  ps_inbox.reserve(P);
+  for (int p = 0; p < P; ++p) ps_inbox.emplace_back(D);
   int64_t n_pull = 0, n_push = 0, n_ans = 0, n_wout = 0, n_psout = 0, turns = 0, n_neg = 0;
   std::vector<double> du(D), di(D);
 
   auto send_pull = [&](int w, int64_t id) {
     const int p = (int)abs_mod(id, P);
-    ps_inbox[p].push_back(PSMsg{id, w, 0});
+    ps_inbox[p].push(id, w, 0, nullptr);
     ++n_pull;
   };
   auto limited_pull = [&](Worker& wk, int w, int64_t id) {  // M/WorkerLogic.scala:176-225
@@ -248,11 +287,12 @@ FPS_HOST_API int fps_mf_online_record(const int64_t* user, const int64_t* item, 
     for (int w = 0; w < W; ++w) {
       Worker& wk = workers[w];
       // ---- pull answers (limiter first: release one queued pull per answer)
-      for (int a = 0; a < kBatch && !wk.ans_id.empty(); ++a) {
-        const int64_t iid = wk.ans_id.front();
-        wk.ans_id.pop_front();
+      for (int a = 0; a < kBatch && !wk.answers.empty(); ++a) {
+        const size_t slot_a = wk.answers.front();
+        const int64_t iid = wk.answers.id[slot_a];
         double iv[256];
-        for (int j = 0; j < D; ++j) { iv[j] = wk.ans_val.front(); wk.ans_val.pop_front(); }
+        std::memcpy(iv, wk.answers.payload(slot_a), sizeof(double) * D);
+        wk.answers.pop();
         int64_t u;
         double r;
         const int32_t slot = wk.item_slot.find(iid);
@@ -284,8 +324,7 @@ FPS_HOST_API int fps_mf_online_record(const int64_t* user, const int64_t* item, 
         }
         ++n_wout;  // output((user, vec))
         const int p = (int)abs_mod(iid, P);
-        ps_inbox[p].push_back(PSMsg{iid, w, 1});
-        for (int j = 0; j < D; ++j) ps_payload[p].push_back(di[j]);
+        ps_inbox[p].push(iid, w, 1, di.data());
         ++n_push;
         ++n_ans;
         // limiter after the logic (its push goes first): release one queued pull
@@ -345,32 +384,33 @@ FPS_HOST_API int fps_mf_online_record(const int64_t* user, const int64_t* item, 
     for (int p = 0; p < P; ++p) {
       RowStore& st = ps[p];
       for (int a = 0; a < kBatch && !ps_inbox[p].empty(); ++a) {
-        const PSMsg m = ps_inbox[p].front();
-        ps_inbox[p].pop_front();
-        int32_t i = st.map.find(m.id);
-        if (m.kind == 0) {  // pull: lazy init, answer to the asking worker
+        MsgRing& box = ps_inbox[p];
+        const size_t slot_m = box.front();
+        const int64_t mid = box.id[slot_m];
+        const int32_t mworker = box.worker[slot_m], mkind = box.kind[slot_m];
+        int32_t i = st.map.find(mid);
+        if (mkind == 0) {  // pull: lazy init, answer to the asking worker
           if (i < 0) {
-            i = st.add(m.id);
+            i = st.add(mid);
             st.init_row(i, lo, hi, seed);
           }
-          Worker& wk = workers[m.worker];
-          wk.ans_id.push_back(m.id);
-          const double* v = st.row(i);
-          for (int j = 0; j < D; ++j) wk.ans_val.push_back(v[j]);
+          workers[mworker].answers.push(mid, 0, 0, st.row(i));
         } else {  // push: add (or store the delta for an unknown id), output (id, value)
+          const double* d = box.payload(slot_m);
           double* v;
           if (i < 0) {
-            i = st.add(m.id);
+            i = st.add(mid);
             v = st.row(i);
-            for (int j = 0; j < D; ++j) { v[j] = ps_payload[p].front(); ps_payload[p].pop_front(); }
+            for (int j = 0; j < D; ++j) v[j] = d[j];
           } else {
             v = st.row(i);
-            for (int j = 0; j < D; ++j) { v[j] += ps_payload[p].front(); ps_payload[p].pop_front(); }
+            for (int j = 0; j < D; ++j) v[j] += d[j];
           }
           for (int j = 0; j < D; ++j)
             if (std::isnan(v[j])) return -1;
           ++n_psout;
         }
+        box.pop();
         progressed = true;
       }
     }
