@@ -309,6 +309,174 @@ __global__ void mark_rows_kernel(uint8_t* __restrict__ touched, const int32_t* _
 }
 }  // namespace
 
+namespace {
+// ---- flag dedup: for batches that cover a large part of a dense key space (MF
+// items: 64M requests over 1M ids), the claim-map dedup spends its time in
+// contended atomicMax / owner lookups (2.5 + 1.75 ms for 64M keys).  Here every
+// request just stores the epoch into flag[key] (plain, idempotent), one scan over
+// the key space in shard-major order numbers the present keys, and each request
+// reads its slot back: no atomics, deterministic layout (unique keys sorted by
+// shard, then local key).
+constexpr int FLAG_CH = 4096;  // keys of the (virtual) key space per scan workgroup
+
+__global__ void flag_keys_kernel(const int32_t* __restrict__ keys, int64_t n, uint32_t* __restrict__ flag,
+                                 uint32_t epoch) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[b];
+    if (flag[k] != epoch) flag[k] = epoch;  // repeats of a key (64 per step for MF items) only read
+  }
+}
+
+// virtual index v (shard-major) -> key; hash: v = d * L + l, key = d + W * l; range: key = v
+__device__ __forceinline__ int64_t flag_key_of(int64_t v, int64_t num_ids, int W, int part_kind, int64_t L) {
+  if (part_kind != 0) return v;
+  const int64_t d = v / L, l = v - d * L;
+  return d + (int64_t)W * l;
+}
+
+__device__ __forceinline__ int32_t block_exclusive_scan_1024(int32_t x, int32_t* wsum, int32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int32_t before = 0;
+  total = 0;
+  for (int q = 0; q < 16; ++q) {
+    if (q < w) before += wsum[q];
+    total += wsum[q];
+  }
+  __syncthreads();  // wsum reused by the caller's next scan
+  return before + inc - x;
+}
+
+// pass 1: present keys per chunk of the virtual key space
+__global__ void __launch_bounds__(1024) flag_count_kernel(const uint32_t* __restrict__ flag, int64_t num_ids,
+                                                          int64_t V, int W, int part_kind, int64_t L,
+                                                          uint32_t epoch, int32_t* __restrict__ bsum) {
+  __shared__ int32_t wsum[16];
+  const int64_t v0 = (int64_t)blockIdx.x * FLAG_CH + threadIdx.x * 4;
+  int32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t v = v0 + q;
+    if (v < V) {
+      const int64_t k = flag_key_of(v, num_ids, W, part_kind, L);
+      c += (k < num_ids && flag[k] == epoch) ? 1 : 0;
+    }
+  }
+  int32_t total;
+  block_exclusive_scan_1024(c, wsum, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// pass 2 (one workgroup): exclusive scan of the chunk counts in place; bsum[nb] = total
+__global__ void __launch_bounds__(1024) flag_scan_kernel(int32_t* __restrict__ bsum, int nb) {
+  __shared__ int32_t wsum[16];
+  int32_t carry = 0;
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int32_t x = i < nb ? bsum[i] : 0;
+    int32_t total;
+    const int32_t ex = block_exclusive_scan_1024(x, wsum, total);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+// pass 3: slot of every present key, its local key in uniq, shard starts in prefix
+__global__ void __launch_bounds__(1024) flag_assign_kernel(const uint32_t* __restrict__ flag, int64_t num_ids,
+                                                           int64_t V, int W, int part_kind, int64_t L,
+                                                           int64_t block, uint32_t epoch,
+                                                           const int32_t* __restrict__ bsum,
+                                                           int32_t* __restrict__ slot, int32_t* __restrict__ uniq,
+                                                           int32_t* __restrict__ prefix) {
+  __shared__ int32_t wsum[16];
+  const int64_t v0 = (int64_t)blockIdx.x * FLAG_CH + threadIdx.x * 4;
+  bool pres[4];
+  int64_t key[4];
+  int32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t v = v0 + q;
+    key[q] = v < V ? flag_key_of(v, num_ids, W, part_kind, L) : num_ids;
+    pres[q] = key[q] < num_ids && flag[key[q]] == epoch;
+    c += pres[q] ? 1 : 0;
+  }
+  int32_t total;
+  int32_t at = bsum[blockIdx.x] + block_exclusive_scan_1024(c, wsum, total);
+  const int64_t shard_len = part_kind == 0 ? L : block;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t v = v0 + q;
+    if (v < V && v % shard_len == 0 && v / shard_len < W) prefix[v / shard_len] = at;  // first v of shard d
+    if (pres[q]) {
+      const int64_t k = key[q];
+      int64_t local;
+      if (part_kind == 0) local = k / W;
+      else { int64_t d = k / block; if (d >= W) d = W - 1; local = k - d * block; }
+      slot[k] = at;
+      uniq[at] = (int32_t)local;
+      ++at;
+    }
+  }
+}
+
+__global__ void flag_pos_kernel(const int32_t* __restrict__ keys, int64_t n, const int32_t* __restrict__ slot,
+                                int32_t* __restrict__ pos) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x)
+    pos[b] = slot[keys[b]];
+}
+
+__global__ void flag_counts_kernel(const int32_t* __restrict__ bsum, int nb, int W, int64_t V, int64_t shard_len,
+                                   int32_t* __restrict__ prefix, int32_t* __restrict__ counts) {
+  if (threadIdx.x != 0) return;
+  prefix[W] = bsum[nb];
+  for (int d = 0; d < W; ++d)
+    if ((int64_t)d * shard_len >= V) prefix[d] = bsum[nb];  // empty trailing range shard: never scanned
+  for (int d = 0; d < W; ++d) counts[d] = prefix[d + 1] - prefix[d];
+}
+}  // namespace
+
+// Flag dedup (see flag_keys_kernel).  flag / slot: num_ids entries (flag epoch-tagged,
+// never cleared); bsum: fps_dedup_flags_ws_ints(num_ids, W) ints.  Same outputs as
+// fps_dedup: counts[W], prefix[W+1], uniq (shard-major, ascending local keys), pos[n].
+FPS_API int64_t fps_dedup_flags_ws_ints(int64_t num_ids, int W) {
+  const int64_t L = (num_ids + W - 1) / W;
+  const int64_t V = (int64_t)W * L;
+  return (V + FLAG_CH - 1) / FLAG_CH + 1;
+}
+
+FPS_API int fps_dedup_flags(const int32_t* keys, int64_t n, uint32_t* flag, int32_t* slot, uint32_t epoch,
+                            int64_t num_ids, int W, int part_kind, int64_t block, int32_t* bsum, int32_t* counts,
+                            int32_t* prefix, int32_t* uniq, int32_t* pos, void* stream) {
+  if (W <= 0 || num_ids <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t L = (num_ids + W - 1) / W;
+  const int64_t V = part_kind == 0 ? (int64_t)W * L : num_ids;
+  const int nb = (int)((V + FLAG_CH - 1) / FLAG_CH);
+  if (part_kind != 0 && block <= 0) return (int)hipErrorInvalidValue;
+  if (n > 0)
+    hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, s, keys, n, flag, epoch);
+  hipLaunchKernelGGL(flag_count_kernel, dim3(nb), dim3(1024), 0, s, (const uint32_t*)flag, num_ids, V, W, part_kind,
+                     L, epoch, bsum);
+  hipLaunchKernelGGL(flag_scan_kernel, dim3(1), dim3(1024), 0, s, bsum, nb);
+  hipLaunchKernelGGL(flag_assign_kernel, dim3(nb), dim3(1024), 0, s, (const uint32_t*)flag, num_ids, V, W, part_kind,
+                     L, block, epoch, (const int32_t*)bsum, slot, uniq, prefix);
+  hipLaunchKernelGGL(flag_counts_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)bsum, nb, W, V,
+                     part_kind == 0 ? L : block, prefix, counts);
+  if (n > 0)
+    hipLaunchKernelGGL(flag_pos_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, s, keys, n,
+                       (const int32_t*)slot, pos);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_mark_rows(uint8_t* touched, const int32_t* rows, int64_t n, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mark_rows_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, touched,

@@ -104,16 +104,17 @@ class DistributedMF:
         #            atomics (atomic-rate bound: 3.9e9 ratings/s, profiles/README.md);
         #  "grouped" ratings sorted by item, each item row updated in registers
         #            (exact per-item order; latency bound, 2.8e9/s).
-        # local: the table as 2 blocks (halves) of one shard; rotate: 2W blocks
-        tile_w = 1 if exchange == "local" else W
-        block_rows = max(block_rows_of(cfg.num_items, tile_w))
+        # local: the table as 2 blocks (halves) of one shard; rotate: 2W blocks; ps:
+        # the pulled rows of a micro-batch (<= num_items unique items) as one block
+        tile_w = W if exchange == "rotate" else 1
+        block_rows = cfg.num_items if exchange == "ps" else max(block_rows_of(cfg.num_items, tile_w))
         tile_R = ops.tile_rows_for(cfg.dim, block_rows, tile_w)
         mode = cfg.sgd_mode
         if mode == "auto":
-            mode = "tiled" if (exchange != "ps" and tile_R is not None and not self.user_atomic) else "flat"
-        if mode == "tiled" and (exchange == "ps" or tile_R is None or self.user_atomic):
-            raise ValueError("sgd_mode 'tiled' needs exchange local/rotate, dim in ops.TILED_DIMS, "
-                             "a table small enough for the LDS bucket counters and user_update='store'")
+            mode = "tiled" if (tile_R is not None and not self.user_atomic) else "flat"
+        if mode == "tiled" and (tile_R is None or self.user_atomic):
+            raise ValueError("sgd_mode 'tiled' needs dim in ops.TILED_DIMS, a table small enough for the LDS "
+                             "bucket counters and user_update='store'")
         if mode == "grouped" and exchange == "rotate":
             raise ValueError("sgd_mode 'grouped' is not available with the rotation exchange")
         self.sgd_mode = mode
@@ -134,12 +135,14 @@ class DistributedMF:
                 P -= 1
             self.user_phases = max(1, P)
             upp = -(-self.users.n_local // self.user_phases)
-            self._tilers = [ops.TilePartitioner(tile_w, shard_halves(cfg.num_items, tile_w), tile_R, self.tile_T,
-                                                dev, rec8=rec8, phases=self.user_phases, users_per_phase=upp)
-                            for _ in range(2)]
+            halves = [cfg.num_items] if exchange == "ps" else shard_halves(cfg.num_items, tile_w)
+            self._tilers = [ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8,
+                                                phases=self.user_phases, users_per_phase=upp)
+                            for _ in range(2 if exchange != "ps" else 1)]
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
-            self._prefetch = cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
+            self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
+                              and exchange != "ps")
             self._side = torch.cuda.Stream(dev) if self._prefetch else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
@@ -185,7 +188,7 @@ class DistributedMF:
             ops.check_index(iid, c.num_items, "MF step iid")
         if c.negative_sample_rate > 0:
             uid_local, iid, rating = self._with_negatives(uid_local, iid, rating)
-        tiled = self.sgd_mode == "tiled"
+        tiled = self.sgd_mode == "tiled" and self.exchange != "ps"  # ps: tiled inside _compute_push
         if tiled and self._graphs is not None:
             self._graph_step(uid_local, iid, rating)
         elif tiled:
@@ -314,6 +317,16 @@ class DistributedMF:
 
     def _compute_push(self, rows, plan, uid_local, rating):
         c = self.cfg
+        if self.sgd_mode == "tiled":
+            # tile-grouped SGD on a working copy of the pulled rows (one block, no item
+            # atomics); the pushed delta is what the micro-batch added to each row
+            orig = rows.float()
+            work = orig.clone()
+            ptr, rec = self._tilers[0].run(uid_local, plan.pos, rating)
+            for p in range(self.user_phases):
+                ops.mf_sgd_tiled(self.U, work, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate, c.lam)
+            self.ps.push(plan, work.sub_(orig))
+            return
         if self.sgd_mode == "grouped":
             ptr, order = self.grouper.run(plan.pos, plan.n_unique)
             delta = torch.empty((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)

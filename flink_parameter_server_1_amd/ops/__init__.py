@@ -135,10 +135,18 @@ class DedupWorkspace:
     #: table, ~32 B per request) instead of a dense ``uint64[num_ids]`` map
     #: (1B-feature PA tables would otherwise need an 8 GB map per worker)
     DENSE_MAP_MAX_IDS = 1 << 28
+    #: dense id spaces at most this many times the batch use the flag dedup
+    #: (flag store per request + one scan of the key space, no atomics):
+    #: 64M MF item keys over 1M ids took 4.9 ms with the claim map
+    FLAGS_MAX_RATIO = 8
 
     def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu",
-                 hashed: Optional[bool] = None):
+                 hashed: Optional[bool] = None, method: Optional[str] = None):
         self.num_ids, self.W, self.part_kind, self.block = num_ids, W, part_kind, block
+        self.method = method or os.environ.get("FPS_DEDUP")  # None = auto | "claim" | "flags"
+        if self.method not in (None, "claim", "flags"):
+            raise ValueError(f"dedup method must be 'claim' or 'flags', not {self.method!r}")
+        self.flag = None
         self.device = torch.device(device)
         self.epoch = 0
         self.cap = 0
@@ -175,10 +183,24 @@ class DedupWorkspace:
         if self.epoch >= 0xFFFFFFFF:  # wrap: clear the tags once every 4e9 steps
             self.epoch = 1
             (self.tab if self.hashed else self.map).zero_()
+            if self.flag is not None:
+                self.flag.zero_()
         self.counts.zero_()
         lib = N.require()
         s = N.stream_ptr(self.device)
-        if self.hashed:
+        use_flags = not self.hashed and (self.method == "flags" or
+                                         (self.method is None and self.num_ids <= self.FLAGS_MAX_RATIO * n))
+        if use_flags:
+            if self.flag is None:
+                self.flag = torch.zeros(self.num_ids, dtype=torch.int32, device=self.device)
+                self.slot = torch.empty(self.num_ids, dtype=torch.int32, device=self.device)
+                self.bsum = torch.empty(lib.fps_dedup_flags_ws_ints(self.num_ids, self.W), dtype=torch.int32,
+                                        device=self.device)
+            N.check(lib.fps_dedup_flags(_c(keys).data_ptr(), n, self.flag.data_ptr(), self.slot.data_ptr(),
+                                        self.epoch, self.num_ids, self.W, self.part_kind, self.block,
+                                        self.bsum.data_ptr(), self.counts.data_ptr(), self.prefix.data_ptr(),
+                                        self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup_flags")
+        elif self.hashed:
             N.check(lib.fps_dedup_hashed(_c(keys).data_ptr(), n, self.tab.data_ptr(), self.hash_cap, self.epoch,
                                          self.W, self.part_kind, self.block, self.counts.data_ptr(),
                                          self.prefix.data_ptr(), self.hslot.data_ptr(), self.owner_slot_h.data_ptr(),

@@ -59,15 +59,19 @@ def test_apply_adagrad_bf16_delta():
     torch.testing.assert_close(state.cpu(), ref_s, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("method", ["claim", "flags"])
 @pytest.mark.parametrize("W,kind,hashed,num_ids", [(1, 0, False, 10007), (3, 0, False, 10007), (8, 0, False, 10007),
-                                                   (4, 1, False, 10007), (1, 0, True, 10007),
-                                                   (8, 0, True, 2_000_000_011), (4, 1, True, 2_000_000_011)])
-def test_dedup(W, kind, hashed, num_ids):
+                                                   (4, 1, False, 10007), (4, 1, False, 9), (3, 0, False, 300_000),
+                                                   (1, 0, True, 10007), (8, 0, True, 2_000_000_011),
+                                                   (4, 1, True, 2_000_000_011)])
+def test_dedup(W, kind, hashed, num_ids, method):
+    if hashed and method == "flags":
+        pytest.skip("flags is a dense-map method")
     block = -(-num_ids // W)
     keys = torch.randint(0, num_ids, (50000,), dtype=torch.int32)
-    if num_ids > 100000:  # make duplicates likely in a huge id space
+    if num_ids > 1_000_000:  # make duplicates likely in a huge id space
         keys = keys[torch.randint(0, 8000, (50000,))]
-    ws = ops.DedupWorkspace(num_ids, W, kind, block, DEV, hashed=hashed)
+    ws = ops.DedupWorkspace(num_ids, W, kind, block, DEV, hashed=hashed, method=method)
     for it in range(3):  # epoch tagging: later calls must not see earlier ones; 3rd call grows the hash table
         counts, prefix, uniq, pos = ws.run(keys.to(DEV))
         c_ref, p_ref, u_ref, pos_ref = R.dedup(keys, W, kind, block)
@@ -81,7 +85,7 @@ def test_dedup(W, kind, hashed, num_ids):
         _, local = R.shard_of(keys, W, kind, block)
         assert torch.equal(uniq[:U].cpu()[pos.cpu().long()].long(), local)
         keys = torch.randint(0, num_ids, (30000 if it == 0 else 90000,), dtype=torch.int32)
-        if num_ids > 100000:
+        if num_ids > 1_000_000:
             keys = keys[torch.randint(0, 5000, (keys.numel(),))]
 
 

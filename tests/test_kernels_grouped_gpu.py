@@ -55,7 +55,7 @@ def test_distributed_mf_grouped_vs_flat_converge():
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     res = {}
-    for mode in ("grouped", "flat"):
+    for mode in ("grouped", "flat", "tiled"):  # tiled + force_ps_path: tile-grouped SGD on the pulled rows
         for force in (False, True):
             cfg = MFConfig(num_users=5000, num_items=800, dim=16, learning_rate=0.1, range_min=0.0, range_max=0.3,
                            sgd_mode=mode, force_ps_path=force, wire_dtype="bf16" if force else "fp32")

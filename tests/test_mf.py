@@ -186,3 +186,21 @@ def test_tensor_mf_negative_sampling_implicit_feedback():
         for t in range(4):
             v = int(negs[b * 4 + t])
             assert v != int(iid[b]) and v not in ring[int(uid[b])].tolist()
+
+
+@pytest.mark.parametrize("mode", ["tiled", "flat"])
+def test_ps_path_tiled_on_pulled_rows_converges_cpu(mode):
+    """The pull/push path with the tile-grouped SGD on a working copy of the pulled
+    rows (delta = what the batch added) trains like the flat atomic kernel."""
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+
+    cfg = MFConfig(num_users=3000, num_items=500, dim=16, learning_rate=0.1, range_min=0.0, range_max=0.3,
+                   sgd_mode=mode, force_ps_path=True)
+    m = DistributedMF(cfg)
+    assert m.exchange == "ps" and m.sgd_mode == mode
+    data = SyntheticRatings(3000, 500, 60000, truth_dim=4)
+    uid, iid, r = data.batch(0, 60000)
+    before = m.rmse(uid, iid, r)
+    for s in range(30):
+        m.step(*data.batch(s, 6000))
+    assert m.rmse(uid, iid, r) < 0.5 * before
