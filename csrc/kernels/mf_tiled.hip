@@ -528,7 +528,8 @@ template <int TPR, int V, int PF, bool REC8>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
-                                                               int64_t block_rows, float lr, float lambda) {
+                                                               int64_t block_rows, float lr, float lambda,
+                                                               float* __restrict__ I1, int64_t block_rows1, int T0) {
   using Rec = typename RecT<REC8>::type;
   const Rec* __restrict__ rec = reinterpret_cast<const Rec*>(rec_);
   __shared__ Rec srec[TG_CAP];
@@ -537,8 +538,13 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
   __shared__ int32_t start[TG_MAX_R + 1];
   constexpr int D4 = TPR * V;
   constexpr int GPW = 64 / TPR;  // lane groups per wave
+  // tiles [0, T0) cover item block I, tiles [T0, grid) the next block I1 (one launch
+  // for two blocks with disjoint item rows: half the launch tails)
   const int t = blockIdx.x;
-  const int64_t r0 = (int64_t)t * R;
+  const bool second = t >= T0;
+  const int tl = second ? t - T0 : t;
+  if (second) { I = I1; block_rows = block_rows1; }
+  const int64_t r0 = (int64_t)tl * R;
   const int nr = (int)min((int64_t)R, block_rows - r0);
   const int32_t beg = ptr[t], end = ptr[t + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -789,17 +795,31 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
 
 // One launch per item block: T tiles of R (<= 256) rows of I[block_rows, D];
 // ptr = the block's T+1 tile offsets (device).  D must be 16, 32, 64, 128 or 256.
+FPS_API int fps_mf_sgd_tiled2(float* U, float* I, const void* rec, int rec8, const int32_t* ptr, int T, int R,
+                              int64_t block_rows, float* I1, int64_t block_rows1, int nblk, int D, float lr,
+                              float lambda, void* stream);
+
 FPS_API int fps_mf_sgd_tiled(float* U, float* I, const void* rec, int rec8, const int32_t* ptr, int T, int R,
                              int64_t block_rows, int D, float lr, float lambda, void* stream) {
+  return fps_mf_sgd_tiled2(U, I, rec, rec8, ptr, T, R, block_rows, I, block_rows, 1, D, lr, lambda, stream);
+}
+
+// nblk = 2: tiles ptr[0..2T] of two consecutive item blocks (I: block_rows, I1:
+// block_rows1) in one launch of 2T workgroups.
+FPS_API int fps_mf_sgd_tiled2(float* U, float* I, const void* rec, int rec8, const int32_t* ptr, int T, int R,
+                              int64_t block_rows, float* I1, int64_t block_rows1, int nblk, int D, float lr,
+                              float lambda, void* stream) {
   if (T <= 0) return 0;
+  if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
+  const int grid = nblk * T;
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
 #define FPS_TILED(TPR_, V_)                                                                                    \
-  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(T), dim3(512), 0, s, U, I,  \
-                               rec, ptr, R, block_rows, lr, lambda);                                          \
-  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(T), dim3(512), 0, s, U, I, rec, \
-                          ptr, R, block_rows, lr, lambda)
+  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, U, I, \
+                               rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T);                        \
+  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(grid), dim3(512), 0, s, U, I,    \
+                          rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T)
   switch (D) {
     case 16: FPS_TILED(4, 1); break;
     case 32: FPS_TILED(8, 1); break;

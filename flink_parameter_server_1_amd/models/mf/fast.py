@@ -32,6 +32,8 @@ row of ``dim`` floats), see BASELINE.md.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -147,6 +149,8 @@ class DistributedMF:
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
+            # both item blocks of a phase in one launch (FPS_MF_PAIR=0: one launch per block)
+            self.pair_blocks = os.environ.get("FPS_MF_PAIR", "1") == "1"
         if self.exchange == "rotate":
             self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
             self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
@@ -297,10 +301,15 @@ class DistributedMF:
         if ev is not None:
             torch.cuda.current_stream(self.U.device).wait_event(ev)
         if self.exchange == "local":
+            b0, b1 = self._local_blocks
             for p in range(self.user_phases):
-                for b, blk in enumerate(self._local_blocks):
-                    ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R, c.learning_rate,
-                                     c.lam)
+                if self.pair_blocks:
+                    ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
+                                          c.learning_rate, c.lam)
+                else:
+                    for b, blk in enumerate((b0, b1)):
+                        ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R,
+                                         c.learning_rate, c.lam)
             return
         for _ in range(self.rot.K):
             self.rot.begin()  # transfer of the next block overlaps this sub-step

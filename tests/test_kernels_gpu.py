@@ -248,6 +248,27 @@ def test_mf_sgd_tiled_unique_rows(D, rec8):
     torch.testing.assert_close(I.cpu(), Ir, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("rec8", [False, True])
+def test_mf_sgd_tiled_pair_matches_two_launches(rec8):
+    """Both item blocks in one launch (``mf_sgd_tiled_pair``): unique users and items,
+    so it equals the batch reference; blocks of unequal size."""
+    D, nu, ni, B = 64, 9000, 5001, 4000
+    U = torch.rand(nu, D, device=DEV) * 0.1
+    I = torch.rand(ni, D, device=DEV) * 0.1
+    uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
+    iid = torch.randperm(ni, device=DEV)[:B].to(torch.int32)
+    r = torch.rand(B, device=DEV)
+    h0 = 2600
+    Rt = ops.tile_rows_for(D, ni, 2)
+    T = -(-h0 // Rt)
+    ptr, rec = ops.TilePartitioner(1, [h0], Rt, T, DEV, rec8=rec8).run(uid, iid, r)
+    Ur, Ir = U.cpu().clone(), I.cpu().clone()
+    R.mf_sgd_local(Ur, Ir, uid.cpu(), iid.cpu(), r.cpu(), 0.05, 0.01)
+    ops.mf_sgd_tiled_pair(U, I[:h0], I[h0:], rec, ptr, 0, T, Rt, 0.05, 0.01)
+    torch.testing.assert_close(U.cpu(), Ur, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(I.cpu(), Ir, rtol=1e-5, atol=1e-6)
+
+
 def test_mf_sgd_tiled_duplicate_items_accumulate():
     """Many ratings per item: LDS atomics must keep every item delta (no lost update)."""
     D, B, ni = 64, 20000, 300

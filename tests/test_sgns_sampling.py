@@ -140,4 +140,8 @@ def test_sgns_local_direct_matches_ps_path_on_one_rank():
         res[direct] = (l0, l1, set(ids.tolist()))
     assert res[True][1] < res[True][0] and res[False][1] < res[False][0]
     assert abs(res[True][1] - res[False][1]) < 0.05 * res[False][1]
-    assert res[True][2] == res[False][2]
+    # both dumps cover every word that occurred; rows touched only as sampled negatives
+    # may differ (the two paths draw their negatives from different streams)
+    seen = set(c[:4096].tolist()) | set(o[:4096].tolist())
+    assert seen <= res[True][2] and seen <= res[False][2]
+    assert len(res[True][2] ^ res[False][2]) <= 0.01 * len(res[False][2])
