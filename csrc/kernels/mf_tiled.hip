@@ -30,6 +30,8 @@
 // wave-quarter).
 #include "common.h"
 
+#include <type_traits>
+
 using namespace fps;
 
 namespace {
@@ -607,13 +609,16 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
       }
       for (int k0 = a; k0 < b; k0 += PF) {
         float4 uv[PF][V];
-        int64_t ur[PF];
+        // float4 offsets of the user rows: 32-bit for 8-B records (user < 2^24, D4 <= 64),
+        // 14 fewer live VGPRs than 64-bit offsets
+        using Off = typename std::conditional<REC8, uint32_t, int64_t>::type;
+        Off ur[PF];
         float rv[PF];
 #pragma unroll
         for (int q = 0; q < PF; ++q) {  // all PF user rows in flight (index clamped, result masked)
           int32_t u; int rw;
           get_rec<REC8>(srec[min(k0 + q, b - 1)], r0, u, rw, rv[q]);
-          ur[q] = (int64_t)u * D4;
+          ur[q] = (Off)u * D4;
 #pragma unroll
           for (int v = 0; v < V; ++v) uv[q][v] = Ug[ur[q] + j + v * TPR];
         }

@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  (must precede the library load, see docstring)
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
-KERNELS_SO = os.path.join(_LIB_DIR, "libfps_kernels.so")
+KERNELS_SO = os.environ.get("FPS_KERNELS_SO") or os.path.join(_LIB_DIR, "libfps_kernels.so")  # override: A/B of builds
 
 _lock = threading.Lock()
 _lib = None
