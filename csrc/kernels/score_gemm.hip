@@ -25,17 +25,10 @@ constexpr int LDK = KB + 1;
 
 __device__ __forceinline__ int acc_row(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-__global__ void __launch_bounds__(256) score_gemm_kernel(const float* __restrict__ Q, const float* __restrict__ X,
-                                                         float* __restrict__ S, int B, int N, int D, int64_t ldS) {
-  __shared__ float Qs[TB * LDK];
-  __shared__ float Xs[TB * LDK];
-  const int nbx = (N + TB - 1) / TB, nby = (B + TB - 1) / TB;
-  const int nwg = nbx * nby;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  // query tiles fastest: the (few) blocks that read one item panel are
-  // consecutive logical ids, i.e. on one XCD, so X is fetched into one L2
-  const int by = wg % nby, bx = wg / nby;
-  const int i0 = bx * TB, q0 = by * TB;
+// The 64 x 64 score tile (q0.., i0..) of this workgroup: wave (wr, wc) holds the
+// 32 x 32 sub-tile in acc (row wr*32 + acc_row(lane, r), column wc*32 + lane%32).
+__device__ __forceinline__ floatx16 score_tile(const float* __restrict__ Q, const float* __restrict__ X, int B,
+                                               int N, int D, int q0, int i0, float* Qs, float* Xs) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   floatx16 acc = {0};
@@ -79,6 +72,28 @@ __global__ void __launch_bounds__(256) score_gemm_kernel(const float* __restrict
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Qs[ar * LDK + kk + kh], Xs[br * LDK + kk + kh], acc, 0, 0, 0);
     __syncthreads();
   }
+  return acc;
+}
+
+// workgroup -> (query tile, item tile): query tiles fastest, so the (few) blocks
+// that read one item panel are consecutive logical ids, i.e. on one XCD, and X
+// is fetched into one L2
+__device__ __forceinline__ void tile_of(int B, int N, int& q0, int& i0) {
+  const int nbx = (N + TB - 1) / TB, nby = (B + TB - 1) / TB;
+  const int wg = xcd_remap(blockIdx.x, nbx * nby);
+  q0 = (wg % nby) * TB;
+  i0 = (wg / nby) * TB;
+}
+
+__global__ void __launch_bounds__(256) score_gemm_kernel(const float* __restrict__ Q, const float* __restrict__ X,
+                                                         float* __restrict__ S, int B, int N, int D, int64_t ldS) {
+  __shared__ float Qs[TB * LDK];
+  __shared__ float Xs[TB * LDK];
+  int q0, i0;
+  tile_of(B, N, q0, i0);
+  const floatx16 acc = score_tile(Q, X, B, N, D, q0, i0, Qs, Xs);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
   const int col = i0 + wc * 32 + (lane & 31);
   if (col < N) {
 #pragma unroll
@@ -89,7 +104,67 @@ __global__ void __launch_bounds__(256) score_gemm_kernel(const float* __restrict
   }
 }
 
+__device__ __forceinline__ uint32_t score_key(float f) {  // order-preserving float -> uint32 (as topk.hip)
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Scoring fused with the top-K threshold filter: scores are never stored; each
+// one strictly above its query's current k-th best (best_s[q, k-1]) is appended
+// to the query's candidate list (key, item id) -- after the first items of a
+// length-sorted scan, only a few hundred of a bucket's 64k items per query pass.
+// cnt[q] counts every passing score; entries beyond cap are dropped (the caller
+// sees cnt > cap and rescans the segment unfused).
+__global__ void __launch_bounds__(256) score_filter_kernel(const float* __restrict__ Q, const float* __restrict__ X,
+                                                           const int64_t* __restrict__ ids, int B, int N, int D,
+                                                           const float* __restrict__ best_s, int k,
+                                                           uint32_t* __restrict__ cand_key,
+                                                           int64_t* __restrict__ cand_id, int32_t* __restrict__ cnt,
+                                                           int cap) {
+  __shared__ float Qs[TB * LDK];
+  __shared__ float Xs[TB * LDK];
+  __shared__ uint32_t ktau[TB];
+  int q0, i0;
+  tile_of(B, N, q0, i0);
+  if (threadIdx.x < TB) {
+    const int q = q0 + threadIdx.x;
+    ktau[threadIdx.x] = q < B ? score_key(best_s[(int64_t)q * k + k - 1]) : 0xffffffffu;
+  }
+  // (score_tile's first __syncthreads orders the ktau stores before the reads below)
+  const floatx16 acc = score_tile(Q, X, B, N, D, q0, i0, Qs, Xs);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int col = i0 + wc * 32 + (lane & 31);
+  if (col >= N) return;
+  const int64_t id = ids[col];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rl = wr * 32 + acc_row(lane, r);
+    const uint32_t key = score_key(acc[r]);
+    if (key > ktau[rl]) {  // rows past B have ktau = max: never pass
+      const int q = q0 + rl;
+      const int slot = atomicAdd(cnt + q, 1);
+      if (slot < cap) {
+        cand_key[(int64_t)q * cap + slot] = key;
+        cand_id[(int64_t)q * cap + slot] = id;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+FPS_API int fps_score_filter(const float* Q, const float* X, const int64_t* ids, int B, int N, int D,
+                             const float* best_s, int k, uint32_t* cand_key, int64_t* cand_id, int32_t* cnt, int cap,
+                             void* stream) {
+  if (B <= 0 || N <= 0) return 0;
+  if (k <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  const int nwg = ((N + TB - 1) / TB) * ((B + TB - 1) / TB);
+  hipLaunchKernelGGL(score_filter_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, Q, X, ids, B, N, D, best_s, k,
+                     cand_key, cand_id, cnt, cap);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
 
 FPS_API int fps_score_gemm(const float* Q, const float* X, float* S, int B, int N, int D, int64_t ldS, void* stream) {
   if (B <= 0 || N <= 0) return 0;

@@ -55,6 +55,42 @@ __device__ int select_bin(const uint32_t* hist, uint32_t need, uint32_t* above, 
   return *bin_out;
 }
 
+// LDS skey/sid[0, nc) hold candidates: append the running top-k (bs, bi), sort
+// (key desc, ties: smaller id first) and write back the first k
+__device__ void sort_keep_k(uint32_t* skey, int64_t* sid, int nc, float* bs, int64_t* bi, int k) {
+  const int tid = threadIdx.x;
+  // append the running top-k, pad to a power of two
+  int m = nc + k;
+  int P = 1;
+  while (P < m) P <<= 1;
+  for (int i = tid; i < P; i += TK_NT) {
+    if (i >= nc && i < m) { skey[i] = fkey(bs[i - nc]); sid[i] = bi[i - nc]; }
+    else if (i >= m) { skey[i] = 0u; sid[i] = INT64_MAX; }
+  }
+  __syncthreads();
+  // 4. bitonic sort, descending by key (ties: smaller id first)
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P; i += TK_NT) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const uint32_t ki = skey[i], kj = skey[j];
+          const int64_t ii = sid[i], ij = sid[j];
+          // "i before j" in the final order: larger key, or equal key and smaller id
+          const bool i_first = ki > kj || (ki == kj && ii < ij);
+          if (desc != i_first) { skey[i] = kj; skey[j] = ki; sid[i] = ij; sid[j] = ii; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += TK_NT) {
+    bs[i] = kfloat(skey[i]);
+    bi[i] = skey[i] == 0u ? -1 : sid[i];
+  }
+}
+
 __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restrict__ S, int64_t ldS, int n,
                                                            const int64_t* __restrict__ ids,
                                                            float* __restrict__ best_s, int64_t* __restrict__ best_i,
@@ -124,36 +160,27 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   }
   __syncthreads();
   const int nc = (int)min(cnt, (uint32_t)TK_CAP);
-  // append the running top-k, pad to a power of two
-  int m = nc + k;
-  int P = 1;
-  while (P < m) P <<= 1;
-  for (int i = tid; i < P; i += TK_NT) {
-    if (i >= nc && i < m) { skey[i] = fkey(bs[i - nc]); sid[i] = bi[i - nc]; }
-    else if (i >= m) { skey[i] = 0u; sid[i] = INT64_MAX; }
+  sort_keep_k(skey, sid, nc, bs, bi, k);
+}
+
+// Candidate lists from the fused scoring (score_gemm.hip: score_filter_kernel):
+// query row's cnt[row] (<= cap, checked by the caller) candidates are merged into
+// its running top-k exactly as above.
+__global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* __restrict__ cand_key,
+                                                                const int64_t* __restrict__ cand_id,
+                                                                const int32_t* __restrict__ cnt, int cap,
+                                                                float* __restrict__ best_s,
+                                                                int64_t* __restrict__ best_i, int k) {
+  __shared__ uint32_t skey[TK_SORT];
+  __shared__ int64_t sid[TK_SORT];
+  const int row = blockIdx.x;
+  const int nc = min(min(cnt[row], cap), TK_CAP);
+  if (nc == 0) return;  // nothing beat the k-th best: the list stands
+  for (int i = threadIdx.x; i < nc; i += TK_NT) {
+    skey[i] = cand_key[(int64_t)row * cap + i];
+    sid[i] = cand_id[(int64_t)row * cap + i];
   }
-  __syncthreads();
-  // 4. bitonic sort, descending by key (ties: smaller id first)
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < P; i += TK_NT) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool desc = (i & size) == 0;
-          const uint32_t ki = skey[i], kj = skey[j];
-          const int64_t ii = sid[i], ij = sid[j];
-          // "i before j" in the final order: larger key, or equal key and smaller id
-          const bool i_first = ki > kj || (ki == kj && ii < ij);
-          if (desc != i_first) { skey[i] = kj; skey[j] = ki; sid[i] = ij; sid[j] = ii; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = tid; i < k; i += TK_NT) {
-    bs[i] = kfloat(skey[i]);
-    bi[i] = skey[i] == 0u ? -1 : sid[i];
-  }
+  sort_keep_k(skey, sid, nc, best_s + (int64_t)row * k, best_i + (int64_t)row * k, k);
 }
 
 }  // namespace
@@ -165,6 +192,17 @@ FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int6
   if (k <= 0 || k > TK_MAXK) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s, best_i,
                      k);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// candidate lists [B, cap] from fps_score_filter; every cnt[q] must be <= cap (TK_CAP at most)
+FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id, const int32_t* cnt, int cap, int B,
+                                float* best_s, int64_t* best_i, int k, void* stream) {
+  if (B <= 0) return 0;
+  if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
+                     best_s, best_i, k);
   FPS_CHECK_LAUNCH();
   return 0;
 }

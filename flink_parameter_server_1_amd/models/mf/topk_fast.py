@@ -36,6 +36,11 @@ class LempTopK:
         self.lengths = lengths[order]
         self.bucket = bucket_size
         self.buckets_scanned = 0
+        #: GPU: score the first ``seed_items`` items unfused (sets every query's k-th
+        #: best), then fuse scoring with the threshold filter (``ops.score_filter``)
+        self.fused = True
+        self.seed_items = 4096
+        self.overflows = 0
 
     def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None):
         """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
@@ -47,15 +52,36 @@ class LempTopK:
         best_s = torch.full((B, k), float("-inf"), device=dev)
         best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
         N = self.vecs.shape[0]
+        fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
+        # segments: the first ``seed_items`` (longest) items, then the rest of each bucket
+        seed = min(N, self.seed_items) if fused else 0
+        bounds = sorted({0, seed, *range(self.bucket, N, self.bucket), N} - {N}) + [N]
         S = None
-        for s in range(0, N, self.bucket):
-            e = min(N, s + self.bucket)
+        cand = None
+        for s, e in zip(bounds[:-1], bounds[1:]):
             # LEMP bucket bound: no item of this or later buckets can beat the k-th best
             if s > 0 and bool((qlen * self.lengths[s] <= best_s[:, -1]).all()):
                 break
             n = e - s
+            if s % self.bucket == 0:
+                self.buckets_scanned += 1
+            if fused and s > 0:
+                # scoring fused with the k-th-best filter: only the few passing scores
+                # leave the kernel (no [B, n] score matrix)
+                if cand is None:
+                    cap = ops.TOPK_CAND_CAP
+                    cand = (torch.empty((B, cap), dtype=torch.int32, device=dev),
+                            torch.empty((B, cap), dtype=torch.long, device=dev),
+                            torch.empty(B, dtype=torch.int32, device=dev))
+                ck, ci, cnt = cand
+                cnt.zero_()
+                ops.score_filter(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt)
+                if int(cnt.max()) <= ck.shape[1]:
+                    ops.topk_merge_cand(ck, ci, cnt, best_s, best_i)
+                    continue
+                self.overflows += 1  # some query passed more than cap scores: rescan unfused
             if S is None or S.shape[1] < n:
-                S = torch.empty((B, self.bucket), device=dev)
+                S = torch.empty((B, max(n, self.bucket)), device=dev)
             ops.score_gemm(Q, self.vecs[s:e], S[:, :n])
             if dev.type == "cuda" and k <= ops.TOPK_MAX_K:
                 ops.topk_merge(S[:, :n], self.ids[s:e], best_s, best_i)  # threshold filter + LDS sort
@@ -64,7 +90,6 @@ class LempTopK:
                 top_s, top_j = torch.topk(cand_s, min(k, cand_s.shape[1]), dim=1)
                 cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
                 best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
-            self.buckets_scanned += 1
         return best_s, best_i
 
 

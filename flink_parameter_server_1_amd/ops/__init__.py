@@ -683,6 +683,33 @@ def topk_merge(S: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, best_i:
     best_i.copy_(torch.gather(cand_i, 1, j))
 
 
+#: candidates kept per query and segment by ``score_filter`` (<= the merge's LDS capacity)
+TOPK_CAND_CAP = 2048
+
+
+def score_filter(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, cand_key: torch.Tensor,
+                 cand_id: torch.Tensor, cnt: torch.Tensor) -> None:
+    """Fused K8 scoring + threshold filter (GPU only): every ``<Q[b], X[i]>`` strictly above
+    ``best_s[b, -1]`` is appended to row ``b`` of ``cand_key``/``cand_id`` ``[B, cap]``
+    (order-preserving uint32 keys as int32 storage); ``cnt[b]`` (zeroed by the caller)
+    counts all of them, so ``cnt > cap`` means the row overflowed."""
+    B, D = Q.shape
+    cap = cand_key.shape[1]
+    N.check(N.require().fps_score_filter(_c(Q).data_ptr(), _c(X).data_ptr(), _c(ids).data_ptr(), B, X.shape[0], D,
+                                         _c(best_s).data_ptr(), best_s.shape[1], _c(cand_key).data_ptr(),
+                                         _c(cand_id).data_ptr(), _c(cnt).data_ptr(), cap, N.stream_ptr(Q.device)),
+            "score_filter")
+
+
+def topk_merge_cand(cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Tensor, best_s: torch.Tensor,
+                    best_i: torch.Tensor) -> None:
+    """Merge ``score_filter`` candidate lists into the running top-k in place (K13)."""
+    B, cap = cand_key.shape
+    N.check(N.require().fps_topk_merge_cand(_c(cand_key).data_ptr(), _c(cand_id).data_ptr(), _c(cnt).data_ptr(), cap,
+                                            B, _c(best_s).data_ptr(), _c(best_i).data_ptr(), best_s.shape[1],
+                                            N.stream_ptr(best_s.device)), "topk_merge_cand")
+
+
 def score_gemm(Q: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """``out[b, i] = <Q[b], X[i]>`` on MFMA (fp32 in/accumulate, K8 scoring).  ``out`` may be
     a column slice of a wider buffer (row stride taken from it)."""

@@ -82,6 +82,52 @@ def test_lemp_topk_gpu_exact():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4096, 1])
+def test_lemp_topk_fused_equals_unfused(seed):
+    """Fused scoring + filter (``ops.score_filter``) == the materialised-score scan; seed 1
+    leaves the k-th best at ~-inf, so the fused segments overflow and rescan unfused."""
+    g = torch.Generator().manual_seed(4)
+    X = (torch.randn(100000, 64, generator=g) * torch.rand(100000, 1, generator=g) ** 2).cuda()
+    ids = torch.arange(100000, device="cuda") * 3 + 1
+    Q = torch.randn(300, 64, generator=g).cuda()
+    fused = LempTopK(ids, X, bucket_size=16384)
+    fused.seed_items = seed
+    s, i = fused.query(Q, 100)
+    plain = LempTopK(ids, X, bucket_size=16384)
+    plain.fused = False
+    s0, i0 = plain.query(Q, 100)
+    torch.testing.assert_close(s, s0, rtol=0, atol=0)
+    assert float((i == i0).float().mean()) > 0.999
+    assert (fused.overflows > 0) == (seed == 1)
+    bs, _ = torch.topk(Q @ X.T, 100, dim=1)
+    torch.testing.assert_close(s, bs, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_score_filter_counts_and_candidates():
+    """Every score strictly above the row's k-th best is listed, with its item id."""
+    torch.manual_seed(0)
+    B, n, D, k = 130, 3000, 64, 10
+    Q, X = torch.randn(B, D, device="cuda"), torch.randn(n, D, device="cuda")
+    ids = torch.arange(n, device="cuda") + 100
+    best_s = torch.sort(torch.randn(B, k, device="cuda") * 3 + 6, dim=1, descending=True)[0]
+    cap = 512
+    ck = torch.empty((B, cap), dtype=torch.int32, device="cuda")
+    ci = torch.empty((B, cap), dtype=torch.long, device="cuda")
+    cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ops.score_filter(Q, X, ids, best_s, ck, ci, cnt)
+    S = (Q.double() @ X.double().T).float().cpu()
+    thr = best_s[:, -1].cpu()
+    for b in range(B):
+        want = set((torch.nonzero(S[b] > thr[b]).flatten() + 100).tolist())
+        c = int(cnt[b])
+        got = set(ci[b, :min(c, cap)].cpu().tolist())
+        # scores within float rounding of the threshold may fall either way
+        near = set((torch.nonzero((S[b] - thr[b]).abs() < 1e-4).flatten() + 100).tolist())
+        assert got - near == want - near or c > cap
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [1, 10, 100, 256])
 @pytest.mark.parametrize("n", [100, 5000, 65536])
 def test_topk_merge_kernel_exact(k, n):
