@@ -38,18 +38,40 @@ __device__ __forceinline__ float kfloat(uint32_t k) {
 }
 
 // among hist[0..TK_BINS), find the highest bin b with (#elements in bins >= b) >= need;
-// returns b and the count of elements in bins > b via *above (one thread scans:
-// at most two calls per query row, 2048 bins)
+// returns b and the count of elements in bins > b via *above.  One wave: lane l
+// sums the 32 bins [32*(63-l), 32*(64-l)) (lane 0 the highest), a shuffle scan
+// over lanes finds the lane whose range crosses need, and that lane walks its
+// 32 bins (the walk of all 2048 bins by one thread took ~85 us per query row)
 __device__ int select_bin(const uint32_t* hist, uint32_t need, uint32_t* above, int* bin_out) {
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    int b = -1;
-    for (int i = TK_BINS - 1; i >= 0; --i) {
-      if (run + hist[i] >= need) { b = i; break; }
-      run += hist[i];
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int base = 32 * (63 - lane);
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) sum += hist[base + i];
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
     }
-    *bin_out = b < 0 ? 0 : b;
-    *above = run;
+    const uint64_t hit = __ballot(inc >= need);
+    const int first = hit ? __ffsll((unsigned long long)hit) - 1 : 63;
+    if (lane == first) {
+      if (inc >= need) {
+        uint32_t run = inc - sum;  // elements in the bins above this lane's range
+        int b = base;
+        for (int i = 31; i >= 0; --i) {
+          if (run + hist[base + i] >= need) { b = base + i; break; }
+          run += hist[base + i];
+        }
+        *bin_out = b;
+        *above = run;
+      } else {  // fewer than need in total: every bin
+        *bin_out = 0;
+        *above = inc;
+      }
+    }
   }
   __syncthreads();
   return *bin_out;
