@@ -68,6 +68,7 @@ class MFConfig:
     user_memory: int = 128            # per-user ring of recent items excluded from the negatives
     user_phases: int = 0              # tiled: run the SGD in P user-range phases (0 = auto: ~2.5M users
                                       # per phase, so a launch's user rows mostly hit the Infinity Cache)
+    sgd_high_priority: bool = False   # tiled + prefetch: SGD on a priority -1 stream (measured 1 % slower, off)
     graph_capture: bool = False       # tiled, W = 1: replay each batch size's step as one hipGraph
                                       # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
@@ -146,6 +147,12 @@ class DistributedMF:
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
                               and exchange != "ps")
             self._side = torch.cuda.Stream(dev) if self._prefetch else None
+            # the SGD of batch k gets dispatch priority over the partition of k+1
+            # (FPS_SGD_HP=0 forces it off for A/B runs); local layout only: the ring
+            # rotation orders its copy stream against the stream it was built on
+            hp = (self._prefetch and exchange == "local" and cfg.sgd_high_priority
+                  and os.environ.get("FPS_SGD_HP", "1") != "0")
+            self._hp = torch.cuda.Stream(dev, priority=-1) if hp else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
@@ -202,7 +209,13 @@ class DistributedMF:
             staged = self._stage_partition(uid_local, iid, rating)
             if self._prefetch:
                 prev, self._staged = self._staged, staged
-                if prev is not None:
+                if prev is not None and self._hp is not None:
+                    main = torch.cuda.current_stream(self.U.device)
+                    self._hp.wait_stream(main)
+                    with torch.cuda.stream(self._hp):
+                        self._tiled_sgd(prev)
+                    main.wait_stream(self._hp)  # later work (and the next partition) orders after it
+                elif prev is not None:
                     self._tiled_sgd(prev)
             else:
                 self._tiled_sgd(staged)
