@@ -37,7 +37,42 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_guard(argv) -> None:
+    """``--gpus N`` (N > 1) must run N ranks.  Without torchrun env vars the
+    launcher is started as a CHILD process (nothing GPU-related has been loaded
+    in this parent: torch is not imported yet) and this process exits with its
+    code; under torchrun a WORLD_SIZE that disagrees with ``--gpus`` is an error.
+    A mis-launched scaling run can therefore never report N = 1 numbers as N."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args(argv)
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if a.gpus > 1:
+            import subprocess
+
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+                   "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+            cmd += list(argv)
+            print(f"[bench] --gpus {a.gpus} without torchrun: launching {a.gpus} ranks", file=sys.stderr, flush=True)
+            sys.exit(subprocess.call(cmd))
+        return
+    if int(world) != a.gpus:
+        print(f"[bench] error: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    _launch_guard(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -65,6 +100,10 @@ def main(argv=None):
                     help="tiled SGD: user-range phases per step (0 = auto, ~2.5M users per phase)")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
+    ap.add_argument("--sgd-high-priority", action="store_true",
+                    help="tiled SGD with prefetch: run the SGD on a priority -1 stream (A/B knob, off by default)")
+    ap.add_argument("--metrics-jsonl", default=None,
+                    help="append per-step stage timings (HIP events) and counters of rank 0 to this JSON-lines file")
     a = ap.parse_args(argv)
 
     import torch
@@ -77,12 +116,12 @@ def main(argv=None):
     if comm.device.type == "cuda" and not ops.native_available():
         raise RuntimeError("gfx950 kernel library not built: run python csrc/build.py")
     n = comm.world
-    if a.gpus != n:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    if a.gpus != n:  # unreachable after _launch_guard; kept as a hard invariant
+        raise SystemExit(f"[bench] --gpus {a.gpus} but the process group has {n} ranks")
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
-                   user_phases=a.user_phases)
+                   user_phases=a.user_phases, sgd_high_priority=a.sgd_high_priority)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -91,6 +130,11 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    timer = None
+    if a.metrics_jsonl:
+        from flink_parameter_server_1_amd.utils.metrics import StageTimer
+
+        timer = StageTimer(device=dev.type == "cuda")
     step = 0
     for _ in range(a.warmup):
         model.step(*data.batch(step, a.batch))
@@ -98,16 +142,26 @@ def main(argv=None):
     model.flush()
     comm.barrier()
     sync()
+    model.set_timer(timer)  # None unless --metrics-jsonl: event records only, no syncs
     t0 = time.perf_counter()
     for _ in range(a.steps):
         model.step(*data.batch(step, a.batch))
         step += 1
+        if timer is not None:
+            timer.step_end()
     model.flush()  # the last micro-batch's SGD + push run inside the timed region
     sync()
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
     dt_max = comm.max_over_ranks(dt)
+    # per-rank bytes this rank put on the wire (all-to-all + ring rotation)
+    sent = float(comm.bytes_sent + (model.rot.bytes_sent if model.exchange == "rotate" else 0))
+    bytes_per_rank = comm.gather_floats(sent)
+    import torch.distributed as dist
+
+    world_seen = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else "none (single process)"
     total_updates = a.batch * a.steps * n
     value = total_updates / dt_max
     if comm.rank == 0:
@@ -116,6 +170,8 @@ def main(argv=None):
             "value": value,
             "unit": "updates/s",
             "n_gpus": n,
+            "world_size": world_seen,
+            "backend": backend,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": dt_max / a.steps * 1e3,
@@ -139,12 +195,22 @@ def main(argv=None):
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
                 if model.exchange == "ps" else None,
                 "rotation_bytes_sent_rank0": model.rot.bytes_sent if model.exchange == "rotate" else None,
+                "bytes_sent_per_rank": bytes_per_rank,
             },
         }
         print(json.dumps(out), flush=True)
-    if n > 1:
-        import torch.distributed as dist
+    if timer is not None:
+        timer.step_end()  # the flush's stages
+        steps_ms = timer.per_step_ms()
+        if comm.rank == 0:
+            from flink_parameter_server_1_amd.utils.metrics import JsonlWriter
 
+            w = JsonlWriter(a.metrics_jsonl)
+            for i, st in enumerate(steps_ms):
+                w.write(kind="step", step=i, stage_ms=st)
+            w.write(kind="summary", ms_per_step=dt_max / a.steps * 1e3, counters=model.metrics(), n_gpus=n)
+            w.close()
+    if n > 1:
         dist.destroy_process_group()
 
 

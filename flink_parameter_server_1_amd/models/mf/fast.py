@@ -44,8 +44,11 @@ from ... import ops
 from ...parallel.comm import Comm
 from ...parallel.rotation import RingRotation, shard_halves
 from ...parallel.rotation import block_rows as block_rows_of
+from ...parallel.staleness import BoundedStalenessPipeline
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
+from ...utils.metrics import Counters
+from ...utils.tracing import stage
 
 
 @dataclass
@@ -147,11 +150,10 @@ class DistributedMF:
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
                               and exchange != "ps")
             self._side = torch.cuda.Stream(dev) if self._prefetch else None
-            # the SGD of batch k gets dispatch priority over the partition of k+1
-            # (FPS_SGD_HP=0 forces it off for A/B runs); local layout only: the ring
-            # rotation orders its copy stream against the stream it was built on
-            hp = (self._prefetch and exchange == "local" and cfg.sgd_high_priority
-                  and os.environ.get("FPS_SGD_HP", "1") != "0")
+            # cfg.sgd_high_priority: the SGD of batch k gets dispatch priority over the
+            # partition of k+1 (bench.py --sgd-high-priority); local layout only: the
+            # ring rotation orders its copy stream against the stream it was built on
+            hp = self._prefetch and exchange == "local" and cfg.sgd_high_priority
             self._hp = torch.cuda.Stream(dev, priority=-1) if hp else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
@@ -165,6 +167,10 @@ class DistributedMF:
             # so the close-time dump still covers exactly the touched parameters
             self._seen = torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev)
         self.pipeline = cfg.pipeline and self.exchange == "ps"
+        if self.pipeline:
+            # staleness 1: the pull of batch k+1 (counts exchanged one call earlier, its
+            # row all-to-all in flight) overlaps the SGD of batch k
+            self._pipe = BoundedStalenessPipeline(self.ps, self._pipe_compute, staleness=1)
         if cfg.negative_sample_rate > 0:
             # PSOnlineMatrixFactorizationWorker.scala:70-79: per rating, negativeSampleRate
             # items (rating 0) drawn among the items this worker has seen, not among the
@@ -177,8 +183,12 @@ class DistributedMF:
             self._known = torch.zeros(cfg.num_items, dtype=torch.int32, device=dev)
             self._known_count = torch.zeros(1, dtype=torch.int32, device=dev)
             self._neg_counter = 0
-        self._pending = None
         self.updates = 0
+        #: observability: ``timer`` (a ``utils.metrics.StageTimer``, set by
+        #: bench.py --metrics-jsonl) times every stage with HIP events; the counters
+        #: are host-side tallies of what was enqueued (no device sync)
+        self.timer = None
+        self.counters = Counters()
 
     @property
     def U(self):
@@ -220,31 +230,36 @@ class DistributedMF:
             else:
                 self._tiled_sgd(staged)
         elif self.exchange == "local":
-            if grouped:
-                ptr, order = self.grouper.run(iid, self.items.n_local)
-                ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
-            else:
-                ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam, self.user_atomic)
+            with stage("mf.sgd", self.timer):
+                if grouped:
+                    ptr, order = self.grouper.run(iid, self.items.n_local)
+                    ops.mf_sgd_grouped(self.U, self.I, uid_local, rating, ptr, order, c.learning_rate, c.lam)
+                else:
+                    ops.mf_sgd_local(self.U, self.I, uid_local, iid, rating, c.learning_rate, c.lam,
+                                     self.user_atomic)
         elif self.exchange == "rotate":
             seen = self._seen if self.items.touched is not None else None
-            ptr, u, row, r = self.partitioner.run(uid_local, iid, rating, seen)
+            with stage("mf.partition", self.timer):
+                ptr, u, row, r = self.partitioner.run(uid_local, iid, rating, seen)
             n = uid_local.numel()
             for _ in range(self.rot.K):
-                self.rot.begin()  # transfer of the next block overlaps this sub-step
-                ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
-                                     c.learning_rate, c.lam, self.user_atomic)
-                self.rot.end()
+                with stage("mf.rotate.begin", self.timer):
+                    self.rot.begin()  # transfer of the next block overlaps this sub-step
+                with stage("mf.sgd", self.timer):
+                    ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
+                                         c.learning_rate, c.lam, self.user_atomic)
+                with stage("mf.rotate.end", self.timer):
+                    self.rot.end()
         elif self.pipeline:
             # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD
             # of batch k; k's push follows.  Staleness bound: one micro-batch.
-            nxt = (self.ps.pull_async(iid), uid_local, rating)
-            if self._pending is not None:
-                self._finish(self._pending)
-            self._pending = nxt
+            self._pipe.submit(iid, (uid_local, rating))
         else:
             rows, plan = self.ps.pull(iid)
             self._compute_push(rows, plan, uid_local, rating)
         self.updates += uid_local.numel()
+        self.counters.add("ratings", uid_local.numel())
+        self.counters.add("micro_batches")
         if ops.DEBUG:  # FactorIsNotANumberException, M/matrix/factorization/utils/Vector.scala:78-80
             from .core import FactorIsNotANumberException
 
@@ -296,12 +311,14 @@ class DistributedMF:
         tiler = self._tilers[self._tiler_i]
         self._tiler_i ^= 1
         if self._side is None:
-            ptr, rec = tiler.run(uid_local, iid, rating, seen)
+            with stage("mf.partition", self.timer):
+                ptr, rec = tiler.run(uid_local, iid, rating, seen)
             return ptr, rec, None
         main = torch.cuda.current_stream(self.U.device)
         self._side.wait_stream(main)  # inputs written, and this buffer's previous SGD done
         with torch.cuda.stream(self._side):
-            ptr, rec = tiler.run(uid_local, iid, rating, seen)
+            with stage("mf.partition", self.timer):  # timed on the side stream
+                ptr, rec = tiler.run(uid_local, iid, rating, seen)
             ev = torch.cuda.Event()
             ev.record(self._side)
         for t in (uid_local, iid, rating):
@@ -315,27 +332,30 @@ class DistributedMF:
             torch.cuda.current_stream(self.U.device).wait_event(ev)
         if self.exchange == "local":
             b0, b1 = self._local_blocks
-            for p in range(self.user_phases):
-                if self.pair_blocks:
-                    ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
-                                          c.learning_rate, c.lam)
-                else:
-                    for b, blk in enumerate((b0, b1)):
-                        ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R,
-                                         c.learning_rate, c.lam)
+            with stage("mf.sgd", self.timer):
+                for p in range(self.user_phases):
+                    if self.pair_blocks:
+                        ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
+                                              c.learning_rate, c.lam)
+                    else:
+                        for b, blk in enumerate((b0, b1)):
+                            ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R,
+                                             c.learning_rate, c.lam)
             return
         for _ in range(self.rot.K):
-            self.rot.begin()  # transfer of the next block overlaps this sub-step
-            for p in range(self.user_phases):
-                ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, p * self.rot.K + self.rot.active_block(),
-                                 self.tile_T, self.tile_R, c.learning_rate, c.lam)
-            self.rot.end()
+            with stage("mf.rotate.begin", self.timer):
+                self.rot.begin()  # transfer of the next block overlaps this sub-step
+            with stage("mf.sgd", self.timer):
+                for p in range(self.user_phases):
+                    ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, p * self.rot.K + self.rot.active_block(),
+                                     self.tile_T, self.tile_R, c.learning_rate, c.lam)
+            with stage("mf.rotate.end", self.timer):
+                self.rot.end()
 
-    def _finish(self, pending):
-        (rows, work, plan), uid_local, rating = pending
-        if work is not None:
-            work.wait()
+    def _pipe_compute(self, rows, plan, payload):
+        uid_local, rating = payload
         self._compute_push(rows, plan, uid_local, rating)
+        return None, None
 
     def _compute_push(self, rows, plan, uid_local, rating):
         c = self.cfg
@@ -371,9 +391,23 @@ class DistributedMF:
                 seen = self.comm.all_reduce(self._seen.clone(), op=torch.distributed.ReduceOp.MAX)
                 loc = torch.arange(self.items.n_local, device=seen.device)
                 self.items.touched |= seen[self.items.global_ids(loc)]
-        if self._pending is not None:
-            p, self._pending = self._pending, None
-            self._finish(p)
+        if self.pipeline:
+            self._pipe.drain()
+
+    def set_timer(self, timer) -> None:
+        """Attach a ``utils.metrics.StageTimer`` to the model and its PS."""
+        self.timer = timer
+        self.ps.timer = timer
+
+    def metrics(self) -> dict:
+        """Host counters of this rank (ratings, micro-batches, PS pulls / unique keys,
+        bytes put on the wire by the all-to-alls and the ring rotation)."""
+        m = self.counters.snapshot()
+        m.update({f"ps.{k}": v for k, v in self.ps.stats.items()})
+        m["bytes_sent.a2a"] = self.comm.bytes_sent
+        if self.exchange == "rotate":
+            m["bytes_sent.rotation"] = self.rot.bytes_sent
+        return m
 
     @torch.no_grad()
     def sq_err(self, uid_local, iid, rating) -> float:

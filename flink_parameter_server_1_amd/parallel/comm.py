@@ -177,6 +177,13 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
+    def gather_floats(self, x: float) -> List[float]:
+        """``[x of rank 0, x of rank 1, ...]`` on every rank."""
+        if self.world == 1:
+            return [float(x)]
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        return [float(v.item()) for v in self.all_gather(t)]
+
     def sum_over_ranks(self, x: float) -> float:
         if self.world == 1:
             return x

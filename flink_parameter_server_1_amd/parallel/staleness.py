@@ -6,13 +6,28 @@ pulls may be outstanding, later ones are queued (``M/WorkerLogic.scala:176-225``
 *staleness bound*: with ``staleness = s`` the pull of micro-batch ``k`` is served
 before the pushes of micro-batches ``k-s .. k-1`` are applied, never earlier ones.
 
-* ``s = 0``: synchronous (pull k, compute k, push k);
-* ``s = 1``: the row all-to-all of batch ``k+1`` runs while batch ``k`` computes
-  (what ``models.mf.fast`` does);
+* ``s = 0``: synchronous semantics (pull k sees every earlier push);
+* ``s = 1``: the row all-to-all of batch ``k+1`` runs while batch ``k`` computes;
 * ``s > 1``: deeper pipelines for slow links / large tables (config #5 stress).
 
-Everything is stream-ordered on the device, so the bound is exact: the gather of
-batch ``k`` is enqueued after the apply of batch ``k-s-1``.
+Each micro-batch goes through three stages (``TensorPS``):
+
+* **A** ``plan_begin`` -- dedup + count exchange, counts copied to the host
+  asynchronously;
+* **B** ``plan_end`` + serve + answer all-to-all (async) -- the pull;
+* **C** compute + push.
+
+``submit(k)`` enqueues A(k), then B(k-1) (``lookahead``, the default for
+``s > 0``; B(k) without it), then C of every pulled batch beyond the bound.  B(k-1) therefore waits on counts that were enqueued one call
+earlier: by then the device is busy with older work, so the host never idles
+the device on split sizes.  Everything is stream-ordered on the device, so the
+bound is exact: the gather of batch ``k`` is enqueued after the apply of batch
+``k-s-1``.
+
+End of input: every ``submit`` carries a ``flag`` that reaches all peers with
+the counts; ``all_flagged`` turns True on every rank at the same micro-batch once
+every rank flagged it (the ``FlinkEOF`` barrier, ``M/utils/FlinkEOF.scala:97-107``,
+without an extra collective).
 """
 from __future__ import annotations
 
@@ -28,34 +43,63 @@ ComputeFn = Callable[[torch.Tensor, PullPlan, Any], Tuple[Optional[torch.Tensor]
 
 
 class BoundedStalenessPipeline:
-    def __init__(self, ps: TensorPS, compute: ComputeFn, staleness: int = 1, lr: float = 0.0):
+    def __init__(self, ps: TensorPS, compute: ComputeFn, staleness: int = 1, lr: float = 0.0,
+                 lookahead: Optional[bool] = None):
+        """``lookahead`` (default: ``staleness > 0``): stage B of a batch waits for
+        the next ``submit``, so its counts are never waited for on an idle device.
+        Without it (the default of the synchronous ``staleness = 0`` mode) a
+        batch is pulled, computed and pushed inside its own ``submit``."""
         if staleness < 0:
             raise ValueError("staleness must be >= 0")
         self.ps, self.compute, self.staleness, self.lr = ps, compute, int(staleness), lr
-        self._q: deque = deque()
+        self.lookahead = staleness > 0 if lookahead is None else bool(lookahead)
+        self._planned: deque = deque()  # (pending plan, payload) after stage A
+        self._pulled: deque = deque()   # (rows, work, plan, payload) after stage B
         self.max_observed = 0  # pushes of earlier batches still pending when a pull was served
+        self.all_flagged = False
+        self.submitted = 0
 
-    def submit(self, keys: torch.Tensor, payload: Any = None) -> List[Any]:
-        """Issue the pull of a new micro-batch; finish (compute + push) every
+    def submit(self, keys: torch.Tensor, payload: Any = None, flag: int = 0) -> List[Any]:
+        """Begin the pull of a new micro-batch; finish (compute + push) every
         batch that would otherwise exceed the staleness bound.  Returns the
         results of the batches finished by this call, oldest first."""
-        rows, work, plan = self.ps.pull_async(keys)
-        self.max_observed = max(self.max_observed, len(self._q))
-        self._q.append((rows, work, plan, payload))
-        out = []
-        while len(self._q) > self.staleness:
-            out.append(self._finish(self._q.popleft()))
+        self._planned.append((self.ps.plan_begin(keys, flag), payload))
+        self.submitted += 1
+        out: List[Any] = []
+        while len(self._planned) > (1 if self.lookahead else 0):
+            self._pull_next()
+        while len(self._pulled) > self.staleness:
+            out.append(self._finish(self._pulled.popleft()))
         return out
 
     def drain(self) -> List[Any]:
         out = []
-        while self._q:
-            out.append(self._finish(self._q.popleft()))
+        while self._planned:
+            self._pull_next()
+            while len(self._pulled) > self.staleness:
+                out.append(self._finish(self._pulled.popleft()))
+        while self._pulled:
+            out.append(self._finish(self._pulled.popleft()))
         return out
 
     @property
     def in_flight(self) -> int:
-        return len(self._q)
+        """Micro-batches pulled whose pushes are not applied yet (<= staleness
+        between calls); the batch of the latest ``submit`` is only planned."""
+        return len(self._pulled)
+
+    @property
+    def planned(self) -> int:
+        return len(self._planned)
+
+    def _pull_next(self):
+        pp, payload = self._planned.popleft()
+        plan = self.ps.plan_end(pp)
+        if plan.peer_flags and all(f != 0 for f in plan.peer_flags):
+            self.all_flagged = True
+        rows, work = self.ps.pull_planned(plan, async_op=True)
+        self.max_observed = max(self.max_observed, len(self._pulled))
+        self._pulled.append((rows, work, plan, payload))
 
     def _finish(self, item) -> Any:
         rows, work, plan, payload = item

@@ -3,35 +3,44 @@
 Replaces the reference's per-record Flink iteration
 (``M/FlinkParameterServer.scala:215-335``) with a micro-batch protocol:
 
-``pull(keys)``
+``plan_begin(keys)`` (stage A, nothing blocks the host)
     1. de-duplicate the batch's keys and group them by owning shard (K1,
        ``ops.DedupWorkspace``) -- the batch's own pre-reduction, the GPU
        analogue of the combining senders (``M/common/CombinationLogic.scala``);
-    2. exchange per-shard counts (tiny all-to-all) and bring them to the host
-       (the only host sync of a step: torch needs split sizes on the host);
-    3. X1: all-to-all of the unique local keys to their owners;
-    4. owners gather their rows (K2) into the wire dtype;
-    5. X2: all-to-all of the rows back.  Rows return in request order, so
+    2. exchange per-shard counts (tiny all-to-all, one ``(count, flag)`` pair
+       per peer: the flag carries "this rank's input is exhausted", so the
+       end-of-input barrier of ``FlinkEOF`` rides on the same message);
+    3. copy the counts into pinned host memory (non-blocking) and record an
+       event.
+``plan_end(pending)`` (stage B)
+    4. wait for that event -- recorded one micro-batch earlier in a pipelined
+       loop, so in steady state it has long completed: the host never stalls
+       the device on split sizes (torch needs them on the host);
+    5. X1: all-to-all of the unique local keys to their owners.
+``pull``: 6. owners gather their rows (K2) into the wire dtype;
+    7. X2: all-to-all of the rows back.  Rows return in request order, so
        ``rows[pos[b]]`` is request ``b``'s parameter (positional FIFO).
 ``push(plan, deltas)``
-    6. X1': all-to-all of per-unique-key deltas (pre-reduced on the worker by
-       the compute kernel's atomics) to the owners;
-    7. owners apply them (K3: add / sgd / adagrad).
+    8. X1': all-to-all of per-unique-key deltas (pre-reduced on the worker) to
+       the owners;
+    9. owners apply them (K3: add / set / sgd / adagrad / add_renorm).
 
 ``world == 1`` keeps the same code path with local copies instead of RCCL.
-Staleness: every request in a micro-batch reads the table as of step 3-4;
-``push`` of step k may overlap ``pull`` of step k+1 (``max_inflight``), the
-bounded-staleness analogue of ``pullLimit`` (``M/WorkerLogic.scala:176-225``).
+Staleness: every request in a micro-batch reads the table as of step 6;
+``parallel.staleness.BoundedStalenessPipeline`` orders the stages of several
+micro-batches so pull ``k`` is served before the pushes of ``k-s .. k-1``
+(``max_inflight``), the bounded-staleness analogue of ``pullLimit``
+(``M/WorkerLogic.scala:176-225``).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import List
+from dataclasses import dataclass, field
+from typing import List, Optional
 
 import torch
 
 from .. import ops
-from ..utils.tracing import trace_range
+from ..utils.tracing import stage
 from .comm import Comm
 from .table import ShardedTable
 
@@ -43,6 +52,19 @@ class PullPlan:
     recv_keys: torch.Tensor  # local keys this shard must serve / apply
     pos: torch.Tensor        # request -> row of the pulled/delta buffers
     n_unique: int
+    peer_flags: List[int] = field(default_factory=list)  # flag each rank sent with this plan
+    n_requests: int = 0
+
+
+@dataclass
+class PendingPlan:
+    """A plan after stage A: device-side dedup done, counts on their way to the host."""
+    n: int
+    counts: torch.Tensor     # int32[W] unique keys per owner (own copy)
+    uniq: torch.Tensor       # int32[>= U] unique local keys grouped by owner
+    pos: torch.Tensor        # int32[n]
+    host: torch.Tensor       # int32[W, 4]: (sent count, sent flag, recv count, recv flag) per peer
+    event: Optional[object]  # torch.cuda.Event or None (host tensors: already complete)
 
 
 class TensorPS:
@@ -51,70 +73,166 @@ class TensorPS:
         self.comm = comm
         self.wire_dtype = wire_dtype
         self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device)
-        self.stats = {"pulls": 0, "unique": 0, "steps": 0}
+        #: pulls = requests, unique = unique keys, steps = plans; host_stalls = plan_end
+        #: calls whose counts had not reached the host yet (the host waited on the device)
+        self.stats = {"pulls": 0, "unique": 0, "steps": 0, "host_stalls": 0, "pushes": 0}
+        self.timer = None  # utils.metrics.StageTimer (optional)
+        W = comm.world
+        self._pinned = table.device.type == "cuda"
+        self._flagbuf = torch.zeros((W, 1), dtype=torch.int32, device=table.device)
 
-    def plan(self, keys: torch.Tensor, persistent: bool = False) -> PullPlan:
-        """Dedup + split exchange + key all-to-all.  ``persistent`` copies the
-        request->row map out of the reusable dedup workspace, so the plan
-        survives the next ``plan`` call (pipelined steps)."""
+    # ----------------------------------------------------------------- planning
+    def plan_begin(self, keys: torch.Tensor, flag: int = 0) -> PendingPlan:
+        """Stage A: dedup + count exchange, counts copied to pinned host memory
+        asynchronously.  Collective: every rank calls it once per micro-batch
+        (with empty ``keys`` when it has nothing to pull).  ``flag`` (an int) is
+        delivered to every peer with the counts (``PullPlan.peer_flags``)."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
-        with trace_range("ps.dedup"):
+        n = keys.numel()
+        with stage("ps.dedup", self.timer):
             counts, prefix, uniq, pos = self.dedup.run(keys)
-        recv_counts = self.comm.exchange_counts(counts)
-        both = torch.cat([counts, recv_counts]).cpu().tolist()  # host sync (split sizes)
         W = self.comm.world
-        send_splits, recv_splits = both[:W], both[W:]
+        # the workspace is reused by the next plan_begin: this plan keeps copies
+        counts = counts.clone()
+        uniq = uniq[:n].clone()
+        pos = pos.clone()
+        flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
+        send = torch.cat([counts.view(W, 1).to(torch.int32), flags], dim=1).contiguous()  # [W, 2]
+        with stage("ps.count-a2a", self.timer):
+            recv = self.comm.exchange_counts(send)
+        both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 4]
+        if self._pinned:
+            host = torch.empty((W, 4), dtype=torch.int32, pin_memory=True)
+            host.copy_(both, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = both.to("cpu"), None
+        return PendingPlan(n, counts, uniq, pos, host, ev)
+
+    def plan_end(self, pp: PendingPlan) -> PullPlan:
+        """Stage B: split sizes from the host copy, key all-to-all."""
+        if pp.event is not None:
+            if not pp.event.query():
+                self.stats["host_stalls"] += 1
+            pp.event.synchronize()
+        h = pp.host.tolist()
+        send_splits = [int(r[0]) for r in h]
+        recv_splits = [int(r[2]) for r in h]
+        peer_flags = [int(r[3]) for r in h]
         n_unique = int(sum(send_splits))
-        recv_keys = self.comm.all_to_all(uniq[:n_unique], send_splits, recv_splits)
-        if persistent:
-            pos = pos.clone()
-            if W == 1:
-                recv_keys = recv_keys.clone()
-        self.stats["pulls"] += keys.numel()
+        with stage("ps.key-a2a", self.timer):
+            recv_keys = self.comm.all_to_all(pp.uniq[:n_unique], send_splits, recv_splits)
+        self.stats["pulls"] += pp.n
         self.stats["unique"] += n_unique
         self.stats["steps"] += 1
-        return PullPlan(send_splits, recv_splits, recv_keys, pos, n_unique)
+        return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n)
+
+    def plan(self, keys: torch.Tensor, persistent: bool = False, flag: int = 0) -> PullPlan:
+        """Stages A + B back to back (the host waits on this micro-batch's counts).
+        Plans never alias the dedup workspace, so ``persistent`` is implied."""
+        return self.plan_end(self.plan_begin(keys, flag))
+
+    # --------------------------------------------------------------------- pull
+    def serve(self, plan: PullPlan) -> torch.Tensor:
+        with stage("ps.serve", self.timer):
+            return self.table.serve(plan.recv_keys, self.wire_dtype)
+
+    def pull_planned(self, plan: PullPlan, async_op: bool = False):
+        """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``."""
+        served = self.serve(plan)
+        with stage("ps.answer-a2a", self.timer):
+            if async_op:
+                return self.comm.all_to_all_async(served, plan.recv_splits, plan.send_splits)
+            return self.comm.all_to_all(served, plan.recv_splits, plan.send_splits)
 
     def pull(self, keys: torch.Tensor):
         """Returns ``(rows[U, D] in wire dtype, plan)``; request b's row is ``rows[plan.pos[b]]``."""
         plan = self.plan(keys)
-        with trace_range("ps.serve"):
-            served = self.table.serve(plan.recv_keys, self.wire_dtype)
-        with trace_range("ps.answer-a2a"):
-            rows = self.comm.all_to_all(served, plan.recv_splits, plan.send_splits)
-        return rows, plan
+        return self.pull_planned(plan), plan
 
     def pull_async(self, keys: torch.Tensor):
         """Start a pull whose row all-to-all runs on the communicator's stream while
         the caller keeps computing; returns ``(rows, work, plan)`` -- wait on
         ``work`` (if not None) before reading ``rows``."""
-        plan = self.plan(keys, persistent=True)
-        served = self.table.serve(plan.recv_keys, self.wire_dtype)
-        rows, work = self.comm.all_to_all_async(served, plan.recv_splits, plan.send_splits)
+        plan = self.plan(keys)
+        rows, work = self.pull_planned(plan, async_op=True)
         return rows, work, plan
 
-    def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0):
-        """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply."""
+    # --------------------------------------------------------------------- push
+    def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
+             return_updated: bool = False):
+        """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply
+        with ``op`` (default: the table's rule).  ``return_updated``: also return
+        ``(global ids, new rows)`` of the keys applied on THIS shard -- the
+        per-push ``(id, value)`` output of ``SimplePSLogic``
+        (``M/server/SimplePSLogic.scala:24``)."""
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
-        with trace_range("ps.push-a2a"):
-            recv = self.comm.all_to_all(wire, plan.send_splits, plan.recv_splits)
-        opt = self.table.optimizer
-        seg_add = opt == "add" and len(plan.recv_splits) <= 16
-        if seg_add or opt in ("adagrad", "set"):
-            # Keys are unique within each source's segment but may repeat across
-            # sources; non-atomic rules (adagrad's accumulator RMW, set) must
-            # therefore apply segment by segment.  ``add`` does the same with a
-            # plain read-modify-write (add_unique) instead of one float atomic per
-            # element (the atomic apply ran at ~1 TB/s: 480 us for 2M dim-64
-            # rows, profiles/r1_capacity_kernel_stats.csv; narrow rows are worse).
-            off = 0
-            for n in plan.recv_splits:
-                if n:
-                    self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], lr=lr,
-                                     op="add_unique" if seg_add else None)
-                off += n
-        else:
-            self.table.apply(plan.recv_keys, recv, lr=lr)
+        with stage("ps.push-a2a", self.timer):
+            recv = self.comm.all_to_all(wire.contiguous(), plan.send_splits, plan.recv_splits)
+        opt = op or self.table.optimizer
+        self.stats["pushes"] += plan.n_unique
+        with stage("ps.apply", self.timer):
+            seg_add = opt == "add" and len(plan.recv_splits) <= 16
+            if seg_add or opt in ("adagrad", "set", "add_renorm"):
+                # Keys are unique within each source's segment but may repeat across
+                # sources; non-atomic rules (adagrad's accumulator RMW, set, renorm)
+                # therefore apply segment by segment.  ``add`` does the same with a
+                # plain read-modify-write (add_unique) instead of one float atomic per
+                # element (the atomic apply ran at ~1 TB/s: 480 us for 2M dim-64
+                # rows, profiles/r1_capacity_kernel_stats.csv; narrow rows are worse).
+                off = 0
+                for n in plan.recv_splits:
+                    if n:
+                        self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], lr=lr,
+                                         op="add_unique" if seg_add else opt)
+                    off += n
+            else:
+                self.table.apply(plan.recv_keys, recv, lr=lr, op=opt)
+        if return_updated:
+            return self.table.global_ids(plan.recv_keys), self.table.weight[plan.recv_keys.long()]
+        return None
+
+    def reduce_requests(self, plan: PullPlan, deltas: torch.Tensor, op: str = "add",
+                        mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Per-request ``[B, D]`` deltas -> per-unique-key ``[U, D]``: summed for
+        additive rules, the LAST request's value for ``set`` (last writer wins,
+        the order a per-record PS would apply them in).  ``mask[b] = False``
+        drops request ``b``."""
+        D = deltas.shape[1] if deltas.dim() > 1 else 1
+        d2 = deltas.reshape(deltas.shape[0], D).float()
+        pos = plan.pos.long()
+        if op == "set":
+            rid = torch.arange(pos.numel(), device=pos.device)
+            if mask is not None:
+                rid = torch.where(mask, rid, torch.full_like(rid, -1))
+            last = torch.full((plan.n_unique,), -1, dtype=torch.int64, device=pos.device)
+            last.scatter_reduce_(0, pos, rid, reduce="amax")
+            if mask is not None and bool((last < 0).any()):
+                raise ValueError("set-push with a masked key: every unique key needs a value")
+            return d2[last.clamp_min(0)].contiguous()
+        out = torch.zeros((plan.n_unique, D), dtype=torch.float32, device=d2.device)
+        if mask is not None:
+            d2 = d2 * mask.view(-1, 1).to(d2.dtype)
+        out.index_add_(0, pos, d2)
+        return out
+
+    def push_keys(self, keys: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
+                  return_updated: bool = False):
+        """Push to arbitrary keys (not a pulled plan): plans them (host waits on
+        the counts), pre-reduces duplicates and applies."""
+        plan = self.plan(keys)
+        opt = op or self.table.optimizer
+        red = self.reduce_requests(plan, deltas, "set" if opt == "set" else "add")
+        return self.push(plan, red, lr=lr, op=opt, return_updated=return_updated)
+
+    def load(self, ids: torch.Tensor, values: torch.Tensor) -> None:
+        """Model load (``transformWithModelLoad``, ``M/FlinkParameterServer.scala:377-566``):
+        every rank passes the ``(id, value)`` records IT received; they are routed
+        to their owning shards and written there (last record of an id wins).
+        Collective."""
+        vals = values.to(device=self.table.device, dtype=torch.float32).reshape(ids.numel(), self.table.dim)
+        self.push_keys(ids, vals, op="set")
 
     def pull_values(self, keys: torch.Tensor) -> torch.Tensor:
         """Convenience: fp32 ``[B, D]`` values for every request (expanded)."""

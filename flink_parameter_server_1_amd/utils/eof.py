@@ -23,6 +23,7 @@ from __future__ import annotations
 import copy
 import queue
 import threading
+import time
 from typing import Callable, Iterable, List, Optional, Sequence
 
 from ..api.logic import RuntimeContext
@@ -104,10 +105,14 @@ def flat_map_with_eof(sources: Sequence[Iterable], fn, parallelism: int,
     threads += [threading.Thread(target=run_sink, args=(t,), daemon=True) for t in range(parallelism)]
     for th in threads:
         th.start()
+    deadline = time.monotonic() + timeout  # one overall deadline, not one per thread
     for th in threads:
-        th.join(timeout)
+        th.join(max(0.0, deadline - time.monotonic()))
     if errors:
         raise errors[0]
+    alive = [th.name for th in threads if th.is_alive()]
+    if alive:  # a sink still waiting for EOFs: never hand back partial outputs
+        raise TimeoutError(f"flat_map_with_eof: {len(alive)} subtask(s) did not finish within {timeout} s")
     return outputs
 
 

@@ -122,12 +122,17 @@ class Counters:
 
 
 class StageTimer:
-    """Per-stage timing; ``device=True`` uses HIP events (no host sync per stage)."""
+    """Per-stage timing; ``device=True`` uses HIP events recorded on the stream
+    current at the stage (no host sync per stage; a stage opened under
+    ``torch.cuda.stream(side)`` is timed on ``side``).  ``step_end()`` closes
+    a step so ``per_step_ms()`` can report every stage of every step."""
 
     def __init__(self, device: bool = False):
         self.device = device
         self.wall = defaultdict(float)
         self.events: Dict[str, list] = defaultdict(list)
+        self._step: Dict[str, list] = defaultdict(list)
+        self._steps: list = []
 
     @contextmanager
     def stage(self, name: str):
@@ -136,13 +141,38 @@ class StageTimer:
 
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            yield
-            b.record()
-            self.events[name].append((a, b))
+            try:
+                yield
+            finally:
+                b.record()
+                self.events[name].append((a, b))
+                self._step[name].append((a, b))
         else:
             t0 = time.perf_counter()
-            yield
-            self.wall[name] += time.perf_counter() - t0
+            try:
+                yield
+            finally:
+                dt = time.perf_counter() - t0
+                self.wall[name] += dt
+                self._step[name].append(dt)
+
+    def step_end(self):
+        self._steps.append(self._step)
+        self._step = defaultdict(list)
+
+    @staticmethod
+    def _ms(x) -> float:
+        if isinstance(x, tuple):
+            return x[0].elapsed_time(x[1])
+        return x * 1e3
+
+    def per_step_ms(self) -> list:
+        """``[{stage: ms}]`` per closed step (syncs the device once)."""
+        if self.device:
+            import torch
+
+            torch.cuda.synchronize()
+        return [{k: sum(self._ms(x) for x in v) for k, v in st.items()} for st in self._steps]
 
     def totals_ms(self) -> Dict[str, float]:
         out = {k: v * 1e3 for k, v in self.wall.items()}

@@ -39,6 +39,18 @@ def trace_range(name: str):
 
 
 @contextmanager
+def stage(name: str, timer=None):
+    """A pipeline stage: roctx range (``rocprofv3 --marker-trace``) plus, when a
+    ``utils.metrics.StageTimer`` is attached, HIP-event timing of the stage."""
+    if timer is None:
+        with trace_range(name):
+            yield
+        return
+    with trace_range(name), timer.stage(name):
+        yield
+
+
+@contextmanager
 def profile_to(path: str, enabled: bool = True):
     if not enabled:
         with nullcontext():

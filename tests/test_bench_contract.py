@@ -47,3 +47,39 @@ def test_bench_two_ranks_gloo(exchange):
     d = lines[0]
     assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 4096
     assert d["config"]["exchange"] == exchange
+
+
+def test_bench_gpus_without_torchrun_launches_ranks():
+    """``--gpus 2`` without torchrun must run 2 ranks (never silently 1)."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + TINY, capture_output=True,
+                       text=True, timeout=600, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+    assert len(d["config"]["bytes_sent_per_rank"]) == 2 and min(d["config"]["bytes_sent_per_rank"]) > 0
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + TINY, capture_output=True,
+                       text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    assert _json_lines(p.stdout) == []
+
+
+def test_bench_metrics_jsonl(tmp_path):
+    path = tmp_path / "m.jsonl"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--metrics-jsonl", str(path)] + TINY,
+                       capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    recs = [json.loads(x) for x in path.read_text().splitlines()]
+    steps = [r for r in recs if r["kind"] == "step"]
+    assert len(steps) == 3  # 2 timed steps + the flush
+    assert all("mf.sgd" in s["stage_ms"] for s in steps[:2])
+    summ = [r for r in recs if r["kind"] == "summary"][0]
+    assert summ["counters"]["ratings"] == 3 * 4096
