@@ -61,7 +61,12 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
 }
 
 // op: 0 = add (atomic), 1 = set, 2 = sgd w -= lr*g (atomic), 3 = adagrad
-// (acc += g^2, w -= lr*g/sqrt(acc+eps); keys must be unique in the launch).
+// (acc += g^2, w -= lr*g/sqrt(acc+eps); keys must be unique in the launch),
+// 4 = add (unique keys, plain RMW), 5 = add + renorm: w += g, then the row's
+// euclidean length is recomputed in the epilogue and stored in state[row] (the
+// LengthAndVector PS of psOnlineLearnerAndGenerator: attachLength(vectorSum(v, d)),
+// M/matrix/factorization/PSOnlineMatrixFactorizationAndTopKGenerator.scala:81-84;
+// unique keys in the launch).
 template <int TPR, bool IN_BF16, int OP>
 __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ table, float* __restrict__ state,
                                                          const int32_t* __restrict__ idx, int64_t n, int D,
@@ -73,9 +78,14 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
     const int64_t row = (int64_t)idx[r];
     if (row < 0) continue;  // padding slot
     float* dst = table + row * D;
+    float ss = 0.f;
     for (int j = j0; j < D; j += TPR) {
       float g = IN_BF16 ? bf16_to_f32(((const uint16_t*)delta)[r * D + j]) : ((const float*)delta)[r * D + j];
-      if (OP == 0) {
+      if (OP == 5) {
+        const float v = dst[j] + g;
+        dst[j] = v;
+        ss += v * v;
+      } else if (OP == 0) {
         atomic_add_noret(dst + j, g);
       } else if (OP == 1) {
         dst[j] = g;
@@ -89,6 +99,11 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
         *acc = a;
         dst[j] -= lr * g * rsqrtf(a + eps);
       }
+    }
+    if (OP == 5) {  // the lane group of the row (TPR lanes, all active together) sums the squares
+#pragma unroll
+      for (int o = TPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, TPR);
+      if (j0 == 0) state[row] = sqrtf(ss);
     }
     if (touched != nullptr && j0 == 0) touched[row] = 1;
   }
@@ -522,6 +537,7 @@ static void launch_apply(float* table, float* state, const int32_t* idx, int64_t
       case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 4: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 4>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 5: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 5>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       default: hipLaunchKernelGGL((apply_rows_kernel<TPR, true, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
     }
   } else {
@@ -530,6 +546,7 @@ static void launch_apply(float* table, float* state, const int32_t* idx, int64_t
       case 1: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 1>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 2: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 2>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       case 4: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 4>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
+      case 5: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 5>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched); break;
       default: hipLaunchKernelGGL((apply_rows_kernel<TPR, false, 3>), dim3(g), dim3(256), 0, s, table, state, idx, n, D, delta, lr, eps, touched);
     }
   }
@@ -538,7 +555,7 @@ static void launch_apply(float* table, float* state, const int32_t* idx, int64_t
 FPS_API int fps_apply_rows(float* table, float* state, const int32_t* idx, int64_t n, int D, const void* delta,
                            int delta_bf16, int op, float lr, float eps, uint8_t* touched, void* stream) {
   if (n <= 0) return 0;
-  if (op == 3 && state == nullptr) return (int)hipErrorInvalidValue;
+  if ((op == 3 || op == 5) && state == nullptr) return (int)hipErrorInvalidValue;
   TPR_SWITCH(D, launch_apply<TPR>(table, state, idx, n, D, delta, delta_bf16, op, lr, eps, touched, (hipStream_t)stream));
   FPS_CHECK_LAUNCH();
   return 0;

@@ -1,0 +1,136 @@
+"""Batched (tensor) worker API: the ``WorkerLogic`` contract over micro-batches.
+
+The reference's worker is event-driven per record: ``onRecv(data, ps)`` issues
+``ps.pull(id)``, ``onPullRecv(id, value, ps)`` issues ``ps.push(id, delta)`` and
+``ps.output(out)`` (``M/WorkerLogic.scala:23-58``, ``M/ParameterServerClient.scala:12-20``).
+The tensor engine (``core.tensor_engine``) runs the same contract on device
+micro-batches:
+
+``on_recv_batch(batch, ps)``
+    one call per micro-batch; ``ps.pull(keys, payload)`` requests the
+    parameters of ``keys`` (an int tensor, duplicates allowed).  ``payload`` is
+    handed back with the answer (the reference keeps it in per-id FIFOs, e.g.
+    ``ratingBuffer(item)``; here the answer is positional, so no queue is
+    needed: answer row ``b`` belongs to request ``b``).
+``on_pull_recv_batch(pulled, ps)``
+    one call per ``pull``: ``pulled.values()`` are the ``[B, D]`` parameters in
+    request order.  ``ps.push(deltas)`` pushes one delta row per request to the
+    keys just answered (duplicates are pre-reduced on the worker: summed, or
+    last-writer for ``set`` tables); ``ps.push_unique`` takes already reduced
+    ``[U, D]`` rows (the fast path of fused kernels); ``ps.output(x)`` emits a
+    worker output (``Left``).
+``update_model_batch(ids, values)``
+    worker-resident model load (``transformWithDoubleModelLoad``'s ``Right``
+    records, ``M/FlinkParameterServer.scala:641-644``).
+``on_eof(ps)``
+    called once the whole input of every rank is consumed (the ``FlinkEOF``
+    barrier).  It may return an iterable of further micro-batches, which go
+    through ``on_recv_batch`` again -- how the offline (multi-epoch) MF worker
+    replays its buffered ratings (``M/matrix/factorization/workers/PSOfflineMatrixFactorizationWorker.scala:96-127``).
+    ``None`` ends the job.
+``close(ps)``
+    may emit final outputs.
+
+Every call happens on the single owner thread of the rank (no foreign-thread
+collector use).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Iterable, Optional
+
+import torch
+
+from .logic import RuntimeContext
+
+
+@dataclass
+class PulledBatch:
+    """The answer to one ``pull``: unique rows + request -> row map."""
+
+    keys: torch.Tensor        # [B] requested ids (as passed to pull)
+    rows: torch.Tensor        # [U, D] one row per unique key (wire dtype)
+    pos: torch.Tensor         # [B] int32: request b's row is rows[pos[b]]
+    payload: Any = None
+    #: under a locking PS logic only a subset of a pull is answered per round:
+    #: positions of the answered requests within the original ``pull`` (else None)
+    index: Optional[torch.Tensor] = None
+
+    def values(self) -> torch.Tensor:
+        """``[B, D]`` fp32 parameter of every request, in request order."""
+        return self.rows.float()[self.pos.long()]
+
+    @property
+    def n_unique(self) -> int:
+        return self.rows.shape[0]
+
+    def __len__(self) -> int:
+        return self.keys.numel()
+
+
+class BatchedPSClient:
+    """The worker's handle inside the tensor engine (see module docstring)."""
+
+    def pull(self, keys: torch.Tensor, payload: Any = None) -> None:
+        raise NotImplementedError
+
+    def push(self, deltas: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
+        raise NotImplementedError
+
+    def push_unique(self, deltas: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
+        raise NotImplementedError
+
+    def push_keys(self, keys: torch.Tensor, deltas: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def output(self, out: Any) -> None:
+        raise NotImplementedError
+
+
+class BatchedWorkerLogic:
+    """Subclass and override ``on_recv_batch`` / ``on_pull_recv_batch``.
+
+    ``arbitrary_pushes = True`` declares that ``ps.push_keys`` may be used (to
+    keys that were not pulled): the engine then runs one extra, collective
+    planning round per micro-batch for them."""
+
+    arbitrary_pushes = False
+
+    def open(self, ctx: RuntimeContext) -> None:
+        pass
+
+    def on_recv_batch(self, batch: Any, ps: BatchedPSClient) -> None:
+        raise NotImplementedError
+
+    def on_pull_recv_batch(self, pulled: PulledBatch, ps: BatchedPSClient) -> None:
+        raise NotImplementedError
+
+    def update_model_batch(self, ids: torch.Tensor, values: torch.Tensor) -> None:
+        raise NotImplementedError("this worker has no worker-resident model (double model load)")
+
+    def on_eof(self, ps: BatchedPSClient) -> Optional[Iterable[Any]]:
+        return None
+
+    def close(self, ps: BatchedPSClient) -> None:
+        pass
+
+
+class FunctionBatchedWorkerLogic(BatchedWorkerLogic):
+    """A batched worker from plain callables (tests / scripts)."""
+
+    def __init__(self, on_recv_batch, on_pull_recv_batch, open=None, close=None):  # noqa: A002
+        self._recv, self._answer, self._open, self._close = on_recv_batch, on_pull_recv_batch, open, close
+
+    def open(self, ctx):
+        if self._open:
+            self._open(ctx)
+
+    def on_recv_batch(self, batch, ps):
+        self._recv(batch, ps)
+
+    def on_pull_recv_batch(self, pulled, ps):
+        self._answer(pulled, ps)
+
+    def close(self, ps):
+        if self._close:
+            self._close(ps)

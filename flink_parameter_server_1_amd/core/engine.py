@@ -362,7 +362,8 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
               worker_parallelism: int = 1, ps_parallelism: int = 1,
               worker_receiver=None, worker_sender=None, ps_receiver=None, ps_sender=None,
               iteration_wait_time: Optional[float] = None, data_partitioner: Optional[Callable] = None,
-              runtime=None, output_sink: Optional[Callable] = None) -> List[Any]:
+              runtime=None, output_sink: Optional[Callable] = None, backend: str = "record",
+              comm=None, staleness: int = 0) -> List[Any]:
     """Run a parameter-server job; returns the ``Left(wout)``/``Right(psout)`` stream.
 
     Covers the three reference overloads (``M/FlinkParameterServer.scala:62-336``):
@@ -371,7 +372,22 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
     (b) ``ps_logic`` with hash partitioning ``|id| % P`` and Simple adapters
         (``:108-149``);
     (c) fully custom partitioners / wire adapters (``:195-336``).
+
+    ``backend="tensor"`` runs the job on the tensor engine instead
+    (``core.tensor_engine``, one process per GPU under torchrun):
+    ``training_data`` is this rank's iterable of micro-batches,
+    ``worker_logic`` a ``BatchedWorkerLogic``, ``ps_logic`` a device PS logic
+    (``ps.device_logics``); worker / PS parallelism = the world size of
+    ``comm``; ``staleness`` bounds the micro-batches in flight (the
+    ``pullLimit`` analogue, ``tensor_engine.staleness_for_pull_limit``).
     """
+    if backend == "tensor":
+        from .tensor_engine import transform_tensor
+
+        return transform_tensor(training_data, worker_logic, ps_logic, comm=comm, staleness=staleness,
+                                iteration_wait_time=iteration_wait_time, output_sink=output_sink)
+    if backend != "record":
+        raise ValueError(f"backend must be 'record' or 'tensor', not {backend!r}")
     if ps_logic is None:
         if param_init is None or param_update is None:
             raise ValueError("give ps_logic or (param_init, param_update)")

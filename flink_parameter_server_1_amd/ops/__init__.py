@@ -15,7 +15,7 @@ import torch
 from . import _native as N
 from . import reference as R
 
-_OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3, "add_unique": 4}
+_OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3, "add_unique": 4, "add_renorm": 5}
 
 
 def native_available() -> bool:
@@ -102,7 +102,9 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None
 def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: str = "add", lr: float = 0.0,
                eps: float = 1e-10, state: torch.Tensor = None, touched: torch.Tensor = None) -> torch.Tensor:
     """Push apply (K3): ``add`` (atomic), ``set``, ``sgd`` (w -= lr*g, atomic),
-    ``adagrad`` (unique idx).  ``idx < 0`` marks padding rows."""
+    ``adagrad`` (unique idx; ``state`` = accumulators ``[n, D]``), ``add_renorm``
+    (unique idx; w += g and ``state[row] = |w|``, ``state`` = lengths ``[n]``).
+    ``idx < 0`` marks padding rows."""
     if DEBUG:
         check_index(idx, table.shape[0], "apply_rows", allow_negative=True)
         check_finite(delta.float(), "apply_rows delta")

@@ -34,7 +34,8 @@ def init_rows(table: torch.Tensor, id_base: int, id_stride: int, lo: float, hi: 
     n, d = table.shape
     ids = (id_base + torch.arange(n, dtype=torch.int64) * id_stride).view(-1, 1)
     j = torch.arange(d, dtype=torch.int64).view(1, -1)
-    table.copy_((lo + (hi - lo) * hash_uniform(seed, ids, j)).to(table.device))
+    u = hash_uniform(seed, ids, j).to(table.dtype)  # k / 2^24: exact in any float dtype
+    table.copy_((lo + (hi - lo) * u).to(table.device))
     return table
 
 
@@ -56,7 +57,7 @@ OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3}
 def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touched=None):
     idx = idx.long()
     keep = idx >= 0
-    idx, delta = idx[keep], delta[keep].to(torch.float32)
+    idx, delta = idx[keep], delta[keep].to(table.dtype)
     if touched is not None:
         touched[idx] = 1
     if op in ("add", "add_unique"):
@@ -68,6 +69,9 @@ def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touch
     elif op == "adagrad":
         state[idx] += delta * delta
         table[idx] -= lr * delta * torch.rsqrt(state[idx] + eps)
+    elif op == "add_renorm":  # unique idx: w += g, state[row] = |w|
+        table.index_add_(0, idx, delta.to(table.dtype))
+        state[idx] = table[idx].norm(dim=1).to(state.dtype)
     else:
         raise ValueError(op)
     return table
@@ -131,7 +135,7 @@ def mf_sgd_local(U, I, uid, iid, r, lr, lam=0.0, user_atomic=False):
 
 def mf_sgd_pulled(U, uid, r, rows, pos, delta, lr, lam=0.0, user_atomic=False):
     uid, pos = uid.long(), pos.long()
-    u, i = U[uid], rows[pos].to(torch.float32)
+    u, i = U[uid], rows[pos].to(U.dtype)
     e = r - (u * i).sum(1)
     du = lr * (e[:, None] * i - lam * u)
     di = lr * (e[:, None] * u - lam * i)

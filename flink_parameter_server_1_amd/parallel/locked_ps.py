@@ -49,13 +49,14 @@ class LockedPull:
 
 
 class LockedTensorPS:
-    def __init__(self, table: ShardedTable, comm: Comm, wire_dtype=torch.float32):
+    def __init__(self, table: ShardedTable, comm: Comm, wire_dtype=torch.float32, ps: TensorPS = None):
         self.table, self.comm = table, comm
-        self.ps = TensorPS(table, comm, wire_dtype)
+        self.ps = ps if ps is not None else TensorPS(table, comm, wire_dtype)
         self.lock = torch.full((table.n_local,), -1, dtype=torch.int32, device=table.device)
 
-    def acquire(self, keys: torch.Tensor) -> LockedPull:
-        plan = self.ps.plan(keys, persistent=True)
+    def acquire(self, keys: torch.Tensor, flag: int = 0) -> LockedPull:
+        """``flag`` reaches every peer with the counts (``plan.peer_flags``)."""
+        plan = self.ps.plan(keys, flag=flag)
         n = plan.recv_keys.numel()
         granted_recv = torch.zeros(n, dtype=torch.uint8, device=self.table.device)
         off = 0

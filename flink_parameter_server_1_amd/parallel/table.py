@@ -53,7 +53,14 @@ class ShardedTable:
         self.init_spec = init
         self.weight = torch.empty((self.n_local, self.dim), dtype=dtype, device=self.device)
         self.reset_parameters()
-        self.state = torch.zeros_like(self.weight) if optimizer == "adagrad" else None
+        # optimizer state: Adagrad accumulators [n, D]; add_renorm keeps each row's
+        # euclidean length [n] next to it (LengthAndVector, K3 add+renorm)
+        if optimizer == "adagrad":
+            self.state = torch.zeros_like(self.weight)
+        elif optimizer == "add_renorm":
+            self.state = self.weight.norm(dim=1).to(torch.float32)
+        else:
+            self.state = None
         self.touched = torch.zeros(self.n_local, dtype=torch.uint8, device=self.device) if track_touched else None
 
     # ----------------------------------------------------------- id mapping
@@ -111,8 +118,18 @@ class ShardedTable:
 
     def apply(self, local_keys: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None):
         """Push apply (K3) with the table's update rule."""
-        ops.apply_rows(self.weight, local_keys, deltas, op or self.optimizer, lr=lr, state=self.state,
-                       touched=self.touched)
+        op = op or self.optimizer
+        ops.apply_rows(self.weight, local_keys, deltas, op, lr=lr, state=self.state, touched=self.touched)
+        if op == "set" and self.optimizer == "add_renorm":  # model load: lengths of the written rows
+            k = local_keys.long()
+            k = k[k >= 0]
+            self.state[k] = self.weight[k].norm(dim=1).to(self.state.dtype)
+
+    def lengths(self, local_keys: torch.Tensor) -> torch.Tensor:
+        """Row lengths kept by an ``add_renorm`` table."""
+        if self.optimizer != "add_renorm":
+            raise ValueError("lengths() needs optimizer='add_renorm'")
+        return self.state[local_keys.long()]
 
     def load(self, ids: torch.Tensor, values: torch.Tensor):
         """Model load (``transformWithModelLoad``): set rows owned by this shard."""
@@ -133,5 +150,5 @@ class ShardedTable:
     def nbytes(self) -> int:
         n = self.weight.numel() * self.weight.element_size()
         if self.state is not None:
-            n += self.state.numel() * 4
+            n += self.state.numel() * self.state.element_size()
         return n

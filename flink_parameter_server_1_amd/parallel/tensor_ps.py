@@ -77,9 +77,11 @@ class TensorPS:
         #: calls whose counts had not reached the host yet (the host waited on the device)
         self.stats = {"pulls": 0, "unique": 0, "steps": 0, "host_stalls": 0, "pushes": 0}
         self.timer = None  # utils.metrics.StageTimer (optional)
-        W = comm.world
+        #: pushes carry a validity column (set by the device PS logic on every rank
+        #: alike): rows a worker did not push are skipped by the apply and by the
+        #: per-push output instead of being applied as zero deltas
+        self.masked_push = False
         self._pinned = table.device.type == "cuda"
-        self._flagbuf = torch.zeros((W, 1), dtype=torch.int32, device=table.device)
 
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0) -> PendingPlan:
@@ -161,15 +163,29 @@ class TensorPS:
 
     # --------------------------------------------------------------------- push
     def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
-             return_updated: bool = False):
+             return_updated: bool = False, mask: Optional[torch.Tensor] = None):
         """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply
         with ``op`` (default: the table's rule).  ``return_updated``: also return
         ``(global ids, new rows)`` of the keys applied on THIS shard -- the
         per-push ``(id, value)`` output of ``SimplePSLogic``
-        (``M/server/SimplePSLogic.scala:24``)."""
+        (``M/server/SimplePSLogic.scala:24``).  ``mask[U]`` (bool) marks the keys
+        actually pushed; it travels only when ``masked_push`` is set."""
+        D = self.table.dim
+        deltas = deltas.reshape(plan.n_unique, D)
+        if self.masked_push:
+            m = torch.ones(plan.n_unique, 1, dtype=deltas.dtype, device=deltas.device) if mask is None else \
+                mask.reshape(-1, 1).to(deltas.dtype)
+            deltas = torch.cat([deltas, m], dim=1)
+        elif mask is not None:
+            deltas = deltas * mask.reshape(-1, 1).to(deltas.dtype)
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
         with stage("ps.push-a2a", self.timer):
             recv = self.comm.all_to_all(wire.contiguous(), plan.send_splits, plan.recv_splits)
+        recv_keys = plan.recv_keys
+        if self.masked_push:
+            valid = recv[:, D] > 0.5
+            recv = recv[:, :D].contiguous()
+            recv_keys = torch.where(valid, recv_keys, torch.full_like(recv_keys, -1))
         opt = op or self.table.optimizer
         self.stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
@@ -184,13 +200,14 @@ class TensorPS:
                 off = 0
                 for n in plan.recv_splits:
                     if n:
-                        self.table.apply(plan.recv_keys[off:off + n], recv[off:off + n], lr=lr,
+                        self.table.apply(recv_keys[off:off + n], recv[off:off + n], lr=lr,
                                          op="add_unique" if seg_add else opt)
                     off += n
             else:
-                self.table.apply(plan.recv_keys, recv, lr=lr, op=opt)
+                self.table.apply(recv_keys, recv, lr=lr, op=opt)
         if return_updated:
-            return self.table.global_ids(plan.recv_keys), self.table.weight[plan.recv_keys.long()]
+            k = recv_keys[recv_keys >= 0] if self.masked_push else recv_keys
+            return self.table.global_ids(k), self.table.weight[k.long()]
         return None
 
     def reduce_requests(self, plan: PullPlan, deltas: torch.Tensor, op: str = "add",
