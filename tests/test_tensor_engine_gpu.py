@@ -1,0 +1,153 @@
+"""Tensor engine on the MI355X: the public batched API running the HIP kernels
+(dedup, gather, fused MF SGD, apply incl. add_renorm, lock kernels)."""
+import numpy as np
+import pytest
+import torch
+
+from flink_parameter_server_1_amd import ops
+from flink_parameter_server_1_amd.core.messages import Right
+from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime, fold_outputs
+from flink_parameter_server_1_amd.models.mf.apps import ps_online_mf
+from flink_parameter_server_1_amd.models.mf.core import Rating
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def test_native_library_loaded():
+    assert ops.native_available()
+
+
+def test_tensor_mf_gpu_matches_per_record_engine():
+    """One rating per micro-batch on the GPU kernels (fp32) == per-record psOnlineMF
+    (fp64, pullLimit 1, init='hash') to fp32 rounding."""
+    from flink_parameter_server_1_amd.models.mf.batched import ps_online_mf_tensor
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    rng = np.random.default_rng(3)
+    n, users, items = 200, 16, 24
+    u, i, r = rng.integers(0, users, n), rng.integers(0, items, n), rng.random(n)
+    kw = dict(num_factors=8, range_min=0.0, range_max=0.3, learning_rate=0.05, seed=11)
+    recs = [Rating(int(a), int(b), float(c), t) for t, (a, b, c) in enumerate(zip(u, i, r))]
+    Ur = {}
+    Vr = {}
+    for e in ps_online_mf(recs, init="hash", pull_limit=1, worker_parallelism=1, ps_parallelism=1, **kw):
+        (Ur if e.is_left else Vr)[e.value[0]] = np.asarray(e.value[1])
+    batches = [(torch.tensor(u[k:k + 1], device=DEV), torch.tensor(i[k:k + 1], device=DEV),
+                torch.tensor(r[k:k + 1], dtype=torch.float32, device=DEV)) for k in range(n)]
+    out = ps_online_mf_tensor(batches, users, items, comm=Comm(device=DEV), **kw)
+    U, V = fold_outputs(out)
+    assert set(U) == set(Ur) and set(V) == set(Vr)
+    for k in Ur:
+        np.testing.assert_allclose(U[k], Ur[k], rtol=0, atol=2e-6)
+    for k in Vr:
+        np.testing.assert_allclose(V[k], Vr[k], rtol=0, atol=2e-6)
+
+
+def test_pipelined_engine_issues_no_implicit_sync():
+    """staleness 1: counts reach the host one micro-batch ahead; no implicit
+    device->host sync in the loop (torch sync-debug mode 'error')."""
+    from flink_parameter_server_1_amd.models.mf.batched import OnlineMFWorker
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogicWithClose
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    users, items, B = 5000, 2000, 4096
+
+    def batch():
+        return (torch.randint(0, users, (B,), generator=g, device=DEV),
+                torch.randint(0, items, (B,), generator=g, device=DEV),
+                torch.rand(B, generator=g, device=DEV))
+
+    rt = TensorRuntime(Comm(device=DEV), staleness=1)
+    rt.start(OnlineMFWorker(users, 32, 0.05, emit_users=False),
+             DeviceSimplePSLogicWithClose(items, 32, init=("uniform", 0.0, 0.1)))
+    for _ in range(4):  # warm-up: workspaces allocated
+        rt.submit(batch())
+    data = [batch() for _ in range(20)]
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for b in data:
+            rt.submit(b)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    rt.finish()
+    ps = rt.ps_logic.ps
+    assert ps.stats["steps"] == 24 and ps.stats["pulls"] == 24 * B
+
+
+def test_add_renorm_kernel_matches_reference():
+    from flink_parameter_server_1_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    for D in (8, 64, 100):
+        T = torch.randn(300, D, device=DEV)
+        st = T.norm(dim=1)
+        idx = torch.randperm(300, device=DEV)[:120].to(torch.int32)
+        idx[::7] = -1  # padding rows
+        d = torch.randn(120, D, device=DEV)
+        Tc, stc = T.cpu().clone(), st.cpu().clone()
+        ops.apply_rows(T, idx, d, "add_renorm", state=st)
+        R.apply_rows(Tc, idx.cpu(), d.cpu(), "add_renorm", state=stc)
+        torch.testing.assert_close(T.cpu(), Tc, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(st.cpu(), stc, rtol=1e-5, atol=1e-6)
+
+
+def test_lock_logic_gpu_no_lost_updates():
+    from flink_parameter_server_1_amd.api.batched import BatchedWorkerLogic
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceLockPSLogic
+
+    class W(BatchedWorkerLogic):
+        def on_recv_batch(self, batch, ps):
+            ps.pull(batch)
+
+        def on_pull_recv_batch(self, pulled, ps):
+            ps.push(pulled.values() + 1.0)
+
+    rt = TensorRuntime(Comm(device=DEV)).start(W(), DeviceLockPSLogic(64, 4, op="set"))
+    keys = torch.tensor([0, 0, 0, 5, 9, 9], device=DEV)
+    for _ in range(5):
+        rt.submit(keys)
+    out = rt.finish()
+    w = rt.ps_logic.table.weight.cpu()
+    assert torch.equal(w[0], torch.full((4,), 15.0)) and torch.equal(w[9], torch.full((4,), 10.0))
+    assert torch.equal(w[5], torch.full((4,), 5.0)) and float(w[1].abs().sum()) == 0.0
+    assert sum(1 for e in out if isinstance(e, Right)) > 0
+
+
+def test_model_load_and_double_load_gpu():
+    from flink_parameter_server_1_amd.api.batched import BatchedWorkerLogic
+    from flink_parameter_server_1_amd.core.tensor_engine import transform_tensor_with_double_model_load
+    from flink_parameter_server_1_amd.core.messages import Left
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogicWithClose
+
+    class W(BatchedWorkerLogic):
+        def open(self, ctx):
+            self.local = {}
+
+        def update_model_batch(self, ids, values):
+            for k, v in zip(ids.tolist(), values.reshape(-1).tolist()):
+                self.local[k] = v
+
+        def on_recv_batch(self, batch, ps):
+            ps.pull(batch)
+
+        def on_pull_recv_batch(self, pulled, ps):
+            ps.push(torch.ones(len(pulled), 1, device=DEV))
+
+        def close(self, ps):
+            ps.output(dict(self.local))
+
+    model = [Left((k, [10.0 * k])) for k in range(50)] + [Right((k, [float(-k)])) for k in range(5)]
+    batches = [torch.arange(50, device=DEV) for _ in range(3)]
+    out = transform_tensor_with_double_model_load(model, batches, W(), DeviceSimplePSLogicWithClose(50, 1),
+                                                  comm=Comm(device=DEV))
+    worker_local = [e.value for e in out if not isinstance(e, Right)][0]
+    assert worker_local == {k: float(-k) for k in range(5)}
+    ids, vals = [e.value for e in out if isinstance(e, Right)][0]
+    got = dict(zip(ids.tolist(), vals.reshape(-1).tolist()))
+    assert got == {k: 10.0 * k + 3 for k in range(50)}
