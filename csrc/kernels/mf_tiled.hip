@@ -30,6 +30,7 @@
 // wave-quarter).
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 using namespace fps;
@@ -405,7 +406,7 @@ __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, i
 //          rating bits, bucket}
 // LEVEL 2: tmp[work item] -> out (8- or 16-B records) grouped by bucket; kptr = ptr,
 //          cursor = bcursor; work items from wptr / cptr
-template <int LEVEL, bool REC8>
+template <int LEVEL, bool REC8, bool PIPE = true>
 __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
@@ -449,32 +450,59 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       nk = min(1 << cshift, KT - kb);
       __syncthreads();  // s_item is rewritten for the next work item
     }
+    // software pipeline: the raw inputs of batch b+1 are loaded into registers
+    // while batch b is sorted and written (its loads were issued one batch earlier)
+    int32_t ru[E], ri[E], rr[E];
+    int4 rt[E];
+    auto load_batch = [&](int64_t bs) {
+      const int nbs = (int)min((int64_t)TP3_B, hi - bs);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int p = e * 1024 + tid;
+        if (p < nbs) {
+          const int64_t x = bs + p;
+          if (LEVEL == 1) {
+            ru[e] = uid[x];
+            ri[e] = iid[x];
+            rr[e] = __float_as_int(rating[x]);
+          } else if (REC8) {
+            const int3 t = reinterpret_cast<const int3*>(tmp)[x];
+            rt[e] = make_int4(t.x, t.y, t.z, 0);
+          } else {
+            rt[e] = tmp[x];
+          }
+        }
+      }
+    };
+    if (PIPE && lo < hi) load_batch(lo);
     for (int64_t b0 = lo; b0 < hi; b0 += TP3_B) {
       const int nb = (int)min((int64_t)TP3_B, hi - b0);
+      if (!PIPE) load_batch(b0);  // A/B: loads of a batch right before its use
       if (tid < nk) cnt[tid] = 0;
-      __syncthreads();
       int4 r[E];
       int k[E], slot[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {  // this batch's records (registers loaded last iteration)
+        k[e] = 0;
+        if (e * 1024 + tid >= nb) continue;  // no record: registers hold stale values
+        if (LEVEL == 1) {
+          int bk; int32_t row;
+          tile_bucket(ri[e], ru[e], g, bk, row);
+          if (REC8) r[e] = make_int4(ru[e] | ((row & (g.R - 1)) << 24), rr[e], bk, 0);
+          else r[e] = make_int4(ru[e], row, rr[e], bk);
+          k[e] = bk >> cshift;
+        } else {
+          r[e] = rt[e];
+          k[e] = (REC8 ? rt[e].z : rt[e].w) - kb;
+        }
+      }
+      if (PIPE && b0 + TP3_B < hi) load_batch(b0 + TP3_B);  // in flight during the sort below
+      __syncthreads();  // cnt zeroed
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int p = e * 1024 + tid;
         slot[e] = -1;
         if (p < nb) {
-          const int64_t x = b0 + p;
-          if (LEVEL == 1) {
-            int bk; int32_t row;
-            tile_bucket(iid[x], uid[x], g, bk, row);
-            if (REC8) r[e] = make_int4(uid[x] | ((row & (g.R - 1)) << 24), __float_as_int(rating[x]), bk, 0);
-            else r[e] = make_int4(uid[x], row, __float_as_int(rating[x]), bk);
-            k[e] = bk >> cshift;
-          } else if (REC8) {
-            const int3 t = reinterpret_cast<const int3*>(tmp)[x];
-            r[e] = make_int4(t.x, t.y, t.z, 0);
-            k[e] = t.z - kb;
-          } else {
-            r[e] = tmp[x];
-            k[e] = r[e].w - kb;
-          }
           slot[e] = atomicAdd(cnt + k[e], 1);
         }
       }
@@ -498,6 +526,241 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       }
       __syncthreads();  // LDS reused by the next batch
       if (LEVEL == 1 && tid < nk) base[tid] += cnt[tid];  // same thread zeroes cnt[tid] next
+    }
+  }
+}
+
+// ---- tp4: capacity-slot partition (default).  No counting pass.  tp3's count
+// kernel (one LDS atomic per rating into a 16k-bucket histogram, 79 % of its LDS
+// cycles bank conflicts, profiles/r1_partition_pmc.md) ran ~200 us alone and
+// ~2 ms beside the SGD, whose LDS it starved.  Here every coarse key and every
+// bucket owns a slot of its own in the output, sized from the counts of the
+// previous run of the same partitioner (a stationary stream's bucket sizes barely
+// move between micro-batches): cap_k = floor(prev_k * n * slack / n_prev) + pad
+// (the first run: uniform).  Each LDS-sorted batch reserves its runs with one
+// global atomic per (batch, key) on the key's cursor; the cursors end as the exact
+// counts, which size the next run.  Records past a slot's capacity go to an
+// overflow list (one atomic per (batch, key) again) that a flat SGD kernel
+// processes after the tiles of their block (tp4_ovf_sgd_kernel): nothing is
+// dropped whatever the skew, only slower.  Traffic: level 1 reads the 12-B input
+// and writes 12-B records, level 2 reads them and writes 8-B records (44 B per
+// rating against tp3's 52 B).
+constexpr float TP4_SLACK = 1.125f;
+constexpr int TP4_PAD = 64;
+
+// starts[0..K] = exclusive scan of the capacities (one 1024-thread workgroup, K <= 16384)
+__global__ void __launch_bounds__(1024) tp4_plan_kernel(const int32_t* __restrict__ prev, int K, int64_t n_prev,
+                                                        int64_t n, int32_t* __restrict__ starts) {
+  __shared__ int32_t part[1024];
+  const int per = (K + 1023) / 1024;
+  const int k0 = threadIdx.x * per;
+  const double scale = n_prev > 0 ? (double)n * TP4_SLACK / (double)n_prev : 0.0;
+  const int32_t uni = (int32_t)((double)n * TP4_SLACK / K);
+  auto cap = [&](int k) -> int32_t {
+    return (n_prev > 0 ? (int32_t)((double)prev[k] * scale) : uni) + TP4_PAD;
+  };
+  int32_t s = 0;
+  for (int k = k0; k < min(K, k0 + per); ++k) s += cap(k);
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (int k = k0; k < min(K, k0 + per); ++k) { starts[k] = run; run += cap(k); }
+  if (threadIdx.x == 1023) starts[K] = part[1023];
+}
+
+// level-2 work items over the FILLED part of every coarse slot
+__global__ void tp4_workptr_kernel(const int32_t* __restrict__ ccursor, const int32_t* __restrict__ cstart, int NC,
+                                   int32_t* __restrict__ wptr) {
+  if (threadIdx.x != 0) return;
+  int32_t run = 0;
+  for (int c = 0; c < NC; ++c) {
+    wptr[c] = run;
+    const int32_t filled = min(ccursor[c], cstart[c + 1] - cstart[c]);
+    run += (filled + TP3_CH - 1) / TP3_CH;
+  }
+  wptr[NC] = run;
+}
+
+// overflow record {uid, row in block, rating bits, bucket} from a staged record
+template <bool REC8, int LEVEL>
+__device__ __forceinline__ int4 tp4_ovf_rec(const int4& x, int bk, const TileGeo& g) {
+  if (REC8) {
+    const int32_t u = x.x & 0xffffff;
+    const int rit = (int)((uint32_t)x.x >> 24);
+    return make_int4(u, (bk % g.T) * g.R + rit, x.y, bk);
+  }
+  return x;  // {uid, row, rating bits, bucket}
+}
+
+// LEVEL 1: (uid, iid, rating) of this workgroup's chunk -> coarse slots of tmp
+//          (REC8: 12-B {uid | row_in_tile << 24, rating bits, bucket}; else 16-B
+//          {uid, row, rating bits, bucket}); kstart = cstart, cursor = ccursor.
+// LEVEL 2: the filled part of the coarse slots -> bucket slots of rec (8- or 16-B
+//          records); kstart = bstart, cursor = bcursor; work items from wptr.
+template <int LEVEL, bool REC8>
+__global__ void __launch_bounds__(1024) tp4_scatter_kernel(const int32_t* __restrict__ uid,
+                                                           const int32_t* __restrict__ iid,
+                                                           const float* __restrict__ rating,
+                                                           const void* __restrict__ tmp, int64_t n, int64_t chunk,
+                                                           TileGeo g, int cshift, int NC, int KT,
+                                                           const int32_t* __restrict__ kstart,
+                                                           int32_t* __restrict__ cursor,
+                                                           const int32_t* __restrict__ cstart,
+                                                           const int32_t* __restrict__ ccursor,
+                                                           const int32_t* __restrict__ wptr,
+                                                           void* __restrict__ out, int4* __restrict__ ovf,
+                                                           int32_t* __restrict__ ovf_cnt, uint8_t* __restrict__ seen) {
+  constexpr int E = TP3_B / 1024;
+  __shared__ int4 srt[TP3_B];
+  __shared__ int32_t cnt[TP3_MAXK], off[TP3_MAXK], base[TP3_MAXK], obase[TP3_MAXK];
+  __shared__ int32_t kst[TP3_MAXK], kcap[TP3_MAXK];
+  __shared__ int32_t s_item[3];
+  const int tid = threadIdx.x;
+  const int nwork = LEVEL == 1 ? 1 : wptr[NC];
+  for (int w = LEVEL == 1 ? 0 : blockIdx.x; w < nwork; w += (LEVEL == 1 ? 1 : gridDim.x)) {
+    int64_t lo, hi;
+    int kb, nk;
+    if (LEVEL == 1) {
+      lo = (int64_t)blockIdx.x * chunk;
+      hi = min(n, lo + chunk);
+      kb = 0;
+      nk = NC;
+    } else {
+      if (tid == 0) {
+        int c = 0;
+        while (wptr[c + 1] <= w) ++c;  // NC <= 256: linear search
+        const int32_t filled = min(ccursor[c], cstart[c + 1] - cstart[c]);
+        const int32_t a = (w - wptr[c]) * TP3_CH;
+        s_item[0] = cstart[c] + a;
+        s_item[1] = cstart[c] + min(filled, a + TP3_CH);
+        s_item[2] = c << cshift;
+      }
+      __syncthreads();
+      lo = s_item[0];
+      hi = s_item[1];
+      kb = s_item[2];
+      nk = min(1 << cshift, KT - kb);
+    }
+    if (tid < nk) {
+      kst[tid] = kstart[kb + tid];
+      kcap[tid] = kstart[kb + tid + 1] - kstart[kb + tid];
+    }
+    __syncthreads();  // s_item / kst / kcap visible; s_item rewritten only after the batches below
+    for (int64_t b0 = lo; b0 < hi; b0 += TP3_B) {
+      const int nb = (int)min((int64_t)TP3_B, hi - b0);
+      if (tid < nk) cnt[tid] = 0;
+      __syncthreads();
+      int4 r[E];
+      int k[E], slot[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int p = e * 1024 + tid;
+        slot[e] = -1;
+        if (p < nb) {
+          const int64_t x = b0 + p;
+          int bk;
+          if (LEVEL == 1) {
+            const int32_t i = iid[x], u = uid[x];
+            int32_t row;
+            tile_bucket(i, u, g, bk, row);
+            if (REC8) r[e] = make_int4(u | ((row & (g.R - 1)) << 24), __float_as_int(rating[x]), bk, 0);
+            else r[e] = make_int4(u, row, __float_as_int(rating[x]), bk);
+            if (seen != nullptr) seen[i] = 1;
+            k[e] = bk >> cshift;
+          } else if (REC8) {
+            const int3 t = reinterpret_cast<const int3*>(tmp)[x];
+            r[e] = make_int4(t.x, t.y, t.z, 0);
+            k[e] = t.z - kb;
+          } else {
+            r[e] = reinterpret_cast<const int4*>(tmp)[x];
+            k[e] = r[e].w - kb;
+          }
+          slot[e] = atomicAdd(cnt + k[e], 1);
+        }
+      }
+      __syncthreads();
+      tp3_scan(cnt, off, nk);
+      if (tid < nk && cnt[tid]) {  // this batch's run of key tid: slot range, overflow beyond capacity
+        const int32_t o = atomicAdd(cursor + kb + tid, cnt[tid]);
+        base[tid] = o;
+        const int32_t ex = o + cnt[tid] - kcap[tid];
+        if (ex > 0) obase[tid] = atomicAdd(ovf_cnt, min(ex, cnt[tid]));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (slot[e] >= 0) srt[off[k[e]] + slot[e]] = r[e];
+      __syncthreads();
+      for (int p = tid; p < nb; p += 1024) {
+        const int4 x = srt[p];
+        const int bk = REC8 ? x.z : x.w;
+        const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
+        const int32_t idx = base[kk] + (p - off[kk]);
+        if (idx < kcap[kk]) {
+          const int64_t o = (int64_t)kst[kk] + idx;
+          if (LEVEL == 1 && REC8) reinterpret_cast<int3*>(out)[o] = make_int3(x.x, x.y, x.z);
+          else if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = x;
+          else if (REC8) reinterpret_cast<int2*>(out)[o] = make_int2(x.x, x.y);
+          else put_rec<false>(out, o, x.x, x.y, __int_as_float(x.z), x.w, g.R);
+        } else {
+          ovf[obase[kk] + (idx - max(kcap[kk], base[kk]))] = tp4_ovf_rec<REC8, LEVEL>(x, bk, g);
+        }
+      }
+      __syncthreads();  // LDS reused by the next batch
+    }
+  }
+}
+
+// Flat SGD over the overflow records of buckets [b_lo, b_lo + nblk * T): one lane
+// group per record, user row stored (Hogwild, as in the tiles), item delta by
+// float atomics.  Runs after the tiled launch of the same blocks; a fixed grid
+// reads the record count on the device (no host sync) and exits at once when the
+// list is empty -- the common case.
+template <int TPR, int V>
+__global__ void __launch_bounds__(256) tp4_ovf_sgd_kernel(float* __restrict__ U, float* __restrict__ I0,
+                                                          float* __restrict__ I1, const int4* __restrict__ ovf,
+                                                          const int32_t* __restrict__ ovf_cnt, int b_lo, int T,
+                                                          int nblk, float lr, float lambda) {
+  constexpr int D4 = TPR * V;
+  constexpr int GPW = 64 / TPR;
+  const int n = *ovf_cnt;
+  const int lane = threadIdx.x & 63;
+  const int j = lane % TPR;
+  const int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / TPR;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x / TPR;
+  (void)GPW;
+  for (int64_t x = g0; x < n; x += gs) {
+    const int4 r = ovf[x];
+    const int rel = r.w - b_lo;
+    if (rel < 0 || rel >= nblk * T) continue;  // uniform in the lane group
+    float4* Ig = reinterpret_cast<float4*>(rel < T ? I0 : I1) + (int64_t)r.y * D4;
+    float4* Ug = reinterpret_cast<float4*>(U) + (int64_t)r.x * D4;
+    const float rt = __int_as_float(r.z);
+    float4 uv[V], iv[V];
+    float p = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      uv[v] = Ug[j + v * TPR];
+      iv[v] = Ig[j + v * TPR];
+      p += uv[v].x * iv[v].x + uv[v].y * iv[v].y + uv[v].z * iv[v].z + uv[v].w * iv[v].w;
+    }
+    const float e = rt - group_sum<TPR>(p);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float4 u = uv[v], i = iv[v];
+      Ug[j + v * TPR] = make_float4(u.x + lr * (e * i.x - lambda * u.x), u.y + lr * (e * i.y - lambda * u.y),
+                                    u.z + lr * (e * i.z - lambda * u.z), u.w + lr * (e * i.w - lambda * u.w));
+      float* ip = reinterpret_cast<float*>(Ig + j + v * TPR);
+      atomic_add_noret(ip + 0, lr * (e * u.x - lambda * i.x));
+      atomic_add_noret(ip + 1, lr * (e * u.y - lambda * i.y));
+      atomic_add_noret(ip + 2, lr * (e * u.z - lambda * i.z));
+      atomic_add_noret(ip + 3, lr * (e * u.w - lambda * i.w));
     }
   }
 }
@@ -534,7 +797,8 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
                                                                int64_t block_rows, float lr, float lambda,
-                                                               float* __restrict__ I1, int64_t block_rows1, int T0) {
+                                                               float* __restrict__ I1, int64_t block_rows1, int T0,
+                                                               const int32_t* __restrict__ tcnt) {
   using Rec = typename RecT<REC8>::type;
   constexpr int TG_CAP = tg_cap<REC8>();
   const Rec* __restrict__ rec = reinterpret_cast<const Rec*>(rec_);
@@ -551,7 +815,9 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
   if (second) { I = I1; block_rows = block_rows1; }
   const int64_t r0 = (int64_t)tl * R;
   const int nr = (int)min((int64_t)R, block_rows - r0);
-  const int32_t beg = ptr[t], end = ptr[t + 1];
+  // tp4 slots: the tile's records fill [ptr[t], ptr[t] + count) of its slot (the
+  // cursor may exceed the slot: the excess went to the overflow list)
+  const int32_t beg = ptr[t], end = tcnt != nullptr ? min(ptr[t + 1], beg + tcnt[t]) : ptr[t + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ngroups = (blockDim.x >> 6) * GPW;
   const int grp = wave * GPW + lane / TPR, j = lane % TPR;
@@ -797,22 +1063,20 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   if (n > 0) {
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
     if (g2 > 1024) g2 = 1024;
-    if (rec8)
-      hipLaunchKernelGGL((tp3_scatter_kernel<1, true>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)nullptr, n, chunk, g,  cshift, NC, KT, (const int32_t*)cptr,
-                         ccursor, (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
-    else
-      hipLaunchKernelGGL((tp3_scatter_kernel<1, false>), dim3(G), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)nullptr, n, chunk, g,  cshift, NC, KT, (const int32_t*)cptr,
-                         ccursor, (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)H1, (void*)tmp);
-    if (rec8)
-      hipLaunchKernelGGL((tp3_scatter_kernel<2, true>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, g,  cshift, NC, KT, (const int32_t*)ptr, bcursor,
-                         (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
-    else
-      hipLaunchKernelGGL((tp3_scatter_kernel<2, false>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,
-                         (const int4*)tmp, n, chunk, g,  cshift, NC, KT, (const int32_t*)ptr, bcursor,
-                         (const int32_t*)cptr, (const int32_t*)wptr, (const int32_t*)nullptr, rec);
+    // FPS_TP3_PIPE=0: the scatters without the register prefetch of the next batch (A/B)
+    static const bool pipe = [] { const char* e = getenv("FPS_TP3_PIPE"); return !(e && e[0] == '0'); }();
+#define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
+    if (pipe) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, true>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, \
+                                 TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr,                \
+                                 (const int32_t*)wptr, H1P, OUT);                                                  \
+    else hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating,     \
+                            TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, \
+                            H1P, OUT)
+    if (rec8) { FPS_TP3(1, true, G, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
+    else { FPS_TP3(1, false, G, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
+    if (rec8) { FPS_TP3(2, true, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }
+    else { FPS_TP3(2, false, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }
+#undef FPS_TP3
   }
   FPS_CHECK_LAUNCH();
   return 0;
@@ -831,9 +1095,21 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I, const void* rec, int rec8, cons
 
 // nblk = 2: tiles ptr[0..2T] of two consecutive item blocks (I: block_rows, I1:
 // block_rows1) in one launch of 2T workgroups.
+FPS_API int fps_mf_sgd_tiled3(float* U, float* I, const void* rec, int rec8, const int32_t* ptr,
+                              const int32_t* tcnt, int T, int R, int64_t block_rows, float* I1, int64_t block_rows1,
+                              int nblk, int D, float lr, float lambda, void* stream);
+
 FPS_API int fps_mf_sgd_tiled2(float* U, float* I, const void* rec, int rec8, const int32_t* ptr, int T, int R,
                               int64_t block_rows, float* I1, int64_t block_rows1, int nblk, int D, float lr,
                               float lambda, void* stream) {
+  return fps_mf_sgd_tiled3(U, I, rec, rec8, ptr, nullptr, T, R, block_rows, I1, block_rows1, nblk, D, lr, lambda,
+                           stream);
+}
+
+// tcnt (tp4 slots, may be null): per-tile record counts, ptr = the slot starts
+FPS_API int fps_mf_sgd_tiled3(float* U, float* I, const void* rec, int rec8, const int32_t* ptr,
+                              const int32_t* tcnt, int T, int R, int64_t block_rows, float* I1, int64_t block_rows1,
+                              int nblk, int D, float lr, float lambda, void* stream) {
   if (T <= 0) return 0;
   if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
   const int grid = nblk * T;
@@ -842,9 +1118,9 @@ FPS_API int fps_mf_sgd_tiled2(float* U, float* I, const void* rec, int rec8, con
   constexpr int PF = 8;
 #define FPS_TILED(TPR_, V_)                                                                                    \
   if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, U, I, \
-                               rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T);                        \
+                               rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt);                  \
   else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(grid), dim3(512), 0, s, U, I,    \
-                          rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T)
+                          rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt)
   switch (D) {
     case 16: FPS_TILED(4, 1); break;
     case 32: FPS_TILED(8, 1); break;
@@ -854,6 +1130,89 @@ FPS_API int fps_mf_sgd_tiled2(float* U, float* I, const void* rec, int rec8, con
     default: return (int)hipErrorInvalidValue;
   }
 #undef FPS_TILED
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- tp4 host side.  Workspace (int32, fps_tile_partition4_ws_ints): cstart[NC+1],
+// ccursor[NC], wptr[NC+1]; bstart[KT+1] / bcursor[KT] are the caller's (the SGD
+// reads them: slot starts and counts); tmp holds fps_tile_partition4_cap(n, NC)
+// 12- or 16-B records, rec fps_tile_partition4_cap(n, KT) 8- or 16-B records,
+// ovf n 16-B records.  n_prev: the n of this partitioner's previous run (0: first),
+// whose cursors (still in ccursor / bcursor) size this run's slots.
+FPS_API int64_t fps_tile_partition4_ws_ints(int W, int T, int P) {
+  const int KT = P * 2 * W * T;
+  const int NC = ((KT - 1) >> tp3_cshift(KT)) + 1;
+  return 3 * (int64_t)NC + 2;
+}
+
+FPS_API int64_t fps_tile_partition4_cap(int64_t n, int K) {
+  return (int64_t)((double)n * TP4_SLACK) + (int64_t)K * (TP4_PAD + 1) + 16;
+}
+
+FPS_API int fps_tile_partition4(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n,
+                                int64_t n_prev, int W, const int32_t* half, int R, int T, int P, int upp,
+                                int32_t* ws, void* tmp, int32_t* bstart, int32_t* bcursor, void* rec, int rec8,
+                                int4* ovf, int32_t* ovf_cnt, uint8_t* seen, void* stream) {
+  const int KT = P * 2 * W * T;
+  if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
+  const int cshift = tp3_cshift(KT);
+  const int NC = ((KT - 1) >> cshift) + 1;
+  if (NC > TP3_MAXK || (1 << cshift) > TP3_MAXK) return (int)hipErrorInvalidValue;
+  const TileGeo g = make_geo(W, half, R, T, upp);
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* cstart = ws;
+  int32_t* ccursor = cstart + NC + 1;
+  int32_t* wptr = ccursor + NC;
+  // slots from the previous run's cursors, then zero the cursors
+  hipLaunchKernelGGL(tp4_plan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccursor, NC, n_prev, n, cstart);
+  hipLaunchKernelGGL(tp4_plan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bcursor, KT, n_prev, n, bstart);
+  hipError_t e = hipMemsetAsync(ccursor, 0, sizeof(int32_t) * (size_t)NC, s);
+  if (e == hipSuccess) e = hipMemsetAsync(bcursor, 0, sizeof(int32_t) * (size_t)KT, s);
+  if (e == hipSuccess) e = hipMemsetAsync(ovf_cnt, 0, sizeof(int32_t), s);
+  if (e != hipSuccess) return (int)e;
+  if (n > 0) {
+    const int G = fps_tile_partition_groups(n);
+    const int64_t chunk = (n + G - 1) / G;
+#define FPS_TP4_L1(R8)                                                                                         \
+    hipLaunchKernelGGL((tp4_scatter_kernel<1, R8>), dim3(G), dim3(1024), 0, s, uid, iid, rating,             \
+                       (const void*)nullptr, n, chunk, g, cshift, NC, KT, (const int32_t*)cstart, ccursor,    \
+                       (const int32_t*)cstart, (const int32_t*)ccursor, (const int32_t*)wptr, tmp, ovf, ovf_cnt, \
+                       seen)
+    if (rec8) FPS_TP4_L1(true); else FPS_TP4_L1(false);
+#undef FPS_TP4_L1
+    hipLaunchKernelGGL(tp4_workptr_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)ccursor, (const int32_t*)cstart,
+                       NC, wptr);
+    int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
+    if (g2 > 1024) g2 = 1024;
+#define FPS_TP4_L2(R8)                                                                                         \
+    hipLaunchKernelGGL((tp4_scatter_kernel<2, R8>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,        \
+                       (const void*)tmp, n, (int64_t)0, g, cshift, NC, KT, (const int32_t*)bstart, bcursor,     \
+                       (const int32_t*)cstart, (const int32_t*)ccursor, (const int32_t*)wptr, rec, ovf, ovf_cnt,  \
+                       (uint8_t*)nullptr)
+    if (rec8) FPS_TP4_L2(true); else FPS_TP4_L2(false);
+#undef FPS_TP4_L2
+  }
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// Overflow records of buckets [b_lo, b_lo + nblk*T) (item rows I0: first block, I1: second)
+FPS_API int fps_mf_sgd_ovf(float* U, float* I0, float* I1, const int4* ovf, const int32_t* ovf_cnt, int b_lo, int T,
+                           int nblk, int D, float lr, float lambda, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = 512;  // fixed: the count lives on the device
+#define FPS_OVF(TPR_, V_) hipLaunchKernelGGL((tp4_ovf_sgd_kernel<TPR_, V_>), dim3(grid), dim3(256), 0, s, U, I0, I1, \
+                                             ovf, ovf_cnt, b_lo, T, nblk, lr, lambda)
+  switch (D) {
+    case 16: FPS_OVF(4, 1); break;
+    case 32: FPS_OVF(8, 1); break;
+    case 64: FPS_OVF(16, 1); break;
+    case 128: FPS_OVF(16, 2); break;
+    case 256: FPS_OVF(16, 4); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FPS_OVF
   FPS_CHECK_LAUNCH();
   return 0;
 }

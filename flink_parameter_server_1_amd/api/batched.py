@@ -92,9 +92,11 @@ class BatchedWorkerLogic:
 
     ``arbitrary_pushes = True`` declares that ``ps.push_keys`` may be used (to
     keys that were not pulled): the engine then runs one extra, collective
-    planning round per micro-batch for them."""
+    planning round per micro-batch for them.  ``pushes = False`` declares a
+    query-only worker (top-K serving): the engine skips the push round."""
 
     arbitrary_pushes = False
+    pushes = True
 
     def open(self, ctx: RuntimeContext) -> None:
         pass

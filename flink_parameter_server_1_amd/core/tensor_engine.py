@@ -272,6 +272,8 @@ class TensorRuntime:
         return None, None
 
     def _push(self, plan, c) -> None:
+        if not self.worker_logic.pushes:  # a query-only worker: no push round at all
+            return
         ps = self.ps_logic.ps
         if c._direct is not None:
             deltas, mask = c._direct, None

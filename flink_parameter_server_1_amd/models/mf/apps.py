@@ -137,14 +137,22 @@ def ps_online_learner_and_generator(src: Iterable, num_factors: int = 10, range_
                                     worker_k: int = 75, bucket_size: int = 100, pruning_algorithm=LI(5, 2.5),
                                     pull_limit: int = 500, worker_parallelism: int = 4, ps_parallelism: int = 4,
                                     iteration_wait_time: Optional[float] = None, seed: Optional[int] = None,
-                                    reference_quirks: bool = False, runtime=None):
-    desc = RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed)
+                                    reference_quirks: bool = False, runtime=None, init: str = "ranged"):
+    """``init="hash"``: per-id hash init (PS users: seed, worker items: seed ^
+    USER_SEED_XOR) -- the init of the tensor-engine app, for exact parity runs."""
+    if init == "hash":
+        desc = HashFactorInitializerDescriptor(num_factors, range_min, range_max, ((seed or 0) ^ USER_SEED_XOR))
+        ps_desc = HashFactorInitializerDescriptor(num_factors, range_min, range_max, seed or 0)
+    elif init == "ranged":
+        desc = ps_desc = RangedRandomFactorInitializerDescriptor(num_factors, range_min, range_max, seed)
+    else:
+        raise ValueError(f"init must be 'ranged' or 'hash', not {init!r}")
     worker = PSOnlineMatrixFactorizationAndTopKGeneratorWorker(
         negative_sample_rate=negative_sample_rate, user_memory=user_memory, worker_k=worker_k,
         bucket_size=bucket_size, pruning=pruning_algorithm, worker_parallelism=worker_parallelism,
         factor_init_desc=desc, factor_update=SGDUpdater(learning_rate), seed=seed,
         reference_quirks=reference_quirks)
-    init = desc.open()
+    init = ps_desc.open() if ps_desc is not desc else desc.open()
     ps_logic = SimplePSLogic(lambda x: attach_length(init.next_factor(x)),
                              lambda vec, delta: attach_length(vector_sum(vec[1], delta[1])))
     out = transform(_broadcast(src, worker_parallelism), add_pull_limiter(worker, pull_limit), ps_logic,

@@ -1,0 +1,493 @@
+"""Top-K recommendation apps on the tensor engine (SURVEY C34-C39 on MI355X).
+
+* ``ps_top_k_generator_tensor`` -- ``psTopKGenerator``
+  (``M/matrix/factorization/PSTopKGenerator.scala:47-107``): user vectors on the
+  PS (``set`` rule; unloaded users are invalid, ``:62,74-76``), item vectors
+  worker-resident (double model load, ``Right`` records), every query rating
+  broadcast to all ranks (``:78-89``), partial top-``workerK`` lists gathered and
+  merged with the user's seen items dropped (``CollectTopKFromEachWorker``,
+  ``M/matrix/factorization/utils/CollectTopKFromEachWorker.scala:30-59``).
+* ``ps_online_learner_and_generator_tensor`` -- ``psOnlineLearnerAndGenerator``
+  (``M/matrix/factorization/PSOnlineMatrixFactorizationAndTopKGenerator.scala:50-100``,
+  worker ``M/matrix/factorization/workers/PSOnlineMatrixFactorizationAndTopKGeneratorWorker.scala:59-166``):
+  per broadcast rating the user is pulled, a top-K is served from the current
+  item shards, then ONLY the rank owning the item (``item % W``) runs the SGD
+  step on its local item (and negatives) and pushes the user delta to the PS,
+  whose rule is ``attachLength(vectorSum(v, d))`` (``add_renorm``, K3).
+
+Device pieces: LEMP scoring on MFMA (``LempTopK``, K8) with the pruning
+strategies as candidate masks (``lemp_candidate_mask``), an ``all_gather`` of the
+partial lists (X7), the merge kernel (``ops.topk_merge_cand``, K13) fed with
+candidates from which the seen items were removed by a device seen store
+(``SeenStore``).
+
+Semantics inside a micro-batch: every rating of the batch is served from the
+item vectors as of the batch start and the batch's SGD steps follow; with one
+rating per micro-batch this is the reference's per-record order (the parity
+tests run that way).
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+
+from ... import ops
+from ...api.batched import BatchedWorkerLogic
+from ...core.messages import Left
+from ...core.tensor_engine import TensorRuntime
+from ...parallel.comm import Comm
+from ...ps.device_logics import DeviceSimplePSLogic
+from ...utils.tracing import stage
+from .core import USER_SEED_XOR
+from .pruning import COORD, INCR, LC, LENGTH, LI
+from .topk_fast import LempTopK
+
+
+# ----------------------------------------------------------------- seen store
+class SeenStore:
+    """Per-user memory of the last ``memory`` recommended-for items
+    (``CollectTopKFromEachWorker``'s ``seenSet`` / ``seenList``; ``memory = -1``:
+    unbounded, 0: none).  Device-side: sorted ``(user << 32 | item)`` keys with
+    the per-user sequence number of their latest insertion; an item is seen by a
+    user iff that insertion is among the user's last ``memory`` ones.  (The
+    reference drops an item from the set when its OLDEST list entry is evicted
+    even if it was re-added since; here it stays excluded while any occurrence is
+    inside the window -- documented deviation.)"""
+
+    def __init__(self, memory: int, device):
+        self.memory = int(memory)
+        self.device = torch.device(device)
+        self.keys = torch.zeros(0, dtype=torch.int64, device=self.device)
+        self.seq = torch.zeros(0, dtype=torch.int64, device=self.device)
+        self.ucount_keys = torch.zeros(0, dtype=torch.int64, device=self.device)
+        self.ucount = torch.zeros(0, dtype=torch.int64, device=self.device)
+
+    def _user_count(self, users: torch.Tensor) -> torch.Tensor:
+        if self.ucount_keys.numel() == 0:
+            return torch.zeros_like(users)
+        i = torch.searchsorted(self.ucount_keys, users).clamp(max=self.ucount_keys.numel() - 1)
+        return torch.where(self.ucount_keys[i] == users, self.ucount[i], torch.zeros_like(users))
+
+    def contains(self, users: torch.Tensor, items: torch.Tensor) -> torch.Tensor:
+        """``[B, M]`` bool: ``items[b, m]`` is in user ``users[b]``'s window."""
+        if self.memory == 0 or self.keys.numel() == 0:
+            return torch.zeros(items.shape, dtype=torch.bool, device=items.device)
+        u = users.long().view(-1, 1)
+        key = (u << 32) | (items.long() & 0xFFFFFFFF)
+        i = torch.searchsorted(self.keys, key).clamp(max=self.keys.numel() - 1)
+        found = self.keys[i] == key
+        if self.memory < 0:
+            return found & (items >= 0)
+        lo = self._user_count(users.long()).view(-1, 1) - self.memory
+        return found & (self.seq[i] >= lo) & (items >= 0)
+
+    def add(self, users: torch.Tensor, items: torch.Tensor) -> None:
+        """Record one item per user, in order (users distinct within the call)."""
+        if self.memory == 0 or users.numel() == 0:
+            return
+        users, items = users.long(), items.long()
+        cnt = self._user_count(users)
+        key = (users << 32) | (items & 0xFFFFFFFF)
+        keys = torch.cat([self.keys, key])
+        seq = torch.cat([self.seq, cnt])
+        # keep the latest insertion of every key
+        order = torch.argsort(keys * 0 + seq, stable=True)  # by seq ...
+        keys, seq = keys[order], seq[order]
+        order = torch.argsort(keys, stable=True)             # ... then by key: last of a run = latest
+        keys, seq = keys[order], seq[order]
+        last = torch.ones_like(keys, dtype=torch.bool)
+        if keys.numel() > 1:
+            last[:-1] = keys[1:] != keys[:-1]
+        self.keys, self.seq = keys[last], seq[last]
+        # per-user insertion counts
+        uk = torch.cat([self.ucount_keys, users])
+        uc = torch.cat([self.ucount, cnt + 1])
+        order = torch.argsort(uk, stable=True)
+        uk, uc = uk[order], uc[order]
+        lastu = torch.ones_like(uk, dtype=torch.bool)
+        if uk.numel() > 1:
+            lastu[:-1] = uk[1:] != uk[:-1]
+        self.ucount_keys, self.ucount = uk[lastu], uc[lastu]
+        if self.memory > 0 and self.keys.numel() > 4096:  # drop entries that left every window
+            lo = self._user_count(self.keys >> 32) - self.memory
+            keep = self.seq >= lo
+            self.keys, self.seq = self.keys[keep], self.seq[keep]
+
+
+def occurrence_rounds(users: torch.Tensor) -> torch.Tensor:
+    """Round of every entry: 0 for a user's first entry in the batch, 1 for its
+    second ... (rounds are processed in order, each holding a user at most once)."""
+    order = torch.argsort(users, stable=True)
+    su = users[order]
+    start = torch.ones_like(su, dtype=torch.bool)
+    if su.numel() > 1:
+        start[1:] = su[1:] != su[:-1]
+    idx = torch.arange(su.numel(), device=users.device)
+    run_start = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
+    rnd = torch.empty_like(idx)
+    rnd[order] = idx - run_start
+    return rnd
+
+
+# ------------------------------------------------------------- LEMP pruning
+def _theta(best_s: torch.Tensor) -> torch.Tensor:
+    """k-th best so far; 0 while fewer than k candidates were kept (the reference's
+    ``if (topK.length < K) 0.0 else topK.head._1``)."""
+    t = best_s[:, -1]
+    return torch.where(torch.isfinite(t), t, torch.zeros_like(t))
+
+
+def lemp_candidate_mask(Q: torch.Tensor, qlen: torch.Tensor, theta: torch.Tensor, X: torch.Tensor,
+                        xlen: torch.Tensor, strategy, reference_quirks: bool = False) -> torch.Tensor:
+    """``[B, n]`` bool: candidates the LEMP strategy keeps for a length-sorted
+    bucket ``X`` (``M/matrix/factorization/pruning/LEMPPruningFunctions.scala:20-89``,
+    selection as ``M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:72-96``).
+    The bound is exact, so masking only skips work; the top-K is unchanged."""
+    B, n = Q.shape[0], X.shape[0]
+    head, last = float(xlen[0]), float(xlen[-1])
+    if isinstance(strategy, (LC, LI)):
+        use_len = head > last * strategy.algorithm_switch_threshold
+        if use_len:
+            strategy = LENGTH()
+        else:
+            strategy = COORD() if isinstance(strategy, LC) else INCR(strategy.num_focus_coordinates)
+    if isinstance(strategy, LENGTH):
+        mn = theta / qlen.clamp_min(1e-30)
+        x2 = (xlen * xlen).view(1, -1)
+        if reference_quirks:  # squared length vs the unsquared bound
+            return x2 >= mn.view(-1, 1)
+        bound = torch.where(mn > 0, mn * mn, torch.full_like(mn, float("-inf")))
+        return x2 >= bound.view(-1, 1)
+    if isinstance(strategy, COORD):
+        denom = head * qlen
+        tbq = torch.where(denom > 0, theta / denom.clamp_min(1e-30), torch.zeros_like(theta))
+        f = torch.argmax(Q * Q, dim=1)
+        qf = Q.gather(1, f.view(-1, 1)).view(-1)
+        qbf = torch.where(qlen > 0, qf / qlen.clamp_min(1e-30), torch.zeros_like(qf))
+        a = qbf * tbq
+        b = torch.sqrt(torch.clamp((1 - tbq * tbq) * (1 - qbf * qbf), min=0.0))
+        lfp, ufp = a - b, a + b
+        ratio = torch.where(qbf != 0, tbq / torch.where(qbf != 0, qbf, torch.ones_like(qbf)),
+                            torch.full_like(qbf, float("inf")))
+        lf = torch.where((qbf >= 0) | (lfp > ratio), lfp, torch.full_like(lfp, -1.0))
+        uf = torch.where((qbf <= 0) | (ufp < ratio), ufp, torch.full_like(ufp, 1.0))
+        pf = X.t()[f]  # [B, n]: coordinate f of every item
+        pbf = torch.where(xlen.view(1, -1) > 0, pf / xlen.clamp_min(1e-30).view(1, -1), torch.zeros_like(pf))
+        return (lf.view(-1, 1) <= pbf) & (pbf <= uf.view(-1, 1))
+    if isinstance(strategy, INCR):
+        D = Q.shape[1]
+        d = D - 1 if reference_quirks else D  # the reference skips the last coordinate
+        nf = min(strategy.num_focus_coordinates, d)
+        F = torch.argsort(-(Q[:, :d] * Q[:, :d]), dim=1, stable=True)[:, :nf]
+        M = torch.zeros_like(Q).scatter_(1, F, 1.0)  # focus-set mask per query
+        QF = Q * M
+        q_mF_sqr = qlen * qlen - (QF * QF).sum(1)
+        qFpF = QF @ X.t()                        # [B, n]
+        pF_sqr = M @ (X * X).t()                 # [B, n]
+        ub = theta.view(-1, 1) - qFpF
+        return (ub < 0) | (q_mF_sqr.view(-1, 1) * ((xlen * xlen).view(1, -1) - pF_sqr) >= ub * ub)
+    raise ValueError(f"unknown LEMP strategy {strategy!r}")
+
+
+class PrunedLempTopK(LempTopK):
+    """``LempTopK`` whose buckets are filtered by a LEMP strategy's candidate mask
+    before the merge (statistics in ``pruned`` / ``scored``)."""
+
+    def __init__(self, item_ids, item_vecs, bucket_size: int = 4096, strategy=None, reference_quirks=False):
+        super().__init__(item_ids, item_vecs, bucket_size)
+        self.strategy, self.quirks = strategy, reference_quirks
+        self.pruned = 0
+        self.scored = 0
+
+    def query(self, Q: torch.Tensor, k: int, exclude=None):
+        if self.strategy is None:
+            return super().query(Q, k)
+        Q = Q.float().contiguous()
+        B, dev = Q.shape[0], Q.device
+        qlen = torch.linalg.vector_norm(Q, dim=1)
+        best_s = torch.full((B, k), float("-inf"), device=dev)
+        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+        N = self.vecs.shape[0]
+        for s in range(0, N, self.bucket):
+            e = min(N, s + self.bucket)
+            theta = _theta(best_s)
+            full = torch.isfinite(best_s[:, -1])
+            if s > 0 and bool((full & (qlen * self.lengths[s] <= theta)).all()):
+                break
+            self.buckets_scanned += 1
+            X, xl = self.vecs[s:e], self.lengths[s:e]
+            S = ops.score_gemm(Q, X) if dev.type == "cuda" else Q @ X.t()
+            keep = lemp_candidate_mask(Q, qlen, theta, X, xl, self.strategy, self.quirks)
+            # queries already settled (reference: the bucket loop stopped) take nothing more
+            live = ~(full & (qlen * self.lengths[s] <= theta))
+            keep &= live.view(-1, 1)
+            self.scored += int(keep.sum())
+            self.pruned += int(keep.numel() - keep.sum())
+            S = torch.where(keep, S, torch.full_like(S, float("-inf")))
+            if dev.type == "cuda" and k <= ops.TOPK_MAX_K:
+                ops.topk_merge(S.contiguous(), self.ids[s:e], best_s, best_i)
+            else:
+                cs = torch.cat([best_s, S], 1)
+                ts, tj = torch.topk(cs, min(k, cs.shape[1]), dim=1)
+                ci = torch.cat([best_i, self.ids[s:e].expand(B, e - s)], 1)
+                best_s, best_i = ts, torch.gather(ci, 1, tj)
+        best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
+        return best_s, best_i
+
+
+# ------------------------------------------------------------------ merging
+def _fkey(s: torch.Tensor) -> torch.Tensor:
+    """Order-preserving float -> uint32 key (int32 storage), as ``fkey`` in topk.hip."""
+    u = s.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    k = torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    return torch.where(k >= 0x80000000, k - (1 << 32), k).to(torch.int32)
+
+
+def merge_partials(scores: torch.Tensor, ids: torch.Tensor, K: int, excluded: torch.Tensor):
+    """Merge gathered partial lists ``[B, m]`` into the best ``K`` with ``excluded``
+    entries (seen items, empty slots) removed (K13: ``ops.topk_merge_cand`` on the
+    GPU -- the kept candidates are compacted to the front of each row first)."""
+    B, m = scores.shape
+    dev = scores.device
+    if m < K:  # fewer candidates than K: pad (the list is shorter, as in the reference)
+        pad = K - m
+        scores = torch.cat([scores, torch.full((B, pad), float("-inf"), device=dev)], 1)
+        ids = torch.cat([ids, torch.full((B, pad), -1, dtype=ids.dtype, device=dev)], 1)
+        excluded = torch.cat([excluded, torch.ones((B, pad), dtype=torch.bool, device=dev)], 1)
+        m = K
+    keep = ~excluded & (ids >= 0) & torch.isfinite(scores)
+    if dev.type == "cuda" and K <= ops.TOPK_MAX_K and m <= ops.TOPK_CAND_CAP:
+        order = torch.argsort((~keep).to(torch.int8), dim=1, stable=True)  # kept candidates first
+        ck = _fkey(torch.gather(scores, 1, order))
+        ci = torch.gather(ids.long(), 1, order)
+        cnt = keep.sum(1).to(torch.int32)
+        best_s = torch.full((B, K), float("-inf"), device=dev)
+        best_i = torch.full((B, K), -1, dtype=torch.long, device=dev)
+        ops.topk_merge_cand(ck.contiguous(), ci.contiguous(), cnt, best_s, best_i)
+    else:
+        s = torch.where(keep, scores, torch.full_like(scores, float("-inf")))
+        best_s, j = torch.topk(s, min(K, m), dim=1)
+        best_i = torch.gather(ids.long(), 1, j)
+    best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
+    return best_s, best_i
+
+
+def _gather_partials(comm: Comm, s: torch.Tensor, i: torch.Tensor):
+    if comm.world == 1:
+        return s, i
+    return torch.cat(comm.all_gather(s.contiguous()), 1), torch.cat(comm.all_gather(i.contiguous()), 1)
+
+
+def as_reference_records(outputs) -> List[tuple]:
+    """Rank 0's tensor outputs -> the reference's ``(user, item, ts, [(score, item)])``
+    records (``CollectTopKFromEachWorker`` output order)."""
+    recs = []
+    for e in outputs:
+        if not isinstance(e, Left) or not isinstance(e.value, tuple) or len(e.value) != 3:
+            continue
+        (u, it, ts), S, I = e.value
+        S, I = S.cpu().tolist(), I.cpu().tolist()
+        for b, (uu, ii, tt) in enumerate(zip(u.tolist(), it.tolist(), ts.tolist())):
+            recs.append((uu, ii, tt, [(float(x), int(y)) for x, y in zip(S[b], I[b]) if y >= 0]))
+    return recs
+
+
+class _TopKServing:
+    """Shared query path: partial LEMP top-K on the local items, gather, seen-aware merge."""
+
+    def _serve(self, Q, valid, users, items, ts, ps):
+        with stage("topk.score", None):
+            if self.index is not None and self.index.vecs.shape[0] > 0:
+                s, i = self.index.query(Q, self.worker_k)
+            else:
+                s = torch.full((Q.shape[0], self.worker_k), float("-inf"), device=Q.device)
+                i = torch.full((Q.shape[0], self.worker_k), -1, dtype=torch.long, device=Q.device)
+            s = torch.where(valid.view(-1, 1), s, torch.full_like(s, float("-inf")))
+            i = torch.where(valid.view(-1, 1), i, torch.full_like(i, -1))
+        with stage("topk.merge", None):
+            ss, ii = _gather_partials(self.comm, s, i)
+            rnd = occurrence_rounds(users)
+            best_s = torch.empty((users.numel(), self.K), device=Q.device)
+            best_i = torch.empty((users.numel(), self.K), dtype=torch.long, device=Q.device)
+            for r in range(int(rnd.max()) + 1 if rnd.numel() else 0):
+                sel = torch.nonzero(rnd == r).flatten()
+                exc = self.seen.contains(users[sel], ii[sel])
+                bs, bi = merge_partials(ss[sel], ii[sel], self.K, exc)
+                best_s[sel], best_i[sel] = bs, bi
+                self.seen.add(users[sel], items[sel])  # the rated item counts as seen afterwards
+        if self.rank == 0:  # the merge of the reference runs at parallelism 1
+            ps.output(((users, items, ts), best_s, best_i))
+
+
+class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
+    """``PSTopKGeneratorWorker`` + the gather/merge; batches are ``(user, item, ts)``
+    tensors, identical on every rank (broadcast input)."""
+
+    pushes = False
+
+    def __init__(self, K: int = 100, worker_k: int = 75, memory: int = 0, bucket_size: int = 4096, pruning=None,
+                 reference_quirks: bool = False):
+        self.K, self.worker_k, self.memory = K, worker_k, memory
+        self.bucket_size, self.pruning, self.quirks = bucket_size, pruning, reference_quirks
+        self._ids: List[torch.Tensor] = []
+        self._vecs: List[torch.Tensor] = []
+        self.index = None
+
+    def open(self, ctx):
+        self.rank, self.device = ctx.rank, torch.device(ctx.device)
+        self.comm = Comm(device=self.device)
+        self.seen = SeenStore(self.memory, self.device)
+
+    def update_model_batch(self, ids, values):
+        """Worker-resident items ``(id, [vec..., len])`` or ``(id, vec)``."""
+        self._ids.append(ids.to(self.device).long())
+        self._vecs.append(values.to(self.device).float())
+        self.index = None
+
+    def _build(self, D):
+        if self.index is None and self._ids:
+            ids, vecs = torch.cat(self._ids), torch.cat(self._vecs)
+            if vecs.shape[1] == D + 1:
+                vecs = vecs[:, :D]
+            self.index = PrunedLempTopK(ids, vecs, self.bucket_size, self.pruning, self.quirks)
+
+    def on_recv_batch(self, batch, ps):
+        users, items, ts = (t.to(self.device) for t in batch)
+        ps.pull(users, (users, items, ts))
+
+    def on_pull_recv_batch(self, pulled, ps):
+        users, items, ts = pulled.payload
+        rows = pulled.values()
+        D = rows.shape[1] - 1
+        valid = rows[:, D] >= 0  # (len, vec) stores; len -1 = invalid (never loaded)
+        self._build(D)
+        self._serve(rows[:, :D].contiguous(), valid, users, items, ts, ps)
+
+
+def ps_top_k_generator_tensor(queries: Iterable, ps_model, worker_model, num_users: int, num_factors: int = 10,
+                              user_memory: int = 0, K: int = 100, worker_k: int = 75, bucket_size: int = 4096,
+                              pruning_algorithm=None, comm: Optional[Comm] = None, reference_quirks: bool = False):
+    """``psTopKGenerator`` on the tensor engine (this rank's part of the job).
+
+    ``queries``: the broadcast ``(user, item, ts)`` micro-batches (the same on every
+    rank); ``ps_model``: this rank's ``(user, [vec..., len])`` records (``Left``);
+    ``worker_model``: this rank's ``(item, [vec..., len])`` records (``Right``).
+    Returns rank 0's ``Left(((user, item, ts), scores [B, K], items [B, K]))``."""
+    worker = TopKQueryWorker(K, worker_k, user_memory, bucket_size, pruning_algorithm, reference_quirks)
+    logic = DeviceSimplePSLogic(num_users, num_factors + 1, op="set", init=("const", -1.0), track_touched=False)
+    logic.emit = "none"
+    rt = TensorRuntime(comm, staleness=0)
+    return rt.execute(queries, worker, logic, model=ps_model, worker_model=worker_model)
+
+
+class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
+    """``PSOnlineMatrixFactorizationAndTopKGeneratorWorker`` on device tensors.
+
+    Item ``i`` lives on rank ``i % W`` (local row ``i // W``), initialised on first
+    use by its owner (deterministic hash init by id, so the value does not depend
+    on when it is first touched).  Per micro-batch: serve top-K for every rating
+    (current items), then the owned ratings' SGD: negatives drawn among this
+    rank's initialised items (<= 32 rejections against the user's recent items on
+    this rank), item rows updated in place, the summed user delta pushed."""
+
+    def __init__(self, num_items: int, num_factors: int, learning_rate: float, K: int = 100, worker_k: int = 75,
+                 memory: int = 65535, negative_sample_rate: int = 0, bucket_size: int = 4096, pruning=None,
+                 range_min: float = -0.001, range_max: float = 0.001, seed: int = 0, neg_memory: int = 128,
+                 reference_quirks: bool = False):
+        self.num_items, self.dim, self.lr = int(num_items), int(num_factors), learning_rate
+        self.K, self.worker_k, self.memory = K, worker_k, memory
+        self.neg_rate, self.bucket_size, self.pruning, self.quirks = negative_sample_rate, bucket_size, pruning, \
+            reference_quirks
+        self.range, self.seed, self.neg_memory = (range_min, range_max), seed, int(neg_memory)
+
+    def open(self, ctx):
+        from ...parallel.table import ShardedTable
+
+        self.W, self.rank, self.device = ctx.world_size, ctx.rank, torch.device(ctx.device)
+        self.comm = Comm(device=self.device)
+        self.seen = SeenStore(self.memory, self.device)
+        self.items = ShardedTable(self.num_items, self.dim, self.rank, self.W, "hash",
+                                  ("uniform", self.range[0], self.range[1]), (self.seed ^ USER_SEED_XOR) & 0xFFFFFFFF,
+                                  self.device, track_touched=False)
+        self.valid = torch.zeros(self.items.n_local, dtype=torch.bool, device=self.device)
+        self.index = None
+        if self.neg_rate > 0:
+            n_u = 1 << 20  # per-user rings are keyed by user id modulo this (bounded state)
+            self._ring_users = n_u
+            self._ring = torch.full((n_u * self.neg_memory,), -1, dtype=torch.int32, device=self.device)
+            self._ring_cur = torch.zeros(n_u, dtype=torch.int32, device=self.device)
+            self._known_flag = torch.zeros(self.num_items, dtype=torch.int32, device=self.device)
+            self._known = torch.zeros(self.num_items, dtype=torch.int32, device=self.device)
+            self._known_cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._neg_counter = 0
+
+    def on_recv_batch(self, batch, ps):
+        users, items, ts, rating = (t.to(self.device) for t in batch)
+        ps.pull(users, (users, items, ts, rating.float()))
+
+    def _rebuild_index(self):
+        loc = torch.nonzero(self.valid).flatten()
+        ids = self.items.global_ids(loc)
+        self.index = PrunedLempTopK(ids, self.items.weight[loc], self.bucket_size, self.pruning, self.quirks) \
+            if loc.numel() else None
+
+    def on_pull_recv_batch(self, pulled, ps):
+        users, items, ts, rating = pulled.payload
+        U = pulled.values()  # [B, D] user vectors (length recomputed on the worker)
+        self._rebuild_index()
+        self._serve(U, torch.ones(users.numel(), dtype=torch.bool, device=U.device), users, items, ts, ps)
+        # learning: the owner of each rated item
+        own = (items.long() % self.W) == self.rank
+        loc = (items.long() // self.W)
+        self.valid[loc[own]] = True  # lazily initialised by the owner (hash init: any order)
+        du = torch.zeros_like(U)
+        lr = self.lr
+        if self.neg_rate > 0 and bool(own.any()):
+            ou, oi = users[own].to(torch.int32), items[own].to(torch.int32)
+            uring = (ou.long() % self._ring_users).to(torch.int32)
+            ops.ring_push(self._ring, self._ring_cur, uring, oi, self.neg_memory)
+            ops.known_append(self._known_flag, self._known, self._known_cnt, oi)
+            negs = ops.sample_uniform_reject(ou.numel(), self.neg_rate, self.num_items, oi, uring, self._ring,
+                                             self.neg_memory, seed=self.seed + 7 * self.rank,
+                                             counter=self._neg_counter, device=self.device, known=self._known,
+                                             known_count=self._known_cnt).view(-1, self.neg_rate)
+            self._neg_counter += 1
+            rows_own = torch.nonzero(own).flatten()
+            for j in range(self.neg_rate):  # reference order: negatives first, then the rating
+                ng = negs[:, j].long()
+                ok = ng >= 0
+                if not bool(ok.any()):
+                    continue
+                b = rows_own[ok]
+                nl = ng[ok] // self.W
+                iv = self.items.weight[nl]
+                e = 0.0 - (U[b] * iv).sum(1)
+                du.index_add_(0, b, lr * e.view(-1, 1) * iv)
+                self.items.weight.index_add_(0, nl, lr * e.view(-1, 1) * U[b])
+        if bool(own.any()):
+            b = torch.nonzero(own).flatten()
+            il = loc[own]
+            iv = self.items.weight[il]
+            e = rating[own] - (U[b] * iv).sum(1)
+            du.index_add_(0, b, lr * e.view(-1, 1) * iv)
+            self.items.weight.index_add_(0, il, lr * e.view(-1, 1) * U[b])
+        ps.push(du, mask=own)
+
+
+def ps_online_learner_and_generator_tensor(batches: Iterable, num_users: int, num_items: int, num_factors: int = 10,
+                                           range_min: float = -0.001, range_max: float = 0.001,
+                                           learning_rate: float = 0.01, negative_sample_rate: int = 0,
+                                           user_memory: int = 65535, K: int = 100, worker_k: int = 75,
+                                           bucket_size: int = 4096, pruning_algorithm=None, seed: int = 0,
+                                           comm: Optional[Comm] = None, output_sink=None):
+    """``psOnlineLearnerAndGenerator`` on the tensor engine (this rank's part):
+    ``batches`` = the broadcast ``(user, item, ts, rating)`` micro-batches (same on
+    every rank).  Outputs: rank 0's top-K records (``Left``) and every rank's PS
+    user updates ``Right((users, vectors))`` (``SimplePSLogic`` emits on push)."""
+    worker = OnlineMFTopKWorker(num_items, num_factors, learning_rate, K, worker_k, user_memory,
+                                negative_sample_rate, bucket_size, pruning_algorithm, range_min, range_max, seed)
+    logic = DeviceSimplePSLogic(num_users, num_factors, op="add_renorm", init=("uniform", range_min, range_max),
+                                seed=seed)
+    rt = TensorRuntime(comm, staleness=0, output_sink=output_sink)
+    return rt.execute(batches, worker, logic)

@@ -8,7 +8,7 @@ fallback on a GPU box).
 from __future__ import annotations
 
 import os
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 
@@ -362,6 +362,45 @@ def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
     return r if kt(r) <= TILE_MAX_BUCKETS and r <= 256 else None
 
 
+class TileLayout(NamedTuple):
+    """Output layout of the level-4 (capacity slot) tile partition: tile ``k``'s
+    records are ``rec[ptr[k] : ptr[k] + min(cnt[k], ptr[k+1] - ptr[k])]``; records
+    past a slot's capacity are in ``ovf[:ovf_cnt]`` ({uid, row in block, rating
+    bits, bucket}, int32 ``[n, 4]``), run by ``mf_sgd_tiled`` after the tiles."""
+
+    ptr: torch.Tensor
+    cnt: torch.Tensor
+    ovf: torch.Tensor
+    ovf_cnt: torch.Tensor
+
+    def compact(self, rec, T: int, R: int):
+        """(ptr[KT+1], uid, row-in-block, rating) grouped by bucket, overflow
+        records included -- the layout of levels 1-3 (tests / debugging; syncs)."""
+        ptr, cnt = self.ptr.long().cpu(), self.cnt.long().cpu()
+        take = torch.minimum(cnt, ptr[1:] - ptr[:-1])
+        KT = cnt.numel()
+        bucket = torch.repeat_interleave(torch.arange(KT), take)
+        first = torch.cumsum(take, 0) - take
+        idx = torch.repeat_interleave(ptr[:-1], take) + torch.arange(int(take.sum())) - \
+            torch.repeat_interleave(first, take)
+        x = rec.cpu()[idx]
+        if x.shape[1] == 2:
+            u = x[:, 0] & 0xFFFFFF
+            row = (bucket % T) * R + ((x[:, 0].long() >> 24) & 0xFF)
+            rt = x[:, 1].contiguous().view(torch.float32)
+        else:
+            u, row, rt = x[:, 0], x[:, 1].long(), x[:, 2].contiguous().view(torch.float32)
+        o = self.ovf[: int(self.ovf_cnt.item())].cpu()
+        b_all = torch.cat([bucket, o[:, 3].long()])
+        order = torch.argsort(b_all, stable=True)
+        u = torch.cat([u.to(torch.int32), o[:, 0]])[order]
+        row = torch.cat([row.to(torch.int32), o[:, 1]])[order]
+        rt = torch.cat([rt, o[:, 2].contiguous().view(torch.float32)])[order]
+        p = torch.zeros(KT + 1, dtype=torch.int32)
+        p[1:] = torch.cumsum(torch.bincount(b_all, minlength=KT), 0).to(torch.int32)
+        return p, u, row, rt
+
+
 class TilePartitioner:
     """Buckets a micro-batch's ratings by (user phase, item block, tile of ``R``
     rows) for ``mf_sgd_tiled`` (``mf_tiled.hip``): a few kernels, nothing
@@ -388,13 +427,17 @@ class TilePartitioner:
         # 1 = single level (per-workgroup histograms of every bucket + column scan);
         # 2 = two-level (coarse key, then bucket; atomic range reservations, no
         # histogram matrix); 3 (default) = two-level with LDS-sorted batches, so
-        # consecutive lanes store consecutive records of one output run.  Levels
-        # 1 / 2 measured 1.66 / 1.83 ms at 64M ratings, KT = 3.9k buckets
-        # (profiles/r1_mf_partition_levels.md).
+        # consecutive lanes store consecutive records of one output run; 4 = level
+        # 3's scatters into capacity slots sized from the previous run's counts, no
+        # counting pass (returns a ``TileLayout``).  Levels 1 / 2 measured 1.66 /
+        # 1.83 ms at 64M ratings, KT = 3.9k buckets (profiles/r1_mf_partition_levels.md);
+        # level 4's scatters ran 627 + 474 us against level 3's 200 + 406 + 430 us
+        # (128 contended coarse cursors), 3 % slower end to end (profiles/r2_tp4.md).
         env = os.environ.get("FPS_TILE_PARTITION_LEVELS")
         self.levels = int(levels or env or 3)
-        if self.levels not in (1, 2, 3):
-            raise ValueError(f"tile partition levels must be 1, 2 or 3, not {self.levels}")
+        if self.levels not in (1, 2, 3, 4):
+            raise ValueError(f"tile partition levels must be 1, 2, 3 or 4, not {self.levels}")
+        self.n_prev = 0
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
@@ -412,6 +455,8 @@ class TilePartitioner:
             return ptr, (u, row, r)
         lib = N.require()
         n = uid.numel()
+        if self.levels == 4:
+            return self._run4(lib, uid, iid, rating, seen)
         G = lib.fps_tile_partition_groups(n)
         if self.levels == 1 and G * self.KT > self.g_cap:
             self.g_cap = G * self.KT
@@ -437,6 +482,33 @@ class TilePartitioner:
                                        int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]
 
+    def _run4(self, lib, uid, iid, rating, seen):
+        n = uid.numel()
+        if not hasattr(self, "ws4"):
+            dev = self.device
+            self.ws4 = torch.zeros(lib.fps_tile_partition4_ws_ints(self.W, self.T, self.P), dtype=torch.int32,
+                                   device=dev)
+            self.bstart = torch.zeros(self.KT + 1, dtype=torch.int32, device=dev)
+            self.bcursor = torch.zeros(self.KT, dtype=torch.int32, device=dev)
+            self.ovf_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.cap4 = 0
+        if n > self.cap4:
+            self.cap4 = max(n, int(self.cap4 * 1.25))
+            NC = (self.ws4.numel() - 2) // 3
+            self.tmp4 = torch.empty((lib.fps_tile_partition4_cap(self.cap4, NC), 3 if self.rec8 else 4),
+                                    dtype=torch.int32, device=self.device)
+            self.rec = torch.empty((lib.fps_tile_partition4_cap(self.cap4, self.KT), self.rec_cols),
+                                   dtype=torch.int32, device=self.device)
+            self.ovf = torch.empty((self.cap4, 4), dtype=torch.int32, device=self.device)
+        N.check(lib.fps_tile_partition4(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.n_prev,
+                                        self.W, self.half.data_ptr(), self.R, self.T, self.P, self.upp,
+                                        self.ws4.data_ptr(), self.tmp4.data_ptr(), self.bstart.data_ptr(),
+                                        self.bcursor.data_ptr(), self.rec.data_ptr(), int(self.rec8),
+                                        self.ovf.data_ptr(), self.ovf_cnt.data_ptr(), N.ptr(seen),
+                                        N.stream_ptr(self.device)), "tile_partition4")
+        self.n_prev = n
+        return TileLayout(self.bstart, self.bcursor, self.ovf, self.ovf_cnt), self.rec
+
     @staticmethod
     def device_is_cuda(device) -> bool:
         return torch.device(device).type == "cuda"
@@ -446,6 +518,8 @@ class TilePartitioner:
         8-B records need ``ptr`` to recover the tile of every record."""
         if isinstance(rec, tuple):
             return rec
+        if isinstance(ptr, TileLayout):
+            return ptr.compact(rec, self.T, self.R)[1:]
         if rec.shape[1] == 4:
             return rec[:, 0], rec[:, 1], rec[:, 2].contiguous().view(torch.float32)
         x = rec[:, 0]
@@ -457,10 +531,26 @@ class TilePartitioner:
         return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
+def _tiled_launch(lib, U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float, nblk: int):
+    """Tiled SGD launch over ``nblk`` consecutive item blocks from a ``TileLayout``
+    (slot starts + counts), then the flat kernel over their overflow records."""
+    s = N.stream_ptr(U.device)
+    off = 4 * block * T
+    N.check(lib.fps_mf_sgd_tiled3(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(), int(rec.shape[1] == 2),
+                                  ptr.ptr.data_ptr() + off, ptr.cnt.data_ptr() + off, T, tile_rows, I0.shape[0],
+                                  _c(I1).data_ptr(), I1.shape[0], nblk, U.shape[1], lr, lam, s), "mf_sgd_tiled3")
+    N.check(lib.fps_mf_sgd_ovf(U.data_ptr(), I0.data_ptr(), I1.data_ptr(), ptr.ovf.data_ptr(), ptr.ovf_cnt.data_ptr(),
+                               block * T, T, nblk, U.shape[1], lr, lam, s), "mf_sgd_ovf")
+
+
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
     records from ``TilePartitioner``): one workgroup per tile, every item row owned
-    by one lane group (registers), item deltas summed per row -- no item atomics."""
+    by one lane group (registers), item deltas summed per row -- no item atomics.
+    ``ptr`` may be a ``TileLayout`` (level-4 partition)."""
+    if isinstance(ptr, TileLayout):
+        _tiled_launch(N.require(), U, I_block, I_block, rec, ptr, block, T, tile_rows, lr, lam, 1)
+        return
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
@@ -476,6 +566,9 @@ def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, l
     """``mf_sgd_tiled`` of item blocks ``block`` (rows ``I0``) and ``block + 1`` (rows ``I1``)
     in one launch of 2T workgroups: the blocks share no item row, so they need no
     ordering, and one launch instead of two halves the tail of partly filled waves."""
+    if isinstance(ptr, TileLayout):
+        _tiled_launch(N.require(), U, I0, I1, rec, ptr, block, T, tile_rows, lr, lam, 2)
+        return
     if _on_gpu(U):
         lib = N.require()
         N.check(lib.fps_mf_sgd_tiled2(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),

