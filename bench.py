@@ -102,6 +102,8 @@ def main(argv=None):
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     ap.add_argument("--sgd-high-priority", action="store_true",
                     help="tiled SGD with prefetch: run the SGD on a priority -1 stream (A/B knob, off by default)")
+    ap.add_argument("--watchdog-s", type=float, default=0.0,
+                    help="fail fast: end this rank (exit 17) when a step makes no progress for this long (0 = off)")
     ap.add_argument("--metrics-jsonl", default=None,
                     help="append per-step stage timings (HIP events) and counters of rank 0 to this JSON-lines file")
     a = ap.parse_args(argv)
@@ -135,10 +137,17 @@ def main(argv=None):
         from flink_parameter_server_1_amd.utils.metrics import StageTimer
 
         timer = StageTimer(device=dev.type == "cuda")
+    wd = None
+    if a.watchdog_s > 0:
+        from flink_parameter_server_1_amd.utils.watchdog import Watchdog
+
+        wd = Watchdog(a.watchdog_s, name=f"bench rank {comm.rank}").start()
     step = 0
     for _ in range(a.warmup):
         model.step(*data.batch(step, a.batch))
         step += 1
+        if wd is not None:
+            wd.beat(step)
     model.flush()
     comm.barrier()
     sync()
@@ -147,6 +156,8 @@ def main(argv=None):
     for _ in range(a.steps):
         model.step(*data.batch(step, a.batch))
         step += 1
+        if wd is not None:
+            wd.beat(step)
         if timer is not None:
             timer.step_end()
     model.flush()  # the last micro-batch's SGD + push run inside the timed region
@@ -210,6 +221,8 @@ def main(argv=None):
                 w.write(kind="step", step=i, stage_ms=st)
             w.write(kind="summary", ms_per_step=dt_max / a.steps * 1e3, counters=model.metrics(), n_gpus=n)
             w.close()
+    if wd is not None:
+        wd.stop()
     if n > 1:
         dist.destroy_process_group()
 

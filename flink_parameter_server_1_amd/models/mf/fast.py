@@ -394,6 +394,25 @@ class DistributedMF:
         if self.pipeline:
             self._pipe.drain()
 
+    # -------------------------------------------------------------- checkpoint
+    _AUX = ("_ring", "_ring_cursor", "_known_flag", "_known", "_known_count")
+
+    def aux_state(self) -> dict:
+        """Per-rank state besides the tables (``utils.io.Checkpointer``): the
+        negative-sampling RNG counter and rings, the update count."""
+        st = {"updates": self.updates}
+        if self.cfg.negative_sample_rate > 0:
+            st["neg_counter"] = self._neg_counter
+            st.update({k: getattr(self, k) for k in self._AUX})
+        return st
+
+    def load_aux_state(self, st: dict) -> None:
+        self.updates = int(st.get("updates", 0))
+        if self.cfg.negative_sample_rate > 0:
+            self._neg_counter = int(st["neg_counter"])
+            for k in self._AUX:
+                getattr(self, k).copy_(st[k])
+
     def set_timer(self, timer) -> None:
         """Attach a ``utils.metrics.StageTimer`` to the model and its PS."""
         self.timer = timer

@@ -48,8 +48,12 @@ class Comm:
 
     # ------------------------------------------------------------- set-up
     @staticmethod
-    def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> "Comm":
-        """Initialise the default group from torchrun env vars (or world=1)."""
+    def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> "Comm":
+        """Initialise the default group from torchrun env vars (or world=1).
+        ``timeout_s`` (default ``FPS_PG_TIMEOUT_S`` or 600): collective timeout;
+        pair with ``utils.watchdog.Watchdog`` to fail faster than that."""
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("FPS_PG_TIMEOUT_S", "600"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))

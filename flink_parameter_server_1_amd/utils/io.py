@@ -140,7 +140,9 @@ def synthetic_ratings_host(n: int, n_local_users: int, n_items: int, seed: int =
 def save_snapshot(path: str, ids: torch.Tensor, values: torch.Tensor, *, part_kind: int, num_ids: int, world: int,
                   rank: int, step: int = 0) -> None:
     ids_np = np.ascontiguousarray(ids.detach().to("cpu", torch.int64).numpy())
-    vals_np = np.ascontiguousarray(values.detach().to("cpu", torch.float32).numpy()).reshape(ids_np.size, -1)
+    v = values.detach().to("cpu", torch.float32)
+    width = v.shape[-1] if v.dim() > 1 else (v.numel() // max(ids_np.size, 1) if ids_np.size else 1)
+    vals_np = np.ascontiguousarray(v.reshape(ids_np.size, width).numpy())
     L = NH.lib()
     if L is not None:
         rc = L.fps_write_snapshot(path.encode(), part_kind, num_ids, vals_np.shape[1], world, rank, step,
@@ -172,40 +174,124 @@ def load_snapshot(path: str):
 
 
 def save_table(table, path: str, step: int = 0, only_touched: bool = False) -> None:
+    """Shard snapshot of a ``ShardedTable``: the rows, plus -- next to it -- the
+    optimizer state (Adagrad accumulators / add_renorm lengths: ``<path>.state``)
+    and the touched flags (``<path>.touched``), so a resumed run applies the same
+    update rule to the same state and dumps the same touched rows."""
     ids, vals = table.dump(only_touched)
     save_snapshot(path, ids, vals, part_kind=table.part_kind, num_ids=table.num_ids, world=table.world,
                   rank=table.rank, step=step)
+    loc = table.local_of(ids.to(table.device)) if ids.numel() else ids.long()
+    if table.state is not None:
+        st = table.state[loc.long()].reshape(ids.numel(), -1)
+        save_snapshot(path + ".state", ids, st, part_kind=table.part_kind, num_ids=table.num_ids, world=table.world,
+                      rank=table.rank, step=step)
+    if table.touched is not None:
+        t = torch.nonzero(table.touched, as_tuple=False).flatten()
+        tid = table.global_ids(t)
+        save_snapshot(path + ".touched", tid, torch.ones(tid.numel(), 1), part_kind=table.part_kind,
+                      num_ids=table.num_ids, world=table.world, rank=table.rank, step=step)
+
+
+def _shard_file_coords(path: str):
+    """(rank, world) of a ``<name>.shard<r>-of-<w>.bin`` file, or None."""
+    import re
+
+    m = re.search(r"\.shard(\d+)-of-(\d+)\.bin$", path)
+    return (int(m.group(1)), int(m.group(2))) if m else None
+
+
+def shard_files_for(table, files: List[str]) -> List[str]:
+    """The shard files that can hold ids this rank owns: with hash partitioning a
+    file of shard ``r`` of ``W`` (ids ``= r mod W``) overlaps shard ``r'`` of ``W'``
+    iff ``r = r' (mod gcd(W, W'))`` -- only its own file when the world size is
+    unchanged; with range partitioning the id ranges are intersected.  Lookup
+    (custom) partitioning and unnamed files: every file."""
+    from math import gcd
+
+    out = []
+    for f in files:
+        c = _shard_file_coords(f)
+        if c is None or table.partition == "lookup":
+            out.append(f)
+            continue
+        r, w = c
+        if table.partition == "hash":
+            if (r - table.rank) % gcd(w, table.world) == 0:
+                out.append(f)
+        else:
+            blk = -(-table.num_ids // w)
+            lo, hi = r * blk, min(table.num_ids, (r + 1) * blk) if r < w - 1 else table.num_ids
+            mlo = table.rank * table.block
+            mhi = table.num_ids if table.rank == table.world - 1 else min(table.num_ids, mlo + table.block)
+            if lo < mhi and mlo < hi:
+                out.append(f)
+    return out
+
+
+#: bytes of snapshot files read by ``restore_table`` in this process (restore-IO tests)
+RESTORE_BYTES = {"bytes": 0}
 
 
 def restore_table(table, pattern: str) -> int:
-    """Load every shard file matching ``pattern`` and keep this rank's ids (re-sharding)."""
+    """Restore this rank's rows (and optimizer state / touched flags) from the
+    shard files matching ``pattern``; re-shards to the current world size, and
+    reads only the files that can hold ids of this rank (``shard_files_for``)."""
     n = 0
-    for f in sorted(glob.glob(pattern)):
+    files = [f for f in sorted(glob.glob(pattern)) if not f.endswith((".state", ".touched"))]
+    for f in shard_files_for(table, files):
+        RESTORE_BYTES["bytes"] += os.path.getsize(f)
         _, ids, vals = load_snapshot(f)
-        if ids.size:
-            table.load(torch.from_numpy(ids), torch.from_numpy(vals))
-            n += int((table.part.shard_tensor(torch.from_numpy(ids)) == table.rank).sum())
+        if not ids.size:
+            continue
+        ids_t = torch.from_numpy(ids)
+        mine = table.part.shard_tensor(ids_t) == table.rank
+        table.load(ids_t, torch.from_numpy(vals))
+        n += int(mine.sum())
+        if table.touched is not None and os.path.exists(f + ".touched"):
+            loc = table.local_of(ids_t[mine].to(table.device))  # load() marked them: the saved flags decide
+            table.touched[loc] = 0
+        if table.state is not None and os.path.exists(f + ".state"):
+            RESTORE_BYTES["bytes"] += os.path.getsize(f + ".state")
+            _, sid, sv = load_snapshot(f + ".state")
+            sid_t = torch.from_numpy(sid)
+            m2 = table.part.shard_tensor(sid_t) == table.rank
+            loc = table.local_of(sid_t[m2].to(table.device)).long()
+            table.state[loc] = torch.from_numpy(sv)[m2].to(table.state.device).reshape(
+                (loc.numel(),) + tuple(table.state.shape[1:]))
+        if table.touched is not None and os.path.exists(f + ".touched"):
+            RESTORE_BYTES["bytes"] += os.path.getsize(f + ".touched")
+            _, tid, _ = load_snapshot(f + ".touched")
+            tid_t = torch.from_numpy(tid)
+            m3 = table.part.shard_tensor(tid_t) == table.rank
+            table.touched[table.local_of(tid_t[m3].to(table.device)).long()] = 1
     return n
 
 
 class Checkpointer:
-    """Periodic snapshots of named ``ShardedTable``s.
+    """Periodic snapshots of named ``ShardedTable``s (+ optimizer state + touched
+    flags) and of per-rank auxiliary state (RNG counters, negative-sampling rings,
+    the data cursor: ``aux_state() -> {name: tensor or number}`` /
+    ``load_aux_state(dict)``).
 
-    Layout: ``<dir>/step_<k>/<name>.shard<rank>-of-<world>.bin`` + ``manifest.json``
-    written by rank 0 after a barrier (the snapshot is complete when the
-    manifest exists).  ``restore_latest`` re-shards to the current world size.
-    ``before_save`` (e.g. ``DistributedMF.flush``) runs first, so in-flight
-    pushes land and rotating item blocks are back in their shards.
+    Layout: ``<dir>/step_<k>/<name>.shard<rank>-of-<world>.bin`` (+ ``.state``,
+    ``.touched``), ``aux.rank<r>-of-<w>.pt`` and ``manifest.json`` written by rank
+    0 after a barrier (the snapshot is complete when the manifest exists).
+    ``restore_latest`` re-shards to the current world size, reading only the
+    shard files that can hold this rank's ids; aux state is restored when the
+    world size is unchanged.  ``before_save`` (e.g. ``DistributedMF.flush``) runs
+    first, so in-flight pushes land and rotating item blocks are back home.
     """
 
     def __init__(self, directory: str, tables: Dict[str, object], comm=None, every_steps: int = 0, keep: int = 2,
-                 before_save=None):
+                 before_save=None, aux=None):
         self.before_save = before_save
         self.dir = directory
         self.tables = tables
         self.comm = comm
         self.every = every_steps
         self.keep = keep
+        self.aux = aux  # object with aux_state() / load_aux_state(d)
         os.makedirs(directory, exist_ok=True)
 
     def _rank_world(self):
@@ -227,6 +313,11 @@ class Checkpointer:
         os.makedirs(d, exist_ok=True)
         for name, t in self.tables.items():
             save_table(t, os.path.join(d, f"{name}.shard{rank}-of-{world}.bin"), step)
+        if self.aux is not None:
+            st = {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in self.aux.aux_state().items()}
+            tmp = os.path.join(d, f"aux.rank{rank}-of-{world}.pt.tmp")
+            torch.save(st, tmp)
+            os.replace(tmp, tmp[:-4])
         if self.comm is not None:
             self.comm.barrier()
         if rank == 0:
@@ -261,4 +352,8 @@ class Checkpointer:
             manifest = json.load(f)
         for name, t in self.tables.items():
             restore_table(t, os.path.join(d, f"{name}.shard*-of-*.bin"))
+        rank, world = self._rank_world()
+        aux_path = os.path.join(d, f"aux.rank{rank}-of-{world}.pt")
+        if self.aux is not None and os.path.exists(aux_path) and manifest.get("world") == world:
+            self.aux.load_aux_state(torch.load(aux_path, weights_only=True))
         return manifest

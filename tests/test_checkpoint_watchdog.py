@@ -1,0 +1,172 @@
+"""Faithful checkpoint / resume (optimizer state, touched flags, aux state),
+restore reading only the overlapping shard files, and the fail-fast watchdog."""
+import os
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+import torch
+
+from dist_utils import free_port, run_ranks
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _pairs_job(rank, world, ckpt_dir, resume, stop_at):
+    from flink_parameter_server_1_amd.models.emb.pairs import (DistributedPairEmbedding, PairEmbeddingConfig,
+                                                               synthetic_pairs)
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.utils.io import Checkpointer
+
+    comm = Comm()
+    cfg = PairEmbeddingConfig(num_ids=3000, dim=8, learning_rate=0.1, optimizer="adagrad", staleness=1,
+                              init_scale=0.5)
+    m = DistributedPairEmbedding(cfg, comm, track_touched=True)
+    ck = Checkpointer(ckpt_dir, {"emb": m.table}, comm, every_steps=4, before_save=m.flush)
+    start = ck.restore_latest()["step"] if resume else 0
+    for s in range(start, stop_at):
+        m.step(*synthetic_pairs(cfg.num_ids, 500, seed=rank, step=s, zipf=1.0))
+        ck.maybe_save(s + 1)
+    m.flush()
+    return m.table.weight.clone(), m.table.state.clone(), m.table.touched.clone(), start
+
+
+def test_adagrad_resume_is_bit_identical(tmp_path):
+    """Adagrad accumulators and touched flags are part of the snapshot: a run
+    killed after its step-8 snapshot and resumed ends bit-identical."""
+    full = run_ranks(_pairs_job, 2, str(tmp_path / "full"), False, 12)
+    d = str(tmp_path / "ck")
+    run_ranks(_pairs_job, 2, d, False, 10)
+    resumed = run_ranks(_pairs_job, 2, d, True, 12)
+    for a, b in zip(full, resumed):
+        assert b[3] == 8
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
+def _save_tables(rank, world, d):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.parallel.table import ShardedTable
+    from flink_parameter_server_1_amd.utils.io import Checkpointer
+
+    comm = Comm()
+    t = ShardedTable(40_000, 16, rank, world, "hash", ("uniform", -1.0, 1.0), seed=3)
+    r = ShardedTable(40_000, 16, rank, world, "range", ("uniform", -1.0, 1.0), seed=4)
+    Checkpointer(d, {"h": t, "r": r}, comm).save(1)
+    return None
+
+
+def _restore_tables(rank, world, d):
+    from flink_parameter_server_1_amd.ops import reference as R
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.parallel.table import ShardedTable
+    from flink_parameter_server_1_amd.utils import io
+
+    comm = Comm()
+    out = {}
+    for name, part, seed in (("h", "hash", 3), ("r", "range", 4)):
+        t = ShardedTable(40_000, 16, rank, world, part, ("zeros",), seed=0)
+        io.RESTORE_BYTES["bytes"] = 0
+        n = io.restore_table(t, os.path.join(d, "step_000000001", f"{name}.shard*-of-*.bin"))
+        ids = t.global_ids(torch.arange(t.n_local))
+        exp = R.init_values(ids, 16, -1.0, 1.0, seed)
+        assert n == t.n_local and torch.allclose(t.weight, exp, atol=1e-6)
+        out[name] = io.RESTORE_BYTES["bytes"]
+    return out
+
+
+@pytest.mark.parametrize("w_save,w_load", [(4, 4), (4, 2), (2, 3)])
+def test_restore_reads_only_overlapping_shards(tmp_path, w_save, w_load):
+    d = str(tmp_path / "ck")
+    run_ranks(_save_tables, w_save, d)
+    total = {n: sum(os.path.getsize(os.path.join(d, "step_000000001", f))
+                    for f in os.listdir(os.path.join(d, "step_000000001")) if f.startswith(n + ".") and
+                    f.endswith(".bin")) for n in ("h", "r")}
+    res = run_ranks(_restore_tables, w_load, d)
+    for name in ("h", "r"):
+        per_rank = [r[name] for r in res]
+        if w_save == w_load:  # exactly its own file
+            assert all(abs(b - total[name] / w_save) < 0.05 * total[name] for b in per_rank), per_rank
+        elif w_save % w_load == 0:  # hash: files r = rank (mod w_load); range: the covered blocks
+            assert all(b <= total[name] / w_load * 1.05 for b in per_rank), per_rank
+        elif name == "r":  # range re-shard: a new range overlaps at most two old ones
+            assert sum(per_rank) <= total[name] * 2 + 4096  # + the small .touched side files
+        # (hash at coprime world sizes: every new shard draws ids from every old file)
+
+
+def _mf_neg_job(ckpt_dir, resume, stop_at):
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.utils.io import Checkpointer
+
+    cfg = MFConfig(num_users=400, num_items=250, dim=8, learning_rate=0.05, negative_sample_rate=2, user_memory=4)
+    m = DistributedMF(cfg)
+    data = SyntheticRatings(400, 250, 300 * 12, seed=5)
+    ck = Checkpointer(ckpt_dir, {"u": m.users, "i": m.items}, every_steps=3, before_save=m.flush, aux=m)
+    start = ck.restore_latest()["step"] if resume else 0
+    for s in range(start, stop_at):
+        m.step(*data.batch(s, 300))
+        ck.maybe_save(s + 1)
+    m.flush()
+    return m.U.clone(), m.I.clone(), m._neg_counter
+
+
+def test_mf_negative_sampling_resume_uses_aux_state(tmp_path):
+    """Negative-sampling rings and the RNG counter are restored: bit-identical.
+    (One intra-op thread: the CPU reference's duplicate-user row stores are
+    ordered by thread scheduling otherwise, as in the gloo tests' ranks.)"""
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        a = _mf_neg_job(str(tmp_path / "a"), False, 8)
+        d = str(tmp_path / "b")
+        _mf_neg_job(d, False, 7)
+        b = _mf_neg_job(d, True, 8)
+    finally:
+        torch.set_num_threads(nt)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and a[2] == b[2]
+
+
+WATCHDOG_SCRIPT = textwrap.dedent("""
+    import os, sys, time
+    sys.path.insert(0, {root!r})
+    import torch, torch.distributed as dist
+    from flink_parameter_server_1_amd.utils.watchdog import Watchdog
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    wd = Watchdog(2.0, name="test").start()
+    t = torch.ones(1)
+    for step in range(3):
+        dist.all_reduce(t)
+        wd.beat(step)
+    if rank == 1:
+        time.sleep(120)          # a hung peer: never joins the next collective
+    dist.all_reduce(t)           # rank 0 blocks here; its watchdog must end it
+    print("unreachable", flush=True)
+""")
+
+
+def test_watchdog_ends_a_rank_stuck_on_a_hung_peer(tmp_path):
+    script = tmp_path / "job.py"
+    script.write_text(WATCHDOG_SCRIPT.format(root=ROOT))
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    t0 = time.monotonic()
+    try:
+        out0, err0 = procs[0].communicate(timeout=90)
+        elapsed = time.monotonic() - t0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    from flink_parameter_server_1_amd.utils.watchdog import WATCHDOG_EXIT
+
+    assert procs[0].returncode == WATCHDOG_EXIT, (procs[0].returncode, err0[-2000:])
+    assert "watchdog: no progress" in err0 and "unreachable" not in out0
+    assert elapsed < 60

@@ -97,7 +97,8 @@ def test_tiled_exact_when_users_unique_per_batch(prefetch, phases):
     """Users repeat across micro-batches but never inside one (and items repeat a lot
     inside each): no Hogwild race is possible, so the whole tiled pipeline (partition,
     user phases, pair launch, prefetch, flush) must equal the sequential batch
-    reference (gather, then add the summed item deltas) to fp32 rounding."""
+    reference (gather, then add the summed item deltas; one sub-batch per user
+    phase) to fp32 rounding."""
     from flink_parameter_server_1_amd.ops import reference as R
 
     nu, ni, B, steps = 50_000, 3_000, 20_000, 6
@@ -112,7 +113,11 @@ def test_tiled_exact_when_users_unique_per_batch(prefetch, phases):
         iid = torch.randint(0, ni, (B,), generator=g, dtype=torch.int32)  # ~7 ratings per item per batch
         r = torch.rand(B, generator=g)
         m.step(uid.cuda(), iid.cuda(), r.cuda())
-        R.mf_sgd_local(U, I, uid, iid, r, 0.05)
+        # a user phase is a sequential sub-batch (users [p*upp, (p+1)*upp))
+        upp = -(-nu // phases)
+        for p in range(phases):
+            sel = (uid.long() // upp) == p
+            R.mf_sgd_local(U, I, uid[sel], iid[sel], r[sel], 0.05)
     m.flush()
     torch.testing.assert_close(m.U.cpu(), U, rtol=1e-4, atol=2e-6)
     torch.testing.assert_close(m.I.cpu(), I, rtol=1e-4, atol=2e-6)
