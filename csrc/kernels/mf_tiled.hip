@@ -1063,8 +1063,10 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   if (n > 0) {
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
     if (g2 > 1024) g2 = 1024;
-    // FPS_TP3_PIPE=0: the scatters without the register prefetch of the next batch (A/B)
-    static const bool pipe = [] { const char* e = getenv("FPS_TP3_PIPE"); return !(e && e[0] == '0'); }();
+    // FPS_TP3_PIPE=1: the scatters with the register prefetch of the next batch --
+    // measured slower (level 1: 530 vs 401 us per 64M ratings, bench 9.73-9.76e9 vs
+    // 9.75-9.78e9, profiles/r2_partition.md), so off by default
+    static const bool pipe = [] { const char* e = getenv("FPS_TP3_PIPE"); return e && e[0] == '1'; }();
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
     if (pipe) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, true>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, \
                                  TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr,                \

@@ -44,7 +44,7 @@ from ... import ops
 from ...parallel.comm import Comm
 from ...parallel.rotation import RingRotation, shard_halves
 from ...parallel.rotation import block_rows as block_rows_of
-from ...parallel.staleness import BoundedStalenessPipeline
+from ...api.batched import BatchedWorkerLogic
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
 from ...utils.metrics import Counters
@@ -167,10 +167,18 @@ class DistributedMF:
             # so the close-time dump still covers exactly the touched parameters
             self._seen = torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev)
         self.pipeline = cfg.pipeline and self.exchange == "ps"
-        if self.pipeline:
-            # staleness 1: the pull of batch k+1 (counts exchanged one call earlier, its
-            # row all-to-all in flight) overlaps the SGD of batch k
-            self._pipe = BoundedStalenessPipeline(self.ps, self._pipe_compute, staleness=1)
+        if self.exchange == "ps":
+            # the reference's pull / push protocol through the public batched API on
+            # the tensor engine: a worker over this model's user rows + the item
+            # shard as a SimplePSLogic(add) device logic.  pipeline = staleness 1: the
+            # pull of batch k+1 (counts exchanged one call earlier, its row
+            # all-to-all in flight) overlaps the SGD of batch k.
+            from ...core.tensor_engine import TensorRuntime
+            from ...ps.device_logics import DeviceSimplePSLogicWithClose
+
+            logic = DeviceSimplePSLogicWithClose(cfg.num_items, cfg.dim, table=self.items, ps=self.ps)
+            self.runtime = TensorRuntime(self.comm, staleness=1 if self.pipeline else 0)
+            self.runtime.start(_MFPSWorker(self), logic)
         if cfg.negative_sample_rate > 0:
             # PSOnlineMatrixFactorizationWorker.scala:70-79: per rating, negativeSampleRate
             # items (rating 0) drawn among the items this worker has seen, not among the
@@ -250,13 +258,8 @@ class DistributedMF:
                                          c.learning_rate, c.lam, self.user_atomic)
                 with stage("mf.rotate.end", self.timer):
                     self.rot.end()
-        elif self.pipeline:
-            # pull of batch k+1 (its row all-to-all in flight) overlaps the SGD
-            # of batch k; k's push follows.  Staleness bound: one micro-batch.
-            self._pipe.submit(iid, (uid_local, rating))
-        else:
-            rows, plan = self.ps.pull(iid)
-            self._compute_push(rows, plan, uid_local, rating)
+        else:  # PS path: one micro-batch through the tensor engine
+            self.runtime.submit((uid_local, iid, rating))
         self.updates += uid_local.numel()
         self.counters.add("ratings", uid_local.numel())
         self.counters.add("micro_batches")
@@ -352,32 +355,31 @@ class DistributedMF:
             with stage("mf.rotate.end", self.timer):
                 self.rot.end()
 
-    def _pipe_compute(self, rows, plan, payload):
-        uid_local, rating = payload
-        self._compute_push(rows, plan, uid_local, rating)
-        return None, None
-
-    def _compute_push(self, rows, plan, uid_local, rating):
+    def _item_deltas(self, rows, pos, n_unique, uid_local, rating):
+        """SGD of one micro-batch on its pulled item rows ``rows[pos[b]]``; returns
+        the per-unique-item deltas to push (user rows are updated in place)."""
         c = self.cfg
         if self.sgd_mode == "tiled":
             # tile-grouped SGD on a working copy of the pulled rows (one block, no item
             # atomics); the pushed delta is what the micro-batch added to each row
             orig = rows.float()
             work = orig.clone()
-            ptr, rec = self._tilers[0].run(uid_local, plan.pos, rating)
-            for p in range(self.user_phases):
-                ops.mf_sgd_tiled(self.U, work, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate, c.lam)
-            self.ps.push(plan, work.sub_(orig))
-            return
-        if self.sgd_mode == "grouped":
-            ptr, order = self.grouper.run(plan.pos, plan.n_unique)
-            delta = torch.empty((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
-            ops.mf_sgd_grouped(self.U, rows, uid_local, rating, ptr, order, c.learning_rate, c.lam, delta)
-        else:
-            delta = torch.zeros((plan.n_unique, c.dim), dtype=torch.float32, device=self.U.device)
-            ops.mf_sgd_pulled(self.U, uid_local, rating, rows, plan.pos, delta, c.learning_rate, c.lam,
-                              self.user_atomic)
-        self.ps.push(plan, delta)
+            ptr, rec = self._tilers[0].run(uid_local, pos, rating)
+            with stage("mf.sgd", self.timer):
+                for p in range(self.user_phases):
+                    ops.mf_sgd_tiled(self.U, work, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
+                                     c.lam)
+            return work.sub_(orig)
+        with stage("mf.sgd", self.timer):
+            if self.sgd_mode == "grouped":
+                ptr, order = self.grouper.run(pos, n_unique)
+                delta = torch.empty((n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+                ops.mf_sgd_grouped(self.U, rows, uid_local, rating, ptr, order, c.learning_rate, c.lam, delta)
+            else:
+                delta = torch.zeros((n_unique, c.dim), dtype=torch.float32, device=self.U.device)
+                ops.mf_sgd_pulled(self.U, uid_local, rating, rows, pos, delta, c.learning_rate, c.lam,
+                                  self.user_atomic)
+        return delta
 
     def flush(self):
         """Complete the in-flight micro-batch of the pipelined path / bring the
@@ -391,8 +393,8 @@ class DistributedMF:
                 seen = self.comm.all_reduce(self._seen.clone(), op=torch.distributed.ReduceOp.MAX)
                 loc = torch.arange(self.items.n_local, device=seen.device)
                 self.items.touched |= seen[self.items.global_ids(loc)]
-        if self.pipeline:
-            self._pipe.drain()
+        if self.exchange == "ps":
+            self.runtime.pipe.drain()
 
     # -------------------------------------------------------------- checkpoint
     _AUX = ("_ring", "_ring_cursor", "_known_flag", "_known", "_known_count")
@@ -450,6 +452,24 @@ class DistributedMF:
     def item_vectors(self, only_touched=True):
         self.flush()
         return self.items.dump(only_touched)
+
+
+class _MFPSWorker(BatchedWorkerLogic):
+    """``DistributedMF``'s PS path as a batched worker: pull the items of a
+    micro-batch of ``(local user row, item, rating)``, run the model's SGD kernel on
+    the answered rows, push the per-item deltas
+    (``PSOnlineMatrixFactorizationWorker``, ``M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-89``)."""
+
+    def __init__(self, model: "DistributedMF"):
+        self.m = model
+
+    def on_recv_batch(self, batch, ps):
+        uid_local, iid, rating = batch
+        ps.pull(iid, (uid_local, rating))
+
+    def on_pull_recv_batch(self, pulled, ps):
+        uid_local, rating = pulled.payload
+        ps.push_unique(self.m._item_deltas(pulled.rows, pulled.pos, pulled.n_unique, uid_local, rating))
 
 
 @dataclass

@@ -18,9 +18,12 @@ from typing import Optional
 import torch
 
 from ... import ops
+from ...core.tensor_engine import TensorRuntime
 from ...parallel.comm import Comm
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
+from ...ps.device_logics import DeviceRangePSLogicWithClose, DeviceSimplePSLogicWithClose
+from .batched import PAWorker
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
@@ -55,6 +58,14 @@ class DistributedPA:
         else:
             self.cost = None
         self.examples = 0
+        # the pull / push path is the public batched API on the tensor engine: a
+        # PAWorker + the range / hash WithClose device logic over this model's shard
+        Logic = DeviceRangePSLogicWithClose if cfg.partition == "range" else DeviceSimplePSLogicWithClose
+        kw = dict(table=self.table, ps=self.ps)
+        logic = Logic(cfg.feature_count, self.L, **kw) if cfg.partition == "range" else \
+            Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
+        self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
+        self.runtime = TensorRuntime(self.comm, staleness=0).start(self.worker, logic)
 
     @property
     def _direct(self) -> bool:
@@ -81,19 +92,14 @@ class DistributedPA:
             if train:
                 self.examples += indptr.numel() - 1
             return pred, loss
-        rows, plan = self.ps.pull(indices)
-        w = rows.float().contiguous()
-        delta = torch.zeros((plan.n_unique, self.L), dtype=torch.float32, device=w.device)
-        if c.kind == "binary":
-            pred, loss = ops.pa_binary(indptr, values, plan.pos, w.view(-1), labels, c.variant, c.aggressiveness,
-                                       delta.view(-1), with_loss)
-        else:
-            pred, loss = ops.pa_multi(indptr, values, plan.pos, w, labels, c.kind, c.variant, c.aggressiveness,
-                                      self.cost, delta, with_loss)
+        # one micro-batch through the engine (staleness 0: done inside submit); a
+        # predict-only call skips the push round (collective: every rank predicts)
+        self.worker.with_loss = with_loss
+        self.worker.pushes = train
+        self.runtime.submit((indptr, indices, values, labels))
         if train:
-            self.ps.push(plan, delta)
             self.examples += indptr.numel() - 1
-        return pred, loss
+        return self.worker.last
 
     def train_step(self, indptr, indices, values, labels, with_loss=False):
         """Labels: binary +1/-1 (int8, 0 = predict only); multiclass class id (int32, -1 = predict only)."""

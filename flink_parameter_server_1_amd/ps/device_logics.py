@@ -52,9 +52,13 @@ class DevicePSLogic:
 
     def __init__(self, num_ids: int, dim: int = 1, *, op: str = "add", init: Tuple = ("zeros",), seed: int = 0,
                  partition: str = "hash", wire_dtype: str = "fp32", lr: float = 0.0, dtype=torch.float32,
-                 track_touched: bool = True):
+                 track_touched: bool = True, table: Optional[ShardedTable] = None, ps: Optional[TensorPS] = None):
+        """``table`` / ``ps``: serve an existing shard (and its PS front) instead of
+        allocating one at ``open`` -- how the model classes (``DistributedMF``,
+        ``DistributedPA``) run their PS path through this engine."""
         if op not in OPS:
             raise ValueError(f"op must be one of {OPS}, not {op!r}")
+        self._given = (table, ps)
         self.num_ids, self.dim, self.op, self.init, self.seed = int(num_ids), int(dim), op, init, seed
         self.partition, self.wire_dtype, self.lr, self.dtype = partition, _WIRE[wire_dtype], lr, dtype
         self.track_touched = track_touched
@@ -64,10 +68,14 @@ class DevicePSLogic:
     # ------------------------------------------------------------- lifecycle
     def open(self, comm: Comm) -> None:
         """Allocate this rank's shard (``ParameterServerLogic.open``)."""
-        self.table = ShardedTable(self.num_ids, self.dim, comm.rank, comm.world, self.partition, self.init, self.seed,
-                                  comm.device, optimizer=self.op, track_touched=self.track_touched or
-                                  self.emit == "close", dtype=self.dtype)
-        self.ps = TensorPS(self.table, comm, self.wire_dtype)
+        table, ps = self._given
+        if table is not None:
+            self.table = table
+        else:
+            self.table = ShardedTable(self.num_ids, self.dim, comm.rank, comm.world, self.partition, self.init,
+                                      self.seed, comm.device, optimizer=self.op,
+                                      track_touched=self.track_touched or self.emit == "close", dtype=self.dtype)
+        self.ps = ps if ps is not None else TensorPS(self.table, comm, self.wire_dtype)
         # set-rules and per-push outputs must tell pushed keys from merely pulled ones
         self.ps.masked_push = self.op == "set" or self.emit == "push"
 

@@ -1,0 +1,105 @@
+"""Streaming micro-batch assembly (core.microbatch): the reference's Count / Timer /
+AND / OR combination semantics (T/SenderReceiverTest.scala, scaled timings) on the
+tensor path, idle-timeout termination, and a streaming MF run that ends by it."""
+import queue
+import threading
+import time
+
+import torch
+
+from flink_parameter_server_1_amd.core.microbatch import CountPolicy, MicroBatcher, TimerPolicy, all_of, any_of
+
+T = 0.25  # timer interval (s); the reference test uses 5 s
+
+
+def _feed(schedule):
+    """A blocking source: ``schedule`` = [(sleep_before_s, record), ...]."""
+    q = queue.Queue()
+    end = object()
+
+    def run():
+        for delay, rec in schedule:
+            if delay:
+                time.sleep(delay)
+            q.put(rec)
+        q.put(end)
+
+    threading.Thread(target=run, daemon=True).start()
+    return iter(q.get, end)
+
+
+def _drain(mb):
+    t0 = time.monotonic()
+    return [(time.monotonic() - t0, b) for b in mb]
+
+
+def test_count_policy_flushes_every_n_and_the_tail():
+    mb = MicroBatcher(range(7), [CountPolicy(3)])
+    assert [b for b in mb] == [[0, 1, 2], [3, 4, 5], [6]]
+    assert mb.ended_by == "source"
+
+
+def test_count_or_timer():
+    # 5 records at once -> the count flushes; one more -> the timer flushes it after ~T
+    src = _feed([(0, i) for i in range(5)] + [(0.05, 5), (4 * T, "late")])
+    mb = MicroBatcher(src, [CountPolicy(5), TimerPolicy(T * 1000)], any_of)
+    out = _drain(mb)
+    assert [b for _, b in out[:2]] == [[0, 1, 2, 3, 4], [5]]
+    assert out[1][0] >= T * 0.8  # the lone record waited for a tick
+    assert out[-1][1] == ["late"]
+
+
+def test_count_and_timer():
+    """Reference: one record, a timer tick (no flush: the count is not reached),
+    then five more: the count fires on the 4th (the first record counted) and
+    both flags are up -> 5 records flushed, the 6th waits."""
+    src = _feed([(0, "pull")] + [(T * 1.6 if i == 0 else 0, f"push{i}") for i in range(5)] + [(4 * T, "end")])
+    mb = MicroBatcher(src, [CountPolicy(5), TimerPolicy(T * 1000)], all_of)
+    out = _drain(mb)
+    assert out[0][1] == ["pull", "push0", "push1", "push2", "push3"]
+    assert out[0][0] >= T * 1.5
+    assert "push4" in out[1][1]
+
+
+def test_idle_timeout_ends_an_unbounded_stream():
+    stop = threading.Event()
+
+    def forever():
+        for i in range(10):
+            yield i
+        stop.wait(30)  # then silence: an unbounded source that stalls
+
+    t0 = time.monotonic()
+    mb = MicroBatcher(forever(), [CountPolicy(4)], idle_timeout_ms=300)
+    out = list(mb)
+    stop.set()
+    assert out == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+    assert mb.ended_by == "idle" and time.monotonic() - t0 < 5
+
+
+def test_streaming_mf_on_the_tensor_engine_ends_by_idle_timeout():
+    """A rating stream that stalls: the tensor engine (iteration_wait_time) and the
+    micro-batcher end the job; every rating was trained on."""
+    from flink_parameter_server_1_amd.core.messages import Left
+    from flink_parameter_server_1_amd.models.mf.batched import ps_online_mf_tensor
+
+    stop = threading.Event()
+    g = torch.Generator().manual_seed(0)
+
+    def ratings():
+        for _ in range(700):
+            yield (int(torch.randint(0, 50, (1,), generator=g)), int(torch.randint(0, 30, (1,), generator=g)),
+                   float(torch.rand(1, generator=g)))
+        stop.wait(30)
+
+    def collate(recs):
+        u, i, r = zip(*recs)
+        return torch.tensor(u), torch.tensor(i), torch.tensor(r, dtype=torch.float32)
+
+    mb = MicroBatcher(ratings(), [CountPolicy(64), TimerPolicy(50)], any_of, collate=collate, idle_timeout_ms=400)
+    t0 = time.monotonic()
+    out = ps_online_mf_tensor(mb, 50, 30, num_factors=4, learning_rate=0.05)
+    stop.set()
+    assert mb.ended_by == "idle" and time.monotonic() - t0 < 20
+    assert sum(mb.flushes) == 700
+    assert sum(e.value[0].numel() for e in out if isinstance(e, Left)) == 700
