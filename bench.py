@@ -207,6 +207,7 @@ def main(argv=None):
                 if model.exchange == "ps" else None,
                 "rotation_bytes_sent_rank0": model.rot.bytes_sent if model.exchange == "rotate" else None,
                 "bytes_sent_per_rank": bytes_per_rank,
+                "bytes_per_peer_rank0": list(comm.peer_bytes),
             },
         }
         print(json.dumps(out), flush=True)

@@ -142,6 +142,11 @@ def cmd_mf_gpu(args):
     if ck and args.resume:
         man = ck.restore_latest()
         start = man["step"] if man else 0
+    if args.model_in_users or args.model_in_items:  # warm start from id;value dumps
+        from .utils.io import read_factors_text
+
+        m.load_model(read_factors_text(args.model_in_users) if args.model_in_users else None,
+                     read_factors_text(args.model_in_items) if args.model_in_items else None)
     t0 = time.time()
     for s in range(start, start + args.steps):
         m.step(*batch(s))
@@ -152,11 +157,18 @@ def cmd_mf_gpu(args):
     if comm.rank == 0:
         print(json.dumps({"steps": args.steps, "seconds": time.time() - t0, "updates": m.updates * comm.world,
                           "rmse_first_batch": rmse}))
-    if args.items_out:
-        from .utils.io import write_factors_text
+    from .utils.io import write_factors_text
 
-        ids, vals = m.item_vectors()
-        write_factors_text(f"{args.items_out}.{comm.rank}", ids.cpu().numpy(), vals.cpu().numpy())
+    def out_path(p):  # one file per rank at N > 1 (each holds its shard's rows)
+        return p if comm.world == 1 else f"{p}.{comm.rank}"
+
+    if args.items_out:
+        ids, vals = m.item_vectors(only_touched=False)
+        o = torch.argsort(ids)
+        write_factors_text(out_path(args.items_out), ids[o].cpu().numpy(), vals[o].cpu().numpy())
+    if args.users_out:
+        ids, vals = m.user_vectors()
+        write_factors_text(out_path(args.users_out), ids.cpu().numpy(), vals.detach().cpu().numpy())
 
 
 def cmd_topk(args):
@@ -296,7 +308,10 @@ def build_parser():
     p.add_argument("--checkpoint-dir")
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--resume", action="store_true")
-    p.add_argument("--items-out")
+    p.add_argument("--items-out", help="id;value dump of the item factors (per-rank suffix at N > 1)")
+    p.add_argument("--users-out", help="id;value dump of the user factors (per-rank suffix at N > 1)")
+    p.add_argument("--model-in-users", help="warm start: id;value user factors")
+    p.add_argument("--model-in-items", help="warm start: id;value item factors")
 
     p = sub.add_parser("topk")
     p.add_argument("--users", required=True)

@@ -33,6 +33,7 @@ from ...parallel.comm import Comm
 from ...parallel.staleness import BoundedStalenessPipeline
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
+from ...utils.tracing import stage
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
 MAX_IDS = (1 << 31) - 1  # keys travel as int32
@@ -81,8 +82,9 @@ class DistributedPairEmbedding:
         n_pairs, labels, with_loss = payload
         delta = torch.zeros((plan.n_unique, self.cfg.dim), dtype=torch.float32, device=rows.device)
         pos = plan.pos
-        loss = ops.pair_sgd_pulled(rows, pos[:n_pairs], pos[n_pairs:], labels, delta, self._kernel_lr,
-                                   self.cfg.loss, with_loss)
+        with stage("pairs.step", None):
+            loss = ops.pair_sgd_pulled(rows, pos[:n_pairs], pos[n_pairs:], labels, delta, self._kernel_lr,
+                                       self.cfg.loss, with_loss)
         self.rows_pushed += plan.n_unique
         return delta, (loss, n_pairs)
 

@@ -78,6 +78,17 @@ class MFConfig:
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
 
 
+    def user_seed(self) -> int:
+        """Hash-init seed of the user table (the per-record apps' ``init="hash"``
+        user side: seed ^ USER_SEED_XOR), so both engines start from one model."""
+        from .core import USER_SEED_XOR
+
+        return (self.seed ^ USER_SEED_XOR) & 0xFFFFFFFF
+
+    def item_seed(self) -> int:
+        return self.seed & 0xFFFFFFFF
+
+
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
 #: user rows per SGD phase (auto ``user_phases``): 2.5M x 64 fp32 = 640 MB
@@ -91,9 +102,10 @@ class DistributedMF:
         W, r, dev = self.comm.world, self.comm.rank, self.comm.device
         init = ("uniform", cfg.range_min, cfg.range_max)
         # worker-resident user shard: users u with u % W == r, local row u // W
-        self.users = ShardedTable(cfg.num_users, cfg.dim, r, W, "hash", init, cfg.seed, dev, track_touched=False)
+        self.users = ShardedTable(cfg.num_users, cfg.dim, r, W, "hash", init, cfg.user_seed(), dev,
+                                  track_touched=False)
         # PS item shard
-        self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.seed + 7919, dev, optimizer="add")
+        self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.item_seed(), dev, optimizer="add")
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
         self.user_atomic = cfg.user_update == "atomic"
         exchange = cfg.exchange
@@ -155,6 +167,15 @@ class DistributedMF:
             # ring rotation orders its copy stream against the stream it was built on
             hp = self._prefetch and exchange == "local" and cfg.sgd_high_priority
             self._hp = torch.cuda.Stream(dev, priority=-1) if hp else None
+            # FPS_PARTITION_CUS=k: the partition of batch k+1 runs on ~k CUs of its own
+            # and the SGD of batch k on the others (CU-masked streams), instead of both
+            # sharing every CU
+            k_cu = int(os.environ.get("FPS_PARTITION_CUS", "0"))
+            if k_cu > 0 and self._prefetch and exchange == "local":
+                n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+                stride = max(2, n_cu // k_cu)
+                self._side = ops.cu_masked_stream(dev, stride, stride - 1)
+                self._hp = ops.cu_masked_stream(dev, stride, stride - 1, complement=True)
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
@@ -444,6 +465,25 @@ class DistributedMF:
         se = self.comm.sum_over_ranks(self.sq_err(uid_local, iid, rating))
         n = self.comm.sum_over_ranks(float(uid_local.numel()))
         return (se / max(n, 1.0)) ** 0.5
+
+    def load_model(self, users=None, items=None) -> None:
+        """Warm start (``transformWithDoubleModelLoad``: users are worker-resident,
+        items live on the PS): ``users`` / ``items`` = ``(ids, values)`` tensors or
+        ``{id: vector}`` dicts (``utils.io.read_factors_text``).  Every rank may pass
+        the whole model; each keeps the rows it owns."""
+        self.flush()
+
+        def as_t(m):
+            if isinstance(m, dict):
+                ids = torch.tensor(sorted(m), dtype=torch.int64)
+                vals = torch.tensor([list(m[int(i)]) for i in ids.tolist()], dtype=torch.float32)
+                return ids, vals.reshape(ids.numel(), -1)
+            return m[0].long(), m[1].float()
+
+        if users is not None:
+            self.users.load(*as_t(users))
+        if items is not None:
+            self.items.load(*as_t(items))
 
     def user_vectors(self):
         ids = self.users.global_ids(torch.arange(self.users.n_local, device=self.U.device))

@@ -24,6 +24,7 @@ from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
 from ...ps.device_logics import DeviceRangePSLogicWithClose, DeviceSimplePSLogicWithClose
 from .batched import PAWorker
+from ...utils.tracing import stage
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
@@ -66,6 +67,7 @@ class DistributedPA:
             Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
         self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
         self.runtime = TensorRuntime(self.comm, staleness=0).start(self.worker, logic)
+        self.timer = None  # utils.metrics.StageTimer (optional)
 
     @property
     def _direct(self) -> bool:
@@ -83,12 +85,13 @@ class DistributedPA:
             idx = indices.to(device=w.device, dtype=torch.int32).contiguous()
             if train and self.table.touched is not None:
                 ops.mark_rows(self.table.touched, idx)
-            if c.kind == "binary":
-                pred, loss = ops.pa_binary(indptr, values, idx, w.view(-1), labels, c.variant, c.aggressiveness,
-                                           w.view(-1), with_loss)
-            else:
-                pred, loss = ops.pa_multi(indptr, values, idx, w, labels, c.kind, c.variant, c.aggressiveness,
-                                          self.cost, w, with_loss)
+            with stage("pa.step", self.timer):
+                if c.kind == "binary":
+                    pred, loss = ops.pa_binary(indptr, values, idx, w.view(-1), labels, c.variant,
+                                               c.aggressiveness, w.view(-1), with_loss)
+                else:
+                    pred, loss = ops.pa_multi(indptr, values, idx, w, labels, c.kind, c.variant, c.aggressiveness,
+                                              self.cost, w, with_loss)
             if train:
                 self.examples += indptr.numel() - 1
             return pred, loss
@@ -96,7 +99,8 @@ class DistributedPA:
         # predict-only call skips the push round (collective: every rank predicts)
         self.worker.with_loss = with_loss
         self.worker.pushes = train
-        self.runtime.submit((indptr, indices, values, labels))
+        with stage("pa.step", self.timer):
+            self.runtime.submit((indptr, indices, values, labels))
         if train:
             self.examples += indptr.numel() - 1
         return self.worker.last

@@ -30,6 +30,7 @@ from ... import ops
 from ...parallel.comm import Comm
 from ...parallel.table import ShardedTable
 from ...parallel.tensor_ps import TensorPS
+from ...utils.tracing import stage
 
 _WIRE = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
@@ -68,6 +69,7 @@ class DistributedSGNS:
         self.prob, self.alias = prob.to(dev), alias.to(dev)
         self.counter = 0
         self.pairs_seen = 0
+        self.timer = None  # utils.metrics.StageTimer (optional)
 
     def step(self, centers: torch.Tensor, contexts: torch.Tensor, lr: Optional[float] = None,
              with_loss: bool = False):
@@ -114,9 +116,10 @@ class DistributedSGNS:
         if self.w_out.touched is not None:
             ops.mark_rows(self.w_out.touched, ctx)
             ops.mark_rows(self.w_out.touched, negs)
-        loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
-                             c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
-                             with_loss=with_loss, neg_k=c.shared_negatives)
+        with stage("sgns.step", self.timer):
+            loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
+                                 c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
+                                 with_loss=with_loss, neg_k=c.shared_negatives)
         self.pairs_seen += P
         if with_loss:
             return float(loss.item()) / max(P, 1)
@@ -136,8 +139,9 @@ class DistributedSGNS:
         c = self.cfg
         P = centers.numel()
         nb = (P + self.BLOCK - 1) // self.BLOCK
-        negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives, seed=c.seed + 17 * self.comm.rank,
-                                counter=self.counter)
+        with stage("sgns.negatives", self.timer):
+            negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives,
+                                    seed=c.seed + 17 * self.comm.rank, counter=self.counter)
         self.counter += 1
         outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
         if async_rows:
@@ -159,9 +163,10 @@ class DistributedSGNS:
         d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
-        loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
-                             c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
-                             neg_k=c.shared_negatives)
+        with stage("sgns.step", self.timer):
+            loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
+                                 c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
+                                 neg_k=c.shared_negatives)
         self.ps_in.push(plan_in, d_in)
         self.ps_out.push(plan_out, d_out)
         self.pairs_seen += P

@@ -58,6 +58,20 @@ def _c(t):
     return t
 
 
+def cu_masked_stream(device, stride: int, offset: int, complement: bool = False):
+    """A HIP stream restricted to the CUs ``i`` with ``i % stride == offset`` (or the
+    complement), wrapped as a torch stream.  The stream lives for the process."""
+    import ctypes
+
+    dev = torch.device(device)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    out = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        N.check(N.require().fps_stream_create_cu_mask(n_cu, stride, offset, int(complement), ctypes.byref(out)),
+                "stream_create_cu_mask")
+    return torch.cuda.ExternalStream(out.value, device=dev)
+
+
 def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: float = 0.0, hi: float = 1.0,
               seed: int = 0) -> torch.Tensor:
     """Fill ``table[r] = U[lo,hi)`` keyed by global id ``id_base + r*id_stride`` (K9)."""

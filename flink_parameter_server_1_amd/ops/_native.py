@@ -89,7 +89,7 @@ _SIGNATURES = {
     "fps_pa_multi": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
-OPTIONAL = {}
+OPTIONAL = {"fps_stream_create_cu_mask": [c_int, c_int, c_int, c_int, c_vp], "fps_stream_destroy": [c_vp]}
 #: launchers / sizers returning int64 (the rest return an int status)
 RESTYPE_I64 = {"fps_tile_partition2_ws_ints", "fps_tile_partition3_ws_ints", "fps_tile_partition4_ws_ints",
                "fps_tile_partition4_cap", "fps_dedup_flags_ws_ints"}

@@ -45,6 +45,8 @@ class Comm:
                 device = torch.device("cpu")
         self.device = torch.device(device)
         self.bytes_sent = 0
+        #: bytes this rank put on the wire to each peer (all-to-alls + point-to-point)
+        self.peer_bytes = [0] * self.world
 
     # ------------------------------------------------------------- set-up
     @staticmethod
@@ -111,8 +113,7 @@ class Comm:
             return out
         if out is None:
             out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-        row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
-        self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
+        self._count(send, send_splits)
         if self._staged(send):
             host_out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype)
             dist.all_to_all_single(host_out, send[: int(sum(send_splits))].cpu(), list(map(int, recv_splits)),
@@ -132,11 +133,17 @@ class Comm:
         if self._staged(send):  # host-staged transport is synchronous
             return self.all_to_all(send, send_splits, recv_splits), None
         out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-        row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
-        self.bytes_sent += (int(sum(send_splits)) - int(send_splits[self.rank])) * row_bytes
+        self._count(send, send_splits)
         work = dist.all_to_all_single(out, send[: int(sum(send_splits))], list(map(int, recv_splits)),
                                       list(map(int, send_splits)), group=self.group, async_op=True)
         return out, work
+
+    def _count(self, send: torch.Tensor, send_splits: Sequence[int]) -> None:
+        row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
+        for j, n in enumerate(send_splits):
+            if j != self.rank and n:
+                self.peer_bytes[j] += int(n) * row_bytes
+                self.bytes_sent += int(n) * row_bytes
 
     def all_reduce(self, t: torch.Tensor, op=None) -> torch.Tensor:
         if self.world > 1:
@@ -161,6 +168,8 @@ class Comm:
         """Batched point-to-point: ``sends`` / ``recvs`` are ``(tensor, peer)`` pairs,
         posted as one group (no ordering deadlock between pairs of ranks).  Returns
         the works to wait on (empty when the transfer already completed: staged)."""
+        for t, peer in sends:
+            self.peer_bytes[peer] += t.numel() * t.element_size()
         if self.backend == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs)):
             host_recvs = [(torch.empty(t.shape, dtype=t.dtype), peer) for t, peer in recvs]
             ops = [dist.P2POp(dist.isend, t.cpu(), peer, group=self.group) for t, peer in sends]

@@ -71,3 +71,18 @@ def test_cli_topk_and_pa(tmp_path):
             f.write(f"{lab} " + " ".join(f"{i}:1.0" for i in idx) + "\n")
     out = _run(["pa-train", "--input", str(svm), "--feature-count", "50", "--epochs", "3", "--batch", "16"], tmp_path)
     assert json.loads(out.strip().splitlines()[-1])["examples"] == 300
+
+
+def test_cli_mf_gpu_warm_start_from_its_own_dump(tmp_path):
+    """mf-gpu dumps users and items as id;value files; a run warm-started from them
+    (0 training steps) reports the same RMSE -- the text format round-trips fp32."""
+    base = ["mf-gpu", "--num-users", "300", "--num-items", "120", "--dim", "8", "--batch", "600",
+            "--learning-rate", "0.1"]
+    out = _run(base + ["--steps", "5", "--users-out", str(tmp_path / "U.map"), "--items-out", str(tmp_path / "I.map")],
+               tmp_path)
+    rmse = json.loads(out.strip().splitlines()[-1])["rmse_first_batch"]
+    assert len(open(tmp_path / "U.map").read().splitlines()) == 300 * 8
+    out2 = _run(base + ["--steps", "0", "--model-in-users", str(tmp_path / "U.map"), "--model-in-items",
+                        str(tmp_path / "I.map")], tmp_path)
+    rmse2 = json.loads(out2.strip().splitlines()[-1])["rmse_first_batch"]
+    assert rmse2 == rmse

@@ -63,8 +63,8 @@ def _emulate(world, steps, dim=D, phases=0):
 
     cfg = MFConfig(num_users=NU, num_items=NI, dim=dim, learning_rate=0.1, range_min=0.0, range_max=0.3)
     init = ("uniform", cfg.range_min, cfg.range_max)
-    users = [ShardedTable(NU, dim, r, world, "hash", init, cfg.seed, track_touched=False) for r in range(world)]
-    items = ShardedTable(NI, dim, 0, 1, "hash", init, cfg.seed + 7919, track_touched=False).weight
+    users = [ShardedTable(NU, dim, r, world, "hash", init, cfg.user_seed(), track_touched=False) for r in range(world)]
+    items = ShardedTable(NI, dim, 0, 1, "hash", init, cfg.item_seed(), track_touched=False).weight
     tiled = dim in ops.TILED_DIMS
     if tiled:  # same tile geometry as DistributedMF
         rows_max = max(block_rows(NI, world))

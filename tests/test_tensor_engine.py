@@ -224,3 +224,28 @@ def test_staleness_for_pull_limit():
     assert staleness_for_pull_limit(1600, 1600) == 0
     assert staleness_for_pull_limit(1600, 800) == 1
     assert staleness_for_pull_limit(1600, 500) == 3
+
+
+@pytest.mark.parametrize("sgd_mode", ["flat", "grouped"])
+def test_distributed_mf_ps_path_equals_per_record_engine(sgd_mode):
+    """DistributedMF's PS path (the batched worker on the tensor engine, CPU
+    reference ops, fp32) with one rating per micro-batch == per-record psOnlineMF
+    with pullLimit 1 and the same hash init (fp64)."""
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig
+
+    users, items = 20, 30
+    u, i, r = _ratings(200, users, items, seed=11)
+    recs = [Rating(int(a), int(b), float(c), t) for t, (a, b, c) in enumerate(zip(u, i, r))]
+    U_ref, V_ref = _fold_records(ps_online_mf(recs, init="hash", pull_limit=1, worker_parallelism=1,
+                                              ps_parallelism=1, **KW))
+    cfg = MFConfig(num_users=users, num_items=items, dim=4, learning_rate=0.05, range_min=0.0, range_max=0.3,
+                   seed=7, exchange="ps", sgd_mode=sgd_mode, pipeline=False)
+    m = DistributedMF(cfg)
+    for a, b, c in zip(u, i, r):
+        m.step(torch.tensor([a], dtype=torch.int32), torch.tensor([b], dtype=torch.int32),
+               torch.tensor([c], dtype=torch.float32))
+    m.flush()
+    for k, v in U_ref.items():
+        np.testing.assert_allclose(m.U[k].numpy(), v, rtol=0, atol=2e-6)
+    for k, v in V_ref.items():
+        np.testing.assert_allclose(m.I[k].numpy(), v, rtol=0, atol=2e-6)
