@@ -115,9 +115,17 @@ __device__ __forceinline__ uint32_t score_key(float f) {  // order-preserving fl
 // length-sorted scan, only a few hundred of a bucket's 64k items per query pass.
 // cnt[q] counts every passing score; entries beyond cap are dropped (the caller
 // sees cnt > cap and rescans the segment unfused).
+//
+// With qlen / xlen (vector norms) the LEMP length bound is applied per tile on
+// the device: a tile none of whose 64 queries can be beaten by its longest item
+// (|q| * max|x| * slack <= theta_q) exits before loading anything -- exact, and
+// it replaces the host-side "every query settled" test per bucket (a host sync).
+
 __global__ void __launch_bounds__(256) score_filter_kernel(const float* __restrict__ Q, const float* __restrict__ X,
                                                            const int64_t* __restrict__ ids, int B, int N, int D,
                                                            const float* __restrict__ best_s, int k,
+                                                           const float* __restrict__ qlen,
+                                                           const float* __restrict__ xlen, float slack,
                                                            uint32_t* __restrict__ cand_key,
                                                            int64_t* __restrict__ cand_id, int32_t* __restrict__ cnt,
                                                            int cap) {
@@ -126,17 +134,25 @@ __global__ void __launch_bounds__(256) score_filter_kernel(const float* __restri
   __shared__ uint32_t ktau[TB];
   int q0, i0;
   tile_of(B, N, q0, i0);
-  if (threadIdx.x < TB) {
-    const int q = q0 + threadIdx.x;
-    ktau[threadIdx.x] = q < B ? score_key(best_s[(int64_t)q * k + k - 1]) : 0xffffffffu;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float theta = INFINITY;
+  if (tid < TB && q0 + tid < B) theta = best_s[(int64_t)(q0 + tid) * k + k - 1];
+  if (xlen != nullptr) {
+    float xl = (tid < TB && i0 + tid < N) ? xlen[i0 + tid] : 0.f;
+    xl = group_max<64>(xl);  // wave 0 holds the tile's 64 items
+    int live = 0;
+    if (tid < TB && q0 + tid < B) live = !(theta > -INFINITY && qlen[q0 + tid] * xl * slack <= theta);
+    if (!__syncthreads_or(live)) return;  // uniform: the whole workgroup leaves
   }
+  if (tid < TB) ktau[tid] = q0 + tid < B ? score_key(theta) : 0xffffffffu;
   // (score_tile's first __syncthreads orders the ktau stores before the reads below)
   const floatx16 acc = score_tile(Q, X, B, N, D, q0, i0, Qs, Xs);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int col = i0 + wc * 32 + (lane & 31);
   if (col >= N) return;
   const int64_t id = ids[col];
+  // (one counter atomic per passing score: a per-wave aggregated reservation was
+  // measured slower -- its registers cost occupancy, 8 -> 6 waves/SIMD)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int rl = wr * 32 + acc_row(lane, r);
@@ -161,7 +177,22 @@ FPS_API int fps_score_filter(const float* Q, const float* X, const int64_t* ids,
   if (k <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
   const int nwg = ((N + TB - 1) / TB) * ((B + TB - 1) / TB);
   hipLaunchKernelGGL(score_filter_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, Q, X, ids, B, N, D, best_s, k,
-                     cand_key, cand_id, cnt, cap);
+                     nullptr, nullptr, 1.f, cand_key, cand_id, cnt, cap);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same with the per-tile LEMP length bound (qlen [B], xlen [N]; both or neither)
+FPS_API int fps_score_filter_lemp(const float* Q, const float* X, const int64_t* ids, int B, int N, int D,
+                                  const float* best_s, int k, const float* qlen, const float* xlen, float slack,
+                                  uint32_t* cand_key, int64_t* cand_id, int32_t* cnt, int cap, void* stream) {
+  if (B <= 0 || N <= 0) return 0;
+  if (k <= 0 || cap <= 0 || D <= 0) return (int)hipErrorInvalidValue;
+  if ((qlen == nullptr) != (xlen == nullptr)) return (int)hipErrorInvalidValue;
+  const int64_t nwg = (int64_t)((N + TB - 1) / TB) * ((B + TB - 1) / TB);
+  if (nwg > INT32_MAX) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(score_filter_kernel, dim3((unsigned)nwg), dim3(256), 0, (hipStream_t)stream, Q, X, ids, B, N, D,
+                     best_s, k, qlen, xlen, slack, cand_key, cand_id, cnt, cap);
   FPS_CHECK_LAUNCH();
   return 0;
 }

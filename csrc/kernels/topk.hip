@@ -192,17 +192,68 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* 
                                                                 const int64_t* __restrict__ cand_id,
                                                                 const int32_t* __restrict__ cnt, int cap,
                                                                 float* __restrict__ best_s,
-                                                                int64_t* __restrict__ best_i, int k) {
+                                                                int64_t* __restrict__ best_i, int k,
+                                                                int32_t* __restrict__ ovf) {
   __shared__ uint32_t skey[TK_SORT];
   __shared__ int64_t sid[TK_SORT];
   const int row = blockIdx.x;
-  const int nc = min(min(cnt[row], cap), TK_CAP);
+  const int c = cnt[row];
+  // an overflowed row (more than cap passed the filter) is merged incompletely: flag it
+  // for the caller, which checks once per query batch (no host sync per segment)
+  if (ovf != nullptr && c > cap && threadIdx.x == 0) ovf[0] = 1;
+  const int nc = min(min(c, cap), TK_CAP);
   if (nc == 0) return;  // nothing beat the k-th best: the list stands
+  float* bs = best_s + (int64_t)row * k;
+  int64_t* bi = best_i + (int64_t)row * k;
+  if (nc <= TK_NT) {
+    // few candidates (every segment after the first): merge by rank instead of a
+    // full bitonic sort -- each candidate's and each kept entry's final position is
+    // the number of entries ahead of it (key desc, then id asc; the running list is
+    // already in that order), so 3 barriers instead of ~40.
+    uint32_t* bkey = skey + TK_CAP;  // the running list's keys / ids
+    int64_t* bid = sid + TK_CAP;
+    float* out_s = (float*)(skey + TK_CAP + TK_MAXK);
+    int64_t* out_i = sid + TK_CAP + TK_MAXK;
+    const int tid = threadIdx.x;
+    if (tid < nc) {
+      skey[tid] = cand_key[(int64_t)row * cap + tid];
+      sid[tid] = cand_id[(int64_t)row * cap + tid];
+    }
+    if (tid < k) {
+      bkey[tid] = fkey(bs[tid]);
+      bid[tid] = bi[tid];
+    }
+    __syncthreads();
+    if (tid < nc) {  // candidate tid: running entries and candidates ahead of it
+      const uint32_t kc = skey[tid];
+      const int64_t ic = sid[tid];
+      int pos = 0;
+      for (int i = 0; i < k; ++i) pos += bkey[i] > kc || (bkey[i] == kc && bid[i] <= ic);
+      for (int j = 0; j < nc; ++j) {
+        const uint32_t kj = skey[j];
+        pos += kj > kc || (kj == kc && (sid[j] < ic || (sid[j] == ic && j < tid)));
+      }
+      if (pos < k) { out_s[pos] = kfloat(kc); out_i[pos] = ic; }
+    }
+    if (tid < k) {  // running entry tid: its index + the candidates ahead of it
+      const uint32_t kb = bkey[tid];
+      const int64_t ib = bid[tid];
+      int pos = tid;
+      for (int j = 0; j < nc; ++j) pos += skey[j] > kb || (skey[j] == kb && sid[j] < ib);
+      if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = ib; }
+    }
+    __syncthreads();
+    if (tid < k) {
+      bs[tid] = out_s[tid];
+      bi[tid] = out_i[tid];
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < nc; i += TK_NT) {
     skey[i] = cand_key[(int64_t)row * cap + i];
     sid[i] = cand_id[(int64_t)row * cap + i];
   }
-  sort_keep_k(skey, sid, nc, best_s + (int64_t)row * k, best_i + (int64_t)row * k, k);
+  sort_keep_k(skey, sid, nc, bs, bi, k);
 }
 
 }  // namespace
@@ -219,12 +270,13 @@ FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int6
 }
 
 // candidate lists [B, cap] from fps_score_filter; every cnt[q] must be <= cap (TK_CAP at most)
+// ovf (nullable): set to 1 when some cnt[q] > cap (that row's merge is incomplete)
 FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id, const int32_t* cnt, int cap, int B,
-                                float* best_s, int64_t* best_i, int k, void* stream) {
+                                float* best_s, int64_t* best_i, int k, int32_t* ovf, void* stream) {
   if (B <= 0) return 0;
   if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
-                     best_s, best_i, k);
+                     best_s, best_i, k, ovf);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -19,6 +19,7 @@ seen items excluded (``CollectTopKFromEachWorker``, ``M/matrix/factorization/uti
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -31,16 +32,40 @@ class LempTopK:
         vecs = item_vecs.float().contiguous()
         lengths = torch.linalg.vector_norm(vecs, dim=1)
         order = torch.argsort(lengths, descending=True)
+        #: index position -> row of ``item_vecs`` (incremental updates address rows by it)
+        self.order = order
         self.vecs = vecs[order].contiguous()
         self.ids = item_ids.to(vecs.device).long()[order]
         self.lengths = lengths[order]
         self.bucket = bucket_size
         self.buckets_scanned = 0
         #: GPU: score the first ``seed_items`` items unfused (sets every query's k-th
-        #: best), then fuse scoring with the threshold filter (``ops.score_filter``)
+        #: best), then fuse scoring with the threshold filter; ``sync_free``: the LEMP
+        #: length bound applied per tile on the device (``ops.score_filter_lemp``) and
+        #: overflow flagged on the device, instead of two host syncs per segment
         self.fused = True
+        self.sync_free = os.environ.get("FPS_TOPK_SYNC_SCAN", "0") != "1"
         self.seed_items = 4096
+        #: fused path: test "every query settled" on the host (one sync) only every
+        #: ``break_check`` segments; the device tile bound skips settled work anyway
+        self.break_check = 4
         self.overflows = 0
+        self._suffix = None  # False once rows were updated out of order
+
+    def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
+        """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
+        values) with new vectors, in place: the length order is no longer exact, so the
+        bucket bounds switch to the suffix maximum of the lengths (still exact)."""
+        v = vecs.float()
+        self.vecs[pos] = v
+        self.lengths[pos] = torch.linalg.vector_norm(v, dim=1)
+        self._suffix = False  # the order is stale: bounds take the max of the tail
+
+    def _bound(self, s: int) -> torch.Tensor:
+        """max |x| over index positions >= s (a 0-dim tensor)."""
+        if self._suffix is None:
+            return self.lengths[s]
+        return self.lengths[s:].max()
 
     def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None):
         """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
@@ -49,10 +74,16 @@ class LempTopK:
         B = Q.shape[0]
         dev = Q.device
         qlen = torch.linalg.vector_norm(Q, dim=1)
-        best_s = torch.full((B, k), float("-inf"), device=dev)
-        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
         N = self.vecs.shape[0]
         fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
+        if fused and self.sync_free and N > self.seed_items:
+            res = self._query_fused(Q, qlen, k)
+            if res is not None:
+                return res
+            self.overflows += 1  # some query passed more than cap scores: rescan unfused
+            fused = False
+        best_s = torch.full((B, k), float("-inf"), device=dev)
+        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
         # segments: the first ``seed_items`` (longest) items, then the rest of each bucket
         seed = min(N, self.seed_items) if fused else 0
         bounds = sorted({0, seed, *range(self.bucket, N, self.bucket), N} - {N}) + [N]
@@ -60,7 +91,7 @@ class LempTopK:
         cand = None
         for s, e in zip(bounds[:-1], bounds[1:]):
             # LEMP bucket bound: no item of this or later buckets can beat the k-th best
-            if s > 0 and bool((qlen * self.lengths[s] <= best_s[:, -1]).all()):
+            if s > 0 and bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
             n = e - s
             if s % self.bucket == 0:
@@ -90,6 +121,40 @@ class LempTopK:
                 top_s, top_j = torch.topk(cand_s, min(k, cand_s.shape[1]), dim=1)
                 cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
                 best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
+        return best_s, best_i
+
+    def _query_fused(self, Q, qlen, k):
+        """GPU scan without a host sync per segment: seed segment scored + merged,
+        then per segment the fused 128 x 128 scorer (tiles that cannot beat any of
+        their queries' k-th best skip themselves) and the candidate merge, which
+        flags overflowing rows on the device.  One sync per ``break_check``
+        segments (early exit) and one at the end (overflow -> ``None``: rescan)."""
+        B, dev = Q.shape[0], Q.device
+        N = self.vecs.shape[0]
+        best_s = torch.full((B, k), float("-inf"), device=dev)
+        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+        seed = self.seed_items
+        S = ops.score_gemm(Q, self.vecs[:seed])
+        ops.topk_merge(S, self.ids[:seed], best_s, best_i)
+        del S
+        self.buckets_scanned += 1
+        bounds = sorted({seed, *range(self.bucket, N, self.bucket)}) + [N]
+        cap = ops.TOPK_CAND_CAP
+        ck = torch.empty((B, cap), dtype=torch.int32, device=dev)
+        ci = torch.empty((B, cap), dtype=torch.long, device=dev)
+        cnt = torch.empty(B, dtype=torch.int32, device=dev)
+        ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
+            if self.break_check and j and j % self.break_check == 0 and \
+                    bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
+                break
+            if s % self.bucket == 0:
+                self.buckets_scanned += 1
+            cnt.zero_()
+            ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen, self.lengths[s:e])
+            ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf)
+        if int(ovf.item()):
+            return None
         return best_s, best_i
 
 

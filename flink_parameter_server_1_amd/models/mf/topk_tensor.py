@@ -55,9 +55,19 @@ class SeenStore:
     even if it was re-added since; here it stays excluded while any occurrence is
     inside the window -- documented deviation.)"""
 
-    def __init__(self, memory: int, device):
+    #: dense per-user rings when ``num_users * memory`` is at most this many slots
+    RING_SLOTS = 1 << 28
+
+    def __init__(self, memory: int, device, num_users: Optional[int] = None):
+        """With ``num_users`` known and a small window, the store is a dense ring of
+        the last ``memory`` items per user (``[num_users, memory]`` int32: O(1) add,
+        O(memory) lookup -- the same window semantics); otherwise sorted keys."""
         self.memory = int(memory)
         self.device = torch.device(device)
+        self.ring = None
+        if num_users is not None and 0 < self.memory <= 256 and int(num_users) * self.memory <= self.RING_SLOTS:
+            self.ring = torch.full((int(num_users), self.memory), -1, dtype=torch.int32, device=self.device)
+            self.ring_cur = torch.zeros(int(num_users), dtype=torch.int64, device=self.device)
         self.keys = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.seq = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.ucount_keys = torch.zeros(0, dtype=torch.int64, device=self.device)
@@ -71,6 +81,9 @@ class SeenStore:
 
     def contains(self, users: torch.Tensor, items: torch.Tensor) -> torch.Tensor:
         """``[B, M]`` bool: ``items[b, m]`` is in user ``users[b]``'s window."""
+        if self.ring is not None:
+            R = self.ring[users.long()]  # [B, memory]
+            return (items.to(torch.int32).unsqueeze(2) == R.unsqueeze(1)).any(2) & (items >= 0)
         if self.memory == 0 or self.keys.numel() == 0:
             return torch.zeros(items.shape, dtype=torch.bool, device=items.device)
         u = users.long().view(-1, 1)
@@ -87,6 +100,11 @@ class SeenStore:
         if self.memory == 0 or users.numel() == 0:
             return
         users, items = users.long(), items.long()
+        if self.ring is not None:
+            c = self.ring_cur[users]
+            self.ring[users, c % self.memory] = items.to(torch.int32)
+            self.ring_cur[users] = c + 1
+            return
         cnt = self._user_count(users)
         key = (users << 32) | (items & 0xFFFFFFFF)
         keys = torch.cat([self.keys, key])
@@ -327,8 +345,8 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
     pushes = False
 
     def __init__(self, K: int = 100, worker_k: int = 75, memory: int = 0, bucket_size: int = 4096, pruning=None,
-                 reference_quirks: bool = False):
-        self.K, self.worker_k, self.memory = K, worker_k, memory
+                 reference_quirks: bool = False, num_users: Optional[int] = None):
+        self.K, self.worker_k, self.memory, self.num_users = K, worker_k, memory, num_users
         self.bucket_size, self.pruning, self.quirks = bucket_size, pruning, reference_quirks
         self._ids: List[torch.Tensor] = []
         self._vecs: List[torch.Tensor] = []
@@ -337,7 +355,7 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
     def open(self, ctx):
         self.rank, self.device = ctx.rank, torch.device(ctx.device)
         self.comm = Comm(device=self.device)
-        self.seen = SeenStore(self.memory, self.device)
+        self.seen = SeenStore(self.memory, self.device, self.num_users)
 
     def update_model_batch(self, ids, values):
         """Worker-resident items ``(id, [vec..., len])`` or ``(id, vec)``."""
@@ -374,7 +392,7 @@ def ps_top_k_generator_tensor(queries: Iterable, ps_model, worker_model, num_use
     rank); ``ps_model``: this rank's ``(user, [vec..., len])`` records (``Left``);
     ``worker_model``: this rank's ``(item, [vec..., len])`` records (``Right``).
     Returns rank 0's ``Left(((user, item, ts), scores [B, K], items [B, K]))``."""
-    worker = TopKQueryWorker(K, worker_k, user_memory, bucket_size, pruning_algorithm, reference_quirks)
+    worker = TopKQueryWorker(K, worker_k, user_memory, bucket_size, pruning_algorithm, reference_quirks, num_users)
     logic = DeviceSimplePSLogic(num_users, num_factors + 1, op="set", init=("const", -1.0), track_touched=False)
     logic.emit = "none"
     rt = TensorRuntime(comm, staleness=0)
@@ -389,29 +407,47 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
     on when it is first touched).  Per micro-batch: serve top-K for every rating
     (current items), then the owned ratings' SGD: negatives drawn among this
     rank's initialised items (<= 32 rejections against the user's recent items on
-    this rank), item rows updated in place, the summed user delta pushed."""
+    this rank), item rows updated in place, the summed user delta pushed.
+
+    The LEMP index over the initialised items is built once and then kept current
+    in place (``LempTopK.update_rows`` on the rows the SGD touched); it is rebuilt
+    when new items were initialised and re-sorted every ``resort_every`` batches.
+    Non-owned ratings ride through the SGD masked (no compaction, no host sync)."""
 
     def __init__(self, num_items: int, num_factors: int, learning_rate: float, K: int = 100, worker_k: int = 75,
                  memory: int = 65535, negative_sample_rate: int = 0, bucket_size: int = 4096, pruning=None,
                  range_min: float = -0.001, range_max: float = 0.001, seed: int = 0, neg_memory: int = 128,
-                 reference_quirks: bool = False):
+                 reference_quirks: bool = False, prefill_items: bool = False, num_users: Optional[int] = None,
+                 resort_every: int = 64):
+        """``prefill_items``: every owned item counts as initialised from the start
+        (a warm catalogue, e.g. a benchmark) instead of on its first rating.
+        ``num_users`` (optional) lets the seen store use dense per-user rings."""
         self.num_items, self.dim, self.lr = int(num_items), int(num_factors), learning_rate
         self.K, self.worker_k, self.memory = K, worker_k, memory
         self.neg_rate, self.bucket_size, self.pruning, self.quirks = negative_sample_rate, bucket_size, pruning, \
             reference_quirks
         self.range, self.seed, self.neg_memory = (range_min, range_max), seed, int(neg_memory)
+        self.prefill_items, self.num_users, self.resort_every = prefill_items, num_users, int(resort_every)
+        self.served = 0
+        self.trained = 0
+        self.rebuilds = 0
 
     def open(self, ctx):
         from ...parallel.table import ShardedTable
 
         self.W, self.rank, self.device = ctx.world_size, ctx.rank, torch.device(ctx.device)
         self.comm = Comm(device=self.device)
-        self.seen = SeenStore(self.memory, self.device)
+        self.seen = SeenStore(self.memory, self.device, self.num_users)
         self.items = ShardedTable(self.num_items, self.dim, self.rank, self.W, "hash",
                                   ("uniform", self.range[0], self.range[1]), (self.seed ^ USER_SEED_XOR) & 0xFFFFFFFF,
                                   self.device, track_touched=False)
-        self.valid = torch.zeros(self.items.n_local, dtype=torch.bool, device=self.device)
+        n = self.items.n_local
+        # one spare slot: masked writes of non-owned ratings land there
+        self._valid_buf = torch.full((n + 1,), bool(self.prefill_items), dtype=torch.bool, device=self.device)
+        self.valid = self._valid_buf[:n]
         self.index = None
+        self._stale = True      # the index must be (re)built before the next query
+        self._since_sort = 0
         if self.neg_rate > 0:
             n_u = 1 << 20  # per-user rings are keyed by user id modulo this (bounded state)
             self._ring_users = n_u
@@ -431,20 +467,52 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         ids = self.items.global_ids(loc)
         self.index = PrunedLempTopK(ids, self.items.weight[loc], self.bucket_size, self.pruning, self.quirks) \
             if loc.numel() else None
+        self.rebuilds += 1
+        self._stale = False
+        self._since_sort = 0
+        if self.index is not None:
+            self._index_rows = loc[self.index.order]  # index position -> local row
+            self._pos = torch.full((self.items.n_local,), -1, dtype=torch.long, device=self.device)
+            self._pos[self._index_rows] = torch.arange(loc.numel(), device=self.device)
+
+    def _refresh_index(self, rows: torch.Tensor):
+        """Write the current vectors of local ``rows`` (initialised items; repeats and
+        spurious rows are harmless: every write is the row's current value) into the index."""
+        if self.index is None or self._stale:
+            return
+        if self.pruning is not None or self._since_sort >= self.resort_every:
+            self._stale = True  # LEMP strategies read the sorted order: rebuild instead
+            return
+        p = self._pos[rows]
+        ok = p >= 0
+        rows = torch.where(ok, rows, self._index_rows[0])
+        p = torch.where(ok, p, torch.zeros_like(p))
+        self.index.update_rows(p, self.items.weight[rows])
 
     def on_pull_recv_batch(self, pulled, ps):
         users, items, ts, rating = pulled.payload
         U = pulled.values()  # [B, D] user vectors (length recomputed on the worker)
-        self._rebuild_index()
+        self.served += users.numel()
+        if self._stale or self.index is None:
+            self._rebuild_index()
+        self._since_sort += 1
         self._serve(U, torch.ones(users.numel(), dtype=torch.bool, device=U.device), users, items, ts, ps)
-        # learning: the owner of each rated item
+        # learning: the owner of each rated item (non-owned rows masked, not compacted)
+        n = self.items.n_local
         own = (items.long() % self.W) == self.rank
-        loc = (items.long() // self.W)
-        self.valid[loc[own]] = True  # lazily initialised by the owner (hash init: any order)
+        loc = torch.where(own, items.long() // self.W, torch.zeros_like(items, dtype=torch.long))
+        if not self.prefill_items:
+            # a first rating initialises the item: the index must take it in (one sync)
+            if bool((own & ~self.valid[loc]).any()):
+                self._stale = True
+            self._valid_buf[torch.where(own, loc, torch.full_like(loc, n))] = True
         du = torch.zeros_like(U)
         lr = self.lr
-        if self.neg_rate > 0 and bool(own.any()):
-            ou, oi = users[own].to(torch.int32), items[own].to(torch.int32)
+        W_ = self.items.weight
+        touched = [loc]
+        if self.neg_rate > 0:
+            rows_own = torch.arange(users.numel(), device=U.device) if self.W == 1 else torch.nonzero(own).flatten()
+            ou, oi = users[rows_own].to(torch.int32), items[rows_own].to(torch.int32)
             uring = (ou.long() % self._ring_users).to(torch.int32)
             ops.ring_push(self._ring, self._ring_cur, uring, oi, self.neg_memory)
             ops.known_append(self._known_flag, self._known, self._known_cnt, oi)
@@ -453,25 +521,23 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
                                              counter=self._neg_counter, device=self.device, known=self._known,
                                              known_count=self._known_cnt).view(-1, self.neg_rate)
             self._neg_counter += 1
-            rows_own = torch.nonzero(own).flatten()
+            Ub = U[rows_own]
             for j in range(self.neg_rate):  # reference order: negatives first, then the rating
                 ng = negs[:, j].long()
-                ok = ng >= 0
-                if not bool(ok.any()):
-                    continue
-                b = rows_own[ok]
-                nl = ng[ok] // self.W
-                iv = self.items.weight[nl]
-                e = 0.0 - (U[b] * iv).sum(1)
-                du.index_add_(0, b, lr * e.view(-1, 1) * iv)
-                self.items.weight.index_add_(0, nl, lr * e.view(-1, 1) * U[b])
-        if bool(own.any()):
-            b = torch.nonzero(own).flatten()
-            il = loc[own]
-            iv = self.items.weight[il]
-            e = rating[own] - (U[b] * iv).sum(1)
-            du.index_add_(0, b, lr * e.view(-1, 1) * iv)
-            self.items.weight.index_add_(0, il, lr * e.view(-1, 1) * U[b])
+                okf = (ng >= 0).to(U.dtype).view(-1, 1)
+                nl = torch.where(ng >= 0, ng // self.W, torch.zeros_like(ng))
+                iv = W_[nl]
+                e = 0.0 - (Ub * iv).sum(1, keepdim=True)
+                du.index_add_(0, rows_own, lr * e * iv * okf)
+                W_.index_add_(0, nl, lr * e * Ub * okf)
+                touched.append(nl)
+        ownf = own.to(U.dtype).view(-1, 1)
+        iv = W_[loc]
+        e = rating.view(-1, 1) - (U * iv).sum(1, keepdim=True)
+        du += lr * e * iv * ownf
+        W_.index_add_(0, loc, lr * e * U * ownf)
+        self._refresh_index(torch.cat(touched))
+        self.trained += users.numel() // self.W * (1 + self.neg_rate)  # expected owned share (no sync)
         ps.push(du, mask=own)
 
 
@@ -486,7 +552,8 @@ def ps_online_learner_and_generator_tensor(batches: Iterable, num_users: int, nu
     every rank).  Outputs: rank 0's top-K records (``Left``) and every rank's PS
     user updates ``Right((users, vectors))`` (``SimplePSLogic`` emits on push)."""
     worker = OnlineMFTopKWorker(num_items, num_factors, learning_rate, K, worker_k, user_memory,
-                                negative_sample_rate, bucket_size, pruning_algorithm, range_min, range_max, seed)
+                                negative_sample_rate, bucket_size, pruning_algorithm, range_min, range_max, seed,
+                                num_users=num_users)
     logic = DeviceSimplePSLogic(num_users, num_factors, op="add_renorm", init=("uniform", range_min, range_max),
                                 seed=seed)
     rt = TensorRuntime(comm, staleness=0, output_sink=output_sink)

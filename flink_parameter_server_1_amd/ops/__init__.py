@@ -810,12 +810,39 @@ def score_filter(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: to
             "score_filter")
 
 
+def score_filter_lemp(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor,
+                      cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Tensor,
+                      qlen: Optional[torch.Tensor] = None, xlen: Optional[torch.Tensor] = None) -> None:
+    """``score_filter`` with the LEMP length bound applied per 64 x 64 tile on the device:
+    with ``qlen`` [B] / ``xlen`` [n] (vector norms), a tile none of whose
+    queries can be beaten by its longest item (``|q| max|x| <= best_s[q, -1]``, with an
+    fp32 rounding slack) is skipped -- exact, and no host sync."""
+    B, D = Q.shape
+    n = X.shape[0]
+    cap = cand_key.shape[1]
+    if X.shape[1] != D or ids.numel() != n or best_s.shape[0] != B or cnt.numel() != B or cand_id.shape != (B, cap):
+        raise ValueError("score_filter_lemp: shape mismatch")
+    if (qlen is None) != (xlen is None):
+        raise ValueError("score_filter_lemp: qlen and xlen go together")
+    if qlen is not None and (qlen.numel() != B or xlen.numel() != n):
+        raise ValueError("score_filter_lemp: qlen [B] / xlen [n]")
+    slack = 1.0 + 1e-4 + D * 2.4e-7  # > the relative fp32 error of a D-term dot product and of |q| |x|
+    N.check(N.require().fps_score_filter_lemp(
+        _c(Q).data_ptr(), _c(X).data_ptr(), _c(ids).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
+        None if qlen is None else _c(qlen.float()).data_ptr(), None if xlen is None else _c(xlen.float()).data_ptr(),
+        slack, _c(cand_key).data_ptr(), _c(cand_id).data_ptr(), _c(cnt).data_ptr(), cap, N.stream_ptr(Q.device)),
+        "score_filter_lemp")
+
+
 def topk_merge_cand(cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Tensor, best_s: torch.Tensor,
-                    best_i: torch.Tensor) -> None:
-    """Merge ``score_filter`` candidate lists into the running top-k in place (K13)."""
+                    best_i: torch.Tensor, overflow: Optional[torch.Tensor] = None) -> None:
+    """Merge ``score_filter`` candidate lists into the running top-k in place (K13).
+    ``overflow`` (int32 [1]): set to 1 on the device when a row had more than ``cap``
+    candidates (its merge is incomplete; the caller rescans)."""
     B, cap = cand_key.shape
     N.check(N.require().fps_topk_merge_cand(_c(cand_key).data_ptr(), _c(cand_id).data_ptr(), _c(cnt).data_ptr(), cap,
                                             B, _c(best_s).data_ptr(), _c(best_i).data_ptr(), best_s.shape[1],
+                                            None if overflow is None else overflow.data_ptr(),
                                             N.stream_ptr(best_s.device)), "topk_merge_cand")
 
 

@@ -201,18 +201,31 @@ def _shard_file_coords(path: str):
     return (int(m.group(1)), int(m.group(2))) if m else None
 
 
+def snapshot_meta(path: str) -> dict:
+    """A snapshot's header (partitioner kind, num ids, dim, world, rank, rows, step)
+    without reading its rows."""
+    L = NH.lib()
+    if L is not None:
+        meta = np.zeros(7, dtype=np.int64)
+        if L.fps_read_snapshot_header(path.encode(), NH._p(meta)) == 0:
+            return dict(zip(["part_kind", "num_ids", "dim", "world", "rank", "n_rows", "step"], meta.tolist()))
+    return load_snapshot(path)[0]
+
+
 def shard_files_for(table, files: List[str]) -> List[str]:
-    """The shard files that can hold ids this rank owns: with hash partitioning a
-    file of shard ``r`` of ``W`` (ids ``= r mod W``) overlaps shard ``r'`` of ``W'``
-    iff ``r = r' (mod gcd(W, W'))`` -- only its own file when the world size is
-    unchanged; with range partitioning the id ranges are intersected.  Lookup
-    (custom) partitioning and unnamed files: every file."""
+    """The shard files that can hold ids this rank owns, when the files were written
+    with the same partitioning as ``table`` (header ``part_kind``): with hash
+    partitioning a file of shard ``r`` of ``W`` (ids ``= r mod W``) overlaps shard
+    ``r'`` of ``W'`` iff ``r = r' (mod gcd(W, W'))`` -- only its own file when the
+    world size is unchanged; with range partitioning the id ranges are
+    intersected.  A different partitioning (e.g. hash shards restored into a
+    range-partitioned table), lookup partitioning and unnamed files: every file."""
     from math import gcd
 
     out = []
     for f in files:
         c = _shard_file_coords(f)
-        if c is None or table.partition == "lookup":
+        if c is None or table.partition == "lookup" or snapshot_meta(f)["part_kind"] != table.part_kind:
             out.append(f)
             continue
         r, w = c

@@ -35,8 +35,10 @@ def test_pruned_lemp_is_exact(strategy):
         assert idx.pruned > 0  # the masks did skip candidates
 
 
-def test_seen_store_window_and_rounds():
-    st = SeenStore(2, "cpu")
+@pytest.mark.parametrize("num_users", [None, 5])  # sorted keys / dense per-user rings
+def test_seen_store_window_and_rounds(num_users):
+    st = SeenStore(2, "cpu", num_users)
+    assert (st.ring is not None) == (num_users is not None)
     ref = {}
     rng = np.random.default_rng(0)
     for step in range(200):
