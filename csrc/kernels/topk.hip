@@ -186,74 +186,86 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
 }
 
 // Candidate lists from the fused scoring (score_gemm.hip: score_filter_kernel):
-// query row's cnt[row] (<= cap, checked by the caller) candidates are merged into
-// its running top-k exactly as above.
-__global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* __restrict__ cand_key,
+// query row's cnt[row] candidates are merged into its running top-k.  Two
+// kernels split the rows: few candidates (<= TK_NT: every segment after the
+// first of a length-sorted scan) merge by rank in a small-LDS kernel, more
+// keep the bitonic sort.
+
+// rank merge: each candidate's and each kept entry's final position is the
+// number of entries ahead of it (key desc, then id asc; the running list is
+// already in that order) -- 3 barriers instead of the sort's ~40, 6 KB of LDS.
+// Also flags overflowed rows (cnt > cap: merged incompletely) in ovf.
+__global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* __restrict__ cand_key,
                                                                 const int64_t* __restrict__ cand_id,
                                                                 const int32_t* __restrict__ cnt, int cap,
                                                                 float* __restrict__ best_s,
                                                                 int64_t* __restrict__ best_i, int k,
                                                                 int32_t* __restrict__ ovf) {
-  __shared__ uint32_t skey[TK_SORT];
-  __shared__ int64_t sid[TK_SORT];
-  const int row = blockIdx.x;
+  __shared__ uint32_t ckey[TK_NT];
+  __shared__ int64_t cid[TK_NT];
+  __shared__ uint32_t bkey[TK_MAXK];
+  __shared__ int64_t bid[TK_MAXK];
+  __shared__ float out_s[TK_MAXK];
+  __shared__ int64_t out_i[TK_MAXK];
+  const int row = blockIdx.x, tid = threadIdx.x;
   const int c = cnt[row];
   // an overflowed row (more than cap passed the filter) is merged incompletely: flag it
   // for the caller, which checks once per query batch (no host sync per segment)
-  if (ovf != nullptr && c > cap && threadIdx.x == 0) ovf[0] = 1;
+  if (ovf != nullptr && c > cap && tid == 0) ovf[0] = 1;
   const int nc = min(min(c, cap), TK_CAP);
-  if (nc == 0) return;  // nothing beat the k-th best: the list stands
+  if (nc == 0 || nc > TK_NT) return;  // nothing to merge / the bitonic kernel's row
   float* bs = best_s + (int64_t)row * k;
   int64_t* bi = best_i + (int64_t)row * k;
-  if (nc <= TK_NT) {
-    // few candidates (every segment after the first): merge by rank instead of a
-    // full bitonic sort -- each candidate's and each kept entry's final position is
-    // the number of entries ahead of it (key desc, then id asc; the running list is
-    // already in that order), so 3 barriers instead of ~40.
-    uint32_t* bkey = skey + TK_CAP;  // the running list's keys / ids
-    int64_t* bid = sid + TK_CAP;
-    float* out_s = (float*)(skey + TK_CAP + TK_MAXK);
-    int64_t* out_i = sid + TK_CAP + TK_MAXK;
-    const int tid = threadIdx.x;
-    if (tid < nc) {
-      skey[tid] = cand_key[(int64_t)row * cap + tid];
-      sid[tid] = cand_id[(int64_t)row * cap + tid];
-    }
-    if (tid < k) {
-      bkey[tid] = fkey(bs[tid]);
-      bid[tid] = bi[tid];
-    }
-    __syncthreads();
-    if (tid < nc) {  // candidate tid: running entries and candidates ahead of it
-      const uint32_t kc = skey[tid];
-      const int64_t ic = sid[tid];
-      int pos = 0;
-      for (int i = 0; i < k; ++i) pos += bkey[i] > kc || (bkey[i] == kc && bid[i] <= ic);
-      for (int j = 0; j < nc; ++j) {
-        const uint32_t kj = skey[j];
-        pos += kj > kc || (kj == kc && (sid[j] < ic || (sid[j] == ic && j < tid)));
-      }
-      if (pos < k) { out_s[pos] = kfloat(kc); out_i[pos] = ic; }
-    }
-    if (tid < k) {  // running entry tid: its index + the candidates ahead of it
-      const uint32_t kb = bkey[tid];
-      const int64_t ib = bid[tid];
-      int pos = tid;
-      for (int j = 0; j < nc; ++j) pos += skey[j] > kb || (skey[j] == kb && sid[j] < ib);
-      if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = ib; }
-    }
-    __syncthreads();
-    if (tid < k) {
-      bs[tid] = out_s[tid];
-      bi[tid] = out_i[tid];
-    }
-    return;
+  if (tid < nc) {
+    ckey[tid] = cand_key[(int64_t)row * cap + tid];
+    cid[tid] = cand_id[(int64_t)row * cap + tid];
   }
+  if (tid < k) {
+    bkey[tid] = fkey(bs[tid]);
+    bid[tid] = bi[tid];
+  }
+  __syncthreads();
+  if (tid < nc) {  // candidate tid: running entries and candidates ahead of it
+    const uint32_t kc = ckey[tid];
+    const int64_t ic = cid[tid];
+    int pos = 0;
+    for (int i = 0; i < k; ++i) pos += bkey[i] > kc || (bkey[i] == kc && bid[i] <= ic);
+    for (int j = 0; j < nc; ++j) {
+      const uint32_t kj = ckey[j];
+      pos += kj > kc || (kj == kc && (cid[j] < ic || (cid[j] == ic && j < tid)));
+    }
+    if (pos < k) { out_s[pos] = kfloat(kc); out_i[pos] = ic; }
+  }
+  if (tid < k) {  // running entry tid: its index + the candidates ahead of it
+    const uint32_t kb = bkey[tid];
+    const int64_t ib = bid[tid];
+    int pos = tid;
+    for (int j = 0; j < nc; ++j) pos += ckey[j] > kb || (ckey[j] == kb && cid[j] < ib);
+    if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = ib; }
+  }
+  __syncthreads();
+  if (tid < k) {
+    bs[tid] = out_s[tid];
+    bi[tid] = out_i[tid];
+  }
+}
+
+// bitonic merge of the rows with more than TK_NT candidates (<= TK_CAP kept)
+__global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* __restrict__ cand_key,
+                                                                const int64_t* __restrict__ cand_id,
+                                                                const int32_t* __restrict__ cnt, int cap,
+                                                                float* __restrict__ best_s,
+                                                                int64_t* __restrict__ best_i, int k) {
+  __shared__ uint32_t skey[TK_SORT];
+  __shared__ int64_t sid[TK_SORT];
+  const int row = blockIdx.x;
+  const int nc = min(min(cnt[row], cap), TK_CAP);
+  if (nc <= TK_NT) return;  // the rank kernel's row
   for (int i = threadIdx.x; i < nc; i += TK_NT) {
     skey[i] = cand_key[(int64_t)row * cap + i];
     sid[i] = cand_id[(int64_t)row * cap + i];
   }
-  sort_keep_k(skey, sid, nc, bs, bi, k);
+  sort_keep_k(skey, sid, nc, best_s + (int64_t)row * k, best_i + (int64_t)row * k, k);
 }
 
 }  // namespace
@@ -275,8 +287,11 @@ FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id
                                 float* best_s, int64_t* best_i, int k, int32_t* ovf, void* stream) {
   if (B <= 0) return 0;
   if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
+  hipLaunchKernelGGL(topk_merge_rank_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
                      best_s, best_i, k, ovf);
+  FPS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
+                     best_s, best_i, k);
   FPS_CHECK_LAUNCH();
   return 0;
 }

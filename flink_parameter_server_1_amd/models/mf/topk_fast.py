@@ -49,6 +49,8 @@ class LempTopK:
         #: fused path: test "every query settled" on the host (one sync) only every
         #: ``break_check`` segments; the device tile bound skips settled work anyway
         self.break_check = 4
+        #: fused path: segments double from ``seed_items`` up to the bucket size
+        self.geometric = True
         self.overflows = 0
         self._suffix = None  # False once rows were updated out of order
 
@@ -138,7 +140,15 @@ class LempTopK:
         ops.topk_merge(S, self.ids[:seed], best_s, best_i)
         del S
         self.buckets_scanned += 1
-        bounds = sorted({seed, *range(self.bucket, N, self.bucket)}) + [N]
+        # segments grow geometrically up to the bucket size: a segment of n items after
+        # s scanned ones passes ~k ln(1 + n / s) scores per query, so doubling keeps
+        # every merge on the small rank path (one 4096 -> 65536 step passed ~1100)
+        cuts = {*range(self.bucket, N, self.bucket)}
+        c = seed if self.geometric else N
+        while c < min(N, self.bucket):
+            cuts.add(c)
+            c *= 2
+        bounds = sorted(cuts) + [N]
         cap = ops.TOPK_CAND_CAP
         ck = torch.empty((B, cap), dtype=torch.int32, device=dev)
         ci = torch.empty((B, cap), dtype=torch.long, device=dev)
