@@ -1,0 +1,17 @@
+#!/bin/bash
+# Multi-rank rehearsal on a one-GPU box: 2 and 4 ranks share cuda:0 over gloo (host-staged
+# transport) and run bench.py end to end (tiled SGD + item-block ring rotation + user
+# phases, and the PS exchange), plus the tiled GPU tests.
+set -e
+mkdir -p gpurun_out/rehearse
+export TMPDIR=/tmp FPS_SHARE_GPU=1
+timeout -k 10 300 python -u -m pytest tests/test_mf_tiled_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/rehearse/tiled_tests.log 2>&1 || { tail -30 gpurun_out/rehearse/tiled_tests.log; exit 1; }
+tail -1 gpurun_out/rehearse/tiled_tests.log
+timeout -k 10 300 python bench.py --gpus 2 --steps 4 --warmup 1 --batch 4194304 > gpurun_out/rehearse/share2.log 2>&1 || { tail -30 gpurun_out/rehearse/share2.log; exit 1; }
+tail -1 gpurun_out/rehearse/share2.log | cut -c1-400
+timeout -k 10 300 python bench.py --gpus 2 --steps 4 --warmup 1 --batch 4194304 --exchange ps > gpurun_out/rehearse/share2ps.log 2>&1 || { tail -30 gpurun_out/rehearse/share2ps.log; exit 1; }
+tail -1 gpurun_out/rehearse/share2ps.log | cut -c1-400
+timeout -k 10 300 python bench.py --gpus 4 --steps 3 --warmup 1 --batch 2097152 --users 2000000 > gpurun_out/rehearse/share4.log 2>&1 || { tail -30 gpurun_out/rehearse/share4.log; exit 1; }
+tail -1 gpurun_out/rehearse/share4.log | cut -c1-400
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench/bench_mf_topk.py --users 100000 --items 200000 --batch 1024 --steps 3 --warmup 1 > gpurun_out/rehearse/mftopk2.log 2>&1 || { tail -30 gpurun_out/rehearse/mftopk2.log; exit 1; }
+tail -1 gpurun_out/rehearse/mftopk2.log | cut -c1-300
