@@ -31,6 +31,8 @@ def main(argv=None):
     ap.add_argument("--kind", default="binary", choices=["binary", "ova", "pb", "ml"])
     ap.add_argument("--labels", type=int, default=1)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--ps-path", action="store_true",
+                    help="N = 1: run the pull / push protocol through the tensor engine instead of updating in place")
     a = ap.parse_args(argv)
 
     import torch
@@ -40,7 +42,8 @@ def main(argv=None):
 
     comm = Comm.init_from_env()
     dev = comm.device
-    m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire),
+    m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire,
+                               local_direct=not a.ps_path),
                       comm)
     batches = [synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=comm.rank + 1, step=s, label_count=a.labels,
                                       device=dev, zipf=a.zipf) for s in range(4)]

@@ -30,6 +30,10 @@ def main(argv=None):
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--lr", type=float, default=0.005)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--neg-group", type=int, default=None, choices=[1, 2, 4],
+                    help="32-pair blocks sharing one set of negatives (default: SGNSConfig)")
+    ap.add_argument("--ps-path", action="store_true",
+                    help="N = 1: run the pull / push protocol instead of updating the tables in place")
     ap.add_argument("--shared-negatives", type=int, default=16, choices=[16, 32],
                     help="negatives shared by each block of 32 pairs (16: kernel v4, 32: kernel v3)")
     a = ap.parse_args(argv)
@@ -43,7 +47,9 @@ def main(argv=None):
     comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
-                                   wire_dtype=a.wire, shared_negatives=a.shared_negatives), comm=comm)
+                                   wire_dtype=a.wire, shared_negatives=a.shared_negatives,
+                                   local_direct=not a.ps_path,
+                                   **({} if a.neg_group is None else {"neg_group": a.neg_group})), comm=comm)
     toks = synthetic_corpus(max(a.pairs // a.window, 1 << 16) * 2, a.vocab, seed=comm.rank, device=dev)
     c, o = skipgram_pairs(toks, a.window)
     n = c.numel()
@@ -78,6 +84,7 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
             "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared {a.shared_negatives}/block)",
+                       "neg_group": m.cfg.neg_group,
                        "exchange": "local-direct" if m._direct else "ps",
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)

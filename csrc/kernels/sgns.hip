@@ -243,8 +243,14 @@ constexpr int K4 = 16;
 constexpr int NT4 = 512;
 constexpr int NW4 = NT4 / 64;
 
-template <bool BF16>
-__global__ void __launch_bounds__(NT4) sgns_v4_kernel(const void* __restrict__ rows_in,
+// GROUP > 1: GROUP consecutive blocks of 32 pairs share one set of K4 negatives
+// (pos_neg holds K4 rows per 32 * GROUP pairs).  The negative rows are staged once
+// per group and their gradient dN = sum over the group's blocks of G^T H stays in
+// registers until the group ends: per 32 pairs the dN float atomics (16 of the
+// ~33 rows a v4 block pushes) and the N staging loads shrink by 1 / GROUP.  Each
+// pair still sees K4 negatives of weight negatives / K4 (same expected gradient).
+template <bool BF16, int GROUP>
+__global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))) sgns_v4_kernel(const void* __restrict__ rows_in,
                                                       const void* __restrict__ rows_out,
                                                       const int32_t* __restrict__ pos_c,
                                                       const int32_t* __restrict__ pos_o,
@@ -264,167 +270,234 @@ __global__ void __launch_bounds__(NT4) sgns_v4_kernel(const void* __restrict__ r
   int32_t* lead = pn + K4;          // [M] first pair of the block with the same context
   int32_t* nxt = lead + M;          // [M] next pair with the same context (-1: none)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t n_blocks = (n_pairs + M - 1) / M;
+  const int64_t n_groups = (n_pairs + M * GROUP - 1) / (M * GROUP);
   constexpr int RPW = (M + K4) / NW4;  // staged rows per wave (6)
+  const int ntile = Dp / 32;
+  const int i = lane & 31, kh = lane >> 5;
 
-  for (int64_t blk = blockIdx.x; blk < n_blocks; blk += gridDim.x) {
-    const int64_t p0 = blk * M;
-    const int npairs = (int)((n_pairs - p0) < M ? (n_pairs - p0) : M);
-    if (tid < M) {
-      pc[tid] = tid < npairs ? pos_c[p0 + tid] : -1;
-      po[tid] = tid < npairs ? pos_o[p0 + tid] : -1;
-    } else if (tid < M + K4) {
-      pn[tid - M] = pos_neg[blk * K4 + (tid - M)];
-    }
-    __syncthreads();
-    if (tid < M) {  // adjacent centers share most of their window: one dO row per distinct
-                    // context (12.9 distinct contexts per 32 pairs on the bench corpus)
-      int l = tid, nx = -1;
-      for (int j = 0; j < tid; ++j)
-        if (po[j] == po[tid]) { l = j; break; }
-      for (int j = tid + 1; j < M; ++j)
-        if (po[j] == po[tid]) { nx = j; break; }
-      lead[tid] = l;
-      nxt[tid] = nx;
-    }
-    {
-      float4 v[RPW][2];
+  for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+    // dN accumulators of this wave's (<= 2) negative-gradient column tiles t = wave + 8 j,
+    // t >= ntile, kept across the group's blocks
+    floatx16 dn0 = {0}, dn1 = {0};
+    for (int sb = 0; sb < GROUP; ++sb) {
+      const int64_t p0 = (grp * GROUP + sb) * M;
+      if (p0 >= n_pairs) break;  // uniform: the group's tail
+      const int npairs = (int)((n_pairs - p0) < M ? (n_pairs - p0) : M);
+      if (tid < M) {
+        pc[tid] = tid < npairs ? pos_c[p0 + tid] : -1;
+        po[tid] = tid < npairs ? pos_o[p0 + tid] : -1;
+      } else if (sb == 0 && tid < M + K4) {
+        pn[tid - M] = pos_neg[grp * K4 + (tid - M)];
+      }
+      __syncthreads();
+      if (wave == 0) {  // adjacent centers share most of their window: one dO row per distinct
+                        // context (12.9 distinct contexts per 32 pairs on the bench corpus).
+                        // Lane t < 32 finds the pairs with its context by register shuffles
+                        // (the LDS scan it replaces was two dependent 32-step loops).
+        const int mine = lane < M ? po[lane] : -2;
+        uint32_t same = 0u;
 #pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        const int r = wave + NW4 * j;
-        const bool is_h = r < M;
-        const int32_t rr = is_h ? pc[r] : pn[r - M];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = lane * 4 + 256 * h;
-          v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < M; ++j) same |= (uint32_t)(__shfl(mine, j, 64) == mine) << j;
+        if (lane < M) {
+          const uint32_t above = same & ~((2u << lane) - 1u);  // matches after this pair
+          lead[lane] = __ffs(same) - 1;                        // first match (itself at the latest)
+          nxt[lane] = above ? __ffs(above) - 1 : -1;
         }
       }
+      {
+        float4 v[RPW][2];
 #pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        const int r = wave + NW4 * j;
-        float* dst = r < M ? Hs + r * LD : Ns + (r - M) * LD;
+        for (int j = 0; j < RPW; ++j) {
+          const int r = wave + NW4 * j;
+          const bool is_h = r < M;
+          const int32_t rr = is_h ? pc[r] : (sb == 0 ? pn[r - M] : -1);  // N rows: once per group
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = lane * 4 + 256 * h;
-          if (c < Dp) { dst[c] = v[j][h].x; dst[c + 1] = v[j][h].y; dst[c + 2] = v[j][h].z; dst[c + 3] = v[j][h].w; }
+          for (int h = 0; h < 2; ++h) {
+            const int c = lane * 4 + 256 * h;
+            v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+          const int r = wave + NW4 * j;
+          if (r >= M && sb > 0) continue;  // keep the group's staged negatives
+          float* dst = r < M ? Hs + r * LD : Ns + (r - M) * LD;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = lane * 4 + 256 * h;
+            if (c < Dp) { dst[c] = v[j][h].x; dst[c + 1] = v[j][h].y; dst[c + 2] = v[j][h].z; dst[c + 3] = v[j][h].w; }
+          }
         }
       }
-    }
-    __syncthreads();
-    if (wave < 2) {
-      // ---- S = H N^T [32 x 16]: one 16x16 tile per wave over the full D
-      const int i = lane & 15, kq = lane >> 4;
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* hrow = Hs + (16 * wave + i) * LD + kq;
-      const float* nrow = Ns + i * LD + kq;
-      for (int k = 0; k < Dp; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc, 0, 0, 0);
-      float lsum = 0.f;
+      __syncthreads();
+      if (wave < 2) {
+        // ---- S = H N^T [32 x 16]: one 16x16 tile per wave over the full D
+        const int ii = lane & 15, kq = lane >> 4;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* hrow = Hs + (16 * wave + ii) * LD + kq;
+        const float* nrow = Ns + ii * LD + kq;
+        for (int k = 0; k < Dp; k += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc, 0, 0, 0);
+        float lsum = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * wave + 4 * kq + r;
-        const bool ok = m < npairs;
-        const float sg = sigmoidf_(acc[r]);
-        Gs[m * (K4 + 1) + i] = ok ? -lr * neg_weight * sg : 0.f;
-        if (ok) lsum += -neg_weight * __logf(1.f - sg + 1e-12f);
-      }
-      if (loss_out) {
-        lsum = group_sum<64>(lsum);
-        if (lane == 0) atomicAdd(loss_out, lsum);
-      }
-    } else {
-      // ---- positive scores h.o (O read from global, coalesced), waves 2..7
-      for (int m = wave - 2; m < M; m += NW4 - 2) {
-        float p = 0.f;
-        if (m < npairs) {
-#pragma unroll 5
-          for (int c = lane; c < D; c += 64) p = fmaf(Hs[m * LD + c], ld1<BF16>(rows_out, (int64_t)po[m] * D + c), p);
-        }
-        p = group_sum<64>(p);
-        if (lane == 0) {
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * wave + 4 * kq + r;
           const bool ok = m < npairs;
-          gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
-          if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
+          const float sg = sigmoidf_(acc[r]);
+          Gs[m * (K4 + 1) + ii] = ok ? -lr * neg_weight * sg : 0.f;
+          if (ok) lsum += -neg_weight * __logf(1.f - sg + 1e-12f);
         }
-      }
-    }
-    __syncthreads();
-    // ---- dH = G N + g+ O [32 x 32 cols] and dN = G^T H [16 (of 32) x 32 cols]
-    const int ntile = Dp / 32;
-    const int i = lane & 31, kh = lane >> 5;
-    for (int t = wave; t < 2 * ntile; t += NW4) {
-      const bool is_h = t < ntile;
-      const int c0 = (is_h ? t : t - ntile) * 32;
-      const int col = c0 + i;
-      floatx16 acc = {0};
-      if (is_h) {
-#pragma unroll
-        for (int kk = 0; kk < K4; kk += 2) {
-          const int k = kk + kh;
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[i * (K4 + 1) + k], Ns[k * LD + c0 + i], acc, 0, 0, 0);
+        if (loss_out) {
+          lsum = group_sum<64>(lsum);
+          if (lane == 0) atomicAdd(loss_out, lsum);
         }
-        float v[16], o[16];
+      } else if (Dp <= 320) {
+        // ---- positive scores h.o, waves 2..7: every O value this wave needs (its <= 6
+        // pairs x 5 columns per lane) is loaded before the first is used -- one global
+        // latency per block instead of one per pair
+        constexpr int KP = (M + NW4 - 3) / (NW4 - 2), JP = 5;
+        const int w2 = wave - 2;
+        float ov[KP][JP];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = acc_row(lane, r);
-          v[r] = acc[r];
-          if (row < npairs && col < D) v[r] += gpos[row] * ld1<BF16>(rows_out, (int64_t)po[row] * D + col);
+        for (int k = 0; k < KP; ++k) {
+          const int m = w2 + (NW4 - 2) * k;
+#pragma unroll
+          for (int j = 0; j < JP; ++j) {
+            const int c = lane + 64 * j;
+            ov[k][j] = (m < npairs && c < D) ? ld1<BF16>(rows_out, (int64_t)po[m] * D + c) : 0.f;
+          }
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
-        // this half-wave (kh) owns rows 16*kh .. 16*kh+15 of column col; row q sits in
-        // register (q&3) + 4*(q>>3) of the lane half whose (q>>2)&1 matches
-        const int r1 = min(16, npairs - 16 * kh);
-        float run = 0.f;
+        for (int k = 0; k < KP; ++k) {
+          const int m = w2 + (NW4 - 2) * k;
+          if (m >= M) break;  // uniform in the wave
+          float p = 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int ri0 = (j & 3) + 4 * (j >> 3);         // q = j      (kh = 0)
-          const int ri1 = (j & 3) + 4 * (2 + (j >> 3));   // q = 16 + j (kh = 1)
-          const float a0 = (j & 4) ? o[ri0] : v[ri0];
-          const float a1 = (j & 4) ? v[ri1] : o[ri1];
-          const float val = kh ? a1 : a0;
-          if (j < r1) {
-            const int q = 16 * kh + j;
-            run += val;
-            if (j + 1 == r1 || pc[q + 1] != pc[q]) {
-              if (col < D) atomic_add_noret(d_in + (int64_t)pc[q] * D + col, run);
-              run = 0.f;
-            }
+          for (int j = 0; j < JP; ++j) {
+            const int c = lane + 64 * j;
+            if (c < D) p = fmaf(Hs[m * LD + c], ov[k][j], p);
+          }
+          p = group_sum<64>(p);
+          if (lane == 0) {
+            const bool ok = m < npairs;
+            gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
+            if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
           }
         }
       } else {
-#pragma unroll
-        for (int kk = 0; kk < M; kk += 2) {
-          const int k = kk + kh;
-          const float a = i < K4 ? Gs[k * (K4 + 1) + i] : 0.f;
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Hs[k * LD + c0 + i], acc, 0, 0, 0);
+        // ---- positive scores h.o (O read from global, coalesced), waves 2..7
+        for (int m = wave - 2; m < M; m += NW4 - 2) {
+          float p = 0.f;
+          if (m < npairs) {
+#pragma unroll 5
+            for (int c = lane; c < D; c += 64) p = fmaf(Hs[m * LD + c], ld1<BF16>(rows_out, (int64_t)po[m] * D + c), p);
+          }
+          p = group_sum<64>(p);
+          if (lane == 0) {
+            const bool ok = m < npairs;
+            gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
+            if (ok && loss_out) atomicAdd(loss_out, -__logf(sigmoidf_(p) + 1e-12f));
+          }
         }
+      }
+      __syncthreads();
+      // ---- dH = G N + g+ O [32 x 32 cols] (pushed) and dN += G^T H [16 (of 32) x 32 cols]
+      int slot = 0;
+      for (int t = wave; t < 2 * ntile; t += NW4) {
+        const bool is_h = t < ntile;
+        const int c0 = (is_h ? t : t - ntile) * 32;
+        const int col = c0 + i;
+        if (is_h) {
+          floatx16 acc = {0};
+#pragma unroll
+          for (int kk = 0; kk < K4; kk += 2) {
+            const int k = kk + kh;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[i * (K4 + 1) + k], Ns[k * LD + c0 + i], acc, 0, 0, 0);
+          }
+          float v[16], o[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = acc_row(lane, r);
+            v[r] = acc[r];
+            if (row < npairs && col < D) v[r] += gpos[row] * ld1<BF16>(rows_out, (int64_t)po[row] * D + col);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
+          // this half-wave (kh) owns rows 16*kh .. 16*kh+15 of column col; row q sits in
+          // register (q&3) + 4*(q>>3) of the lane half whose (q>>2)&1 matches
+          const int r1 = min(16, npairs - 16 * kh);
+          float run = 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int ri0 = (j & 3) + 4 * (j >> 3);         // q = j      (kh = 0)
+            const int ri1 = (j & 3) + 4 * (2 + (j >> 3));   // q = 16 + j (kh = 1)
+            const float a0 = (j & 4) ? o[ri0] : v[ri0];
+            const float a1 = (j & 4) ? v[ri1] : o[ri1];
+            const float val = kh ? a1 : a0;
+            if (j < r1) {
+              const int q = 16 * kh + j;
+              run += val;
+              if (j + 1 == r1 || pc[q + 1] != pc[q]) {
+                if (col < D) atomic_add_noret(d_in + (int64_t)pc[q] * D + col, run);
+                run = 0.f;
+              }
+            }
+          }
+        } else {
+          floatx16 acc = {0};
+          if constexpr (GROUP > 1) acc = slot == 0 ? dn0 : dn1;
+#pragma unroll
+          for (int kk = 0; kk < M; kk += 2) {
+            const int k = kk + kh;
+            const float a = i < K4 ? Gs[k * (K4 + 1) + i] : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Hs[k * LD + c0 + i], acc, 0, 0, 0);
+          }
+          if constexpr (GROUP == 1) {  // v4: pushed at once
+            if (col < D) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) atomic_add_noret(d_out + (int64_t)pn[acc_row(lane, r)] * D + col, acc[r]);
+            }
+          } else {
+            if (slot == 0) dn0 = acc; else dn1 = acc;
+            ++slot;
+          }
+        }
+      }
+      // ---- dO = g+ H summed over the pairs of one context: one wave per distinct
+      // context, 256-B atomic wave-instructions
+      for (int m = wave; m < npairs; m += NW4) {
+        if (lead[m] != m) continue;  // uniform in the wave
+        float a[(512 + 63) / 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = 0.f;
+        for (int q = m; q >= 0 && q < npairs; q = nxt[q]) {
+          const float g = gpos[q];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (lane + 64 * u < D) a[u] += g * Hs[q * LD + lane + 64 * u];
+        }
+        float* dst = d_out + (int64_t)po[m] * D;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (lane + 64 * u < D) atomic_add_noret(dst + lane + 64 * u, a[u]);
+      }
+      __syncthreads();
+    }
+    if constexpr (GROUP > 1) {
+      // ---- the group's negative gradients, once
+      int slot = 0;
+      for (int t = wave; t < 2 * ntile; t += NW4) {
+        if (t < ntile) continue;
+        const int col = (t - ntile) * 32 + i;
+        const floatx16 acc = slot == 0 ? dn0 : dn1;
         if (col < D) {
 #pragma unroll
           for (int r = 0; r < 8; ++r) atomic_add_noret(d_out + (int64_t)pn[acc_row(lane, r)] * D + col, acc[r]);
         }
+        ++slot;
       }
+      __syncthreads();  // pn is rewritten by the next group
     }
-    // ---- dO = g+ H summed over the pairs of one context: one wave per distinct
-    // context, 256-B atomic wave-instructions
-    for (int m = wave; m < npairs; m += NW4) {
-      if (lead[m] != m) continue;  // uniform in the wave
-      float a[(512 + 63) / 64];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = 0.f;
-      for (int q = m; q >= 0 && q < npairs; q = nxt[q]) {
-        const float g = gpos[q];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (lane + 64 * u < D) a[u] += g * Hs[q * LD + lane + 64 * u];
-      }
-      float* dst = d_out + (int64_t)po[m] * D;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (lane + 64 * u < D) atomic_add_noret(dst + lane + 64 * u, a[u]);
-    }
-    __syncthreads();
   }
 }
 
@@ -733,27 +806,45 @@ FPS_API size_t fps_sgns_v4_smem_bytes(int D) {
 }
 
 // v4: pos_neg holds 16 negative rows per block of 32 pairs
+// group: blocks of 32 pairs sharing one set of 16 negatives (1, 2 or 4); pos_neg
+// holds 16 rows per 32 * group pairs
+FPS_API int fps_sgns_step_v4g(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
+                              const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
+                              float neg_weight, float* d_in, float* d_out, float* loss_out, int group, void* stream) {
+  if (n_pairs <= 0) return 0;
+  if (((D + 31) & ~31) > 512) return (int)hipErrorInvalidValue;
+  if (group != 1 && group != 2 && group != 4) return (int)hipErrorInvalidValue;
+  const size_t smem = fps_sgns_v4_smem_bytes(D);
+  if (smem > 80 * 1024) return (int)hipErrorInvalidValue;  // two blocks per CU
+  const int64_t ng = (n_pairs + 32 * group - 1) / (32 * group);
+  const int grid = (int)(ng < 256 * 2 * 4 ? ng : 256 * 2 * 4);
+  hipStream_t s = (hipStream_t)stream;
+#define FPS_SGNS_V4(BF, G)                                                                                            \
+  do {                                                                                                               \
+    (void)hipFuncSetAttribute((const void*)sgns_v4_kernel<BF, G>, hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                              (int)smem);                                                                            \
+    hipLaunchKernelGGL((sgns_v4_kernel<BF, G>), dim3(grid), dim3(NT4), smem, s, rows_in, rows_out, pos_c, pos_o,     \
+                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);                                  \
+  } while (0)
+  if (rows_bf16) {
+    if (group == 1) FPS_SGNS_V4(true, 1);
+    else if (group == 2) FPS_SGNS_V4(true, 2);
+    else FPS_SGNS_V4(true, 4);
+  } else {
+    if (group == 1) FPS_SGNS_V4(false, 1);
+    else if (group == 2) FPS_SGNS_V4(false, 2);
+    else FPS_SGNS_V4(false, 4);
+  }
+#undef FPS_SGNS_V4
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_sgns_step_v4(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
                              const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
                              float neg_weight, float* d_in, float* d_out, float* loss_out, void* stream) {
-  if (n_pairs <= 0) return 0;
-  if (((D + 31) & ~31) > 512) return (int)hipErrorInvalidValue;
-  const size_t smem = fps_sgns_v4_smem_bytes(D);
-  if (smem > 80 * 1024) return (int)hipErrorInvalidValue;  // two blocks per CU
-  const int64_t nb = (n_pairs + 31) / 32;
-  const int grid = (int)(nb < 256 * 2 * 4 ? nb : 256 * 2 * 4);
-  hipStream_t s = (hipStream_t)stream;
-  if (rows_bf16) {
-    (void)hipFuncSetAttribute((const void*)sgns_v4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(sgns_v4_kernel<true>, dim3(grid), dim3(NT4), smem, s, rows_in, rows_out, pos_c, pos_o,
-                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
-  } else {
-    (void)hipFuncSetAttribute((const void*)sgns_v4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(sgns_v4_kernel<false>, dim3(grid), dim3(NT4), smem, s, rows_in, rows_out, pos_c, pos_o,
-                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
-  }
-  FPS_CHECK_LAUNCH();
-  return 0;
+  return fps_sgns_step_v4g(rows_in, rows_out, rows_bf16, pos_c, pos_o, pos_neg, n_pairs, D, lr, neg_weight, d_in,
+                           d_out, loss_out, 1, stream);
 }
 
 // pos_neg holds K = 32 negative rows per block of 32 pairs (ceil(n_pairs/32) blocks)

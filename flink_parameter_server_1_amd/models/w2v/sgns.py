@@ -47,6 +47,8 @@ class SGNSConfig:
     wire_dtype: str = "fp32"
     pipeline: bool = True         # W > 1: row all-to-alls of batch k+1 overlap the SGNS step of batch k
     shared_negatives: int = 16    # negatives shared by each block of 32 pairs (16: kernel v4, 32: v3)
+    neg_group: int = 4            # v4: consecutive 32-pair blocks sharing one negative set (1, 2, 4):
+                                  # 4 measured +6 % pairs/s at the same loss curve (profiles/r2_sgns.md)
     local_direct: bool = True     # W = 1: kernel reads / atomically updates the local tables in place
 
 
@@ -103,7 +105,7 @@ class DistributedSGNS:
         added in place by the kernel's atomics."""
         c = self.cfg
         P = centers.numel()
-        nb = (P + self.BLOCK - 1) // self.BLOCK
+        nb = (P + self.BLOCK * c.neg_group - 1) // (self.BLOCK * c.neg_group)  # negative sets
         dev = self.w_in.weight.device
         negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives, seed=c.seed + 17 * self.comm.rank,
                                 counter=self.counter)
@@ -119,7 +121,8 @@ class DistributedSGNS:
         with stage("sgns.step", self.timer):
             loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
                                  c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
-                                 with_loss=with_loss, neg_k=c.shared_negatives)
+                                 with_loss=with_loss, neg_k=c.shared_negatives,
+                                 neg_group=c.neg_group)
         self.pairs_seen += P
         if with_loss:
             return float(loss.item()) / max(P, 1)
@@ -138,7 +141,7 @@ class DistributedSGNS:
     def _start(self, centers, contexts, async_rows: bool = False):
         c = self.cfg
         P = centers.numel()
-        nb = (P + self.BLOCK - 1) // self.BLOCK
+        nb = (P + self.BLOCK * c.neg_group - 1) // (self.BLOCK * c.neg_group)  # negative sets
         with stage("sgns.negatives", self.timer):
             negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives,
                                     seed=c.seed + 17 * self.comm.rank, counter=self.counter)
@@ -166,7 +169,7 @@ class DistributedSGNS:
         with stage("sgns.step", self.timer):
             loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
                                  c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
-                                 neg_k=c.shared_negatives)
+                                 neg_k=c.shared_negatives, neg_group=c.neg_group)
         self.ps_in.push(plan_in, d_in)
         self.ps_out.push(plan_out, d_out)
         self.pairs_seen += P

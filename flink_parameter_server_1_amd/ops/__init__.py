@@ -739,17 +739,22 @@ SGNS_NEG_K = (16, 32)
 
 
 def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: float, d_in, d_out,
-              with_loss: bool = False, neg_k: int = 16, kernel: Optional[str] = None):
+              with_loss: bool = False, neg_k: int = 16, kernel: Optional[str] = None, neg_group: int = 1):
     """Block-shared-negative skip-gram step on MFMA (K6); deltas accumulate into
     ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has ``neg_k`` rows per 32
     pairs: 16 runs kernel v4 (two 512-thread blocks per CU), 32 kernel v3.
     ``kernel`` (or ``FPS_SGNS_KERNEL``) = "v5" runs the loader / atomic wave split
-    variant (D <= 320; measured slower than v4, profiles/r1_w2v_v4.md)."""
+    variant (D <= 320; measured slower than v4, profiles/r1_w2v_v4.md).
+    ``neg_group`` (1, 2 or 4; v4 only): that many consecutive blocks of 32 pairs share
+    one set of ``neg_k`` negatives (``pos_neg`` holds ``neg_k`` rows per 32 * neg_group
+    pairs); their negative-row gradients are summed on chip and pushed once."""
     D = rows_in.shape[1]
     if neg_k not in SGNS_NEG_K:
         raise ValueError(f"sgns_step: neg_k must be one of {SGNS_NEG_K}")
-    if pos_neg.numel() < neg_k * ((pos_c.numel() + 31) // 32):
-        raise ValueError("sgns_step: pos_neg needs neg_k rows per block of 32 pairs")
+    if neg_group not in (1, 2, 4) or (neg_group > 1 and neg_k != 16):
+        raise ValueError("sgns_step: neg_group is 1, 2 or 4 (groups > 1 with neg_k = 16)")
+    if pos_neg.numel() < neg_k * ((pos_c.numel() + 32 * neg_group - 1) // (32 * neg_group)):
+        raise ValueError("sgns_step: pos_neg needs neg_k rows per 32 * neg_group pairs")
     if rows_in.is_cuda:
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
         lib = N.require()
@@ -759,13 +764,23 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
             kern = kernel or os.environ.get("FPS_SGNS_KERNEL") or "v4"
             if kern not in ("v4", "v5"):
                 raise ValueError(f"sgns_step: kernel must be 'v4' or 'v5', not {kern!r}")
-            fn = lib.fps_sgns_step_v5 if kern == "v5" else lib.fps_sgns_step_v4
+            if neg_group > 1 and kern != "v4":
+                raise ValueError("sgns_step: neg_group > 1 runs on kernel v4")
+            if kern == "v4":
+                N.check(lib.fps_sgns_step_v4g(
+                    _c(rows_in).data_ptr(), _c(rows_out).data_ptr(), int(rows_in.dtype == torch.bfloat16),
+                    _c(pos_c).data_ptr(), _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), pos_c.numel(), D, lr,
+                    neg_weight, _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss), neg_group,
+                    N.stream_ptr(rows_in.device)), "sgns_step")
+                return loss
+            fn = lib.fps_sgns_step_v5
         N.check(fn(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
                                   int(rows_in.dtype == torch.bfloat16), _c(pos_c).data_ptr(), _c(pos_o).data_ptr(),
                                   _c(pos_neg).data_ptr(), pos_c.numel(), D, lr, neg_weight, _c(d_in).data_ptr(),
                                   _c(d_out).data_ptr(), N.ptr(loss), N.stream_ptr(rows_in.device)), "sgns_step")
         return loss
-    return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out, neg_k)])
+    return torch.tensor([R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out, neg_k,
+                                     neg_group)])
 
 
 TOPK_MAX_K = 256

@@ -85,6 +85,7 @@ _SIGNATURES = {
     "fps_sample_alias": [c_vp, c_vp, ctypes.c_int32, c_i64, c_u32, ctypes.c_uint64, c_vp, c_vp],
     "fps_sgns_step": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
+    "fps_sgns_step_v4g": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_sgns_step_v5": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_score_gemm": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp],

@@ -308,8 +308,9 @@ def sample_alias(prob, alias, n, seed=0, counter=0):
     return torch.where(u < prob[col], col, alias.long()[col]).to(torch.int32)
 
 
-def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out, neg_k=32):
-    """Block-shared-negative SGNS (32 pairs x ``neg_k`` negatives per block); returns the loss."""
+def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_out, neg_k=32, neg_group=1):
+    """Block-shared-negative SGNS (32 pairs x ``neg_k`` negatives per block; ``neg_group``
+    consecutive blocks share one set of negatives); returns the loss."""
     P = pos_c.numel()
     loss = 0.0
     Hall = rows_in.float()[pos_c.long()]
@@ -317,7 +318,8 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr, neg_weight, d_in, d_
     for blk in range((P + 31) // 32):
         sl = slice(32 * blk, min(P, 32 * blk + 32))
         H, O = Hall[sl], Oall[sl]
-        negs = pos_neg.long()[neg_k * blk: neg_k * blk + neg_k]
+        g = blk // neg_group
+        negs = pos_neg.long()[neg_k * g: neg_k * g + neg_k]
         Nn = rows_out.float()[negs]
         sp = (H * O).sum(1)
         S = H @ Nn.T

@@ -66,23 +66,25 @@ def test_sgns_distributed_gloo():
 @pytest.mark.parametrize("D", [16, 64, 100, 300])
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("runs", [False, True])
-@pytest.mark.parametrize("neg_k,kernel", [(16, "v5"), (16, "v4"), (32, None)])
-def test_sgns_kernel_matches_reference(D, wire, runs, neg_k, kernel):
+@pytest.mark.parametrize("neg_k,kernel,group", [(16, "v5", 1), (16, "v4", 1), (16, "v4", 2), (16, "v4", 4),
+                                                (32, None, 1)])
+def test_sgns_kernel_matches_reference(D, wire, runs, neg_k, kernel, group):
     torch.manual_seed(D)
-    Uin, Uout, P = 300, 400, 200 if kernel != "v5" else 20000  # v5: many blocks per persistent workgroup
+    # v5: many blocks per persistent workgroup; groups: a partial last group (200 = 1.5 groups of 4 x 32 + 8)
+    Uin, Uout, P = 300, 400, 200 if kernel != "v5" else 20000
     rows_in = (torch.randn(Uin, D) * 0.3).to(wire)
     rows_out = (torch.randn(Uout, D) * 0.3).to(wire)
     pos_c = torch.randint(0, Uin, (P,), dtype=torch.int32)
     if runs:  # center-major order: runs of equal centers (summed in LDS before the atomics)
         pos_c = torch.sort(torch.randint(0, 40, (P,), dtype=torch.int32)).values
     pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
-    pos_neg = torch.randint(0, Uout, (((P + 31) // 32) * neg_k,), dtype=torch.int32)
+    pos_neg = torch.randint(0, Uout, (((P + 32 * group - 1) // (32 * group)) * neg_k,), dtype=torch.int32)
     d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
-    loss_r = R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, 0.05, 5 / neg_k, d_in_r, d_out_r, neg_k)
+    loss_r = R.sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, 0.05, 5 / neg_k, d_in_r, d_out_r, neg_k, group)
     dev = "cuda"
     d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
     loss = ops.sgns_step(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), 0.05,
-                         5 / neg_k, d_in, d_out, with_loss=True, neg_k=neg_k, kernel=kernel)
+                         5 / neg_k, d_in, d_out, with_loss=True, neg_k=neg_k, kernel=kernel, neg_group=group)
     torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=2e-6)
     torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=2e-6)
     assert abs(float(loss) - loss_r) / loss_r < 1e-4
