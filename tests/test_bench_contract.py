@@ -83,3 +83,25 @@ def test_bench_metrics_jsonl(tmp_path):
     assert all("mf.sgd" in s["stage_ms"] for s in steps[:2])
     summ = [r for r in recs if r["kind"] == "summary"][0]
     assert summ["counters"]["ratings"] == 3 * 4096
+
+
+@pytest.mark.parametrize("script,args,metric_key", [
+    ("bench/bench_mf_topk.py", ["--users", "3000", "--items", "2000", "--batch", "64", "--bucket", "512", "--steps",
+                                "2", "--warmup", "1"], "learning_updates_per_s"),
+    ("bench/bench_w2v.py", ["--vocab", "5000", "--dim", "32", "--pairs", "4096", "--steps", "2", "--warmup", "1"],
+     "loss_first_last"),
+    ("bench/bench_pa.py", ["--features", "100000", "--batch", "512", "--nnz", "16", "--steps", "2", "--warmup", "1"],
+     "feature_updates_per_s"),
+])
+def test_secondary_benches_two_ranks_gloo(script, args, metric_key):
+    """The secondary benches run end to end at world size 2 (gloo) and report the
+    whole job from rank 0 only."""
+    port = {"bench/bench_mf_topk.py": "29681", "bench/bench_w2v.py": "29682", "bench/bench_pa.py": "29683"}[script]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", port, os.path.join(ROOT, script)] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and metric_key in d
