@@ -151,3 +151,23 @@ def test_model_load_and_double_load_gpu():
     ids, vals = [e.value for e in out if isinstance(e, Right)][0]
     got = dict(zip(ids.tolist(), vals.reshape(-1).tolist()))
     assert got == {k: 10.0 * k + 3 for k in range(50)}
+
+
+def test_offline_mf_tensor_gpu_reaches_reference_rmse():
+    """PSOfflineMatrixFactorizationTest on the GPU tensor engine: 100 java.util.Random(47)
+    ratings, rank 15, 10 epochs with device shuffles, EOF-started replay -> RMSE <= 0.5."""
+    from test_mf import reference_offline_ratings
+
+    from flink_parameter_server_1_amd.models.mf.batched import ps_offline_mf_tensor
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    ratings = reference_offline_ratings()
+    u = torch.tensor([x.user for x in ratings], device=DEV)
+    i = torch.tensor([x.item for x in ratings], device=DEV)
+    r = torch.tensor([x.rating for x in ratings], dtype=torch.float32, device=DEV)
+    batches = [(u[s:s + 10], i[s:s + 10], r[s:s + 10]) for s in range(0, len(ratings), 10)]
+    out = ps_offline_mf_tensor(batches, 20, 15, num_factors=15, range_min=0.0, range_max=1.0, learning_rate=0.01,
+                               iterations=10, micro_batch=10, seed=3, comm=Comm(device=DEV))
+    U, V = fold_outputs(out)
+    err = np.sqrt(np.mean([(float(np.dot(U[x.user], V[x.item])) - x.rating) ** 2 for x in ratings]))
+    assert err <= 0.5, err
