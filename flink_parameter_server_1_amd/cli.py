@@ -199,6 +199,59 @@ def cmd_topk(args):
     print(json.dumps({"periods": agg.periods()[:10], "n": len(known)}))
 
 
+def cmd_mf_topk(args):
+    """psOnlineLearnerAndGenerator on a ``ts,user,item[,rating]`` log
+    (``T/matrix/factorization/PSOnlineMatrixFactorizationAndTopKGeneratorTest.scala``): every rating
+    is a top-K query answered before it is learned; nDCG@K per ``--period`` seconds
+    (``nDCGSink.nDCGPeriodsToCsv``).  ``--engine tensor``: the tensor engine (GPU when present, one
+    process; under torchrun the items are sharded over the ranks), ``record``: the per-record engine."""
+    import numpy as np
+    import torch
+
+    from .models.mf.topk_tensor import as_reference_records, ps_online_learner_and_generator_tensor
+    from .utils.io import read_ratings
+    from .utils.metrics import NDCGAggregator
+
+    ts, u, i, r = read_ratings(args.input)
+    if args.limit:
+        ts, u, i, r = ts[:args.limit], u[:args.limit], i[:args.limit], r[:args.limit]
+    order = np.argsort(ts, kind="stable")
+    ts, u, i, r = ts[order], u[order], i[order], r[order]
+    n_users, n_items = int(u.max()) + 1, int(i.max()) + 1
+    kw = dict(num_factors=args.num_factors, range_min=args.range_min, range_max=args.range_max,
+              learning_rate=args.learning_rate, negative_sample_rate=args.negative_sample_rate,
+              user_memory=args.user_memory, K=args.k, worker_k=args.worker_k, bucket_size=args.bucket,
+              seed=args.seed)
+    agg = NDCGAggregator(args.period)
+    if args.engine == "record":
+        from .models.mf.apps import ps_online_learner_and_generator
+        from .models.mf.core import Rating
+
+        recs = [Rating(int(a), int(b), float(c), int(t)) for a, b, c, t in zip(u, i, r, ts)]
+        out = ps_online_learner_and_generator(recs, init="hash", worker_parallelism=1, ps_parallelism=1, **kw)
+        for uu, ii, tt, top in out:
+            agg.add(tt, [it for _, it in top], ii)
+    else:
+        from .parallel.comm import Comm
+
+        comm = Comm.init_from_env()
+        dev = comm.device
+        B = args.batch
+        batches = [(torch.from_numpy(u[s:s + B].astype(np.int64)).to(dev),
+                    torch.from_numpy(i[s:s + B].astype(np.int64)).to(dev),
+                    torch.from_numpy(ts[s:s + B].astype(np.int64)).to(dev),
+                    torch.from_numpy(r[s:s + B].astype(np.float32)).to(dev)) for s in range(0, len(u), B)]
+        out = ps_online_learner_and_generator_tensor(batches, n_users, n_items, comm=comm, **kw)
+        if comm.rank != 0:
+            return 0
+        for uu, ii, tt, top in as_reference_records(out):
+            agg.add(tt, [it for _, it in top], ii)
+    if args.csv:
+        agg.to_csv(args.csv)
+    print(json.dumps({"ratings": int(len(u)), "periods": agg.periods()[:10]}))
+    return 0
+
+
 def _read_libsvm(path):
     labels, rows = [], []
     for ln in open(path):
@@ -321,6 +374,25 @@ def build_parser():
     p.add_argument("--period", type=int, default=86400)
     p.add_argument("--csv")
 
+    p = sub.add_parser("mf-topk", help="online MF + top-K generation with nDCG per period "
+                                        "(psOnlineLearnerAndGenerator)")
+    p.add_argument("--input", required=True, help="ts,user,item[,rating] lines")
+    p.add_argument("--engine", choices=["tensor", "record"], default="tensor")
+    p.add_argument("--num-factors", type=int, default=10)
+    p.add_argument("--range-min", type=float, default=-0.01)
+    p.add_argument("--range-max", type=float, default=0.01)
+    p.add_argument("--learning-rate", type=float, default=0.2)
+    p.add_argument("--negative-sample-rate", type=int, default=9)
+    p.add_argument("--user-memory", type=int, default=4)
+    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--worker-k", type=int, default=100)
+    p.add_argument("--bucket", type=int, default=100)
+    p.add_argument("--batch", type=int, default=1024, help="tensor engine: ratings per micro-batch")
+    p.add_argument("--period", type=int, default=86400)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--limit", type=int, default=0, help="first N ratings only (0: all)")
+    p.add_argument("--csv", help="nDCG per period (nDCGPeriodsToCsv)")
+
     p = sub.add_parser("pa-train")
     p.add_argument("--config")
     p.add_argument("--input", required=True)
@@ -394,6 +466,8 @@ def main(argv=None):
         return cmd_mf_gpu(args)
     if args.cmd == "topk":
         return cmd_topk(args)
+    if args.cmd == "mf-topk":
+        return cmd_mf_topk(args)
     if args.cmd == "pa-train":
         return cmd_pa(args)
     if args.cmd == "w2v":

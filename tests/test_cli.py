@@ -4,6 +4,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 
 def _run(args, tmp_path):
@@ -86,3 +87,24 @@ def test_cli_mf_gpu_warm_start_from_its_own_dump(tmp_path):
                         str(tmp_path / "I.map")], tmp_path)
     rmse2 = json.loads(out2.strip().splitlines()[-1])["rmse_first_batch"]
     assert rmse2 == rmse
+
+
+@pytest.mark.parametrize("engine", ["record", "tensor"])
+def test_cli_mf_topk_ndcg_periods(tmp_path, engine):
+    """mf-topk (PSOnlineMatrixFactorizationAndTopKGeneratorTest main): a ts,user,item log in, nDCG per
+    period out (csv + JSON), on the per-record engine and on the tensor engine."""
+    rng = np.random.default_rng(0)
+    log = tmp_path / "log.csv"
+    t = 0
+    with open(log, "w") as f:
+        for _ in range(300):
+            t += int(rng.integers(1, 400))
+            f.write(f"{t},{int(rng.integers(0, 30))},{int(rng.integers(0, 50))}\n")
+    csv = tmp_path / "ndcg.csv"
+    out = _run(["mf-topk", "--input", str(log), "--engine", engine, "--k", "10", "--worker-k", "10", "--bucket", "16",
+                "--batch", "16", "--period", "20000", "--csv", str(csv)], tmp_path)
+    d = json.loads(out.strip().splitlines()[-1])
+    assert d["ratings"] == 300
+    assert sum(p[3] for p in d["periods"]) == 300  # every rating was a query
+    assert all(0.0 <= p[1] <= 1.0 for p in d["periods"])
+    assert csv.exists() and len(csv.read_text().splitlines()) >= len(d["periods"])
