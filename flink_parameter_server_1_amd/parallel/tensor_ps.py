@@ -63,8 +63,10 @@ class PendingPlan:
     counts: torch.Tensor     # int32[W] unique keys per owner (own copy)
     uniq: torch.Tensor       # int32[>= U] unique local keys grouped by owner
     pos: torch.Tensor        # int32[n]
-    host: torch.Tensor       # int32[W, 4]: (sent count, sent flag, recv count, recv flag) per peer
+    host: torch.Tensor       # int32[W, 4]: (sent count, sent flag, recv count, recv flag) per peer;
+                             # world 1: int32[1], the count alone (the flag never leaves the rank)
     event: Optional[object]  # torch.cuda.Event or None (host tensors: already complete)
+    flag: int = 0
 
 
 class TensorPS:
@@ -98,6 +100,15 @@ class TensorPS:
         counts = counts.clone()
         uniq = uniq[:n].clone()
         pos = pos.clone()
+        if W == 1:  # no peers: only the count travels (device -> host), no exchange / packing ops
+            if self._pinned:
+                host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                host.copy_(counts[:1].to(torch.int32), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host, ev = counts[:1].to("cpu", torch.int32), None
+            return PendingPlan(n, counts, uniq, pos, host, ev, int(flag))
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
         send = torch.cat([counts.view(W, 1).to(torch.int32), flags], dim=1).contiguous()  # [W, 2]
         with stage("ps.count-a2a", self.timer):
@@ -110,7 +121,7 @@ class TensorPS:
             ev.record()
         else:
             host, ev = both.to("cpu"), None
-        return PendingPlan(n, counts, uniq, pos, host, ev)
+        return PendingPlan(n, counts, uniq, pos, host, ev, int(flag))
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
@@ -118,7 +129,11 @@ class TensorPS:
             if not pp.event.query():
                 self.stats["host_stalls"] += 1
             pp.event.synchronize()
-        h = pp.host.tolist()
+        if pp.host.dim() == 1:  # world 1
+            c = int(pp.host[0])
+            h = [[c, pp.flag, c, pp.flag]]
+        else:
+            h = pp.host.tolist()
         send_splits = [int(r[0]) for r in h]
         recv_splits = [int(r[2]) for r in h]
         peer_flags = [int(r[3]) for r in h]
