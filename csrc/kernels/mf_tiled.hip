@@ -792,7 +792,7 @@ __device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int6
   }
 }
 
-template <int TPR, int V, int PF, bool REC8>
+template <int TPR, int V, int PF, bool REC8, bool PIPE = false>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
@@ -873,20 +873,40 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
         iv[v] = Ig[(int64_t)row * D4 + j + v * TPR];
         acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      for (int k0 = a; k0 < b; k0 += PF) {
-        float4 uv[PF][V];
-        // float4 offsets of the user rows: 32-bit for 8-B records (user < 2^24, D4 <= 64),
-        // 14 fewer live VGPRs than 64-bit offsets
-        using Off = typename std::conditional<REC8, uint32_t, int64_t>::type;
-        Off ur[PF];
-        float rv[PF];
+      // float4 offsets of the user rows: 32-bit for 8-B records (user < 2^24, D4 <= 64),
+      // 14 fewer live VGPRs than 64-bit offsets
+      using Off = typename std::conditional<REC8, uint32_t, int64_t>::type;
+      float4 uvn[PF][V];  // PIPE: the next batch, loaded before this batch's user-row stores
+      Off urn[PF];
+      float rvn[PF];
+      auto load_batch = [&](int k0, float4 (&uvx)[PF][V], Off (&urx)[PF], float (&rvx)[PF]) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {  // all PF user rows in flight (index clamped, result masked)
           int32_t u; int rw;
-          get_rec<REC8>(srec[min(k0 + q, b - 1)], r0, u, rw, rv[q]);
-          ur[q] = (Off)u * D4;
+          get_rec<REC8>(srec[min(k0 + q, b - 1)], r0, u, rw, rvx[q]);
+          urx[q] = (Off)u * D4;
 #pragma unroll
-          for (int v = 0; v < V; ++v) uv[q][v] = Ug[ur[q] + j + v * TPR];
+          for (int v = 0; v < V; ++v) uvx[q][v] = Ug[urx[q] + j + v * TPR];
+        }
+      };
+      if (PIPE) load_batch(a, uvn, urn, rvn);
+      for (int k0 = a; k0 < b; k0 += PF) {
+        float4 uv[PF][V];
+        Off ur[PF];
+        float rv[PF];
+        if (PIPE) {
+          // vmcnt retires in issue order: loads issued after this batch's stores would
+          // wait for them, so the next batch's rows are requested first
+#pragma unroll
+          for (int q = 0; q < PF; ++q) {
+            ur[q] = urn[q];
+            rv[q] = rvn[q];
+#pragma unroll
+            for (int v = 0; v < V; ++v) uv[q][v] = uvn[q][v];
+          }
+          if (k0 + PF < b) load_batch(k0 + PF, uvn, urn, rvn);
+        } else {
+          load_batch(k0, uv, ur, rv);
         }
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
@@ -1118,9 +1138,15 @@ FPS_API int fps_mf_sgd_tiled3(float* U, float* I, const void* rec, int rec8, con
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
+  // FPS_MF_PIPE=1 (A/B): 4 user rows per batch, the next batch requested before this
+  // batch's stores (same registers as 8 rows per batch without the pipeline)
+  static const bool pipe = [] { const char* e = std::getenv("FPS_MF_PIPE"); return e && e[0] == '1'; }();
 #define FPS_TILED(TPR_, V_)                                                                                    \
-  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, U, I, \
-                               rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt);                  \
+  if (pipe && rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF / 2, true, true>), dim3(grid),   \
+                                       dim3(512), 0, s, U, I, rec, ptr, R, block_rows, lr, lambda, I1,         \
+                                       block_rows1, T, tcnt);                                                  \
+  else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, \
+                                    U, I, rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt);      \
   else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(grid), dim3(512), 0, s, U, I,    \
                           rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt)
   switch (D) {
