@@ -275,6 +275,22 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int ntile = Dp / 32;
   const int i = lane & 31, kh = lane >> 5;
 
+  // a block's pair / negative indices (wave 0: lanes < 32 the pairs, 32..47 the negatives)
+  // are requested one block ahead, before the current block's float atomics: vmcnt
+  // retires in issue order, so loads issued after them would wait for the atomics
+  auto fetch_idx = [&](int64_t g, int sb, int32_t& a, int32_t& b) {
+    const int64_t q0 = (g * GROUP + sb) * M;
+    a = -1;
+    b = -1;
+    if (g >= n_groups || q0 >= n_pairs) return;
+    if (tid < M) {
+      if (q0 + tid < n_pairs) { a = pos_c[q0 + tid]; b = pos_o[q0 + tid]; }
+    } else if (sb == 0 && tid < M + K4) {
+      a = pos_neg[g * K4 + (tid - M)];
+    }
+  };
+  int32_t nx_a = -1, nx_b = -1;
+  if (wave == 0) fetch_idx(blockIdx.x, 0, nx_a, nx_b);
   for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
     // dN accumulators of this wave's (<= 2) negative-gradient column tiles t = wave + 8 j,
     // t >= ntile, kept across the group's blocks
@@ -284,12 +300,16 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
       if (p0 >= n_pairs) break;  // uniform: the group's tail
       const int npairs = (int)((n_pairs - p0) < M ? (n_pairs - p0) : M);
       if (tid < M) {
-        pc[tid] = tid < npairs ? pos_c[p0 + tid] : -1;
-        po[tid] = tid < npairs ? pos_o[p0 + tid] : -1;
+        pc[tid] = nx_a;
+        po[tid] = nx_b;
       } else if (sb == 0 && tid < M + K4) {
-        pn[tid - M] = pos_neg[grp * K4 + (tid - M)];
+        pn[tid - M] = nx_a;
       }
       __syncthreads();
+      if (wave == 0) {  // the next block's indices, in flight during this block
+        const bool last = sb + 1 == GROUP || (grp * GROUP + sb + 1) * M >= n_pairs;
+        fetch_idx(last ? grp + gridDim.x : grp, last ? 0 : sb + 1, nx_a, nx_b);
+      }
       if (wave == 0) {  // adjacent centers share most of their window: one dO row per distinct
                         // context (12.9 distinct contexts per 32 pairs on the bench corpus).
                         // Lane t < 32 finds the pairs with its context by register shuffles
