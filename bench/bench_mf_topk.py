@@ -70,7 +70,7 @@ def main(argv=None):
         rt.submit(data[s % 4])
     comm.barrier()
     sync()
-    served0, trained0 = worker.served, worker.trained
+    served0, trained0 = worker.served, worker.trained  # (synchronised above: read before the clock starts)
     t0 = time.perf_counter()
     for s in range(a.steps):
         rt.submit(data[s % 4])

@@ -429,7 +429,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self.range, self.seed, self.neg_memory = (range_min, range_max), seed, int(neg_memory)
         self.prefill_items, self.num_users, self.resort_every = prefill_items, num_users, int(resort_every)
         self.served = 0
-        self.trained = 0
+        self._trained = None  # device counter of SGD updates on this rank (ratings + drawn negatives)
         self.rebuilds = 0
 
     def open(self, ctx):
@@ -437,6 +437,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
 
         self.W, self.rank, self.device = ctx.world_size, ctx.rank, torch.device(ctx.device)
         self.comm = Comm(device=self.device)
+        self._trained = torch.zeros((), dtype=torch.int64, device=self.device)
         self.seen = SeenStore(self.memory, self.device, self.num_users)
         self.items = ShardedTable(self.num_items, self.dim, self.rank, self.W, "hash",
                                   ("uniform", self.range[0], self.range[1]), (self.seed ^ USER_SEED_XOR) & 0xFFFFFFFF,
@@ -461,6 +462,12 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
     def on_recv_batch(self, batch, ps):
         users, items, ts, rating = (t.to(self.device) for t in batch)
         ps.pull(users, (users, items, ts, rating.float()))
+
+    @property
+    def trained(self) -> int:
+        """SGD updates applied on this rank so far (owned ratings + drawn negatives);
+        reading it synchronises with the device."""
+        return 0 if self._trained is None else int(self._trained.item())
 
     def _rebuild_index(self):
         loc = torch.nonzero(self.valid).flatten()
@@ -531,13 +538,14 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
                 du.index_add_(0, rows_own, lr * e * iv * okf)
                 W_.index_add_(0, nl, lr * e * Ub * okf)
                 touched.append(nl)
+                self._trained += (ng >= 0).sum()
         ownf = own.to(U.dtype).view(-1, 1)
         iv = W_[loc]
         e = rating.view(-1, 1) - (U * iv).sum(1, keepdim=True)
         du += lr * e * iv * ownf
         W_.index_add_(0, loc, lr * e * U * ownf)
         self._refresh_index(torch.cat(touched))
-        self.trained += users.numel() // self.W * (1 + self.neg_rate)  # expected owned share (no sync)
+        self._trained += own.sum()
         ps.push(du, mask=own)
 
 
