@@ -9,6 +9,13 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    if os.environ.get("PYTEST_XDIST_WORKER"):
+        # several test processes share the CPUs: one intra-op thread each (OpenMP
+        # workers spin-waiting on oversubscribed cores made the small-op CPU tests
+        # run ~20x slower)
+        import torch
+
+        torch.set_num_threads(1)
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) to run")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
