@@ -68,6 +68,8 @@ class SeenStore:
         if num_users is not None and 0 < self.memory <= 256 and int(num_users) * self.memory <= self.RING_SLOTS:
             self.ring = torch.full((int(num_users), self.memory), -1, dtype=torch.int32, device=self.device)
             self.ring_cur = torch.zeros(int(num_users), dtype=torch.int64, device=self.device)
+        self._adds = 0
+        self._prune_at = 0
         self.keys = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.seq = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.ucount_keys = torch.zeros(0, dtype=torch.int64, device=self.device)
@@ -107,30 +109,46 @@ class SeenStore:
             return
         cnt = self._user_count(users)
         key = (users << 32) | (items & 0xFFFFFFFF)
-        keys = torch.cat([self.keys, key])
-        seq = torch.cat([self.seq, cnt])
-        # keep the latest insertion of every key
-        order = torch.argsort(keys * 0 + seq, stable=True)  # by seq ...
-        keys, seq = keys[order], seq[order]
-        order = torch.argsort(keys, stable=True)             # ... then by key: last of a run = latest
-        keys, seq = keys[order], seq[order]
-        last = torch.ones_like(keys, dtype=torch.bool)
-        if keys.numel() > 1:
-            last[:-1] = keys[1:] != keys[:-1]
-        self.keys, self.seq = keys[last], seq[last]
-        # per-user insertion counts
-        uk = torch.cat([self.ucount_keys, users])
-        uc = torch.cat([self.ucount, cnt + 1])
-        order = torch.argsort(uk, stable=True)
-        uk, uc = uk[order], uc[order]
-        lastu = torch.ones_like(uk, dtype=torch.bool)
-        if uk.numel() > 1:
-            lastu[:-1] = uk[1:] != uk[:-1]
-        self.ucount_keys, self.ucount = uk[lastu], uc[lastu]
-        if self.memory > 0 and self.keys.numel() > 4096:  # drop entries that left every window
+        # keep the latest insertion of every key (keys are distinct within the call)
+        self.keys, self.seq = _upsert_sorted(self.keys, self.seq, key, cnt)
+        self.ucount_keys, self.ucount = _upsert_sorted(self.ucount_keys, self.ucount, users, cnt + 1)
+        self._adds += users.numel()
+        if self.memory > 0 and self.keys.numel() > 4096 and self._adds >= self._prune_at:
+            # drop entries that left every window (now and then: O(store) each time)
             lo = self._user_count(self.keys >> 32) - self.memory
             keep = self.seq >= lo
             self.keys, self.seq = self.keys[keep], self.seq[keep]
+            self._prune_at = self._adds + max(4096, self.keys.numel() // 2)
+
+
+def _upsert_sorted(keys: torch.Tensor, vals: torch.Tensor, nk: torch.Tensor, nv: torch.Tensor):
+    """Sorted unique ``keys`` (values ``vals``) updated with distinct keys ``nk`` ->
+    values ``nv``: existing keys take the new value, new keys are merged in order.
+    O(store + batch) (searchsorted + two scatters) instead of re-sorting the store."""
+    o = torch.argsort(nk)
+    nk, nv = nk[o], nv[o]
+    N = keys.numel()
+    if N:
+        i = torch.searchsorted(keys, nk).clamp(max=N - 1)
+        hit = keys[i] == nk
+        vals = vals.clone()
+        vals[i[hit]] = nv[hit]
+        fresh = ~hit
+        nk, nv = nk[fresh], nv[fresh]
+    n = nk.numel()
+    if n == 0:
+        return keys, vals
+    dev = nk.device
+    out_k = torch.empty(N + n, dtype=nk.dtype, device=dev)
+    out_v = torch.empty(N + n, dtype=nv.dtype, device=dev)
+    if N:
+        at = torch.arange(N, device=dev) + torch.searchsorted(nk, keys)
+        out_k[at] = keys
+        out_v[at] = vals
+    at = torch.arange(n, device=dev) + torch.searchsorted(keys, nk)
+    out_k[at] = nk
+    out_v[at] = nv
+    return out_k, out_v
 
 
 def occurrence_rounds(users: torch.Tensor) -> torch.Tensor:

@@ -146,3 +146,35 @@ def test_tensor_online_learner_and_generator_matches_per_record():
             for k, v in zip(ids.tolist(), vals.tolist()):
                 ps_users[k] = np.asarray(v)
     assert len(ps_users) > 0
+
+
+def test_seen_store_sorted_mode_long_stream_with_pruning():
+    """Sorted-key store (no dense rings) over a long stream -- merges and window pruning
+    -- against a deque per user (items never re-added while inside the window)."""
+    from collections import deque
+
+    st = SeenStore(3, "cpu")
+    ref = {}
+    rng = np.random.default_rng(5)
+    for step in range(3000):
+        users = rng.choice(60, size=4, replace=False)
+        items = []
+        for u in users:
+            dq = ref.setdefault(int(u), deque())
+            it = int(rng.integers(0, 10000))
+            while it in dq:
+                it = int(rng.integers(0, 10000))
+            items.append(it)
+        if step % 50 == 0:
+            cand = torch.tensor([[int(x) for x in rng.integers(0, 10000, 5)] + list(ref.get(int(u), []))[:2]
+                                 for u in users])
+            got = st.contains(torch.tensor(users), cand)
+            exp = torch.tensor([[int(c) in ref.get(int(u), ()) for c in row] for u, row in zip(users, cand.tolist())])
+            assert torch.equal(got, exp), step
+        st.add(torch.tensor(users), torch.tensor(items))
+        for u, it in zip(users, items):
+            dq = ref[int(u)]
+            dq.append(it)
+            if len(dq) > 3:
+                dq.popleft()
+    assert st.keys.numel() < 3000 * 4  # pruned
