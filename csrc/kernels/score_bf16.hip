@@ -1,0 +1,275 @@
+// Top-K scoring on bf16 MFMA with an exact fp32 re-score (gfx950).  Kernel K8, fast path.
+//
+// The fp32 scorer (score_gemm.hip) runs v_mfma_f32_32x32x2_f32: 32 MFMAs per 32 x 32
+// score tile at D = 64, ~100 TF/s -- it was 70 % of an online MF + top-K batch
+// (profiles/r2_mf_topk.md).  v_mfma_f32_32x32x16_bf16 does the same tile in 4
+// MFMAs at 16x the rate, but bf16 operands change the scores, and the reference's
+// top-K (M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:46-110) is exact.
+// Exactness is kept with a filter-then-rescore split:
+//
+//   1. score_filter_bf16_kernel: S~ = bf16(Q) . bf16(X) on MFMA, fp32 accumulate.  Per
+//      product |bf16(q)bf16(x) - qx| <= (2u + u^2)|q||x| with u = 2^-8 (RNE), and by
+//      Cauchy-Schwarz sum_k |q_k||x_k| <= |q| |x|, so |S~ - S| <= c |q| |x| with
+//      c = 2u + u^2 + 2 * D * 2^-24 (the fp32 accumulations of both scorers).  An item
+//      is a candidate iff S~ > theta_q - c |q| max|x| (theta_q = the query's current
+//      k-th best, max over the 32 items of an MFMA block): a superset of the items
+//      with S > theta_q.  Candidate positions go to the query's list (count
+//      atomics, cap as in score_filter_kernel).
+//   2. cand_rescore_kernel: each candidate's exact score with the SAME fp32 MFMA
+//      chain as score_gemm / score_filter (v_mfma_f32_32x32x2_f32 over k pairs 0,1 |
+//      2,3 | ... in order, the query broadcast over the A rows, 32 candidates on the
+//      B columns), so keys are bit-identical to the fp32 path; a candidate whose
+//      exact score is not strictly above theta_q (the fp32 path's test) gets key 0,
+//      below every real key, and never enters the merge.
+//
+// Operand layout (v_mfma_f32_32x32x16_bf16, MI355X guide "A/B operand lane maps"):
+// lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j] and B[k = 8h + j][col r],
+// j = 0..7.  The dot product sums over k, so any k order shared by A and B is
+// valid: k-step s of lane half h takes elements 8s .. 8s+7 of the row's half h
+// (dims h*D/2 + 8s + j) -- each lane reads its D/2 contiguous bf16 (64 B at D = 64)
+// with 16-B loads, no LDS.  A = 32 items, B = 32 queries, so the accumulator
+// column (lane & 31) is one query: its threshold and norm sit in two registers,
+// rows (reg & 3) + 8 (reg >> 2) + 4h are items.
+#include "common.h"
+
+using namespace fps;
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int SB_WAVES = 4;     // waves per workgroup
+constexpr int SB_ITEMS = 1024;  // items per workgroup (32 MFMA blocks of 32)
+constexpr int SB_SLOTS = 16;    // LDS candidate slots per (query block, lane)
+
+__device__ __forceinline__ uint32_t sb_key(float f) {  // order-preserving float -> uint32 (as topk.hip)
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// QB 32-query blocks per wave; a workgroup covers SB_WAVES * QB * 32 queries x
+// SB_ITEMS items.
+template <int D, int QB>
+__global__ void __launch_bounds__(256) score_filter_bf16_kernel(
+    const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
+    const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
+    float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap) {
+  constexpr int S = D / 16;   // k-steps of 16; also 16-B loads per lane per row
+  constexpr int HALF = D / 2;
+  constexpr int WQ = 32 * QB;
+  constexpr int GQ = SB_WAVES * WQ;
+  __shared__ float red[SB_WAVES];
+  const int nqt = (B + GQ - 1) / GQ;
+  const int nit = (N + SB_ITEMS - 1) / SB_ITEMS;
+  // query tiles fastest: the workgroups reading one item range are consecutive
+  // logical ids, i.e. on one XCD (one L2 holds the range)
+  const int wg = xcd_remap(blockIdx.x, nqt * nit);
+  const int qt = wg % nqt, it = wg / nqt;
+  const int i_begin = it * SB_ITEMS, i_end = min(N, i_begin + SB_ITEMS);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+
+  // LEMP bound per workgroup: no query of the tile can be beaten by the range's
+  // longest item -> the whole workgroup leaves before any load of X
+  float xm = 0.f;
+  for (int i = i_begin + tid; i < i_end; i += 256) xm = fmaxf(xm, xlen[i]);
+  xm = group_max<64>(xm);
+  if (lane == 0) red[wave] = xm;
+  __syncthreads();
+  xm = red[0];
+#pragma unroll
+  for (int w = 1; w < SB_WAVES; ++w) xm = fmaxf(xm, red[w]);
+
+  float theta[QB], ql[QB];
+  int qrow[QB];
+  uint4 qv[QB][S];
+  int live = 0;
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int q = qt * GQ + wave * WQ + b * 32 + r;
+    qrow[b] = q;
+    theta[b] = INFINITY;  // rows past B never pass
+    ql[b] = 0.f;
+    if (q < B) {
+      theta[b] = best_s[(int64_t)q * k + k - 1];
+      ql[b] = qlen[q];
+      live |= !(theta[b] > -INFINITY && ql[b] * xm * slack <= theta[b]);
+    }
+  }
+  if (!__syncthreads_or(live)) return;  // uniform
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const uint4* src = reinterpret_cast<const uint4*>(Qb + (int64_t)qrow[b] * D + h * HALF);
+#pragma unroll
+    for (int s = 0; s < S; ++s) qv[b][s] = qrow[b] < B ? src[s] : make_uint4(0, 0, 0, 0);
+  }
+
+  // candidates of each (query block, lane) collect in a private LDS list of item
+  // offsets and leave with ONE count atomic per query and workgroup at the end: a
+  // returning atomic per passing score made every 32 x 32 block with a candidate
+  // (most of them) wait a full memory round trip.  A full list falls back to the
+  // per-candidate atomic (dense segments, theta = -inf).
+  __shared__ uint16_t lst[SB_WAVES][QB][SB_SLOTS][64];
+  int lc[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) lc[b] = 0;
+  // software pipeline: block i0 + 32 is requested before block i0's MFMAs
+  uint4 xv[S];
+  float xl;
+  {
+    const int i = i_begin + r;
+    const bool ok = i < i_end;
+    const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
+#pragma unroll
+    for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
+    xl = ok ? xlen[i] : 0.f;
+  }
+  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
+    uint4 cur[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) cur[s] = xv[s];
+    const float bm = group_max<64>(xl);  // longest item of this block
+    if (i0 + 32 < i_end) {
+      const int i = i0 + 32 + r;
+      const bool ok = i < i_end;
+      const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
+#pragma unroll
+      for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
+      xl = ok ? xlen[i] : 0.f;
+    }
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      floatx16 acc = {0};
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
+                                                      __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
+      const float thr = theta[b] - margin * ql[b] * bm;
+      float m = acc[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
+      if (m > thr) {  // ~k ln(1 + n / s) passes per query and segment
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+          if (acc[j] > thr && item < i_end) {
+            if (lc[b] < SB_SLOTS) {
+              lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+              ++lc[b];
+            } else {
+              const int q = qrow[b];
+              const int slot = atomicAdd(cnt + q, 1);
+              if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
+            }
+          }
+        }
+      }
+    }
+  }
+  // flush: both lane halves hold the same query; half 0 reserves for the pair
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int q = qrow[b];
+    const int c = lc[b];
+    const int other = __shfl_xor(c, 32, 64);
+    int base = 0;
+    if (h == 0 && c + other > 0) base = atomicAdd(cnt + q, c + other);  // c + other > 0 implies q < B
+    base = __shfl(base, r, 64);
+    const int off = base + (h ? other : 0);
+    for (int t = 0; t < c; ++t)
+      if (off + t < cap) cand_pos[(int64_t)q * cap + off + t] = i_begin + lst[wave][b][t][lane];
+  }
+}
+
+// Exact fp32 re-score of the candidates of one query per wave (4 queries per
+// workgroup), 32 candidates per MFMA chain.  A = the query broadcast to all 32 rows
+// (lane l supplies q[kk + (l >> 5)]), B = the 32 candidates' rows (lane l supplies
+// x_{l & 31}[kk + (l >> 5)]); the k pairs run in score_tile's order, so acc[0]
+// (row 0 or 4: every row is the same dot product) is bit-identical to the fp32
+// scorer's value for that (query, item).
+template <int D>
+__global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restrict__ Q, const float* __restrict__ X,
+                                                           const int64_t* __restrict__ ids, int B,
+                                                           const float* __restrict__ best_s, int k,
+                                                           const int32_t* __restrict__ cnt, int cap,
+                                                           uint32_t* __restrict__ cand_key,
+                                                           int64_t* __restrict__ cand_id) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x * SB_WAVES + wave;
+  if (q >= B) return;
+  const int n = min(cnt[q], cap);
+  if (n == 0) return;
+  const int c = lane & 31, h = lane >> 5;
+  const float* qr = Q + (int64_t)q * D;
+  float qh[D / 2];
+#pragma unroll
+  for (int t = 0; t < D / 2; ++t) qh[t] = qr[2 * t + h];
+  const uint32_t ktau = sb_key(best_s[(int64_t)q * k + k - 1]);
+  for (int c0 = 0; c0 < n; c0 += 32) {
+    const bool ok = c0 + c < n;
+    const int64_t pos = ok ? cand_id[(int64_t)q * cap + c0 + c] : 0;
+    const float* xr = X + pos * D;
+    floatx16 acc = {0};
+#pragma unroll
+    for (int t = 0; t < D / 2; ++t)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[t], ok ? xr[2 * t + h] : 0.f, acc, 0, 0, 0);
+    if (ok && h == 0) {  // lanes 0..31: column c
+      const uint32_t key = sb_key(acc[0]);
+      cand_key[(int64_t)q * cap + c0 + c] = key > ktau ? key : 0u;
+      cand_id[(int64_t)q * cap + c0 + c] = ids[pos];
+    }
+  }
+}
+
+}  // namespace
+
+// Qb [B, D], Xb [N, D] bf16 (uint16 storage, RNE from the fp32 vectors); qlen [B],
+// xlen [N] the fp32 norms; cand_pos [B, cap] int64 receives item positions (0..N-1),
+// cnt [B] (zeroed by the caller) counts every candidate.  D in {32, 64, 128}.
+FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
+                                  int k, const float* qlen, const float* xlen, float margin, float slack,
+                                  int64_t* cand_pos, int32_t* cnt, int cap, void* stream) {
+  if (B <= 0 || N <= 0) return 0;
+  if (k <= 0 || cap <= 0 || qlen == nullptr || xlen == nullptr) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nit = (N + SB_ITEMS - 1) / SB_ITEMS;
+#define FPS_SB(D_, QB_)                                                                                     \
+  {                                                                                                         \
+    const int64_t nqt = (B + SB_WAVES * 32 * QB_ - 1) / (SB_WAVES * 32 * QB_);                              \
+    if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
+    hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_>), dim3((unsigned)(nqt * nit)), dim3(256), 0, s, Qb, \
+                       Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, cap);                 \
+  }
+  switch (D) {
+    case 32: FPS_SB(32, 2); break;
+    case 64: FPS_SB(64, 2); break;
+    case 128: FPS_SB(128, 1); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FPS_SB
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// Q [B, D], X [N, D] fp32 (the rows Qb / Xb were rounded from); cand_id holds the
+// positions written by fps_score_filter_bf16 and receives ids[pos]; cand_key the
+// exact keys (0 for candidates not strictly above best_s[q, k-1]).
+FPS_API int fps_cand_rescore(const float* Q, const float* X, const int64_t* ids, int B, int D, const float* best_s,
+                             int k, const int32_t* cnt, int cap, uint32_t* cand_key, int64_t* cand_id, void* stream) {
+  if (B <= 0) return 0;
+  if (k <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (B + SB_WAVES - 1) / SB_WAVES;
+  switch (D) {
+    case 32: hipLaunchKernelGGL((cand_rescore_kernel<32>), dim3(grid), dim3(256), 0, s, Q, X, ids, B, best_s, k, cnt, cap,
+                                cand_key, cand_id); break;
+    case 64: hipLaunchKernelGGL((cand_rescore_kernel<64>), dim3(grid), dim3(256), 0, s, Q, X, ids, B, best_s, k, cnt, cap,
+                                cand_key, cand_id); break;
+    case 128: hipLaunchKernelGGL((cand_rescore_kernel<128>), dim3(grid), dim3(256), 0, s, Q, X, ids, B, best_s, k, cnt,
+                                 cap, cand_key, cand_id); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  FPS_CHECK_LAUNCH();
+  return 0;
+}

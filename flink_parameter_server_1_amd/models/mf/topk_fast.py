@@ -53,6 +53,13 @@ class LempTopK:
         self.geometric = True
         self.overflows = 0
         self._suffix = None  # False once rows were updated out of order
+        #: fused GPU scan on bf16 MFMA (``ops.score_filter_bf16``: candidates within a
+        #: proven rounding margin) + exact fp32 re-score of the candidates
+        #: (``ops.cand_rescore``, bit-identical keys): same result as the fp32 scan.
+        #: ``FPS_TOPK_BF16=0`` keeps the fp32 scorer.
+        self.bf16 = (vecs.is_cuda and vecs.shape[1] in ops.BF16_SCORE_DIMS
+                     and os.environ.get("FPS_TOPK_BF16", "1") != "0")
+        self.vecs_bf = self.vecs.bfloat16() if self.bf16 else None
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -60,6 +67,8 @@ class LempTopK:
         bucket bounds switch to the suffix maximum of the lengths (still exact)."""
         v = vecs.float()
         self.vecs[pos] = v
+        if self.vecs_bf is not None:
+            self.vecs_bf[pos] = v.bfloat16()
         self.lengths[pos] = torch.linalg.vector_norm(v, dim=1)
         self._suffix = False  # the order is stale: bounds take the max of the tail
 
@@ -154,6 +163,7 @@ class LempTopK:
         ci = torch.empty((B, cap), dtype=torch.long, device=dev)
         cnt = torch.empty(B, dtype=torch.int32, device=dev)
         ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        Qb = Q.bfloat16() if self.bf16 else None
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
@@ -161,7 +171,12 @@ class LempTopK:
             if s % self.bucket == 0:
                 self.buckets_scanned += 1
             cnt.zero_()
-            ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen, self.lengths[s:e])
+            if self.bf16:
+                ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e])
+                ops.cand_rescore(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt)
+            else:
+                ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen,
+                                      self.lengths[s:e])
             ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf)
         if int(ovf.item()):
             return None

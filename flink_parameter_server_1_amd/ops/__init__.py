@@ -849,6 +849,56 @@ def score_filter_lemp(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_
         "score_filter_lemp")
 
 
+#: embedding dims the bf16 scorer is built for (``csrc/kernels/score_bf16.hip``)
+BF16_SCORE_DIMS = (32, 64, 128)
+
+
+def bf16_score_margin(D: int) -> float:
+    """``c`` with ``|S_bf16 - S_fp32| <= c |q| |x|`` for RNE-rounded bf16 operands and fp32
+    accumulation (``score_bf16.hip`` header: 2u + u^2 + 2 D 2^-24, u = 2^-8), widened by
+    0.1 % for the fp32 norms."""
+    u = 2.0 ** -8
+    return (2 * u + u * u + 2 * D * 2.0 ** -24) * 1.001
+
+
+def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, cand_pos: torch.Tensor,
+                      cnt: torch.Tensor, qlen: torch.Tensor, xlen: torch.Tensor) -> None:
+    """Candidate filter on bf16 MFMA (GPU only, K8 fast path): every item ``i`` whose bf16
+    score can exceed ``best_s[b, -1]`` (margin ``bf16_score_margin(D) |q_b| max|x|``) gets
+    its position appended to row ``b`` of ``cand_pos`` ``[B, cap]`` (int64); ``cnt[b]``
+    (zeroed by the caller) counts them all.  ``cand_rescore`` turns the list into exact
+    (key, id) candidates for ``topk_merge_cand``."""
+    B, D = Qb.shape
+    n = Xb.shape[0]
+    cap = cand_pos.shape[1]
+    if Qb.dtype != torch.bfloat16 or Xb.dtype != torch.bfloat16 or Xb.shape[1] != D or D not in BF16_SCORE_DIMS:
+        raise ValueError(f"score_filter_bf16: bf16 [B, D] / [n, D] with D in {BF16_SCORE_DIMS}")
+    if best_s.shape[0] != B or cnt.numel() != B or cand_pos.dtype != torch.int64 or qlen.numel() != B \
+            or xlen.numel() != n:
+        raise ValueError("score_filter_bf16: shape mismatch")
+    slack = 1.0 + 1e-4 + D * 2.4e-7
+    N.check(N.require().fps_score_filter_bf16(
+        _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
+        _c(qlen.float()).data_ptr(), _c(xlen.float()).data_ptr(), bf16_score_margin(D), slack,
+        _c(cand_pos).data_ptr(), _c(cnt).data_ptr(), cap, N.stream_ptr(Qb.device)), "score_filter_bf16")
+
+
+def cand_rescore(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, cand_key: torch.Tensor,
+                 cand_id: torch.Tensor, cnt: torch.Tensor) -> None:
+    """Exact fp32 scores of ``score_filter_bf16``'s candidates (GPU only): ``cand_id`` holds
+    item positions in ``X`` on entry and ``ids[pos]`` on exit; ``cand_key`` the
+    order-preserving keys, bit-identical to ``score_filter``'s (same fp32 MFMA chain), or 0
+    where the exact score is not strictly above ``best_s[b, -1]``."""
+    B, D = Q.shape
+    cap = cand_key.shape[1]
+    if X.shape[1] != D or D not in BF16_SCORE_DIMS or cand_id.shape != (B, cap) or cnt.numel() != B:
+        raise ValueError("cand_rescore: shape mismatch")
+    N.check(N.require().fps_cand_rescore(_c(Q).data_ptr(), _c(X).data_ptr(), _c(ids.long()).data_ptr(), B, D,
+                                         _c(best_s).data_ptr(), best_s.shape[1], _c(cnt).data_ptr(), cap,
+                                         _c(cand_key).data_ptr(), _c(cand_id).data_ptr(), N.stream_ptr(Q.device)),
+            "cand_rescore")
+
+
 def topk_merge_cand(cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Tensor, best_s: torch.Tensor,
                     best_i: torch.Tensor, overflow: Optional[torch.Tensor] = None) -> None:
     """Merge ``score_filter`` candidate lists into the running top-k in place (K13).

@@ -1,0 +1,141 @@
+"""bf16 MFMA top-K scan with exact fp32 re-score (``csrc/kernels/score_bf16.hip``).
+
+Numerics against the fp32 scorer of the same op (``ops.score_gemm``, itself checked
+against ``Q @ X.T`` in ``test_topk_fast.py``): the candidates that survive the
+re-score are exactly the items whose fp32 score is strictly above the query's
+k-th best, with bit-identical keys, including adversarial near-ties where every
+score sits within the bf16 rounding margin of the threshold.
+"""
+import pytest
+import torch
+
+from flink_parameter_server_1_amd import ops
+from flink_parameter_server_1_amd.models.mf.topk_fast import LempTopK
+from flink_parameter_server_1_amd.models.mf.topk_tensor import _fkey
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_filter(Q, X, theta, cap=2048, k=1):
+    B, D = Q.shape
+    n = X.shape[0]
+    best_s = theta.view(B, 1).expand(B, k).contiguous()
+    ck = torch.empty((B, cap), dtype=torch.int32, device="cuda")
+    ci = torch.empty((B, cap), dtype=torch.long, device="cuda")
+    cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    qlen, xlen = torch.linalg.vector_norm(Q, dim=1), torch.linalg.vector_norm(X, dim=1)
+    ids = torch.arange(n, device="cuda") * 7 + 3
+    ops.score_filter_bf16(Q.bfloat16(), X.bfloat16(), best_s, ci, cnt, qlen, xlen)
+    raw = cnt.clone()
+    ops.cand_rescore(Q, X, ids, best_s, ck, ci, cnt)
+    torch.cuda.synchronize()
+    return ck, ci, raw, ids
+
+
+def _check_exact(Q, X, theta, ck, ci, cnt, ids):
+    S = ops.score_gemm(Q, X)
+    keys = _fkey(S)
+    tk = _fkey(theta.view(-1, 1))
+    ku = keys.to(torch.int64) & 0xFFFFFFFF
+    tku = tk.to(torch.int64) & 0xFFFFFFFF
+    for b in range(Q.shape[0]):
+        n = int(cnt[b])
+        assert n <= ck.shape[1]
+        want = set(ids[(ku[b] > tku[b]).nonzero().flatten()].tolist())
+        kb = ck[b, :n].to(torch.int64) & 0xFFFFFFFF
+        got_ids = ci[b, :n][kb > 0]
+        assert set(got_ids.tolist()) == want, b
+        # keys bit-identical to the fp32 scorer's
+        pos = (got_ids - 3) // 7
+        assert torch.equal(kb[kb > 0], ku[b, pos]), b
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_bf16_filter_superset_and_exact_rescore(D):
+    g = torch.Generator().manual_seed(D)
+    B, n = 200, 5000
+    Q = torch.randn(B, D, generator=g).cuda()
+    X = (torch.randn(n, D, generator=g) * torch.rand(n, 1, generator=g)).cuda()
+    S = Q @ X.T
+    theta = torch.topk(S, 40, dim=1).values[:, -1].contiguous()  # ~39 strictly above per query
+    ck, ci, raw, ids = _run_filter(Q, X, theta)
+    _check_exact(Q, X, theta, ck, ci, raw, ids)
+    assert int(raw.min()) >= 39
+
+
+def test_bf16_filter_near_ties():
+    """Every item's score within ~1e-4 of the threshold (far inside the bf16 margin):
+    the filter passes all of them, the re-score keeps exactly the fp32 winners."""
+    g = torch.Generator().manual_seed(11)
+    B, n, D = 64, 1500, 64
+    x0 = torch.randn(D, generator=g)
+    X = (x0 + 1e-5 * torch.randn(n, D, generator=g)).cuda()
+    Q = torch.randn(B, D, generator=g).cuda()
+    S = ops.score_gemm(Q, X)
+    theta = S.median(dim=1).values.contiguous()
+    ck, ci, raw, ids = _run_filter(Q, X, theta)
+    assert int(raw.min()) == n  # nothing can be ruled out in bf16
+    _check_exact(Q, X, theta, ck, ci, raw, ids)
+
+
+def test_bf16_filter_minus_inf_threshold_and_ragged_shapes():
+    """theta = -inf passes everything; B and n not multiples of the tile sizes."""
+    g = torch.Generator().manual_seed(5)
+    B, n, D = 37, 1111, 64
+    Q = torch.randn(B, D, generator=g).cuda()
+    X = torch.randn(n, D, generator=g).cuda()
+    theta = torch.full((B,), float("-inf"), device="cuda")
+    ck, ci, raw, ids = _run_filter(Q, X, theta)
+    assert raw.tolist() == [n] * B
+    _check_exact(Q, X, theta, ck, ci, raw, ids)
+
+
+def test_bf16_filter_lemp_skip():
+    """A workgroup whose queries are all settled against the range's longest item
+    skips itself: with theta above |q| max|x| nothing is listed."""
+    g = torch.Generator().manual_seed(6)
+    Q = torch.randn(300, 64, generator=g).cuda()
+    X = torch.randn(4000, 64, generator=g).cuda()
+    theta = (torch.linalg.vector_norm(Q, dim=1) * torch.linalg.vector_norm(X, dim=1).max() * 1.01).contiguous()
+    _, _, raw, _ = _run_filter(Q, X, theta)
+    assert int(raw.sum()) == 0
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_lemp_topk_bf16_scan_equals_fp32_scan(D):
+    g = torch.Generator().manual_seed(9)
+    n = 150000
+    X = (torch.randn(n, D, generator=g) * torch.rand(n, 1, generator=g) ** 2).cuda()
+    ids = torch.arange(n, device="cuda") * 5 + 2
+    Q = torch.randn(500, D, generator=g).cuda()
+    a = LempTopK(ids, X, bucket_size=16384)
+    assert a.bf16
+    sa, ia = a.query(Q, 100)
+    b = LempTopK(ids, X, bucket_size=16384)
+    b.bf16 = False
+    sb, ib = b.query(Q, 100)
+    torch.testing.assert_close(sa, sb, rtol=0, atol=0)
+    assert torch.equal(ia, ib)
+    assert a.overflows == 0
+    bs, _ = torch.topk(Q @ X.T, 100, dim=1)
+    torch.testing.assert_close(sa, bs, rtol=1e-5, atol=1e-4)
+
+
+def test_lemp_topk_bf16_incremental_update():
+    """``update_rows`` keeps the bf16 shadow in step with the fp32 index."""
+    g = torch.Generator().manual_seed(10)
+    n, D = 60000, 64
+    X = torch.randn(n, D, generator=g).cuda()
+    ids = torch.arange(n, device="cuda")
+    lemp = LempTopK(ids, X, bucket_size=16384)
+    pos = torch.randperm(n, generator=g)[:5000].cuda()
+    new = torch.randn(5000, D, generator=g).cuda() * 1.5
+    lemp.update_rows(pos, new)
+    assert torch.equal(lemp.vecs_bf, lemp.vecs.bfloat16())
+    Q = torch.randn(128, D, generator=g).cuda()
+    s, i = lemp.query(Q, 50)
+    ref = LempTopK(lemp.ids.clone(), lemp.vecs.clone(), bucket_size=16384)
+    ref.bf16 = False
+    s0, i0 = ref.query(Q, 50)
+    torch.testing.assert_close(s, s0, rtol=0, atol=0)
+    assert torch.equal(i, i0)
