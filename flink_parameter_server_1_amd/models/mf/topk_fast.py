@@ -173,6 +173,8 @@ class LempTopK:
             cnt.zero_()
             if self.bf16:
                 ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e])
+                # (re-score fused into the rank merge, one query per workgroup: 59 us against
+                # 22 + 27 us for the two kernels -- profiles/r2_bf16_topk.md)
                 ops.cand_rescore(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt)
             else:
                 ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen,

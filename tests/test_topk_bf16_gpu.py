@@ -139,3 +139,4 @@ def test_lemp_topk_bf16_incremental_update():
     s0, i0 = ref.query(Q, 50)
     torch.testing.assert_close(s, s0, rtol=0, atol=0)
     assert torch.equal(i, i0)
+
