@@ -32,6 +32,9 @@
 // rows (reg & 3) + 8 (reg >> 2) + 4h are items.
 #include "common.h"
 
+#include <cstdlib>
+#include <string>
+
 using namespace fps;
 
 namespace {
@@ -50,7 +53,7 @@ __device__ __forceinline__ uint32_t sb_key(float f) {  // order-preserving float
 
 // QB 32-query blocks per wave; a workgroup covers SB_WAVES * QB * 32 queries x
 // SB_ITEMS items.
-template <int D, int QB>
+template <int D, int QB, bool MASK = false>
 __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
@@ -149,7 +152,26 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
       float m = acc[0];
 #pragma unroll
       for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
-      if (m > thr) {  // ~k ln(1 + n / s) passes per query and segment
+      if (MASK && m > thr) {  // passing registers as a bit mask, walked by ctz
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) bits |= acc[j] > thr ? (1u << j) : 0u;
+        while (bits) {
+          const int j = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+          if (item < i_end) {
+            if (lc[b] < SB_SLOTS) {
+              lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+              ++lc[b];
+            } else {
+              const int q = qrow[b];
+              const int slot = atomicAdd(cnt + q, 1);
+              if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
+            }
+          }
+        }
+      } else if (!MASK && m > thr) {  // ~k ln(1 + n / s) passes per query and segment
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
@@ -234,17 +256,32 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
   if (k <= 0 || cap <= 0 || qlen == nullptr || xlen == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nit = (N + SB_ITEMS - 1) / SB_ITEMS;
-#define FPS_SB(D_, QB_)                                                                                     \
+#define FPS_SB(D_, QB_, ...)                                                                                \
   {                                                                                                         \
     const int64_t nqt = (B + SB_WAVES * 32 * QB_ - 1) / (SB_WAVES * 32 * QB_);                              \
     if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
-    hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_>), dim3((unsigned)(nqt * nit)), dim3(256), 0, s, Qb, \
+    hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, ##__VA_ARGS__>), dim3((unsigned)(nqt * nit)), dim3(256), 0, s, Qb, \
                        Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, cap);                 \
   }
+  // default at D = 64: 4 query blocks per wave + the bit-mask epilogue (same-box A/B,
+  // profiles/r2_bf16_topk.md).  FPS_SB_VARIANT re-runs the other shapes: "qb2" (2 blocks,
+  // branch per register), "qb1", "qb4" (4 blocks, branches), "mask" (2 blocks, mask)
+  static const int variant = [] {
+    const char* e = std::getenv("FPS_SB_VARIANT");
+    if (!e) return 0;
+    const std::string v(e);
+    return v == "qb1" ? 1 : v == "qb4" ? 2 : v == "mask" ? 3 : v == "qb2" ? 4 : 0;
+  }();
   switch (D) {
-    case 32: FPS_SB(32, 2); break;
-    case 64: FPS_SB(64, 2); break;
-    case 128: FPS_SB(128, 1); break;
+    case 32: FPS_SB(32, 2, true); break;
+    case 64:
+      if (variant == 1) FPS_SB(64, 1)
+      else if (variant == 2) FPS_SB(64, 4)
+      else if (variant == 3) FPS_SB(64, 2, true)
+      else if (variant == 4) FPS_SB(64, 2)
+      else FPS_SB(64, 4, true)
+      break;
+    case 128: FPS_SB(128, 1, true); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef FPS_SB
