@@ -21,6 +21,14 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _scorer() -> str:
+    """Which top-K scan ran: the default bf16 MFMA filter + exact fp32 re-score
+    (results bit-identical to the fp32 scan) or the fp32 scorer (FPS_TOPK_BF16=0)."""
+    if os.environ.get("FPS_TOPK_BF16", "1") == "0":
+        return "fp32 MFMA scan"
+    return "bf16 MFMA filter (proven margin) + fp32 MFMA re-score: exact"
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=1_000_000)
@@ -84,7 +92,7 @@ def main(argv=None):
             "metric": "online MF + top-K: top-K queries/sec (whole node)", "value": queries / dt,
             "unit": "queries/s", "learning_updates_per_s": learned / dt, "n_gpus": comm.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-            "dtype": "fp32", "data": "synthetic ratings, random-init factors (warm item catalogue)",
+            "dtype": "fp32", "scorer": _scorer(), "data": "synthetic ratings, random-init factors (warm item catalogue)",
             "config": {"users": a.users, "items": a.items, "dim": a.dim, "k": a.k, "worker_k": a.worker_k,
                        "batch": a.batch, "negatives": a.negatives, "memory": a.memory, "bucket": a.bucket},
         }), flush=True)

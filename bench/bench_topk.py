@@ -20,6 +20,14 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _scorer() -> str:
+    """Which top-K scan ran: the default bf16 MFMA filter + exact fp32 re-score
+    (results bit-identical to the fp32 scan) or the fp32 scorer (FPS_TOPK_BF16=0)."""
+    if os.environ.get("FPS_TOPK_BF16", "1") == "0":
+        return "fp32 MFMA scan"
+    return "bf16 MFMA filter (proven margin) + fp32 MFMA re-score: exact"
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,7 +86,7 @@ def main(argv=None):
         print(json.dumps({
             "metric": "top-K recommendation queries/sec (whole node)", "value": a.queries * a.steps / dt,
             "unit": "queries/s", "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong", "dtype": "fp32",
+            "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong", "dtype": "fp32", "scorer": _scorer(),
             "data": "synthetic long-tailed item factors, random queries",
             "buckets_scanned_per_query_batch": scanned, "buckets_per_shard": n_buckets, "exact_vs_brute_force": exact,
             "config": {"items": a.items, "dim": a.dim, "k": a.k, "query_batch": a.queries, "bucket": a.bucket},
