@@ -223,19 +223,29 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
   const int n = min(cnt[q], cap);
   if (n == 0) return;
   const int c = lane & 31, h = lane >> 5;
-  const float* qr = Q + (int64_t)q * D;
+  // k pair t = (2t, 2t + 1): lane half h supplies element 2t + h.  Rows are read as
+  // float4 (elements 4m .. 4m + 3 = pairs 2m and 2m + 1), a quarter of the load
+  // instructions of one float per pair
+  const float4* qr = reinterpret_cast<const float4*>(Q + (int64_t)q * D);
   float qh[D / 2];
 #pragma unroll
-  for (int t = 0; t < D / 2; ++t) qh[t] = qr[2 * t + h];
+  for (int m = 0; m < D / 4; ++m) {
+    const float4 v = qr[m];
+    qh[2 * m] = h ? v.y : v.x;
+    qh[2 * m + 1] = h ? v.w : v.z;
+  }
   const uint32_t ktau = sb_key(best_s[(int64_t)q * k + k - 1]);
   for (int c0 = 0; c0 < n; c0 += 32) {
     const bool ok = c0 + c < n;
     const int64_t pos = ok ? cand_id[(int64_t)q * cap + c0 + c] : 0;
-    const float* xr = X + pos * D;
+    const float4* xr = reinterpret_cast<const float4*>(X + pos * D);
     floatx16 acc = {0};
 #pragma unroll
-    for (int t = 0; t < D / 2; ++t)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[t], ok ? xr[2 * t + h] : 0.f, acc, 0, 0, 0);
+    for (int m = 0; m < D / 4; ++m) {
+      const float4 v = ok ? xr[m] : make_float4(0.f, 0.f, 0.f, 0.f);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[2 * m], h ? v.y : v.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[2 * m + 1], h ? v.w : v.z, acc, 0, 0, 0);
+    }
     if (ok && h == 0) {  // lanes 0..31: column c
       const uint32_t key = sb_key(acc[0]);
       cand_key[(int64_t)q * cap + c0 + c] = key > ktau ? key : 0u;
