@@ -193,7 +193,12 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
 
 // rank merge: each candidate's and each kept entry's final position is the
 // number of entries ahead of it (key desc, then id asc; the running list is
-// already in that order) -- 3 barriers instead of the sort's ~40, 6 KB of LDS.
+// already in that order) -- 4 barriers instead of the sort's ~40, 7 KB of LDS.
+// The running entries ahead of a candidate are a prefix of the sorted list
+// (binary search, r_c); the candidates ahead of running entry i are those with
+// r_c <= i (an LDS histogram of r_c and a wave scan) -- the first version
+// walked all k entries per candidate and all candidates per entry (~27 us per
+// 4096-row launch, profiles/r2_bf16_topk.md).
 // Also flags overflowed rows (cnt > cap: merged incompletely) in ovf.
 __global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* __restrict__ cand_key,
                                                                 const int64_t* __restrict__ cand_id,
@@ -205,6 +210,7 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* 
   __shared__ int64_t cid[TK_NT];
   __shared__ uint32_t bkey[TK_MAXK];
   __shared__ int64_t bid[TK_MAXK];
+  __shared__ int32_t hpre[TK_MAXK];  // histogram of r_c, then its inclusive prefix
   __shared__ float out_s[TK_MAXK];
   __shared__ int64_t out_i[TK_MAXK];
   const int row = blockIdx.x, tid = threadIdx.x;
@@ -224,24 +230,54 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* 
     bkey[tid] = fkey(bs[tid]);
     bid[tid] = bi[tid];
   }
+  if (tid < TK_MAXK) hpre[tid] = 0;
   __syncthreads();
-  if (tid < nc) {  // candidate tid: running entries and candidates ahead of it
+  if (tid < nc) {  // candidate tid: running entries (binary search) and candidates ahead of it
     const uint32_t kc = ckey[tid];
     const int64_t ic = cid[tid];
-    int pos = 0;
-    for (int i = 0; i < k; ++i) pos += bkey[i] > kc || (bkey[i] == kc && bid[i] <= ic);
+    int lo = 0, hi = k;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const uint32_t km = bkey[mid];
+      if (km > kc || (km == kc && bid[mid] <= ic)) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < k) atomicAdd(&hpre[lo], 1);  // ahead of running entries lo .. k-1
+    int pos = lo;
+#pragma unroll 4
     for (int j = 0; j < nc; ++j) {
       const uint32_t kj = ckey[j];
       pos += kj > kc || (kj == kc && (cid[j] < ic || (cid[j] == ic && j < tid)));
     }
     if (pos < k) { out_s[pos] = kfloat(kc); out_i[pos] = ic; }
   }
+  __syncthreads();
+  if (tid < 64) {  // inclusive prefix of hpre[0..k): 4 counters per lane + a wave scan
+    int32_t c4[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * tid + q;
+      c4[q] = i < k ? hpre[i] : 0;
+      sum += c4[q];
+    }
+    int32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += y;
+    }
+    int32_t run = inc - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * tid + q;
+      run += c4[q];
+      if (i < k) hpre[i] = run;
+    }
+  }
+  __syncthreads();
   if (tid < k) {  // running entry tid: its index + the candidates ahead of it
-    const uint32_t kb = bkey[tid];
-    const int64_t ib = bid[tid];
-    int pos = tid;
-    for (int j = 0; j < nc; ++j) pos += ckey[j] > kb || (ckey[j] == kb && cid[j] < ib);
-    if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = ib; }
+    const int pos = tid + hpre[tid];
+    if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = bid[tid]; }
   }
   __syncthreads();
   if (tid < k) {
