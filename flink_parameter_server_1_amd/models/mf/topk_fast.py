@@ -48,7 +48,7 @@ class LempTopK:
         self.seed_items = 4096
         #: fused path: test "every query settled" on the host (one sync) only every
         #: ``break_check`` segments; the device tile bound skips settled work anyway
-        self.break_check = 4
+        self.break_check = int(os.environ.get("FPS_TOPK_BREAK_CHECK", "8"))
         #: fused path: segments double from ``seed_items`` up to the bucket size
         self.geometric = True
         self.overflows = 0
