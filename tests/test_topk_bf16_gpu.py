@@ -140,3 +140,21 @@ def test_lemp_topk_bf16_incremental_update():
     torch.testing.assert_close(s, s0, rtol=0, atol=0)
     assert torch.equal(i, i0)
 
+
+
+def test_bf16_filter_tight_margin_worst_case():
+    """Parallel rows of elements just below a bf16 rounding midpoint: bf16 rounds every
+    element down by ~2^-8, so S_bf16 sits ~2^-7 |q||x| under the exact score -- the margin's
+    worst case (Cauchy-Schwarz is tight for parallel rows).  Items differ only below bf16
+    precision, so the filter cannot tell them apart; the re-score keeps exactly the fp32 winners."""
+    D, n, B = 64, 1024, 8
+    base = 1.0 + 2.0 ** -8 - 2.0 ** -20
+    scale = 1.0 + torch.arange(n, dtype=torch.float64) * 2.0 ** -21  # below bf16 resolution
+    X = (torch.full((n, D), base, dtype=torch.float64) * scale.view(-1, 1)).float().cuda()
+    Q = torch.full((B, D), base).cuda()
+    assert torch.equal(X.bfloat16()[0], X.bfloat16()[-1])
+    S = ops.score_gemm(Q, X)
+    theta = S.median(dim=1).values.contiguous()
+    ck, ci, raw, ids = _run_filter(Q, X, theta)
+    assert int(raw.min()) == n
+    _check_exact(Q, X, theta, ck, ci, raw, ids)
