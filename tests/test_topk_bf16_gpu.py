@@ -148,11 +148,13 @@ def test_bf16_filter_tight_margin_worst_case():
     worst case (Cauchy-Schwarz is tight for parallel rows).  Items differ only below bf16
     precision, so the filter cannot tell them apart; the re-score keeps exactly the fp32 winners."""
     D, n, B = 64, 1024, 8
-    base = 1.0 + 2.0 ** -8 - 2.0 ** -20
-    scale = 1.0 + torch.arange(n, dtype=torch.float64) * 2.0 ** -21  # below bf16 resolution
-    X = (torch.full((n, D), base, dtype=torch.float64) * scale.view(-1, 1)).float().cuda()
+    u = 2.0 ** -23  # fp32 ulp at 1
+    base = 1.0 + 2.0 ** -8 - 8 * u
+    # item i bumps its first i % 65 elements by 7 ulps: still below the midpoint 1 + 2^-8
+    bumps = (torch.arange(n) % 65).view(-1, 1) > torch.arange(D).view(1, -1)
+    X = (torch.full((n, D), base) + bumps.float() * 7 * u).cuda()
     Q = torch.full((B, D), base).cuda()
-    assert torch.equal(X.bfloat16()[0], X.bfloat16()[-1])
+    assert bool((X.bfloat16() == 1.0).all())  # every item looks the same in bf16
     S = ops.score_gemm(Q, X)
     theta = S.median(dim=1).values.contiguous()
     ck, ci, raw, ids = _run_filter(Q, X, theta)
