@@ -17,10 +17,10 @@ def load(d):
     return agg, {k: sum(v.values()) for k, v in dur.items()}
 
 
-def main(root="gpurun_out/pmc"):
+def main(root="gpurun_out/pmc", names="mftopk,w2v,mf"):
     print("| run | kernel | time (s, pass 1) | MFMA busy | waves waiting | HBM read | HBM write | read+write rate |")
     print("|---|---|---|---|---|---|---|---|")
-    for name in ("mftopk", "w2v", "mf"):
+    for name in names.split(","):
         a1, t1 = load(f"{root}/{name}_1")
         a2, t2 = load(f"{root}/{name}_2")
         a3, t3 = load(f"{root}/{name}_3")
