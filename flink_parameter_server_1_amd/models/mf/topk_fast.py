@@ -11,6 +11,12 @@ granularity: the scan stops once every query in the batch is settled.  The
 result is exact (equal to brute force), which is what the CPU pruning
 strategies also guarantee; they only change how much work is skipped.
 
+On the GPU the fused scan runs on bf16 MFMA by default: ``ops.score_filter_bf16``
+lists every item whose bf16 score is within a proven rounding margin of the
+query's k-th best, ``ops.cand_rescore`` recomputes those candidates with the fp32
+MFMA chain of the fp32 scorer (bit-identical keys), and the merge is unchanged --
+the same top-K as the fp32 scan at ~2x the rate (``profiles/r2_bf16_topk.md``).
+
 ``DistributedTopK`` reproduces the scatter-gather of ``psTopKGenerator`` /
 ``psOnlineLearnerAndGenerator``: item vectors are sharded over the ranks
 (worker-resident), every rank scores the same broadcast query batch against
