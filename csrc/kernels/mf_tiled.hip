@@ -80,6 +80,33 @@ __device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, const TileGeo&
 
 constexpr int TP_MAX_BUCKETS = 16384;  // 64 KiB of LDS counters
 
+typedef int tp_i2 __attribute__((ext_vector_type(2)));
+typedef int tp_i3 __attribute__((ext_vector_type(3)));
+typedef int tp_i4 __attribute__((ext_vector_type(4)));
+
+// streaming access (NT: non-temporal -- the partition's inputs are read once and
+// its outputs are read by the next step's SGD, long after any cache kept them;
+// marking them streaming keeps the L2 / Infinity Cache for the SGD's user rows)
+template <bool NT, typename T>
+__device__ __forceinline__ T tp_ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void tp_st(T* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Non-temporal scatter accesses are the default (same box, bench.py: 9.12-9.13e9 ->
+// 9.61-9.63e9 updates/s; non-temporal count-kernel loads or tile-SGD record reads on
+// top measured no further gain, profiles/r2_partition.md).  FPS_TP_NT=0: plain accesses.
+static bool tp_nt() {
+  static const bool on = [] { const char* e = getenv("FPS_TP_NT"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+
 // K1: per-workgroup histogram H[w][KT] (plain stores, no global atomics)
 __global__ void __launch_bounds__(1024) tile_hist_kernel(const int32_t* __restrict__ uid,
                                                          const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
@@ -406,7 +433,7 @@ __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, i
 //          rating bits, bucket}
 // LEVEL 2: tmp[work item] -> out (8- or 16-B records) grouped by bucket; kptr = ptr,
 //          cursor = bcursor; work items from wptr / cptr
-template <int LEVEL, bool REC8, bool PIPE = true>
+template <int LEVEL, bool REC8, bool PIPE = true, bool NT = false>
 __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
@@ -462,14 +489,15 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         if (p < nbs) {
           const int64_t x = bs + p;
           if (LEVEL == 1) {
-            ru[e] = uid[x];
-            ri[e] = iid[x];
-            rr[e] = __float_as_int(rating[x]);
+            ru[e] = tp_ld<NT>(uid + x);
+            ri[e] = tp_ld<NT>(iid + x);
+            rr[e] = __float_as_int(tp_ld<NT>(rating + x));
           } else if (REC8) {
-            const int3 t = reinterpret_cast<const int3*>(tmp)[x];
+            const tp_i3 t = tp_ld<NT>(reinterpret_cast<const tp_i3*>(tmp) + x);
             rt[e] = make_int4(t.x, t.y, t.z, 0);
           } else {
-            rt[e] = tmp[x];
+            const tp_i4 t = tp_ld<NT>(reinterpret_cast<const tp_i4*>(tmp) + x);
+            rt[e] = make_int4(t.x, t.y, t.z, t.w);
           }
         }
       }
@@ -519,9 +547,9 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         const int bk = REC8 ? x.z : x.w;
         const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
         const int64_t o = (int64_t)base[kk] + (p - off[kk]);
-        if (LEVEL == 1 && REC8) reinterpret_cast<int3*>(out)[o] = make_int3(x.x, x.y, x.z);
-        else if (LEVEL == 1) reinterpret_cast<int4*>(out)[o] = x;
-        else if (REC8) reinterpret_cast<int2*>(out)[o] = make_int2(x.x, x.y);
+        if (LEVEL == 1 && REC8) tp_st<NT>(reinterpret_cast<tp_i3*>(out) + o, tp_i3{x.x, x.y, x.z});
+        else if (LEVEL == 1) tp_st<NT>(reinterpret_cast<tp_i4*>(out) + o, tp_i4{x.x, x.y, x.z, x.w});
+        else if (REC8) tp_st<NT>(reinterpret_cast<tp_i2*>(out) + o, tp_i2{x.x, x.y});
         else put_rec<false>(out, o, x.x, x.y, __int_as_float(x.z), x.w, g.R);
       }
       __syncthreads();  // LDS reused by the next batch
@@ -1087,10 +1115,14 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
     // measured slower (level 1: 530 vs 401 us per 64M ratings, bench 9.73-9.76e9 vs
     // 9.75-9.78e9, profiles/r2_partition.md), so off by default
     static const bool pipe = [] { const char* e = getenv("FPS_TP3_PIPE"); return e && e[0] == '1'; }();
+    const bool nt = tp_nt();
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
     if (pipe) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, true>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, \
                                  TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr,                \
                                  (const int32_t*)wptr, H1P, OUT);                                                  \
+    else if (nt) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false, true>), dim3(GRID), dim3(1024), 0, s, uid,  \
+                                    iid, rating, TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, \
+                                    (const int32_t*)wptr, H1P, OUT);                                               \
     else hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating,     \
                             TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, \
                             H1P, OUT)
