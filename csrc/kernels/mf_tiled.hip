@@ -101,6 +101,22 @@ __device__ __forceinline__ void tp_st(T* p, T v) {
 // Non-temporal scatter accesses are the default (same box, bench.py: 9.12-9.13e9 ->
 // 9.61-9.63e9 updates/s; non-temporal count-kernel loads or tile-SGD record reads on
 // top measured no further gain, profiles/r2_partition.md).  FPS_TP_NT=0: plain accesses.
+typedef float tp_f4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 f4_ld(const float4* p) {
+  if constexpr (NT) {
+    const tp_f4 v = __builtin_nontemporal_load(reinterpret_cast<const tp_f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void f4_st(float4* p, float4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(tp_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<tp_f4*>(p));
+  else *p = v;
+}
+
 static bool tp_nt() {
   static const bool on = [] { const char* e = getenv("FPS_TP_NT"); return !(e && e[0] == '0'); }();
   return on;
@@ -820,7 +836,10 @@ __device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int6
   }
 }
 
-template <int TPR, int V, int PF, bool REC8, bool PIPE = false>
+// NTI: item rows loaded / stored non-temporal (each is read and written once per
+// chunk; the cache is worth more to the random user rows).  Default on: +0.7 %
+// same box (profiles/r2_partition.md); non-temporal user-row stores: no gain.
+template <int TPR, int V, int PF, bool REC8, bool PIPE = false, bool NTI = false>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
@@ -898,7 +917,7 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
       float4 iv[V], acc[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        iv[v] = Ig[(int64_t)row * D4 + j + v * TPR];
+        iv[v] = f4_ld<NTI>(Ig + (int64_t)row * D4 + j + v * TPR);
         acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       // float4 offsets of the user rows: 32-bit for 8-B records (user < 2^24, D4 <= 64),
@@ -964,7 +983,7 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
       for (int v = 0; v < V; ++v) {
         float4 o = iv[v];
         o.x += acc[v].x; o.y += acc[v].y; o.z += acc[v].z; o.w += acc[v].w;
-        Ig[(int64_t)row * D4 + j + v * TPR] = o;
+        f4_st<NTI>(Ig + (int64_t)row * D4 + j + v * TPR, o);
       }
     }
     __syncthreads();  // LDS reused by the next chunk
@@ -1173,10 +1192,15 @@ FPS_API int fps_mf_sgd_tiled3(float* U, float* I, const void* rec, int rec8, con
   // FPS_MF_PIPE=1 (A/B): 4 user rows per batch, the next batch requested before this
   // batch's stores (same registers as 8 rows per batch without the pipeline)
   static const bool pipe = [] { const char* e = std::getenv("FPS_MF_PIPE"); return e && e[0] == '1'; }();
+  // FPS_SGD_NT=0: item rows with plain accesses (A/B)
+  static const bool nti = [] { const char* e = std::getenv("FPS_SGD_NT"); return !(e && e[0] == '0'); }();
 #define FPS_TILED(TPR_, V_)                                                                                    \
   if (pipe && rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF / 2, true, true>), dim3(grid),   \
                                        dim3(512), 0, s, U, I, rec, ptr, R, block_rows, lr, lambda, I1,         \
                                        block_rows1, T, tcnt);                                                  \
+  else if (rec8 && nti) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, false, true>), dim3(grid), \
+                                           dim3(512), 0, s, U, I, rec, ptr, R, block_rows, lr, lambda, I1,     \
+                                           block_rows1, T, tcnt);                                              \
   else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, \
                                     U, I, rec, ptr, R, block_rows, lr, lambda, I1, block_rows1, T, tcnt);      \
   else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(grid), dim3(512), 0, s, U, I,    \
