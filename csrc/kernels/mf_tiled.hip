@@ -98,9 +98,6 @@ __device__ __forceinline__ void tp_st(T* p, T v) {
   else *p = v;
 }
 
-// Non-temporal scatter accesses are the default (same box, bench.py: 9.12-9.13e9 ->
-// 9.61-9.63e9 updates/s; non-temporal count-kernel loads or tile-SGD record reads on
-// top measured no further gain, profiles/r2_partition.md).  FPS_TP_NT=0: plain accesses.
 typedef float tp_f4 __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ float4 f4_ld(const float4* p) {
@@ -117,9 +114,13 @@ __device__ __forceinline__ void f4_st(float4* p, float4 v) {
   else *p = v;
 }
 
-static bool tp_nt() {
-  static const bool on = [] { const char* e = getenv("FPS_TP_NT"); return !(e && e[0] == '0'); }();
-  return on;
+// Non-temporal scatter accesses are the default (same box, bench.py, 3 alternating runs
+// each: plain 9.85e9, non-temporal 10.05e9 updates/s = +2 %; 12-B level-1 records as
+// three dword accesses beat 16-B slots, 9.93e9; non-temporal count-kernel loads or
+// tile-SGD record reads on top: no further gain; profiles/r2_partition.md).
+static int tp_nt() {  // FPS_TP_NT: 0 plain, 1 non-temporal (12-B records, default), 2 non-temporal (16-B slots)
+  static const int m = [] { const char* e = getenv("FPS_TP_NT"); return e ? atoi(e) : 1; }();
+  return m;
 }
 
 
@@ -449,7 +450,9 @@ __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, i
 //          rating bits, bucket}
 // LEVEL 2: tmp[work item] -> out (8- or 16-B records) grouped by bucket; kptr = ptr,
 //          cursor = bcursor; work items from wptr / cptr
-template <int LEVEL, bool REC8, bool PIPE = true, bool NT = false>
+// NTM: 0 = plain accesses; 1 = non-temporal, 12-B level-1 records as three dwords;
+// 2 = non-temporal, 12-B records in 16-B slots (one 3-dword vector access each)
+template <int LEVEL, bool REC8, bool PIPE = true, int NTM = 0>
 __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
                                                            const int32_t* __restrict__ iid,
                                                            const float* __restrict__ rating,
@@ -504,13 +507,17 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         const int p = e * 1024 + tid;
         if (p < nbs) {
           const int64_t x = bs + p;
+          constexpr bool NT = NTM > 0;
           if (LEVEL == 1) {
             ru[e] = tp_ld<NT>(uid + x);
             ri[e] = tp_ld<NT>(iid + x);
             rr[e] = __float_as_int(tp_ld<NT>(rating + x));
-          } else if (REC8) {
-            const tp_i3 t = tp_ld<NT>(reinterpret_cast<const tp_i3*>(tmp) + x);
+          } else if (REC8 && NTM == 2) {
+            const tp_i3 t = tp_ld<true>(reinterpret_cast<const tp_i3*>(tmp) + x);  // 16-B slots
             rt[e] = make_int4(t.x, t.y, t.z, 0);
+          } else if (REC8) {
+            const int* q = reinterpret_cast<const int*>(tmp) + 3 * x;
+            rt[e] = make_int4(tp_ld<NT>(q), tp_ld<NT>(q + 1), tp_ld<NT>(q + 2), 0);
           } else {
             const tp_i4 t = tp_ld<NT>(reinterpret_cast<const tp_i4*>(tmp) + x);
             rt[e] = make_int4(t.x, t.y, t.z, t.w);
@@ -563,8 +570,14 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         const int bk = REC8 ? x.z : x.w;
         const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
         const int64_t o = (int64_t)base[kk] + (p - off[kk]);
-        if (LEVEL == 1 && REC8) tp_st<NT>(reinterpret_cast<tp_i3*>(out) + o, tp_i3{x.x, x.y, x.z});
-        else if (LEVEL == 1) tp_st<NT>(reinterpret_cast<tp_i4*>(out) + o, tp_i4{x.x, x.y, x.z, x.w});
+        constexpr bool NT = NTM > 0;
+        if (LEVEL == 1 && REC8 && NTM == 2) tp_st<true>(reinterpret_cast<tp_i3*>(out) + o, tp_i3{x.x, x.y, x.z});
+        else if (LEVEL == 1 && REC8) {
+          int* q = reinterpret_cast<int*>(out) + 3 * o;
+          tp_st<NT>(q, x.x);
+          tp_st<NT>(q + 1, x.y);
+          tp_st<NT>(q + 2, x.z);
+        } else if (LEVEL == 1) tp_st<NT>(reinterpret_cast<tp_i4*>(out) + o, tp_i4{x.x, x.y, x.z, x.w});
         else if (REC8) tp_st<NT>(reinterpret_cast<tp_i2*>(out) + o, tp_i2{x.x, x.y});
         else put_rec<false>(out, o, x.x, x.y, __int_as_float(x.z), x.w, g.R);
       }
@@ -1134,12 +1147,15 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
     // measured slower (level 1: 530 vs 401 us per 64M ratings, bench 9.73-9.76e9 vs
     // 9.75-9.78e9, profiles/r2_partition.md), so off by default
     static const bool pipe = [] { const char* e = getenv("FPS_TP3_PIPE"); return e && e[0] == '1'; }();
-    const bool nt = tp_nt();
+    const int ntm = tp_nt();
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
     if (pipe) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, true>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, \
                                  TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr,                \
                                  (const int32_t*)wptr, H1P, OUT);                                                  \
-    else if (nt) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false, true>), dim3(GRID), dim3(1024), 0, s, uid,  \
+    else if (ntm == 1) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false, 1>), dim3(GRID), dim3(1024), 0, s, uid, \
+                                    iid, rating, TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, \
+                                    (const int32_t*)wptr, H1P, OUT);                                               \
+    else if (ntm == 2) hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false, 2>), dim3(GRID), dim3(1024), 0, s, uid, \
                                     iid, rating, TMP, n, chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, \
                                     (const int32_t*)wptr, H1P, OUT);                                               \
     else hipLaunchKernelGGL((tp3_scatter_kernel<L, R8, false>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating,     \
