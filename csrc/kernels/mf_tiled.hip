@@ -1007,7 +1007,10 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
 
 // Ratings per partition workgroup: longer chunks give longer runs per bucket in
 // the scatter (chunk / KT records land contiguously), fewer give more parallelism.
-static int64_t g_tp_chunk = 65536;
+// 262144 (256 level-1 workgroups per 64M ratings) leaves more of the chip to the
+// overlapped SGD: same box, alternating, 65536 10.41 / 10.54e9, 131072 10.58 / 10.61e9,
+// 262144 10.68 / 10.69e9, 524288 10.56 / 10.38e9 updates/s (profiles/r2_partition.md).
+static int64_t g_tp_chunk = 262144;
 
 FPS_API void fps_tile_partition_set_chunk(int64_t chunk) { g_tp_chunk = chunk > 1024 ? chunk : 1024; }
 
