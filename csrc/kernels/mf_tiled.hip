@@ -1145,6 +1145,7 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   hipLaunchKernelGGL(tp3_workptr_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)ccount, NC, wptr);
   if (n > 0) {
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
+    // (capping the level-2 workgroups at 512 / 256 instead: no gain, profiles/r2_partition.md)
     if (g2 > 1024) g2 = 1024;
     // FPS_TP3_PIPE=1: the scatters with the register prefetch of the next batch --
     // measured slower (level 1: 530 vs 401 us per 64M ratings, bench 9.73-9.76e9 vs
@@ -1287,6 +1288,7 @@ FPS_API int fps_tile_partition4(const int32_t* uid, const int32_t* iid, const fl
     hipLaunchKernelGGL(tp4_workptr_kernel, dim3(1), dim3(64), 0, s, (const int32_t*)ccursor, (const int32_t*)cstart,
                        NC, wptr);
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
+    // (capping the level-2 workgroups at 512 / 256 instead: no gain, profiles/r2_partition.md)
     if (g2 > 1024) g2 = 1024;
 #define FPS_TP4_L2(R8)                                                                                         \
     hipLaunchKernelGGL((tp4_scatter_kernel<2, R8>), dim3((int)g2), dim3(1024), 0, s, uid, iid, rating,        \
