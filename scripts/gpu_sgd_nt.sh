@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of non-temporal item-row accesses in the tile SGD (FPS_SGD_NT=0: plain; default: non-temporal),
-# bench.py alternating on one box.  (The user-row variants of profiles/r2_partition.md ran at
-# commit d218c61's parent and were removed: no gain.)
+# bench.py alternating on one box.  (The user-row variants of profiles/r2_partition.md were an A/B
+# patch, not kept: no gain.)
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/snt
