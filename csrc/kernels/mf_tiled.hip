@@ -1007,12 +1007,30 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
 
 // Ratings per partition workgroup: longer chunks give longer runs per bucket in
 // the scatter (chunk / KT records land contiguously), fewer give more parallelism.
-// 262144 (256 level-1 workgroups per 64M ratings) leaves more of the chip to the
-// overlapped SGD: same box, alternating, 65536 10.41 / 10.54e9, 131072 10.58 / 10.61e9,
-// 262144 10.68 / 10.69e9, 524288 10.56 / 10.38e9 updates/s (profiles/r2_partition.md).
-static int64_t g_tp_chunk = 262144;
+// Level 3 (default) sizes the chunk from the bucket count unless set explicitly
+// (FPS_TILE_PARTITION_CHUNK): ~16 records per bucket and workgroup, 65536 .. 262144
+// (tp3_chunk).  Same box, alternating: at KT = 15.6k buckets (10M users, 4 phases)
+// 65536 10.41 / 10.54e9, 262144 10.68 / 10.69e9 updates/s; at KT = 3.9k (2.5M users,
+// 1 phase) 65536 9.89 / 9.88e9, 262144 9.69 / 9.73e9 (profiles/r2_partition.md).
+static int64_t g_tp_chunk = 65536;
+static bool g_tp_chunk_set = false;
 
-FPS_API void fps_tile_partition_set_chunk(int64_t chunk) { g_tp_chunk = chunk > 1024 ? chunk : 1024; }
+FPS_API void fps_tile_partition_set_chunk(int64_t chunk) {
+  g_tp_chunk = chunk > 1024 ? chunk : 1024;
+  g_tp_chunk_set = true;
+}
+
+static int tp3_groups(int64_t n, int KT) {
+  int64_t c = g_tp_chunk;
+  if (!g_tp_chunk_set) {
+    c = 65536;
+    while (c < 16 * (int64_t)KT && c < 262144) c <<= 1;
+  }
+  int64_t g = (n + c - 1) / c;
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  return (int)g;
+}
 
 // Workspace: H holds G * KT int32 (G = fps_tile_partition_groups(n)), totals KT.
 FPS_API int fps_tile_partition_groups(int64_t n) {
@@ -1131,7 +1149,7 @@ FPS_API int fps_tile_partition3(const int32_t* uid, const int32_t* iid, const fl
   int32_t* H1 = wptr + NC + 1;
   hipError_t e = hipMemsetAsync(ws, 0, sizeof(int32_t) * (size_t)(4 * NC + 2 + 2 * KT), s);
   if (e != hipSuccess) return (int)e;
-  const int G = fps_tile_partition_groups(n);
+  const int G = tp3_groups(n, KT);
   const int64_t chunk = (n + G - 1) / G;
   const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
   const int Gc = (G + sub - 1) / sub;
