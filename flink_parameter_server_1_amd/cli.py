@@ -137,12 +137,14 @@ def cmd_mf_gpu(args):
                                 device=comm.device, truth_dim=args.truth_dim)
         batch = lambda s: data.batch(s, args.batch)  # noqa: E731
     ck = Checkpointer(args.checkpoint_dir, {"users": m.users, "items": m.items}, comm,
-                      every_steps=args.checkpoint_every, before_save=m.flush) if args.checkpoint_dir else None
-    start = 0
+                      every_steps=args.checkpoint_every, before_save=m.flush, aux=m) if args.checkpoint_dir else None
+    start, man = 0, None
     if ck and args.resume:
         man = ck.restore_latest()
         start = man["step"] if man else 0
-    if args.model_in_users or args.model_in_items:  # warm start from id;value dumps
+    if man is None and (args.model_in_users or args.model_in_items):
+        # warm start from id;value dumps -- only when no checkpoint was restored
+        # (a restored checkpoint is newer than the initial model and wins)
         from .utils.io import read_factors_text
 
         m.load_model(read_factors_text(args.model_in_users) if args.model_in_users else None,

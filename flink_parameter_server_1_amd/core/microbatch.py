@@ -171,8 +171,14 @@ class MicroBatcher:
                 if buf:
                     yield flush()
                 return
+            # ticks fall due whatever the record rate (``TimerLogic`` fires every
+            # interval, ``M/common/TimerLogic.scala:13-26``): a saturated queue never
+            # reaches the ``Empty`` branch above, so due ticks are handled here too
+            now = self.clock()
+            for p in self.policies:
+                p.on_tick(now)
             buf.append(x)
-            last_rec = self.clock()
+            last_rec = now
             for p in self.policies:
                 p.on_record()
             if self.predicate(self.policies) or (self.max_records and len(buf) >= self.max_records):

@@ -316,6 +316,9 @@ class TensorRuntime:
                 uk, inv = torch.unique(keys[pending], return_inverse=True)
                 cand = torch.full((uk.numel(),), n, dtype=torch.int64, device=self.device)
                 cand.scatter_reduce_(0, inv, pending, reduce="amin")
+                # torch.unique orders by key; the plan slots below are looked up by
+                # request position (searchsorted), so order the candidates by position
+                cand = cand.sort().values
             else:
                 cand = pending
             pull = lps.acquire(keys[cand], flag=int(pending.numel() > 0))

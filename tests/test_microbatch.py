@@ -103,3 +103,43 @@ def test_streaming_mf_on_the_tensor_engine_ends_by_idle_timeout():
     assert mb.ended_by == "idle" and time.monotonic() - t0 < 20
     assert sum(mb.flushes) == 700
     assert sum(e.value[0].numel() for e in out if isinstance(e, Left)) == 700
+
+
+def test_timer_fires_under_a_saturated_source():
+    """a source that never lets the queue run empty must still see the
+    timer tick (``TimerLogic`` fires every interval whatever the message rate).
+    Fake clock that advances 0.25 ms per reading (the consumer reads it about
+    twice per record): Count(1000) AND Timer(10 ms) flushes every 1000 records;
+    Timer alone flushes every ~20 records although the queue is never empty."""
+    t = [0.0]
+
+    def clock():
+        t[0] += 0.00025
+        return t[0]
+
+    ready = threading.Event()
+    q_src = list(range(5000))
+
+    def src():
+        ready.wait()
+        yield from q_src
+
+    mb = MicroBatcher(src(), [CountPolicy(1000), TimerPolicy(10, clock=clock)], predicate=all_of, clock=clock)
+    it = iter(mb)
+    ready.set()
+    time.sleep(0.2)  # the reader fills the queue first: it is never empty for the consumer
+    out = list(it)
+    assert sum(len(b) for b in out) == 5000
+    assert mb.flushes == [1000] * 5, mb.flushes
+    ready2 = threading.Event()
+
+    def src2():
+        ready2.wait()
+        yield from q_src
+
+    mb2 = MicroBatcher(src2(), [TimerPolicy(10, clock=clock)], clock=clock)
+    it2 = iter(mb2)
+    ready2.set()
+    time.sleep(0.2)
+    out2 = list(it2)
+    assert sum(len(b) for b in out2) == 5000 and len(out2) >= 100, mb2.flushes

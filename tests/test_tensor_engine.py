@@ -249,3 +249,31 @@ def test_distributed_mf_ps_path_equals_per_record_engine(sgd_mode):
         np.testing.assert_allclose(m.U[k].numpy(), v, rtol=0, atol=2e-6)
     for k, v in V_ref.items():
         np.testing.assert_allclose(m.I[k].numpy(), v, rtol=0, atol=2e-6)
+
+
+def _locked_unsorted(rank, world):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    rt = TensorRuntime(Comm()).start(_LockWorker(), DeviceLockPSLogic(5, 1, op="set"))
+    rt.load_model([(k, [1000.0 * k]) for k in range(5) if k % world == rank])
+    for _ in range(2):
+        rt.submit(torch.tensor([3, 1, 3, 0]))  # unsorted keys with a duplicate
+    rt.finish()
+    emitted = [(ids.tolist(), v.reshape(-1).tolist()) for ids, v in (e.value for e in rt.outputs if isinstance(e, Right))]
+    return rt.ps_logic.table.dump(only_touched=False), emitted
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_lock_logic_unsorted_keys_route_rows_to_their_key(world):
+    """the lock holder must receive ITS key's row whatever the key order
+    of the pull -- every key starts at 1000*k, so a row routed to another key
+    shows up as a value outside [1000k, 1000k + count]."""
+    res = run_ranks(_locked_unsorted, world) if world > 1 else [_locked_unsorted(0, 1)]
+    vals = {}
+    for (ids, w), emitted in res:
+        vals.update(dict(zip(ids.tolist(), w.reshape(-1).tolist())))
+        for ks, vs in emitted:
+            for k, v in zip(ks, vs):
+                assert 1000.0 * k < v <= 1000.0 * k + 4 * world, (k, v)
+    assert vals[3] == 3000.0 + 4 * world and vals[1] == 1000.0 + 2 * world and vals[0] == 2 * world
+    assert vals[2] == 2000.0 and vals[4] == 4000.0
