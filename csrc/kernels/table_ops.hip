@@ -160,8 +160,13 @@ __global__ void dedup_claim_kernel(const int32_t* __restrict__ keys, int64_t n, 
 }
 
 // owners take a slot inside their destination shard's group
+// part_kind 0 = hash (|id| % W, dense local id / W), 1 = range, 2 = sparse hash:
+// |id| % W over the full signed 32-bit range (int64 |.|: no Math.abs(Int.MinValue)
+// overflow) and the id itself as the key (the owner's device hash
+// table maps it to a row, kernels/hash_table.hip)
 __device__ __forceinline__ void key_dest(int32_t k, int W, int part_kind, int64_t block, int& d, int32_t& local) {
   if (part_kind == 0) { d = k % W; local = k / W; }
+  else if (part_kind == 2) { const int64_t a = k < 0 ? -(int64_t)k : (int64_t)k; d = (int)(a % W); local = k; }
   else { d = (int)(k / block); if (d >= W) d = W - 1; local = (int32_t)(k - (int64_t)d * block); }
 }
 
@@ -287,8 +292,8 @@ __global__ void bucketize_kernel(const int32_t* __restrict__ keys, int64_t n, in
     const int64_t b = w0 + lane;
     int d = 0;
     if (b < n) {
-      const int32_t k = keys[b] < 0 ? -keys[b] : keys[b];
-      if (part_kind == 0) d = k % W;
+      const int64_t k = keys[b] < 0 ? -(int64_t)keys[b] : (int64_t)keys[b];
+      if (part_kind == 0 || part_kind == 2) d = (int)(k % W);
       else { d = (int)(k / block); if (d >= W) d = W - 1; }
       shard[b] = d;
     }
@@ -592,7 +597,8 @@ FPS_API int fps_dedup(const int32_t* keys, int64_t n, unsigned long long* map, u
 }
 
 // Hashed variant for huge id spaces: tab (uint64) and owner_slot (int32) hold
-// cap entries (power of two, >= 2n, <= 2^31); hslot has n entries.  Keys >= 0.
+// cap entries (power of two, >= 2n, <= 2^31); hslot has n entries.  Keys >= 0,
+// or any int32 with part_kind 2 (sparse ids).
 FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long* tab, int64_t cap, uint32_t epoch,
                              int W, int part_kind, int64_t block, int32_t* counts, int32_t* prefix, int32_t* hslot,
                              int32_t* owner_slot, int32_t* uniq, int32_t* pos, void* stream) {

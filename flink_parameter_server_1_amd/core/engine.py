@@ -359,11 +359,11 @@ def _default_partitioners(P: int):
 def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[ParameterServerLogic] = None, *,
               param_init: Optional[Callable] = None, param_update: Optional[Callable] = None,
               param_partitioner: Optional[Callable] = None, w_in_partition: Optional[Callable] = None,
-              worker_parallelism: int = 1, ps_parallelism: int = 1,
+              worker_parallelism: Optional[int] = None, ps_parallelism: Optional[int] = None,
               worker_receiver=None, worker_sender=None, ps_receiver=None, ps_sender=None,
               iteration_wait_time: Optional[float] = None, data_partitioner: Optional[Callable] = None,
               runtime=None, output_sink: Optional[Callable] = None, backend: str = "record",
-              comm=None, staleness: int = 0) -> List[Any]:
+              comm=None, staleness: int = 0, num_ids: Optional[int] = None, combine: str = "sum") -> List[Any]:
     """Run a parameter-server job; returns the ``Left(wout)``/``Right(psout)`` stream.
 
     Covers the three reference overloads (``M/FlinkParameterServer.scala:62-336``):
@@ -376,23 +376,42 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
     ``backend="tensor"`` runs the job on the tensor engine instead
     (``core.tensor_engine``, one process per GPU under torchrun):
     ``training_data`` is this rank's iterable of micro-batches,
-    ``worker_logic`` a ``BatchedWorkerLogic``, ``ps_logic`` a device PS logic
-    (``ps.device_logics``); worker / PS parallelism = the world size of
-    ``comm``; ``staleness`` bounds the micro-batches in flight (the
-    ``pullLimit`` analogue, ``tensor_engine.staleness_for_pull_limit``).
+    ``worker_logic`` a ``BatchedWorkerLogic``; worker / PS parallelism = the
+    world size of ``comm``; ``staleness`` bounds the micro-batches in flight
+    (the ``pullLimit`` analogue, ``tensor_engine.staleness_for_pull_limit``).
+    The three overloads map to:
+
+    (a) ``param_init(ids) -> rows`` / ``param_update(old, delta[, ids]) -> new``
+        (vectorised torch callables) -> ``DeviceFunctionPSLogic``; ``num_ids``
+        sizes a dense shard, ``None`` = a sparse hash-table shard over the whole
+        int32 id space; ``combine`` = how repeated pushes of a key in one
+        micro-batch meet (``sum`` / ``max`` / ``min`` / ``last`` / ``sequential``);
+    (b) ``ps_logic`` = a device PS logic (``ps.device_logics``);
+    (c) ``param_partitioner`` = a vectorised ``ids -> shard`` callable or an
+        ``owner[num_ids]`` tensor (the shard lookup the device path routes by).
+
+    Arguments the tensor engine cannot honour raise ``ValueError`` instead of
+    being dropped: wire adapters (the wire is SoA tensors; batching =
+    ``core.microbatch.MicroBatcher``), ``w_in_partition`` (answers always return
+    to the requester), ``data_partitioner`` / ``runtime`` (each rank passes its
+    own source), parallelisms other than the world size.
     """
     if backend == "tensor":
-        from .tensor_engine import transform_tensor
-
-        return transform_tensor(training_data, worker_logic, ps_logic, comm=comm, staleness=staleness,
-                                iteration_wait_time=iteration_wait_time, output_sink=output_sink)
+        return _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_update, param_partitioner,
+                                 w_in_partition, worker_parallelism, ps_parallelism,
+                                 dict(worker_receiver=worker_receiver, worker_sender=worker_sender,
+                                      ps_receiver=ps_receiver, ps_sender=ps_sender,
+                                      data_partitioner=data_partitioner, runtime=runtime),
+                                 iteration_wait_time, output_sink, comm, staleness, num_ids, combine)
     if backend != "record":
         raise ValueError(f"backend must be 'record' or 'tensor', not {backend!r}")
+    if num_ids is not None or combine != "sum" or comm is not None or staleness:
+        raise ValueError("num_ids / combine / comm / staleness are tensor-backend arguments")
     if ps_logic is None:
         if param_init is None or param_update is None:
             raise ValueError("give ps_logic or (param_init, param_update)")
         ps_logic = SimplePSLogic(param_init, param_update)
-    W, P = int(worker_parallelism), int(ps_parallelism)
+    W, P = int(worker_parallelism or 1), int(ps_parallelism or 1)
     dp, dw = _default_partitioners(P)
     param_partitioner = param_partitioner or dp
     w_in_partition = w_in_partition or dw
@@ -413,6 +432,61 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
                                                             param_partitioner, w_in_partition, W, P,
                                                             worker_receiver, worker_sender, ps_receiver,
                                                             ps_sender, data_partitioner)
+
+
+def _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_update, param_partitioner,
+                      w_in_partition, worker_parallelism, ps_parallelism, adapters, iteration_wait_time, output_sink,
+                      comm, staleness, num_ids, combine):
+    """``transform(backend="tensor")``: map the overloads onto the tensor engine
+    (see ``transform``), refusing what it cannot honour."""
+    import torch
+
+    from ..api.batched import BatchedWorkerLogic
+    from ..parallel.comm import Comm
+    from ..ps.device_logics import DeviceFunctionPSLogic, DevicePSLogic
+    from .tensor_engine import transform_tensor
+
+    given = sorted(k for k, v in adapters.items() if v is not None)
+    if given:
+        raise ValueError(f"backend='tensor' does not take {given}: its wire format is fixed (SoA tensors over "
+                         "all-to-alls), micro-batching is core.microbatch.MicroBatcher, and each rank passes its own "
+                         "source iterable")
+    if w_in_partition is not None:
+        raise ValueError("backend='tensor' always answers a pull to the worker that sent it; w_in_partition "
+                         "cannot be honoured")
+    if not isinstance(worker_logic, BatchedWorkerLogic):
+        raise TypeError("backend='tensor' needs a BatchedWorkerLogic (api.batched)")
+    comm = comm or Comm()
+    for name, par in (("worker_parallelism", worker_parallelism), ("ps_parallelism", ps_parallelism)):
+        if par is not None and int(par) != comm.world:
+            raise ValueError(f"backend='tensor': {name}={par} but the job has {comm.world} ranks (one worker and "
+                             "one PS shard per rank)")
+    if ps_logic is None:
+        if param_init is None or param_update is None:
+            raise ValueError("give ps_logic or (param_init, param_update)")
+        probe = torch.as_tensor(param_init(torch.zeros(1, dtype=torch.int64)))
+        dim = int(probe.reshape(1, -1).shape[1])
+        if param_partitioner is not None and num_ids is None:
+            raise ValueError("a custom param_partitioner on the tensor backend needs num_ids (a dense id space)")
+        # the parameter type P follows the init: fp64 rows (and wire) for a double init
+        f64 = probe.dtype == torch.float64
+        ps_logic = DeviceFunctionPSLogic(dim, param_init, param_update, num_ids, combine=combine,
+                                         partition=param_partitioner if param_partitioner is not None else "hash",
+                                         dtype=torch.float64 if f64 else torch.float32,
+                                         wire_dtype="fp64" if f64 else "fp32")
+    else:
+        if param_init is not None or param_update is not None:
+            raise ValueError("give ps_logic or (param_init, param_update), not both")
+        if num_ids is not None or combine != "sum":
+            raise ValueError("num_ids / combine configure overload (a); set them on the device logic instead")
+        if not isinstance(ps_logic, DevicePSLogic):
+            raise TypeError("backend='tensor' needs a device PS logic (ps.device_logics)")
+        if param_partitioner is not None:
+            if ps_logic.sparse or ps_logic._given[0] is not None:
+                raise ValueError("param_partitioner needs a dense shard allocated by the logic")
+            ps_logic.partition = param_partitioner
+    return transform_tensor(training_data, worker_logic, ps_logic, comm=comm, staleness=staleness,
+                            iteration_wait_time=iteration_wait_time, output_sink=output_sink)
 
 
 def _execute_local(rt: LocalRuntime, training_data, worker_logic, ps_logic, param_partitioner, w_in_partition,
@@ -667,7 +741,7 @@ def transform_with_model_load(model: Iterable, training_data, worker_logic, ps_l
     Model records are pushed into the (empty) PS store before any pull is
     served.  ``ps_logic`` must accept a push for a key it has not seen.
     """
-    W, P = int(worker_parallelism), int(ps_parallelism)
+    W, P = int(worker_parallelism or 1), int(ps_parallelism or 1)
     dp, dw = _default_partitioners(P)
     w2ps, ps2w = _wrap_partitioners(param_partitioner or dp, w_in_partition or dw, double=False)
     inputs = _model_load_inputs(model, training_data, W, data_partitioner, double=False)
@@ -683,7 +757,7 @@ def transform_with_double_model_load(model: Iterable, training_data, worker_logi
     """Warm start of PS model (``Left((id, p))``) and worker-resident model
     (``Right((id, p))``, delivered to ``worker_logic.update_model`` of the worker
     receiving the record) (``M/FlinkParameterServer.scala:607-816``)."""
-    W, P = int(worker_parallelism), int(ps_parallelism)
+    W, P = int(worker_parallelism or 1), int(ps_parallelism or 1)
     dp, dw = _default_partitioners(P)
     w2ps, ps2w = _wrap_partitioners(param_partitioner or dp, w_in_partition or dw, double=True)
     inputs = _model_load_inputs(model, training_data, W, data_partitioner, double=True)

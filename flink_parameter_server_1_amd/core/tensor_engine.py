@@ -73,6 +73,7 @@ class _Client(BatchedPSClient):
         self._acc: Optional[torch.Tensor] = None
         self._mask: Optional[torch.Tensor] = None
         self._direct: Optional[torch.Tensor] = None
+        self._seq: List[tuple] = []  # (pos, deltas, mask) per push, combine="sequential"
         self._arb_keys: List[torch.Tensor] = []
         self._arb_vals: List[torch.Tensor] = []
 
@@ -110,9 +111,31 @@ class _Client(BatchedPSClient):
         pos = self._plan.pos[r.off:r.off + r.n].long()
         if mask is not None:
             mask = mask.to(device=self.rt.device, dtype=torch.bool).reshape(-1)
+        self._accumulate(pos, d, mask)
+
+    def _accumulate(self, pos, d, mask):
+        """Fold request deltas into the per-unique-key push buffer with the
+        logic's ``combine`` rule (``sum`` unless the PS rule says otherwise)."""
+        comb = self.rt.ps_logic.combine
+        if comb == "sequential":  # kept per request; TensorRuntime._push sends one round per repeat
+            self._seq.append((pos, d, mask))
+            return
         self._ensure_acc()
-        if self.rt.ps_logic.op == "set":  # last writer wins, in request order
-            rid = torch.arange(r.n, device=pos.device)
+        if comb in ("max", "min"):
+            U = self._plan.n_unique
+            idx = pos if mask is None else torch.where(mask, pos, torch.full_like(pos, U))
+            tmp = torch.zeros((U + 1, self._dim()), dtype=self._acc.dtype, device=self._acc.device)
+            tmp.scatter_reduce_(0, idx.view(-1, 1).expand(-1, self._dim()), d.to(tmp.dtype),
+                                reduce="amax" if comb == "max" else "amin", include_self=False)
+            hit = torch.zeros(U + 1, dtype=torch.bool, device=pos.device)
+            hit[idx] = True
+            tmp, hit = tmp[:U], hit[:U]
+            both = torch.maximum(self._acc, tmp) if comb == "max" else torch.minimum(self._acc, tmp)
+            self._acc = torch.where((hit & self._mask).view(-1, 1), both,
+                                    torch.where(hit.view(-1, 1), tmp, self._acc))
+            self._mask |= hit
+        elif self.rt.ps_logic.op == "set" or comb == "last":  # last writer wins, in request order
+            rid = torch.arange(pos.numel(), device=pos.device)
             if mask is not None:
                 rid = torch.where(mask, rid, torch.full_like(rid, -1))
             last = torch.full((self._plan.n_unique,), -1, dtype=torch.int64, device=pos.device)
@@ -134,6 +157,11 @@ class _Client(BatchedPSClient):
             raise RuntimeError("push_unique() is only valid inside on_pull_recv_batch")
         U = self._plan.n_unique
         d = deltas.reshape(U, self._dim())
+        if self.rt.ps_logic.combine != "sum":
+            if mask is not None:
+                mask = mask.to(device=d.device, dtype=torch.bool).reshape(-1)
+            self._accumulate(torch.arange(U, device=d.device), d, mask)
+            return
         if self._acc is None and self._direct is None and mask is None:
             self._direct = d  # fast path: the worker's buffer goes on the wire as is
             return
@@ -260,7 +288,7 @@ class TensorRuntime:
     def _compute(self, rows, plan, reqs):
         c = self.client
         c._plan, c._acc, c._mask, c._direct = plan, None, None, None
-        c._arb_keys, c._arb_vals = [], []
+        c._arb_keys, c._arb_vals, c._seq = [], [], []
         with stage("engine.on_pull_recv", self.timer):
             for r in reqs:
                 c._req = r
@@ -275,7 +303,9 @@ class TensorRuntime:
         if not self.worker_logic.pushes:  # a query-only worker: no push round at all
             return
         ps = self.ps_logic.ps
-        if c._direct is not None:
+        if self.ps_logic.combine == "sequential":
+            self._push_rounds(plan, c)
+        elif c._direct is not None:
             deltas, mask = c._direct, None
         elif c._acc is not None:
             deltas, mask = c._acc, c._mask
@@ -283,16 +313,58 @@ class TensorRuntime:
             deltas = torch.zeros((plan.n_unique, self.ps_logic.dim), dtype=self.ps_logic.dtype, device=self.device)
             mask = torch.zeros(plan.n_unique, dtype=torch.bool, device=self.device)
         emit = self.ps_logic.emit == "push"
-        updated = ps.push(plan, deltas, lr=self.ps_logic.lr, return_updated=emit, mask=mask)
-        self.counters.add("pushes", plan.n_unique)
-        for out in self.ps_logic.after_push(updated):
-            self._emit(Right(out))
+        if self.ps_logic.combine != "sequential":
+            updated = ps.push(plan, deltas, lr=self.ps_logic.lr, return_updated=emit, mask=mask)
+            self.counters.add("pushes", plan.n_unique)
+            for out in self.ps_logic.after_push(updated):
+                self._emit(Right(out))
         if self.worker_logic.arbitrary_pushes:
             keys = torch.cat(c._arb_keys) if c._arb_keys else torch.zeros(0, dtype=torch.int64, device=self.device)
             vals = torch.cat(c._arb_vals) if c._arb_vals else \
                 torch.zeros((0, self.ps_logic.dim), dtype=torch.float32, device=self.device)
             upd = ps.push_keys(keys, vals, lr=self.ps_logic.lr, return_updated=emit)
             for out in self.ps_logic.after_push(upd):
+                self._emit(Right(out))
+
+    def _push_rounds(self, plan, c) -> None:
+        """``combine="sequential"``: the j-th push of a key in this micro-batch
+        travels in round j, so a non-associative user rule sees the pushes one
+        at a time in request order, as the reference's per-record PS applies
+        them.  Rounds = the most repeats of a key on any rank (one host sync and
+        a max all-reduce: the price of the exact order)."""
+        U, D = plan.n_unique, self.ps_logic.dim
+        dev = self.device
+        if c._seq:
+            pos = torch.cat([p for p, _, _ in c._seq])
+            d = torch.cat([x.to(self.ps_logic.dtype) for _, x, _ in c._seq])
+            m = torch.cat([torch.ones(p.numel(), dtype=torch.bool, device=dev) if mk is None else mk
+                           for p, _, mk in c._seq])
+        else:
+            pos = torch.zeros(0, dtype=torch.int64, device=dev)
+            d = torch.zeros((0, D), dtype=self.ps_logic.dtype, device=dev)
+            m = torch.zeros(0, dtype=torch.bool, device=dev)
+        pos = torch.where(m, pos, torch.full_like(pos, U))  # masked pushes sit out every round
+        order = torch.argsort(pos, stable=True)
+        sp = pos[order]
+        first = torch.ones(sp.numel(), dtype=torch.bool, device=dev)
+        first[1:] = sp[1:] != sp[:-1]
+        idx = torch.arange(sp.numel(), device=dev)
+        start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+        occ = torch.empty_like(idx)
+        occ[order] = idx - start
+        local = int(occ[pos < U].max()) + 1 if bool((pos < U).any()) else 0
+        rounds = int(self.comm.max_over_ranks(float(local)))
+        emit = self.ps_logic.emit == "push"
+        for j in range(max(rounds, 1)):
+            sel = (occ == j) & (pos < U)
+            p = torch.where(sel, pos, torch.full_like(pos, U))
+            buf = torch.zeros((U + 1, D), dtype=self.ps_logic.dtype, device=dev)
+            buf[p] = d
+            hit = torch.zeros(U + 1, dtype=torch.bool, device=dev)
+            hit[p] = True
+            updated = self.ps_logic.ps.push(plan, buf[:U], lr=self.ps_logic.lr, return_updated=emit, mask=hit[:U])
+            self.counters.add("pushes", plan.n_unique)
+            for out in self.ps_logic.after_push(updated):
                 self._emit(Right(out))
 
     def _locked_step(self, keys, reqs, flag) -> None:

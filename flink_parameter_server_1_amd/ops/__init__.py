@@ -135,6 +135,55 @@ def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: 
     return R.apply_rows(table, idx, delta, op, lr, eps, state, touched)
 
 
+_HT_INIT = {"zeros": 0, "const": 1, "uniform": 2}
+
+
+def ht_lookup(keys: torch.Tensor, tab: torch.Tensor, rowmap: torch.Tensor, rowkey: torch.Tensor, count: torch.Tensor,
+              overflow: torch.Tensor, insert: bool, rows: torch.Tensor = None, init=None, seed: int = 0):
+    """Persistent device hash table (``kernels/hash_table.hip``): rows of int32
+    ``keys`` (any value of the signed 32-bit range), inserting absent keys when
+    ``insert`` (the fresh rows are initialised per ``init`` = ``("zeros",)`` /
+    ``("const", v)`` / ``("uniform", lo, hi)``; ``None`` leaves them).  Returns
+    ``(row int32[n], fresh uint8[n])``; ``row = -1``: absent (lookup) or a full
+    table (``overflow[0]`` set).  The caller sizes ``tab`` / ``rowkey`` first
+    (``parallel.hash_table.HashShardTable.reserve``)."""
+    n = keys.numel()
+    keys = keys.to(torch.int32).contiguous()
+    kind, lo, hi = -1, 0.0, 0.0
+    if init is not None:
+        kind = _HT_INIT[init[0]]
+        lo = float(init[1]) if len(init) > 1 else 0.0
+        hi = float(init[2]) if len(init) > 2 else 0.0
+    if _on_gpu(tab):
+        row = torch.empty(n, dtype=torch.int32, device=tab.device)
+        fresh = torch.zeros(n, dtype=torch.uint8, device=tab.device)
+        if n == 0:
+            return row, fresh
+        slot = torch.empty(n, dtype=torch.int32, device=tab.device)
+        d = rows.shape[1] if rows is not None else 0
+        N.check(N.require().fps_ht_lookup(_c(keys).data_ptr(), n, _c(tab).data_ptr(), tab.numel(),
+                                          _c(rowmap).data_ptr(), _c(rowkey).data_ptr(), _c(count).data_ptr(),
+                                          rowkey.numel(), int(bool(insert)), slot.data_ptr(), fresh.data_ptr(),
+                                          row.data_ptr(), _c(overflow).data_ptr(), N.ptr(rows), d, kind, lo, hi,
+                                          seed & 0xFFFFFFFF, N.stream_ptr(tab.device)), "ht_lookup")
+        return row, fresh
+    row, fresh, ov = R.ht_lookup(keys, tab, rowmap, rowkey, count, insert, rows, kind, lo, hi, seed)
+    if ov:
+        overflow[0] = ov
+    return row, fresh
+
+
+def ht_rehash(rowkey: torch.Tensor, count: int, tab: torch.Tensor, rowmap: torch.Tensor,
+              overflow: torch.Tensor) -> None:
+    """Rebuild a zeroed ``tab`` / ``rowmap`` from the first ``count`` row keys."""
+    if _on_gpu(tab):
+        N.check(N.require().fps_ht_rehash(_c(rowkey).data_ptr(), int(count), _c(tab).data_ptr(), tab.numel(),
+                                          _c(rowmap).data_ptr(), _c(overflow).data_ptr(), N.stream_ptr(tab.device)),
+                "ht_rehash")
+        return
+    R.ht_rehash(rowkey, int(count), tab, rowmap)
+
+
 class DedupWorkspace:
     """Per-step key de-duplication + shard grouping for one worker (K1).
 

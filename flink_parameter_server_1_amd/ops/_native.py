@@ -93,6 +93,9 @@ _SIGNATURES = {
     "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_score_gemm": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp],
     "fps_pa_multi": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_ht_lookup": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                      c_int, c_f32, c_f32, c_u32, c_vp],
+    "fps_ht_rehash": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {"fps_stream_create_cu_mask": [c_int, c_int, c_int, c_int, c_vp], "fps_stream_destroy": [c_vp]}

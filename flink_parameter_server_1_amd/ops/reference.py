@@ -81,6 +81,8 @@ def shard_of(keys: torch.Tensor, W: int, part_kind: int, block: int):
     k = keys.long().abs()
     if part_kind == 0:
         return k % W, k // W
+    if part_kind == 2:  # sparse ids: the id itself is the owner's hash-table key
+        return k % W, keys.long()
     d = torch.clamp(k // block, max=W - 1)
     return d, k - d * block
 
@@ -393,3 +395,72 @@ def pa_multi(indptr, xval, pos, W, y, mode, variant, C, cost, delta):
 def mf_sq_err(U, I, uid, iid, r) -> float:
     e = r - (U[uid.long()] * I[iid.long()]).sum(1)
     return float((e.double() ** 2).sum())
+
+
+HT_SALT = 0x2545F491
+
+
+def ht_lookup(keys, tab, rowmap, rowkey, count, insert, rows=None, init_kind=-1, lo=0.0, hi=0.0, seed=0):  # noqa: C901
+    """CPU twin of ``kernels/hash_table.hip`` ``fps_ht_lookup``: persistent
+    open-addressing table (``tab`` int64: 0 empty, ``1<<32 | uint32(key)``
+    occupied; linear probing from ``fmix32(key ^ SALT)``), compact rows handed
+    out in first-insert order.  Returns ``(row int32[n], fresh uint8[n],
+    overflow int)``."""
+    cap = tab.numel()
+    mask = cap - 1
+    tb, rm, rk = tab.numpy(), rowmap.numpy(), rowkey.numpy()
+    ks = keys.to(torch.int64).tolist()
+    h0 = (fmix32((keys.to(torch.int64) & M32) ^ HT_SALT) & mask).tolist() if ks else []
+    out = torch.full((len(ks),), -1, dtype=torch.int32)
+    fresh = torch.zeros(len(ks), dtype=torch.uint8)
+    overflow = 0
+    cnt = int(count[0])
+    for b, k in enumerate(ks):
+        want = (1 << 32) | (k & M32)
+        h = h0[b]
+        for _ in range(cap):
+            cur = int(tb[h])
+            if cur == want:
+                out[b] = int(rm[h])
+                break
+            if cur == 0:
+                if not insert:
+                    break
+                if cnt >= rk.shape[0]:
+                    overflow = 2
+                    break
+                tb[h] = want
+                rm[h] = cnt
+                rk[cnt] = k
+                out[b] = cnt
+                fresh[b] = 1
+                cnt += 1
+                break
+            h = (h + 1) & mask
+        else:
+            overflow = 1
+    count[0] = cnt
+    if insert and rows is not None and init_kind >= 0 and fresh.any():
+        sel = fresh.bool()
+        r = out[sel].long()
+        if init_kind == 0:
+            rows[r] = 0
+        elif init_kind == 1:
+            rows[r] = lo
+        else:
+            rows[r] = init_values(keys[sel], rows.shape[1], lo, hi, seed).to(rows.dtype)
+    return out, fresh, overflow
+
+
+def ht_rehash(rowkey, count, tab, rowmap):
+    cap = tab.numel()
+    mask = cap - 1
+    tb, rm = tab.numpy(), rowmap.numpy()
+    ks = rowkey[:count].to(torch.int64)
+    h0 = (fmix32((ks & M32) ^ HT_SALT) & mask).tolist()
+    for r, k in enumerate(ks.tolist()):
+        h = h0[r]
+        while tb[h] != 0:
+            h = (h + 1) & mask
+        tb[h] = (1 << 32) | (k & M32)
+        rm[h] = r

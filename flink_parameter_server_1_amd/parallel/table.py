@@ -16,7 +16,8 @@ hash -> ``id // P``; range -> ``id - shard * block``.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+import inspect
+from typing import Callable, Optional, Tuple
 
 import torch
 
@@ -24,14 +25,60 @@ from .. import ops
 from ..core.partitioners import HashPartitioner, LookupPartitioner, RangePartitioner
 
 
+def _arity(fn: Callable) -> int:
+    try:
+        ps = inspect.signature(fn).parameters.values()
+    except (TypeError, ValueError):
+        return 2
+    if any(p.kind == p.VAR_POSITIONAL for p in ps):
+        return 3
+    return sum(p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD) for p in ps)
+
+
+def fn_init_values(init_fn: Callable, gids: torch.Tensor, dim: int, dtype, device) -> torch.Tensor:
+    """``init_fn(global ids int64[n]) -> [n, dim]`` rows (a scalar row broadcasts)."""
+    v = torch.as_tensor(init_fn(gids), device=device)
+    return v.to(dtype).reshape(gids.numel(), -1).expand(gids.numel(), dim).contiguous() if v.numel() else \
+        torch.zeros((0, dim), dtype=dtype, device=device)
+
+
+def fn_apply(store: torch.Tensor, scratch: int, rows: torch.Tensor, deltas: torch.Tensor, update_fn: Callable,
+             global_ids: Callable, fresh: Optional[torch.Tensor] = None) -> None:
+    """User push rule on the owner (the ``paramUpdate: (P, P) => P`` of
+    ``transform`` overload (a), ``M/FlinkParameterServer.scala:62-77``):
+    ``store[r] = update_fn(store[r], delta[, ids])`` for every valid row
+    (``rows >= 0``; rows unique within the call), ``delta`` itself where the id
+    was absent (``fresh``: ``SimplePSLogic``'s ``None => delta``,
+    ``M/server/SimplePSLogic.scala:16-22``).  Masked entries go to the scratch
+    row, so nothing here needs a host sync."""
+    if rows.numel() == 0:
+        return
+    valid = rows >= 0
+    r = torch.where(valid, rows.long(), torch.full_like(rows.long(), scratch))
+    old = store[r]
+    d = deltas.reshape(old.shape).to(old.dtype)
+    if _arity(update_fn) >= 3:
+        new = update_fn(old, d, global_ids(r.clamp_max(scratch - 1)))
+    else:
+        new = update_fn(old, d)
+    new = torch.as_tensor(new, device=old.device).to(old.dtype).reshape(old.shape)
+    if fresh is not None:
+        new = torch.where(fresh.bool().view(-1, 1), d, new)
+    store.index_put_((r,), new)
+
+
 class ShardedTable:
     PART_KIND = {"hash": 0, "range": 1, "lookup": 1}
 
     def __init__(self, num_ids: int, dim: int, rank: int = 0, world: int = 1, partition: str = "hash",
                  init: Tuple = ("uniform", -0.01, 0.01), seed: int = 0, device="cpu", optimizer: str = "add",
-                 track_touched: bool = True, dtype=torch.float32, owner: Optional[torch.Tensor] = None):
+                 track_touched: bool = True, dtype=torch.float32, owner: Optional[torch.Tensor] = None,
+                 init_fn: Optional[Callable] = None, update_fn: Optional[Callable] = None):
         """``partition="lookup"`` takes ``owner[num_ids]`` (id -> shard): an arbitrary
-        assignment, addressed through virtual keys (``LookupPartitioner``)."""
+        assignment, addressed through virtual keys (``LookupPartitioner``).
+        ``optimizer="fn"``: user rules -- ``init_fn(global ids) -> rows`` (applied to
+        the whole shard at construction: deterministic-by-id rules then equal
+        init-on-first-pull) and ``update_fn(old, delta[, ids]) -> new`` (``fn_apply``)."""
         if partition not in self.PART_KIND:
             raise ValueError(partition)
         self.num_ids, self.dim, self.rank, self.world = int(num_ids), int(dim), rank, world
@@ -51,7 +98,12 @@ class ShardedTable:
         self.optimizer = optimizer
         self.seed = seed
         self.init_spec = init
-        self.weight = torch.empty((self.n_local, self.dim), dtype=dtype, device=self.device)
+        self.init_fn, self.update_fn = init_fn, update_fn
+        if optimizer == "fn" and update_fn is None:
+            raise ValueError("optimizer='fn' needs update_fn")
+        # function rules get one scratch row past the shard (masked apply entries)
+        self._store = torch.empty((self.n_local + (optimizer == "fn"), self.dim), dtype=dtype, device=self.device)
+        self.weight = self._store[:self.n_local]
         self.reset_parameters()
         # optimizer state: Adagrad accumulators [n, D]; add_renorm keeps each row's
         # euclidean length [n] next to it (LengthAndVector, K3 add+renorm)
@@ -61,7 +113,11 @@ class ShardedTable:
             self.state = self.weight.norm(dim=1).to(torch.float32)
         else:
             self.state = None
-        self.touched = torch.zeros(self.n_local, dtype=torch.uint8, device=self.device) if track_touched else None
+        self._touched_store = torch.zeros(self.n_local + (optimizer == "fn"), dtype=torch.uint8,
+                                          device=self.device) if track_touched else None
+        self.touched = self._touched_store[:self.n_local] if track_touched else None
+
+    sparse = False
 
     # ----------------------------------------------------------- id mapping
     @property
@@ -94,7 +150,13 @@ class ShardedTable:
     # ----------------------------------------------------------- lifecycle
     def reset_parameters(self):
         kind = self.init_spec[0]
-        if kind == "uniform" and self.partition == "lookup":
+        if self.init_fn is not None:
+            chunk = 1 << 20
+            for s in range(0, self.n_local, chunk):
+                loc = torch.arange(s, min(s + chunk, self.n_local), device=self.device)
+                self.weight[s:s + loc.numel()] = fn_init_values(self.init_fn, self.global_ids(loc), self.dim,
+                                                                self.weight.dtype, self.device)
+        elif kind == "uniform" and self.partition == "lookup":
             _, lo, hi = self.init_spec  # ids are not an arithmetic progression: init by explicit id
             from ..ops import reference as R
 
@@ -112,14 +174,40 @@ class ShardedTable:
             raise ValueError(f"unknown init {kind}")
 
     # ----------------------------------------------------------- PS side
+    @property
+    def scratch_row(self) -> int:
+        return self.n_local
+
+    def rows_for(self, local_keys: torch.Tensor, insert: bool = True, push: bool = False):
+        """``(rows, fresh)``: dense shards store local key k at row k; ``fresh``
+        (function rules only, on a push) marks rows never touched before."""
+        fresh = None
+        if push and self.optimizer == "fn" and self.touched is not None and local_keys.numel():
+            fresh = self.touched[local_keys.long().clamp_min(0)] == 0
+        return local_keys, fresh
+
+    def serve_rows(self, rows: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
+        return ops.gather_rows(self.weight, rows, out_dtype=wire_dtype, touched=self.touched)
+
     def serve(self, local_keys: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
         """Pull serve (K2): rows for the requested local keys."""
-        return ops.gather_rows(self.weight, local_keys, out_dtype=wire_dtype, touched=self.touched)
+        return self.serve_rows(local_keys, wire_dtype)
+
+    def apply_rows(self, rows: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
+                   fresh: Optional[torch.Tensor] = None) -> None:
+        op = op or self.optimizer
+        if op == "fn":
+            fn_apply(self._store, self.scratch_row, rows, deltas, self.update_fn, self.global_ids, fresh)
+            if self.touched is not None:  # masked entries mark the scratch byte
+                r = torch.where(rows >= 0, rows.long(), torch.full_like(rows.long(), self.scratch_row))
+                self._touched_store[r] = 1
+            return
+        ops.apply_rows(self.weight, rows, deltas, op, lr=lr, state=self.state, touched=self.touched)
 
     def apply(self, local_keys: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None):
         """Push apply (K3) with the table's update rule."""
-        op = op or self.optimizer
-        ops.apply_rows(self.weight, local_keys, deltas, op, lr=lr, state=self.state, touched=self.touched)
+        rows, fresh = self.rows_for(local_keys, push=True)
+        self.apply_rows(rows, deltas, lr, op, fresh=fresh)
         if op == "set" and self.optimizer == "add_renorm":  # model load: lengths of the written rows
             k = local_keys.long()
             k = k[k >= 0]

@@ -54,6 +54,7 @@ class PullPlan:
     n_unique: int
     peer_flags: List[int] = field(default_factory=list)  # flag each rank sent with this plan
     n_requests: int = 0
+    recv_rows: Optional[torch.Tensor] = None  # rows of recv_keys in the shard (cached by serve)
 
 
 @dataclass
@@ -74,7 +75,9 @@ class TensorPS:
         self.table = table
         self.comm = comm
         self.wire_dtype = wire_dtype
-        self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device)
+        # sparse-id tables (parallel.hash_table) dedup through the per-batch hashed claim map
+        self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device,
+                                        hashed=True if getattr(table, "sparse", False) else None)
         #: pulls = requests, unique = unique keys, steps = plans; host_stalls = plan_end
         #: calls whose counts had not reached the host yet (the host waited on the device)
         self.stats = {"pulls": 0, "unique": 0, "steps": 0, "host_stalls": 0, "pushes": 0}
@@ -153,7 +156,9 @@ class TensorPS:
     # --------------------------------------------------------------------- pull
     def serve(self, plan: PullPlan) -> torch.Tensor:
         with stage("ps.serve", self.timer):
-            return self.table.serve(plan.recv_keys, self.wire_dtype)
+            if plan.recv_rows is None:  # dense shards: the local key is the row; sparse: lookup-or-insert
+                plan.recv_rows = self.table.rows_for(plan.recv_keys)[0]
+            return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
 
     def pull_planned(self, plan: PullPlan, async_op: bool = False):
         """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``."""
@@ -196,7 +201,12 @@ class TensorPS:
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
         with stage("ps.push-a2a", self.timer):
             recv = self.comm.all_to_all(wire.contiguous(), plan.send_splits, plan.recv_splits)
-        recv_keys = plan.recv_keys
+        fresh = None
+        if plan.recv_rows is not None:  # served by this plan: the rows exist
+            rows = plan.recv_rows
+        else:  # a push without a pull (push_keys, model load)
+            rows, fresh = self.table.rows_for(plan.recv_keys, push=True)
+        recv_keys = rows
         if self.masked_push:
             valid = recv[:, D] > 0.5
             recv = recv[:, :D].contiguous()
@@ -205,7 +215,16 @@ class TensorPS:
         self.stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
             seg_add = opt == "add" and len(plan.recv_splits) <= 16
-            if seg_add or opt in ("adagrad", "set", "add_renorm"):
+            if opt == "fn":  # user rule: sequential over the source segments (keys repeat across them)
+                if fresh is not None:  # the id is absent only for its first push, in segment order
+                    fresh = self._first_fresh(recv_keys, fresh)
+                off = 0
+                for n in plan.recv_splits:
+                    if n:
+                        self.table.apply_rows(recv_keys[off:off + n], recv[off:off + n], lr=lr, op=opt,
+                                              fresh=None if fresh is None else fresh[off:off + n])
+                    off += n
+            elif seg_add or opt in ("adagrad", "set", "add_renorm"):
                 # Keys are unique within each source's segment but may repeat across
                 # sources; non-atomic rules (adagrad's accumulator RMW, set, renorm)
                 # therefore apply segment by segment.  ``add`` does the same with a
@@ -215,15 +234,33 @@ class TensorPS:
                 off = 0
                 for n in plan.recv_splits:
                     if n:
-                        self.table.apply(recv_keys[off:off + n], recv[off:off + n], lr=lr,
-                                         op="add_unique" if seg_add else opt)
+                        self.table.apply_rows(recv_keys[off:off + n], recv[off:off + n], lr=lr,
+                                              op="add_unique" if seg_add else opt)
                     off += n
             else:
-                self.table.apply(recv_keys, recv, lr=lr, op=opt)
+                self.table.apply_rows(recv_keys, recv, lr=lr, op=opt)
         if return_updated:
             k = recv_keys[recv_keys >= 0] if self.masked_push else recv_keys
             return self.table.global_ids(k), self.table.weight[k.long()]
         return None
+
+    @staticmethod
+    def _first_fresh(rows: torch.Tensor, fresh: torch.Tensor) -> torch.Tensor:
+        """Per request: is it the FIRST request (lowest index) of a row any of
+        whose requests found the id absent?  Sort-based, no host sync."""
+        n = rows.numel()
+        if n == 0:
+            return fresh.bool()
+        order = torch.argsort(rows.long(), stable=True)
+        sr = rows.long()[order]
+        first = torch.ones(n, dtype=torch.bool, device=rows.device)
+        first[1:] = sr[1:] != sr[:-1]
+        grp = torch.cumsum(first.long(), 0) - 1
+        gf = torch.zeros(n, dtype=torch.long, device=rows.device)
+        gf.scatter_reduce_(0, grp, fresh.long()[order], reduce="amax")
+        out = torch.empty(n, dtype=torch.bool, device=rows.device)
+        out[order] = first & (gf[grp] > 0) & (sr >= 0)
+        return out
 
     def reduce_requests(self, plan: PullPlan, deltas: torch.Tensor, op: str = "add",
                         mask: Optional[torch.Tensor] = None) -> torch.Tensor:
