@@ -57,8 +57,10 @@ class PulledBatch:
     index: Optional[torch.Tensor] = None
 
     def values(self) -> torch.Tensor:
-        """``[B, D]`` fp32 parameter of every request, in request order."""
-        return self.rows.float()[self.pos.long()]
+        """``[B, D]`` parameter of every request, in request order (fp32; fp64
+        when the rows travel as fp64, the bit-parity configuration)."""
+        r = self.rows if self.rows.dtype == torch.float64 else self.rows.float()
+        return r[self.pos.long()]
 
     @property
     def n_unique(self) -> int:

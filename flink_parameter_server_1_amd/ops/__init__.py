@@ -96,14 +96,16 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
 
 def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
                 touched: torch.Tensor = None) -> torch.Tensor:
-    """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2)."""
+    """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2).
+    The HIP kernel serves fp32 tables; fp64 tables (the bit-parity configuration
+    against the per-record engine's doubles) take the torch twin on any device."""
     n = idx.numel()
     if DEBUG:
         check_index(idx, table.shape[0], "gather_rows")
     d = table.shape[1]
     if out is None:
         out = torch.empty((n, d), dtype=out_dtype, device=table.device)
-    if _on_gpu(table):
+    if _on_gpu(table) and table.dtype == torch.float32 and out.dtype in (torch.float32, torch.bfloat16):
         lib = N.require()
         N.check(lib.fps_gather_rows(_c(table).data_ptr(), _c(idx).data_ptr(), int(idx.dtype == torch.int64), n, d,
                                     _c(out).data_ptr(), int(out.dtype == torch.bfloat16), N.ptr(touched),
@@ -118,13 +120,14 @@ def apply_rows(table: torch.Tensor, idx: torch.Tensor, delta: torch.Tensor, op: 
     """Push apply (K3): ``add`` (atomic), ``set``, ``sgd`` (w -= lr*g, atomic),
     ``adagrad`` (unique idx; ``state`` = accumulators ``[n, D]``), ``add_renorm``
     (unique idx; w += g and ``state[row] = |w|``, ``state`` = lengths ``[n]``).
-    ``idx < 0`` marks padding rows."""
+    ``idx < 0`` marks padding rows.  fp32 tables run the HIP kernel; fp64 tables
+    (bit-parity runs) the torch twin on any device."""
     if DEBUG:
         check_index(idx, table.shape[0], "apply_rows", allow_negative=True)
         check_finite(delta.float(), "apply_rows delta")
     n = idx.numel()
     d = table.shape[1]
-    if _on_gpu(table):
+    if _on_gpu(table) and table.dtype == torch.float32:
         if idx.dtype != torch.int32:
             idx = idx.to(torch.int32)
         lib = N.require()

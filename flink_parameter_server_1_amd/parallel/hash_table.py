@@ -185,13 +185,23 @@ class HashShardTable:
             init = ("zeros",)
         else:
             init = self.init_spec
+        kernel_init = insert and self._store.dtype == torch.float32  # the init kernel writes fp32 rows
         rows, fresh = ops.ht_lookup(keys, self.tab, self.rowmap, self.rowkey, self.count, self.overflow, insert,
-                                    self._store if insert else None, init, self.seed)
+                                    self._store if kernel_init else None, init, self.seed)
         if insert:
             self._after_insert()
-            if self.init_fn is not None and not push and n:
+            torch_init = self.init_fn is not None or (not kernel_init and init[0] != "zeros")
+            if torch_init and not push and n:
                 r = torch.where(rows >= 0, rows.long(), torch.full_like(rows.long(), self.scratch_row))
-                vals = fn_init_values(self.init_fn, keys.long(), self.dim, self.dtype, self.device)
+                if self.init_fn is not None:
+                    vals = fn_init_values(self.init_fn, keys.long(), self.dim, self.dtype, self.device)
+                elif init[0] == "const":
+                    vals = torch.full((n, self.dim), float(init[1]), dtype=self.dtype, device=self.device)
+                else:
+                    from ..ops import reference as R
+
+                    vals = R.init_values(keys, self.dim, float(init[1]), float(init[2]), self.seed).to(
+                        device=self.device, dtype=self.dtype)
                 # fresh rows are still zero: accumulating init * fresh writes each
                 # fresh row exactly once and adds 0 to every other request's row
                 self._store.index_put_((r,), vals * fresh.view(-1, 1).to(vals.dtype), accumulate=True)

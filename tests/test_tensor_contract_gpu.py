@@ -17,8 +17,8 @@ DEV = torch.device("cuda", 0)
 @pytest.mark.parametrize("rule", [T.clip_add, T.vmax])
 def test_user_rule_custom_partitioner_gpu(rule):
     recs = T._records(1, 150, seed=21)
-    ref = T._per_record(recs, 1, rule, T.custom_part)
-    got = T._tensor(recs, 1, rule, num_ids=40, partitioner=T.custom_part, device=DEV)
+    ref = T._per_record(recs, 1, rule, T.custom_part, coef=0.1)
+    got = T._tensor(recs, 1, rule, num_ids=40, partitioner=T.custom_part, device=DEV, coef=0.1)
     assert set(got) == set(ref)
     for k in ref:
         assert got[k] == pytest.approx(ref[k], abs=1e-12), k
@@ -27,8 +27,9 @@ def test_user_rule_custom_partitioner_gpu(rule):
 @pytest.mark.parametrize("combine,mb", [("sum", 1), ("sequential", 16)])
 def test_sparse_ids_gpu(combine, mb):
     recs = T._records(1, 300, seed=22, sparse=True)
-    ref = T._per_record(recs, 1, T.clip_add)
-    got = T._tensor(recs, 1, T.clip_add, combine=combine, mb=mb, device=DEV)
+    coef = 0.1 if mb == 1 else 0.0
+    ref = T._per_record(recs, 1, T.clip_add, coef=coef)
+    got = T._tensor(recs, 1, T.clip_add, combine=combine, mb=mb, device=DEV, coef=coef)
     assert set(got) == set(ref)
     for k in ref:
         assert got[k] == pytest.approx(ref[k], abs=1e-12), k
