@@ -100,8 +100,6 @@ def main(argv=None):
                     help="tiled SGD: user-range phases per step (0 = auto, ~2.5M users per phase)")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
-    ap.add_argument("--sgd-high-priority", action="store_true",
-                    help="tiled SGD with prefetch: run the SGD on a priority -1 stream (A/B knob, off by default)")
     ap.add_argument("--watchdog-s", type=float, default=0.0,
                     help="fail fast: end this rank (exit 17) when a step makes no progress for this long (0 = off)")
     ap.add_argument("--metrics-jsonl", default=None,
@@ -123,7 +121,7 @@ def main(argv=None):
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
-                   user_phases=a.user_phases, sgd_high_priority=a.sgd_high_priority)
+                   user_phases=a.user_phases)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device

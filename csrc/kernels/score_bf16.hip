@@ -32,8 +32,6 @@
 // rows (reg & 3) + 8 (reg >> 2) + 4h are items.
 #include "common.h"
 
-#include <cstdlib>
-#include <string>
 
 using namespace fps;
 
@@ -273,24 +271,11 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
     hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, ##__VA_ARGS__>), dim3((unsigned)(nqt * nit)), dim3(256), 0, s, Qb, \
                        Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, cap);                 \
   }
-  // default at D = 64: 4 query blocks per wave + the bit-mask epilogue (same-box A/B,
-  // profiles/r2_bf16_topk.md).  FPS_SB_VARIANT re-runs the other shapes: "qb2" (2 blocks,
-  // branch per register), "qb1", "qb4" (4 blocks, branches), "mask" (2 blocks, mask)
-  static const int variant = [] {
-    const char* e = std::getenv("FPS_SB_VARIANT");
-    if (!e) return 0;
-    const std::string v(e);
-    return v == "qb1" ? 1 : v == "qb4" ? 2 : v == "mask" ? 3 : v == "qb2" ? 4 : 0;
-  }();
+  // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4
+  // blocks with branch or mask epilogues, same-box A/B, profiles/r2_bf16_topk.md)
   switch (D) {
     case 32: FPS_SB(32, 2, true); break;
-    case 64:
-      if (variant == 1) FPS_SB(64, 1)
-      else if (variant == 2) FPS_SB(64, 4)
-      else if (variant == 3) FPS_SB(64, 2, true)
-      else if (variant == 4) FPS_SB(64, 2)
-      else FPS_SB(64, 4, true)
-      break;
+    case 64: FPS_SB(64, 4, true); break;
     case 128: FPS_SB(128, 1, true); break;
     default: return (int)hipErrorInvalidValue;
   }

@@ -665,23 +665,3 @@ FPS_API int fps_bucketize(const int32_t* keys, int64_t n, int W, int part_kind, 
 }
 
 FPS_API int fps_abi_version() { return 1; }
-
-// ---- CU-masked streams: the tiled MF step can give the bandwidth-bound SGD and the
-// LDS-heavy tile partition of the next batch disjoint CU sets (one of every `stride`
-// CUs, starting at `offset`, or the complement), so the partition's 64-KiB-LDS,
-// 1,024-thread workgroups stop evicting SGD workgroups from the CUs they share.
-FPS_API int fps_stream_create_cu_mask(int n_cu, int stride, int offset, int complement, void** out) {
-  if (n_cu <= 0 || n_cu > 1024 || stride <= 0) return (int)hipErrorInvalidValue;
-  uint32_t mask[32] = {0};
-  for (int i = 0; i < n_cu; ++i) {
-    bool sel = (i % stride) == offset;
-    if (complement) sel = !sel;
-    if (sel) mask[i / 32] |= 1u << (i % 32);
-  }
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)((n_cu + 31) / 32), mask);
-  *out = (void*)s;
-  return (int)e;
-}
-
-FPS_API int fps_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }

@@ -32,8 +32,6 @@ row of ``dim`` floats), see BASELINE.md.
 """
 from __future__ import annotations
 
-import os
-
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -71,7 +69,6 @@ class MFConfig:
     user_memory: int = 128            # per-user ring of recent items excluded from the negatives
     user_phases: int = 0              # tiled: run the SGD in P user-range phases (0 = auto: ~2.5M users
                                       # per phase, so a launch's user rows mostly hit the Infinity Cache)
-    sgd_high_priority: bool = False   # tiled + prefetch: SGD on a priority -1 stream (measured 1 % slower, off)
     graph_capture: bool = False       # tiled, W = 1: replay each batch size's step as one hipGraph
                                       # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
@@ -161,26 +158,13 @@ class DistributedMF:
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
                               and exchange != "ps")
+            # the partition of batch k+1 runs on a side stream beside the SGD of batch k
+            # (a priority stream for the SGD and CU-masked streams splitting the CUs
+            # between them were measured slower and removed, profiles/r2_partition.md)
             self._side = torch.cuda.Stream(dev) if self._prefetch else None
-            # cfg.sgd_high_priority: the SGD of batch k gets dispatch priority over the
-            # partition of k+1 (bench.py --sgd-high-priority); local layout only: the
-            # ring rotation orders its copy stream against the stream it was built on
-            hp = self._prefetch and exchange == "local" and cfg.sgd_high_priority
-            self._hp = torch.cuda.Stream(dev, priority=-1) if hp else None
-            # FPS_PARTITION_CUS=k: the partition of batch k+1 runs on ~k CUs of its own
-            # and the SGD of batch k on the others (CU-masked streams), instead of both
-            # sharing every CU
-            k_cu = int(os.environ.get("FPS_PARTITION_CUS", "0"))
-            if k_cu > 0 and self._prefetch and exchange == "local":
-                n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-                stride = max(2, n_cu // k_cu)
-                self._side = ops.cu_masked_stream(dev, stride, stride - 1)
-                self._hp = ops.cu_masked_stream(dev, stride, stride - 1, complement=True)
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
-            # both item blocks of a phase in one launch (FPS_MF_PAIR=0: one launch per block)
-            self.pair_blocks = os.environ.get("FPS_MF_PAIR", "1") == "1"
         if self.exchange == "rotate":
             self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
             self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
@@ -248,13 +232,7 @@ class DistributedMF:
             staged = self._stage_partition(uid_local, iid, rating)
             if self._prefetch:
                 prev, self._staged = self._staged, staged
-                if prev is not None and self._hp is not None:
-                    main = torch.cuda.current_stream(self.U.device)
-                    self._hp.wait_stream(main)
-                    with torch.cuda.stream(self._hp):
-                        self._tiled_sgd(prev)
-                    main.wait_stream(self._hp)  # later work (and the next partition) orders after it
-                elif prev is not None:
+                if prev is not None:
                     self._tiled_sgd(prev)
             else:
                 self._tiled_sgd(staged)
@@ -357,14 +335,9 @@ class DistributedMF:
         if self.exchange == "local":
             b0, b1 = self._local_blocks
             with stage("mf.sgd", self.timer):
-                for p in range(self.user_phases):
-                    if self.pair_blocks:
-                        ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
-                                              c.learning_rate, c.lam)
-                    else:
-                        for b, blk in enumerate((b0, b1)):
-                            ops.mf_sgd_tiled(self.U, blk, rec, ptr, 2 * p + b, self.tile_T, self.tile_R,
-                                             c.learning_rate, c.lam)
+                for p in range(self.user_phases):  # both item blocks of a phase in one launch
+                    ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
+                                          c.learning_rate, c.lam)
             return
         for _ in range(self.rot.K):
             with stage("mf.rotate.begin", self.timer):

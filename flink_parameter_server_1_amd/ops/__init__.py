@@ -8,7 +8,7 @@ fallback on a GPU box).
 from __future__ import annotations
 
 import os
-from typing import NamedTuple, Optional
+from typing import Optional
 
 import torch
 
@@ -56,20 +56,6 @@ def _c(t):
     if not t.is_contiguous():
         raise ValueError("kernel inputs must be contiguous")
     return t
-
-
-def cu_masked_stream(device, stride: int, offset: int, complement: bool = False):
-    """A HIP stream restricted to the CUs ``i`` with ``i % stride == offset`` (or the
-    complement), wrapped as a torch stream.  The stream lives for the process."""
-    import ctypes
-
-    dev = torch.device(device)
-    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    out = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        N.check(N.require().fps_stream_create_cu_mask(n_cu, stride, offset, int(complement), ctypes.byref(out)),
-                "stream_create_cu_mask")
-    return torch.cuda.ExternalStream(out.value, device=dev)
 
 
 def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: float = 0.0, hi: float = 1.0,
@@ -428,45 +414,6 @@ def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
     return r if kt(r) <= TILE_MAX_BUCKETS and r <= 256 else None
 
 
-class TileLayout(NamedTuple):
-    """Output layout of the level-4 (capacity slot) tile partition: tile ``k``'s
-    records are ``rec[ptr[k] : ptr[k] + min(cnt[k], ptr[k+1] - ptr[k])]``; records
-    past a slot's capacity are in ``ovf[:ovf_cnt]`` ({uid, row in block, rating
-    bits, bucket}, int32 ``[n, 4]``), run by ``mf_sgd_tiled`` after the tiles."""
-
-    ptr: torch.Tensor
-    cnt: torch.Tensor
-    ovf: torch.Tensor
-    ovf_cnt: torch.Tensor
-
-    def compact(self, rec, T: int, R: int):
-        """(ptr[KT+1], uid, row-in-block, rating) grouped by bucket, overflow
-        records included -- the layout of levels 1-3 (tests / debugging; syncs)."""
-        ptr, cnt = self.ptr.long().cpu(), self.cnt.long().cpu()
-        take = torch.minimum(cnt, ptr[1:] - ptr[:-1])
-        KT = cnt.numel()
-        bucket = torch.repeat_interleave(torch.arange(KT), take)
-        first = torch.cumsum(take, 0) - take
-        idx = torch.repeat_interleave(ptr[:-1], take) + torch.arange(int(take.sum())) - \
-            torch.repeat_interleave(first, take)
-        x = rec.cpu()[idx]
-        if x.shape[1] == 2:
-            u = x[:, 0] & 0xFFFFFF
-            row = (bucket % T) * R + ((x[:, 0].long() >> 24) & 0xFF)
-            rt = x[:, 1].contiguous().view(torch.float32)
-        else:
-            u, row, rt = x[:, 0], x[:, 1].long(), x[:, 2].contiguous().view(torch.float32)
-        o = self.ovf[: int(self.ovf_cnt.item())].cpu()
-        b_all = torch.cat([bucket, o[:, 3].long()])
-        order = torch.argsort(b_all, stable=True)
-        u = torch.cat([u.to(torch.int32), o[:, 0]])[order]
-        row = torch.cat([row.to(torch.int32), o[:, 1]])[order]
-        rt = torch.cat([rt, o[:, 2].contiguous().view(torch.float32)])[order]
-        p = torch.zeros(KT + 1, dtype=torch.int32)
-        p[1:] = torch.cumsum(torch.bincount(b_all, minlength=KT), 0).to(torch.int32)
-        return p, u, row, rt
-
-
 class TilePartitioner:
     """Buckets a micro-batch's ratings by (user phase, item block, tile of ``R``
     rows) for ``mf_sgd_tiled`` (``mf_tiled.hip``): a few kernels, nothing
@@ -474,10 +421,15 @@ class TilePartitioner:
     ``rec`` an int32 ``[n, 4]`` array of packed records {uid, row-in-block,
     rating bits, bucket} (``[n, 2]`` with ``rec8``) grouped by bucket (on CPU:
     the three columns as tensors).  Phase ``p`` = local users
-    ``[p*upp, (p+1)*upp)``; bucket ``(p*2W + b)*T + t``."""
+    ``[p*upp, (p+1)*upp)``; bucket ``(p*2W + b)*T + t``.
 
-    def __init__(self, W: int, half, R: int, T: int, device, levels: Optional[int] = None, rec8: bool = False,
-                 phases: int = 1, users_per_phase: Optional[int] = None):
+    The partition is the two-level one with LDS-sorted batches (count, coarse
+    scatter, bucket scatter); the single-level, atomic two-level and
+    capacity-slot variants measured slower (``profiles/r1_mf_partition_levels.md``,
+    ``profiles/r2_tp4.md``) and were removed."""
+
+    def __init__(self, W: int, half, R: int, T: int, device, rec8: bool = False, phases: int = 1,
+                 users_per_phase: Optional[int] = None):
         self.W, self.R, self.T = W, int(R), int(T)
         self.P = max(1, int(phases))
         self.upp = int(users_per_phase) if (self.P > 1 and users_per_phase) else (1 << 30)
@@ -487,29 +439,12 @@ class TilePartitioner:
         self.rec8 = bool(rec8) and self.R <= 256
         self.rec_cols = 2 if self.rec8 else 4
         self.KT = self.P * 2 * W * self.T
-        chunk = os.environ.get("FPS_TILE_PARTITION_CHUNK")
-        if chunk and self.device_is_cuda(device):
-            N.require().fps_tile_partition_set_chunk(int(chunk))
-        # 1 = single level (per-workgroup histograms of every bucket + column scan);
-        # 2 = two-level (coarse key, then bucket; atomic range reservations, no
-        # histogram matrix); 3 (default) = two-level with LDS-sorted batches, so
-        # consecutive lanes store consecutive records of one output run; 4 = level
-        # 3's scatters into capacity slots sized from the previous run's counts, no
-        # counting pass (returns a ``TileLayout``).  Levels 1 / 2 measured 1.66 /
-        # 1.83 ms at 64M ratings, KT = 3.9k buckets (profiles/r1_mf_partition_levels.md);
-        # level 4's scatters ran 627 + 474 us against level 3's 200 + 406 + 430 us
-        # (128 contended coarse cursors), 3 % slower end to end (profiles/r2_tp4.md).
-        env = os.environ.get("FPS_TILE_PARTITION_LEVELS")
-        self.levels = int(levels or env or 3)
-        if self.levels not in (1, 2, 3, 4):
-            raise ValueError(f"tile partition levels must be 1, 2, 3 or 4, not {self.levels}")
-        self.n_prev = 0
+        if self.KT > TILE_MAX_BUCKETS:
+            raise ValueError(f"{self.KT} tile buckets exceed the partition's {TILE_MAX_BUCKETS} LDS counters")
         self.device = torch.device(device)
         self.half = torch.as_tensor(half).to(device=self.device, dtype=torch.int32).contiguous()
         self.cap = 0
-        self.g_cap = 0
         if self.device.type == "cuda":
-            self.totals = torch.empty(self.KT, dtype=torch.int32, device=self.device)
             self.ptr = torch.empty(self.KT + 1, dtype=torch.int32, device=self.device)
 
     def run(self, uid, iid, rating, seen: Optional[torch.Tensor] = None):
@@ -521,71 +456,24 @@ class TilePartitioner:
             return ptr, (u, row, r)
         lib = N.require()
         n = uid.numel()
-        if self.levels == 4:
-            return self._run4(lib, uid, iid, rating, seen)
-        G = lib.fps_tile_partition_groups(n)
-        if self.levels == 1 and G * self.KT > self.g_cap:
-            self.g_cap = G * self.KT
-            self.H = torch.empty(self.g_cap, dtype=torch.int32, device=self.device)
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
             self.rec = torch.empty((self.cap, self.rec_cols), dtype=torch.int32, device=self.device)
-            if self.levels >= 2:
-                self.tmp = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
-        if self.levels >= 2:
-            fn, ws_ints = ((lib.fps_tile_partition2, lib.fps_tile_partition2_ws_ints) if self.levels == 2 else
-                           (lib.fps_tile_partition3, lib.fps_tile_partition3_ws_ints))
-            if not hasattr(self, "ws"):
-                self.ws = torch.empty(ws_ints(self.W, self.T, self.P), dtype=torch.int32, device=self.device)
-            N.check(fn(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
-                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.ws.data_ptr(), self.tmp.data_ptr(),
-                       self.ptr.data_ptr(), self.rec.data_ptr(), int(self.rec8), N.ptr(seen),
-                       N.stream_ptr(self.device)), f"tile_partition{self.levels}")
-            return self.ptr, self.rec[:n]
+            self.tmp = torch.empty((self.cap, 4), dtype=torch.int32, device=self.device)
+        if not hasattr(self, "ws"):
+            self.ws = torch.empty(lib.fps_tile_partition_ws_ints(self.W, self.T, self.P), dtype=torch.int32,
+                                  device=self.device)
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
-                                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.H.data_ptr(),
-                                       self.totals.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(),
-                                       int(self.rec8), N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
+                                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.ws.data_ptr(),
+                                       self.tmp.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(), int(self.rec8),
+                                       N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]
-
-    def _run4(self, lib, uid, iid, rating, seen):
-        n = uid.numel()
-        if not hasattr(self, "ws4"):
-            dev = self.device
-            self.ws4 = torch.zeros(lib.fps_tile_partition4_ws_ints(self.W, self.T, self.P), dtype=torch.int32,
-                                   device=dev)
-            self.bstart = torch.zeros(self.KT + 1, dtype=torch.int32, device=dev)
-            self.bcursor = torch.zeros(self.KT, dtype=torch.int32, device=dev)
-            self.ovf_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.cap4 = 0
-        if n > self.cap4:
-            self.cap4 = max(n, int(self.cap4 * 1.25))
-            NC = (self.ws4.numel() - 2) // 3
-            self.tmp4 = torch.empty((lib.fps_tile_partition4_cap(self.cap4, NC), 3 if self.rec8 else 4),
-                                    dtype=torch.int32, device=self.device)
-            self.rec = torch.empty((lib.fps_tile_partition4_cap(self.cap4, self.KT), self.rec_cols),
-                                   dtype=torch.int32, device=self.device)
-            self.ovf = torch.empty((self.cap4, 4), dtype=torch.int32, device=self.device)
-        N.check(lib.fps_tile_partition4(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.n_prev,
-                                        self.W, self.half.data_ptr(), self.R, self.T, self.P, self.upp,
-                                        self.ws4.data_ptr(), self.tmp4.data_ptr(), self.bstart.data_ptr(),
-                                        self.bcursor.data_ptr(), self.rec.data_ptr(), int(self.rec8),
-                                        self.ovf.data_ptr(), self.ovf_cnt.data_ptr(), N.ptr(seen),
-                                        N.stream_ptr(self.device)), "tile_partition4")
-        self.n_prev = n
-        return TileLayout(self.bstart, self.bcursor, self.ovf, self.ovf_cnt), self.rec
-
-    @staticmethod
-    def device_is_cuda(device) -> bool:
-        return torch.device(device).type == "cuda"
 
     def unpack(self, rec, ptr=None):
         """(uid, row-in-block, rating) columns of packed records (tests / CPU);
         8-B records need ``ptr`` to recover the tile of every record."""
         if isinstance(rec, tuple):
             return rec
-        if isinstance(ptr, TileLayout):
-            return ptr.compact(rec, self.T, self.R)[1:]
         if rec.shape[1] == 4:
             return rec[:, 0], rec[:, 1], rec[:, 2].contiguous().view(torch.float32)
         x = rec[:, 0]
@@ -597,53 +485,39 @@ class TilePartitioner:
         return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
-def _tiled_launch(lib, U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float, nblk: int):
-    """Tiled SGD launch over ``nblk`` consecutive item blocks from a ``TileLayout``
-    (slot starts + counts), then the flat kernel over their overflow records."""
-    s = N.stream_ptr(U.device)
-    off = 4 * block * T
-    N.check(lib.fps_mf_sgd_tiled3(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(), int(rec.shape[1] == 2),
-                                  ptr.ptr.data_ptr() + off, ptr.cnt.data_ptr() + off, T, tile_rows, I0.shape[0],
-                                  _c(I1).data_ptr(), I1.shape[0], nblk, U.shape[1], lr, lam, s), "mf_sgd_tiled3")
-    N.check(lib.fps_mf_sgd_ovf(U.data_ptr(), I0.data_ptr(), I1.data_ptr(), ptr.ovf.data_ptr(), ptr.ovf_cnt.data_ptr(),
-                               block * T, T, nblk, U.shape[1], lr, lam, s), "mf_sgd_ovf")
-
-
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
     records from ``TilePartitioner``): one workgroup per tile, every item row owned
-    by one lane group (registers), item deltas summed per row -- no item atomics.
-    ``ptr`` may be a ``TileLayout`` (level-4 partition)."""
-    if isinstance(ptr, TileLayout):
-        _tiled_launch(N.require(), U, I_block, I_block, rec, ptr, block, T, tile_rows, lr, lam, 1)
-        return
+    by one lane group (registers), item deltas summed per row -- no item atomics."""
     if _on_gpu(U):
         lib = N.require()
+        p0 = _c(ptr).data_ptr() + 4 * block * T
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
-                                     int(rec.shape[1] == 2), _c(ptr).data_ptr() + 4 * block * T, T, tile_rows,
-                                     I_block.shape[0], U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
+                                     int(rec.shape[1] == 2), p0, T, tile_rows, I_block.shape[0], None, None, 0, 1,
+                                     U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
         return
     uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
     R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
 
 
-def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
-    """``mf_sgd_tiled`` of item blocks ``block`` (rows ``I0``) and ``block + 1`` (rows ``I1``)
-    in one launch of 2T workgroups: the blocks share no item row, so they need no
-    ordering, and one launch instead of two halves the tail of partly filled waves."""
-    if isinstance(ptr, TileLayout):
-        _tiled_launch(N.require(), U, I0, I1, rec, ptr, block, T, tile_rows, lr, lam, 2)
-        return
+def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
+                      block1: Optional[int] = None):
+    """``mf_sgd_tiled`` of item blocks ``block`` (rows ``I0``) and ``block1`` (default
+    ``block + 1``; rows ``I1``) in one launch of 2T workgroups: the blocks share no
+    item row, so they need no ordering, and one launch instead of two halves the
+    tail of partly filled waves."""
+    block1 = block + 1 if block1 is None else block1
     if _on_gpu(U):
         lib = N.require()
-        N.check(lib.fps_mf_sgd_tiled2(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),
-                                      int(rec.shape[1] == 2), _c(ptr).data_ptr() + 4 * block * T, T, tile_rows,
-                                      I0.shape[0], _c(I1).data_ptr(), I1.shape[0], 2, U.shape[1], lr, lam,
-                                      N.stream_ptr(U.device)), "mf_sgd_tiled2")
+        base = _c(ptr).data_ptr()
+        N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),
+                                     int(rec.shape[1] == 2), base + 4 * block * T, T, tile_rows, I0.shape[0],
+                                     _c(I1).data_ptr(), base + 4 * block1 * T, I1.shape[0], 2, U.shape[1], lr, lam,
+                                     N.stream_ptr(U.device)), "mf_sgd_tiled_pair")
         return
     mf_sgd_tiled(U, I0, rec, ptr, block, T, tile_rows, lr, lam)
-    mf_sgd_tiled(U, I1, rec, ptr, block + 1, T, tile_rows, lr, lam)
+    mf_sgd_tiled(U, I1, rec, ptr, block1, T, tile_rows, lr, lam)
 
 
 PAIR_LOSSES = {"logistic": 0, "squared": 1}

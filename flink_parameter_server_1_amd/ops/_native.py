@@ -41,27 +41,11 @@ _SIGNATURES = {
     "fps_pair_sgd_pulled": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_int, c_vp, c_vp],
     "fps_mf_sgd_local_seg": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
     "fps_rot_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "fps_tile_partition_groups": [c_i64],
-    "fps_tile_partition_set_chunk": [c_i64],
-    "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
-                           c_vp,
-                           c_vp],
-    "fps_tile_partition2": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
-                           c_vp,
-                            c_vp],
-    "fps_tile_partition2_ws_ints": [c_int, c_int, c_int],
-    "fps_tile_partition3": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
-                           c_vp,
-                            c_vp],
-    "fps_tile_partition3_ws_ints": [c_int, c_int, c_int],
-    "fps_tile_partition4": [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                            c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
-    "fps_tile_partition4_ws_ints": [c_int, c_int, c_int],
-    "fps_tile_partition4_cap": [c_i64, c_int],
-    "fps_mf_sgd_tiled3": [c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_i64, c_vp, c_i64, c_int, c_int, c_f32,
-                          c_f32, c_vp],
-    "fps_mf_sgd_ovf": [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f32, c_f32, c_vp],
-    "fps_mf_sgd_tiled": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_int, c_f32, c_f32, c_vp],
+    "fps_tile_partition_ws_ints": [c_int, c_int, c_int],
+    "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                           c_int, c_vp, c_vp],
+    "fps_mf_sgd_tiled": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_f32,
+                         c_f32, c_vp],
     "fps_score_filter": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_topk_merge_cand": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp],
     "fps_score_filter_lemp": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
@@ -69,8 +53,6 @@ _SIGNATURES = {
     "fps_score_filter_bf16": [c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_int,
                               c_vp],
     "fps_cand_rescore": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
-    "fps_mf_sgd_tiled2": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_vp, c_i64, c_int, c_int, c_f32, c_f32,
-                          c_vp],
     "fps_lock_acquire": [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp],
     "fps_lock_release": [c_vp, c_vp, c_i64, c_vp, c_vp],
     "fps_topk_merge": [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
@@ -98,10 +80,9 @@ _SIGNATURES = {
     "fps_ht_rehash": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
-OPTIONAL = {"fps_stream_create_cu_mask": [c_int, c_int, c_int, c_int, c_vp], "fps_stream_destroy": [c_vp]}
+OPTIONAL = {}
 #: launchers / sizers returning int64 (the rest return an int status)
-RESTYPE_I64 = {"fps_tile_partition2_ws_ints", "fps_tile_partition3_ws_ints", "fps_tile_partition4_ws_ints",
-               "fps_tile_partition4_cap", "fps_dedup_flags_ws_ints"}
+RESTYPE_I64 = {"fps_tile_partition_ws_ints", "fps_dedup_flags_ws_ints"}
 
 
 def register(name, argtypes):

@@ -91,23 +91,21 @@ def test_graph_captured_step_matches_eager():
     torch.testing.assert_close(graphed.I, eager.I, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("prefetch,hp", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("prefetch", [False, True])
 @pytest.mark.parametrize("phases", [1, 3])
-def test_tiled_exact_when_users_unique_per_batch(prefetch, hp, phases):
+def test_tiled_exact_when_users_unique_per_batch(prefetch, phases):
     """Users repeat across micro-batches but never inside one (and items repeat a lot
     inside each): no Hogwild race is possible, so the whole tiled pipeline (partition,
     user phases, pair launch, prefetch, flush) must equal the sequential batch
     reference (gather, then add the summed item deltas; one sub-batch per user
-    phase) to fp32 rounding.  ``hp``: the SGD on the priority stream (its ordering
-    against the side-stream partition keeps both partition buffers intact)."""
+    phase) to fp32 rounding."""
     from flink_parameter_server_1_amd.ops import reference as R
 
     nu, ni, B, steps = 50_000, 3_000, 20_000, 6
     cfg = MFConfig(num_users=nu, num_items=ni, dim=64, learning_rate=0.05, range_min=0.0, range_max=0.2,
-                   prefetch_partition=prefetch, user_phases=phases, sgd_high_priority=hp)
+                   prefetch_partition=prefetch, user_phases=phases)
     m = DistributedMF(cfg, Comm(device=torch.device("cuda")))
     assert m.sgd_mode == "tiled" and m.user_phases == phases
-    assert (m._hp is not None) == hp
     U, I = m.U.detach().cpu().clone(), m.I.detach().cpu().clone()
     g = torch.Generator(device="cpu").manual_seed(3)
     for s in range(steps):
