@@ -88,6 +88,9 @@ def main(argv=None):
     ap.add_argument("--pool", type=int, default=4, help="data pool = pool * batch ratings per GPU")
     ap.add_argument("--exchange", default="auto", choices=["auto", "rotate", "ps", "local"],
                     help="auto = local at N=1, rotate at N>1")
+    ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"],
+                    help="rotate: two counter-rotating rings of quarter-shard blocks (both directions of two xGMI "
+                         "links) or one ring of half-shard blocks")
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"],
                     help="PS-path all-to-all row dtype (bf16 halves the bytes; opt-in: the headline keeps fp32)")
     ap.add_argument("--no-pipeline", action="store_true")
@@ -121,7 +124,7 @@ def main(argv=None):
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
-                   user_phases=a.user_phases)
+                   user_phases=a.user_phases, rotation=a.rotation)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device
@@ -150,6 +153,8 @@ def main(argv=None):
     comm.barrier()
     sync()
     model.set_timer(timer)  # None unless --metrics-jsonl: event records only, no syncs
+    if model.exchange == "rotate":
+        model.rot.wait_ms()  # drop the warm-up's transfer waits
     t0 = time.perf_counter()
     for _ in range(a.steps):
         model.step(*data.batch(step, a.batch))
@@ -164,6 +169,11 @@ def main(argv=None):
     sync()
     dt = time.perf_counter() - t0
     dt_max = comm.max_over_ranks(dt)
+    # time the compute stream waited for rotation transfers (HIP events around each
+    # wait; read after the timed region): "transfer exposed" vs "compute slower"
+    wait_ms = model.rot.wait_ms() / a.steps if model.exchange == "rotate" else 0.0
+    waits = comm.gather_floats(wait_ms)
+    n_local = comm.gather_floats(float(model.users.n_local))
     # per-rank bytes this rank put on the wire (all-to-all + ring rotation)
     sent = float(comm.bytes_sent + (model.rot.bytes_sent if model.exchange == "rotate" else 0))
     bytes_per_rank = comm.gather_floats(sent)
@@ -203,7 +213,11 @@ def main(argv=None):
                 "scalar_params_per_s": value * 2 * a.dim,
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
                 if model.exchange == "ps" else None,
+                "rotation": model.cfg.rotation if model.exchange == "rotate" else None,
                 "rotation_bytes_sent_rank0": model.rot.bytes_sent if model.exchange == "rotate" else None,
+                "comm_wait_ms_per_step": max(waits),
+                "comm_wait_ms_per_step_per_rank": waits,
+                "users_per_rank": [int(x) for x in n_local],
                 "bytes_sent_per_rank": bytes_per_rank,
                 "bytes_per_peer_rank0": list(comm.peer_bytes),
             },

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-GPU step of an N-GPU rotation run, measured on ONE GPU.
+
+At N GPUs every rank holds 10M/N users, takes ``--batch`` ratings per step
+(weak scaling) and runs 2N sub-steps of the tiled SGD over the item blocks it
+holds (``parallel/rotation.py``: two counter-rotating rings of 1M/(4N)-row
+blocks by default).  ``MFConfig(emulate_world=N)`` runs rank 0's exact schedule
+with every block resident (``EmulatedRotation``): the same partition and the
+same launches per sub-step as one GPU of the real job, without the transfers.
+Comparing the emulated step with the N = 1 step separates "compute slower at
+N" from "transfer exposed" before an N-GPU node runs the real thing.
+
+    python bench/bench_emulate_world.py [--ws 1,2,4,8] [--steps 20 --warmup 5]
+
+One JSON line per N: ms_per_step, per-GPU updates/s, ratio to N = 1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ws", default="1,2,4,8")
+    ap.add_argument("--batch", type=int, default=1 << 26)
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pool", type=int, default=4)
+    ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
+    a = ap.parse_args()
+
+    import torch
+
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    dev = torch.device("cuda", 0)
+    comm = Comm(device=dev)
+    base = None
+    for W in [int(x) for x in a.ws.split(",")]:
+        cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
+                       exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0)
+        m = DistributedMF(cfg, comm)
+        data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
+        s = 0
+        for _ in range(a.warmup):
+            m.step(*data.batch(s, a.batch))
+            s += 1
+        m.flush()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            m.step(*data.batch(s, a.batch))
+            s += 1
+        m.flush()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / a.steps * 1e3
+        base = base or ms
+        print(json.dumps({"emulated_world": W, "rotation": a.rotation if W > 1 else "local", "ms_per_step": ms,
+                          "updates_per_s_per_gpu": a.batch / ms * 1e3, "ratio_to_n1": ms / base,
+                          "users_per_gpu": m.users.n_local, "sub_steps": m.rot.K if W > 1 else 1,
+                          "tile_rows": getattr(m, "tile_R", None), "tiles_per_block": getattr(m, "tile_T", None),
+                          "user_phases": getattr(m, "user_phases", None)}), flush=True)
+        del m, data
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,12 +15,15 @@ Execution per micro-batch of B ratings on each GPU:
 * ``W == 1`` — the item shard is local: one fused kernel reads u and i,
   stores u (Hogwild inside the batch; optional atomics) and atomically adds
   di into the item row (``ops.mf_sgd_local``).  No wire buffers at all.
-* ``W > 1``, ``exchange="rotate"`` (default) — the item shards travel around
-  the xGMI ring instead of rows travelling to the ratings
+* ``W > 1``, ``exchange="rotate"`` (default) — the item shards travel between
+  the GPUs instead of rows travelling to the ratings
   (``parallel.rotation.RingRotation``, stratified SGD): the micro-batch is
-  partitioned by item block on the GPU (``ops.RotationPartitioner``), then 2W
-  sub-steps each run the fused local kernel on the resident block while the
-  next block arrives from the neighbour.  No dedup, no pulls, no staleness.
+  partitioned by item block on the GPU, then 2W sub-steps each run the SGD on
+  the resident blocks while the next ones arrive from the neighbours -- two
+  counter-rotating rings of quarter-shard blocks by default (``rotation="bidir"``:
+  both directions of two xGMI links), or one ring (``"ring"``).  No dedup, no
+  pulls, no staleness.  ``emulate_world=N`` runs rank 0's schedule of an N-GPU
+  job on one GPU with every block resident (the per-GPU compute at N).
 * ``W > 1``, ``exchange="ps"`` — ``TensorPS.pull`` (dedup + 2 all-to-alls),
   fused SGD on the pulled rows accumulating per-unique-item deltas
   (``ops.mf_sgd_pulled``), ``TensorPS.push`` (all-to-all + apply); the pull of
@@ -40,7 +43,7 @@ import torch.distributed
 
 from ... import ops
 from ...parallel.comm import Comm
-from ...parallel.rotation import RingRotation, shard_halves
+from ...parallel.rotation import EmulatedRotation, RingRotation, layout_world, shard_halves
 from ...parallel.rotation import block_rows as block_rows_of
 from ...api.batched import BatchedWorkerLogic
 from ...parallel.table import ShardedTable
@@ -73,6 +76,8 @@ class MFConfig:
                                       # (launch-bound small batches; disables the prefetch)
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
+    rotation: str = "bidir"           # rotate: "bidir" (two counter-rotating rings) | "ring" (one ring)
+    emulate_world: int = 0            # W = 1, rotate: rank 0's share of an N-rank job (users / schedule)
 
 
     def user_seed(self) -> int:
@@ -98,8 +103,12 @@ class DistributedMF:
         self.comm = comm or Comm()
         W, r, dev = self.comm.world, self.comm.rank, self.comm.device
         init = ("uniform", cfg.range_min, cfg.range_max)
+        self.emulated = cfg.emulate_world > 1
+        if self.emulated and (W != 1 or cfg.exchange not in ("rotate", "auto")):
+            raise ValueError("emulate_world runs the rotation schedule of N ranks in ONE process")
+        Wn = cfg.emulate_world if self.emulated else W  # the job's world (emulated or real)
         # worker-resident user shard: users u with u % W == r, local row u // W
-        self.users = ShardedTable(cfg.num_users, cfg.dim, r, W, "hash", init, cfg.user_seed(), dev,
+        self.users = ShardedTable(cfg.num_users, cfg.dim, r, Wn, "hash", init, cfg.user_seed(), dev,
                                   track_touched=False)
         # PS item shard
         self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.item_seed(), dev, optimizer="add")
@@ -107,7 +116,7 @@ class DistributedMF:
         self.user_atomic = cfg.user_update == "atomic"
         exchange = cfg.exchange
         if exchange == "auto":
-            exchange = "ps" if cfg.force_ps_path else ("rotate" if W > 1 else "local")
+            exchange = "ps" if cfg.force_ps_path else ("rotate" if Wn > 1 else "local")
         if exchange not in ("rotate", "ps", "local") or (exchange == "local" and W > 1):
             raise ValueError(f"exchange {cfg.exchange!r} invalid at world size {W}")
         self.exchange = exchange
@@ -121,7 +130,7 @@ class DistributedMF:
         #            (exact per-item order; latency bound, 2.8e9/s).
         # local: the table as 2 blocks (halves) of one shard; rotate: 2W blocks; ps:
         # the pulled rows of a micro-batch (<= num_items unique items) as one block
-        tile_w = W if exchange == "rotate" else 1
+        tile_w = layout_world(Wn, cfg.rotation) if exchange == "rotate" else 1
         block_rows = cfg.num_items if exchange == "ps" else max(block_rows_of(cfg.num_items, tile_w))
         tile_R = ops.tile_rows_for(cfg.dim, block_rows, tile_w)
         mode = cfg.sgd_mode
@@ -166,8 +175,13 @@ class DistributedMF:
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
         if self.exchange == "rotate":
-            self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items)
-            self.partitioner = ops.RotationPartitioner(W, torch.tensor(shard_halves(cfg.num_items, W)), dev)
+            if self.emulated:
+                self.rot = EmulatedRotation(self.items.weight, cfg.num_items, Wn, cfg.rotation)
+            else:
+                self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items, cfg.rotation)
+            self.rot_w = tile_w  # hash shards of the block layout the ratings are bucketed by
+            self.partitioner = ops.RotationPartitioner(tile_w, torch.tensor(shard_halves(cfg.num_items, tile_w)),
+                                                       dev)
             # rows are updated in rotating buffers: remember which items were rated
             # so the close-time dump still covers exactly the touched parameters
             self._seen = torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev)
@@ -251,10 +265,11 @@ class DistributedMF:
             n = uid_local.numel()
             for _ in range(self.rot.K):
                 with stage("mf.rotate.begin", self.timer):
-                    self.rot.begin()  # transfer of the next block overlaps this sub-step
+                    self.rot.begin()  # transfer of the next blocks overlaps this sub-step
                 with stage("mf.sgd", self.timer):
-                    ops.mf_sgd_local_seg(self.U, self.rot.active(), u, row, r, ptr, self.rot.active_block(), n,
-                                         c.learning_rate, c.lam, self.user_atomic)
+                    for g, blk in self.rot.active_blocks():
+                        ops.mf_sgd_local_seg(self.U, blk, u, row, r, ptr, g, n, c.learning_rate, c.lam,
+                                             self.user_atomic)
                 with stage("mf.rotate.end", self.timer):
                     self.rot.end()
         else:  # PS path: one micro-batch through the tensor engine
@@ -339,13 +354,21 @@ class DistributedMF:
                     ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
                                           c.learning_rate, c.lam)
             return
+        nb = 2 * self.rot_w  # item blocks per user phase in the partition layout
         for _ in range(self.rot.K):
             with stage("mf.rotate.begin", self.timer):
-                self.rot.begin()  # transfer of the next block overlaps this sub-step
+                self.rot.begin()  # transfer of the next blocks overlaps this sub-step
             with stage("mf.sgd", self.timer):
+                act = self.rot.active_blocks()
                 for p in range(self.user_phases):
-                    ops.mf_sgd_tiled(self.U, self.rot.active(), rec, ptr, p * self.rot.K + self.rot.active_block(),
-                                     self.tile_T, self.tile_R, c.learning_rate, c.lam)
+                    if len(act) == 2:  # one block of each ring: disjoint items, one launch
+                        (g0, b0), (g1, b1) = act
+                        ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
+                                              c.learning_rate, c.lam, block1=p * nb + g1)
+                    else:
+                        (g0, b0), = act
+                        ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
+                                         c.learning_rate, c.lam)
             with stage("mf.rotate.end", self.timer):
                 self.rot.end()
 
@@ -383,7 +406,9 @@ class DistributedMF:
             self._tiled_sgd(staged)
         if self.exchange == "rotate" and not self.rot.at_rest:
             self.rot.home()
-            if self.items.touched is not None:
+            if self.items.touched is not None and self.comm.world == 1:
+                self.items.touched |= self._seen
+            elif self.items.touched is not None:
                 seen = self.comm.all_reduce(self._seen.clone(), op=torch.distributed.ReduceOp.MAX)
                 loc = torch.arange(self.items.n_local, device=seen.device)
                 self.items.touched |= seen[self.items.global_ids(loc)]

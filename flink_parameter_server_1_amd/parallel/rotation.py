@@ -1,35 +1,51 @@
-"""Item-block rotation over the xGMI ring: stratified MF-SGD without a pull/push round trip.
+"""Item-block rotation over xGMI: stratified MF-SGD without a pull/push round trip.
 
 In ``psOnlineMF`` every rating pulls its item vector from the PS shard and
 pushes a delta back (``M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-55``).
 On a node of fully connected GPUs with 288 GB each, the item table (1M x 64
 fp32 = 256 MB) is tiny next to the rating stream, so instead of moving rows to
 the ratings, the *item shards move to the ratings* (stratified SGD, Gemulla et
-al. 2011): the PS shards travel around the ring while each worker updates only
-the block it currently holds.
+al. 2011): the PS shards travel between the GPUs while each worker updates only
+the blocks it currently holds.
 
-Schedule (K = 2W item blocks, block ``2q+h`` = half ``h`` of PS shard ``q``):
+One ring (``_Ring``) of ``K = 2W`` blocks, two per rank at rest:
 
-* at rest rank ``r`` holds its home blocks ``2r`` and ``2r+1`` (its PS shard);
-* in sub-step ``s`` rank ``r`` updates block ``(2r+s) % K`` with the ratings of
-  its users that fall in it; blocks of opposite parity are idle and travel:
-* during sub-step ``s >= 1`` rank ``r`` sends block ``2r+s-1`` (finished in
-  ``s-1``) to rank ``r-1`` and receives block ``2r+s+1`` from rank ``r+1`` --
-  exactly the block it needs next, so the transfer hides behind the compute;
+* in sub-step ``s`` rank ``r`` updates ring block ``(2r + s) % K`` (direction
+  +1) or ``(2r + 1 - s) % K`` (direction -1); blocks of the other parity are idle
+  and travel:
+* during sub-step ``s >= 1`` rank ``r`` sends the block it finished in ``s-1`` to
+  the neighbour that needs it next (``r - d``) and receives the block it needs
+  in ``s+1`` from ``r + d`` -- the transfer hides behind the compute;
 * one micro-batch = K sub-steps = every block once; the schedule is periodic,
   so consecutive micro-batches continue it without a barrier.
 
-Every item block is owned by exactly one GPU at any time and every user row
-by its worker, so no parameter is ever updated concurrently by two GPUs and no
+Schedules:
+
+* ``"bidir"`` (default): each PS shard is split into two *virtual* hash shards
+  (``i % 2W``: shard ``r`` and ``r + W`` of rank ``r``), giving two rings of
+  quarter-shard blocks that rotate in OPPOSITE directions.  Every sub-step a
+  rank updates one block of each ring (one launch, ``ops.mf_sgd_tiled_pair``)
+  and each link direction to both ring neighbours carries a quarter-shard: per
+  link direction and sub-step half the bytes of one ring, on both directions
+  of two xGMI links instead of one direction of one link.
+* ``"ring"``: one ring of half-shard blocks, direction +1.
+
+Every item block is owned by exactly one GPU at any time and every user row by
+its worker, so no parameter is ever updated concurrently by two GPUs and no
 update is stale: the result equals a sequential schedule of the sub-steps
 (serializable), unlike the bounded-staleness PS path.
 
+``EmulatedRotation`` runs rank 0's schedule of an N-rank job on ONE GPU with
+every block resident (no transfers): the per-GPU compute of an N-GPU step
+(``bench/bench_emulate_world.py``).
+
 ``home()`` returns every block to its PS shard (``ShardedTable`` rows) for
-evaluation, dumps and checkpoints.
+evaluation, dumps and checkpoints.  ``wait_ms()`` is the time the compute stream
+spent waiting for transfers (HIP events around each wait).
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -53,107 +69,251 @@ def block_rows(num_ids: int, world: int) -> List[int]:
     return rows
 
 
+def layout_world(world: int, schedule: str) -> int:
+    """Hash shards of the block layout the partitioners bucket by: ``2W`` virtual
+    shards for the bidirectional schedule, ``W`` for the single ring."""
+    return 2 * world if schedule == "bidir" else world
+
+
+class _Ring:
+    """One ring of ``2W`` blocks (see the module docstring)."""
+
+    def __init__(self, W: int, r: int, home: List[torch.Tensor], rows: List[int], direction: int, base: int,
+                 like: torch.Tensor):
+        self.W, self.r, self.K, self.d, self.base = W, r, 2 * W, direction, base
+        self.home_v = home          # this rank's two ring blocks (2r, 2r+1) in the PS shard (views)
+        self.rows = rows            # rows of every ring block
+        cap = max(rows) if rows else 0
+        self.buf = [torch.empty((cap, like.shape[1]), dtype=like.dtype, device=like.device) for _ in range(3)]
+        self.s = 0
+        self.A = self.P = self.F = self.N = None
+
+    def order(self, s: int, r: Optional[int] = None) -> int:
+        r = self.r if r is None else r
+        return (2 * r + s) % self.K if self.d > 0 else (2 * r + 1 - s) % self.K
+
+    def _home_of(self, j: int) -> torch.Tensor:
+        return self.home_v[j - 2 * self.r]
+
+    def leave_rest(self) -> None:
+        o0, o1 = self.order(0), self.order(1)
+        self.buf[0][: self.rows[o0]].copy_(self._home_of(o0))
+        self.buf[1][: self.rows[o1]].copy_(self._home_of(o1))
+        self.A, self.N, self.F, self.P = 0, 1, 2, None
+        self.s = 0
+
+    def transfers(self):
+        """``(send, recv)`` of sub-step ``s`` (None when nothing moves)."""
+        if self.W == 1 or self.P is None:
+            return None
+        out_b, in_b = self.order(self.s - 1), self.order(self.s + 1)
+        return ((self.buf[self.P][: self.rows[out_b]], (self.r - self.d) % self.W),
+                (self.buf[self.F][: self.rows[in_b]], (self.r + self.d) % self.W))
+
+    def rotate(self) -> None:
+        if self.W == 1:  # no peers: the two blocks alternate in place
+            self.A, self.N = self.N, self.A
+        elif self.P is None:
+            self.A, self.P, self.F, self.N = self.N, self.A, self.F, None
+        else:
+            self.A, self.P, self.F = self.F, self.A, self.P
+        self.s += 1
+
+    def active(self) -> Tuple[int, torch.Tensor]:
+        j = self.order(self.s)
+        return self.base + j, self.buf[self.A][: self.rows[j]]
+
+    def held(self) -> dict:
+        """ring block -> buffer index of the blocks this rank holds now."""
+        s = self.s
+        if self.W == 1:
+            return {self.order(s): self.A, self.order(s + 1): self.N}
+        if self.P is None:
+            return {self.order(0): self.A, self.order(1): self.N}
+        return {self.order(s): self.A, self.order(s - 1): self.P}
+
+    def holder(self, j: int) -> int:
+        s = self.s
+        for x in range(self.W):
+            if self.P is None or self.W == 1:
+                if j in (self.order(0, x), self.order(1, x)):
+                    return x
+            elif j in (self.order(s, x), self.order(s - 1, x)):
+                return x
+        raise AssertionError(f"no holder for ring block {j}")
+
+    def home_ops(self):
+        """``(sends, recvs, local copies)`` that return every block home."""
+        sends, recvs, local = [], [], []
+        held = self.held()
+        for j, bi in sorted(held.items()):
+            dst = j // 2
+            if dst != self.r:
+                sends.append((self.buf[bi][: self.rows[j]], dst))
+            else:
+                local.append((self._home_of(j), self.buf[bi][: self.rows[j]]))
+        for j in (2 * self.r, 2 * self.r + 1):
+            src = self.holder(j)
+            if src != self.r:
+                recvs.append((self._home_of(j), src))
+        return sends, recvs, local
+
+
 class RingRotation:
-    def __init__(self, comm: Comm, home: torch.Tensor, num_ids: int):
-        """``home``: this rank's PS shard ``[n_local, D]`` (hash layout ``i % W``)."""
+    """The rotation of one rank: one ring (``schedule="ring"``) or two
+    counter-rotating rings (``"bidir"``) over its PS shard ``home``
+    (``[n_local, D]``, hash layout ``i % W``)."""
+
+    def __init__(self, comm: Comm, home: torch.Tensor, num_ids: int, schedule: str = "bidir"):
+        if schedule not in ("bidir", "ring"):
+            raise ValueError(f"rotation schedule must be 'bidir' or 'ring', not {schedule!r}")
         self.comm = comm
         self.W, self.r = comm.world, comm.rank
-        self.K = 2 * self.W
+        self.schedule = schedule
+        self.K = 2 * self.W  # sub-steps per micro-batch
         self.home_t = home
-        self.half = shard_halves(num_ids, self.W)
-        self.rows = block_rows(num_ids, self.W)
-        cap = max(self.rows)
-        self.buf = [torch.empty((cap, home.shape[1]), dtype=home.dtype, device=home.device) for _ in range(3)]
+        W, r = self.W, self.r
+        if schedule == "ring":
+            hq = shard_halves(num_ids, W)[r]
+            self.rings = [_Ring(W, r, [home[:hq], home[hq:]], block_rows(num_ids, W), +1, 0, home)]
+        else:
+            halves, rows = shard_halves(num_ids, 2 * W), block_rows(num_ids, 2 * W)
+            v0, v1 = home[0::2], home[1::2]  # virtual shards r and r + W of this rank
+            hl, hr = halves[r], halves[r + W]
+            self.rings = [_Ring(W, r, [v0[:hl], v0[hl:]], rows[: 2 * W], +1, 0, home),
+                          _Ring(W, r, [v1[:hr], v1[hr:]], rows[2 * W:], -1, 2 * W, home)]
         self.at_rest = True
         self.s = 0
-        self._A = self._P = self._F = self._N = None
         self._works: Optional[list] = None
+        self._events: List[tuple] = []
+        self._host_wait_s = 0.0
         self.bytes_sent = 0
 
-    # --------------------------------------------------------------- blocks
-    def _home_slice(self, h: int) -> torch.Tensor:
-        hq = self.half[self.r]
-        return self.home_t[:hq] if h == 0 else self.home_t[hq:]
-
-    def active_block(self) -> int:
-        return (2 * self.r + self.s) % self.K
-
-    def active(self) -> torch.Tensor:
-        return self.buf[self._A][: self.rows[self.active_block()]]
-
-    def _peer(self, d: int) -> int:
-        return (self.r + d) % self.W
-
     # --------------------------------------------------------------- schedule
-    def _leave_rest(self):
-        self.buf[0][: self.rows[2 * self.r]].copy_(self._home_slice(0))
-        self.buf[1][: self.rows[2 * self.r + 1]].copy_(self._home_slice(1))
-        self._A, self._N, self._F, self._P = 0, 1, 2, None
-        self.s = 0
-        self.at_rest = False
+    def active_blocks(self) -> List[Tuple[int, torch.Tensor]]:
+        """``(block id in the partition layout, resident rows)`` updated this sub-step."""
+        return [ring.active() for ring in self.rings]
 
     def begin(self):
-        """Start sub-step ``s``: issue the transfers that overlap its compute."""
+        """Start a sub-step: issue the transfers that overlap its compute."""
         if self.at_rest:
-            self._leave_rest()
-        if self.W == 1 or self._P is None:  # both blocks resident (W = 1) / next block already home
-            return
-        out_b = (2 * self.r + self.s - 1) % self.K
-        in_b = (2 * self.r + self.s + 1) % self.K
-        self._works = self.comm.p2p([(self.buf[self._P][: self.rows[out_b]], self._peer(-1))],
-                                    [(self.buf[self._F][: self.rows[in_b]], self._peer(+1))])
-        self.bytes_sent += self.buf[self._P][: self.rows[out_b]].numel() * self.buf[0].element_size()
+            for ring in self.rings:
+                ring.leave_rest()
+            self.at_rest = False
+            self.s = 0
+        sends, recvs = [], []
+        for ring in self.rings:  # every rank posts ring by ring: matched order per peer pair
+            t = ring.transfers()
+            if t is not None:
+                sends.append(t[0])
+                recvs.append(t[1])
+        if sends:
+            self._works = self.comm.p2p(sends, recvs)
+            self.bytes_sent += sum(x.numel() * x.element_size() for x, _ in sends)
 
     def end(self):
-        """Finish sub-step ``s`` (after its compute was enqueued) and rotate roles."""
-        if self.W == 1:  # no peers: the two blocks alternate in place
-            self._A, self._N = self._N, self._A
-        elif self._P is None:
-            self._A, self._P, self._F, self._N = self._N, self._A, self._F, None
-        else:
-            for w in self._works or []:
+        """Finish a sub-step (after its compute was enqueued) and rotate roles."""
+        if self._works:
+            cuda = self.home_t.is_cuda
+            if cuda:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            else:
+                import time
+
+                t0 = time.perf_counter()
+            for w in self._works:
                 w.wait()
-            self._works = None
-            self._A, self._P, self._F = self._F, self._A, self._P
+            if cuda:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self._events.append((e0, e1))
+            else:
+                self._host_wait_s += time.perf_counter() - t0
+        self._works = None
+        for ring in self.rings:
+            ring.rotate()
         self.s += 1
+
+    def wait_ms(self, reset: bool = True) -> float:
+        """Milliseconds the compute stream waited for transfers since the last call
+        (synchronises on the recorded events)."""
+        ms = self._host_wait_s * 1e3 + sum(a.elapsed_time(b) for a, b in self._events)
+        if reset:
+            self._events, self._host_wait_s = [], 0.0
+        return ms
 
     # --------------------------------------------------------------- homing
     def home(self):
         """Send every block back to its PS shard (between sub-steps)."""
         if self.at_rest:
             return
-        s = self.s  # blocks held: A = 2r+s, P = 2r+s-1 (or N = 2r+1 right after rest)
-        if self.W == 1:
-            held = {s % 2: self._A, (s + 1) % 2: self._N}
-        elif self._P is None:  # still at s == 0 layout: A = 2r, N = 2r+1 -- all home
-            held = {2 * self.r: self._A, 2 * self.r + 1: self._N}
-        else:
-            held = {(2 * self.r + s) % self.K: self._A, (2 * self.r + s - 1) % self.K: self._P}
-
-        def holder(b: int) -> int:
-            if self.W == 1 or self._P is None:
-                return b // 2
-            d = (b - s) % self.K
-            return d // 2 if d % 2 == 0 else ((b - s + 1) % self.K) // 2
-
-        # messages between one pair are matched in posting order: post sends and
-        # receives in ascending block id on both sides
-        sends, recvs = [], []
-        for b, bi in sorted(held.items()):
-            dst = b // 2
-            if dst != self.r:
-                sends.append((self.buf[bi][: self.rows[b]], dst))
-        for h in (0, 1):
-            b = 2 * self.r + h
-            src = holder(b)
-            if src != self.r:
-                recvs.append((self._home_slice(h), src))
-        works = self.comm.p2p(sends, recvs)
-        for b, bi in held.items():
-            if b // 2 == self.r:
-                self._home_slice(b % 2).copy_(self.buf[bi][: self.rows[b]])
+        sends, recvs, local = [], [], []
+        for ring in self.rings:  # ring by ring, ascending block ids: same posting order on both sides
+            s_, r_, l_ = ring.home_ops()
+            sends += s_
+            recvs += r_
+            local += l_
+        # NCCL receives need contiguous buffers; the bidir rings' home views are strided
+        staged = [(torch.empty(v.shape, dtype=v.dtype, device=v.device), v, p) for v, p in recvs]
+        works = self.comm.p2p(sends, [(t, p) for t, _, p in staged])
+        for dst, src in local:
+            dst.copy_(src)
         for w in works:
             w.wait()
+        for t, v, _ in staged:
+            v.copy_(t)
         self.at_rest = True
         self.s = 0
-        self._A = self._P = self._F = self._N = None
+
+
+class EmulatedRotation:
+    """Rank 0's rotation schedule of a ``world``-rank job on one device with every
+    block resident: the same launches per sub-step as one GPU of the real job,
+    without transfers (``item`` = the whole ``[num_ids, D]`` table)."""
+
+    def __init__(self, items: torch.Tensor, num_ids: int, world: int, schedule: str = "bidir"):
+        self.items, self.W, self.schedule = items, world, schedule
+        self.Wv = layout_world(world, schedule)
+        self.K = 2 * world
+        self.halves = shard_halves(num_ids, self.Wv)
+        self.rows = block_rows(num_ids, self.Wv)
+        self.ids = []
+        for g in range(2 * self.Wv):
+            q, h = g // 2, g % 2
+            n_local = (num_ids - q + self.Wv - 1) // self.Wv
+            lo, hi = (0, self.halves[q]) if h == 0 else (self.halves[q], n_local)
+            self.ids.append((q + self.Wv * torch.arange(lo, hi, device=items.device)).long())
+        self.blocks = None
+        self.at_rest = True
+        self.s = 0
+        self.bytes_sent = 0
+
+    def active_blocks(self):
+        s, W = self.s, self.W
+        if self.schedule == "ring":
+            g = [s % (2 * W)]
+        else:
+            g = [s % (2 * W), 2 * W + (1 - s) % (2 * W)]
+        return [(b, self.blocks[b]) for b in g]
+
+    def begin(self):
+        if self.at_rest:
+            self.blocks = [self.items[ids].contiguous() for ids in self.ids]
+            self.at_rest = False
+            self.s = 0
+
+    def end(self):
+        self.s += 1
+
+    def wait_ms(self, reset: bool = True) -> float:
+        return 0.0
+
+    def home(self):
+        if self.at_rest:
+            return
+        for ids, blk in zip(self.ids, self.blocks):
+            self.items[ids] = blk
+        self.blocks = None
+        self.at_rest = True
+        self.s = 0
