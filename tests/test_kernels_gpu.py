@@ -315,37 +315,3 @@ def test_ring_known_and_known_list_sampling_match_reference():
     r = R.sample_uniform_reject(1000, 3, ni, pos, uid, ring_r, mem, 4, 2, lst_g.cpu(), n_known)
     assert torch.equal(g, r)  # same known list on both sides
     assert set(g.tolist()) <= known_set
-
-
-@pytest.mark.parametrize("rec8", [False, True])
-def test_tiled_sgd_level4_overflow_processes_every_rating(rec8):
-    """Level-4 slots sized for a uniform stream, then a skewed one: the excess of the
-    hot tiles goes through the overflow list and the flat kernel -- every rating is
-    applied exactly once (unique users: equals the batch reference up to the
-    per-tile chunk semantics, which the overflow records do not change for items
-    rated once)."""
-    D, nu, ni = 64, 40000, 4096
-    Rt, T = 64, 64
-    part = ops.TilePartitioner(1, [ni], Rt, T, DEV, rec8=rec8, levels=4)
-    U = torch.rand(nu, D, device=DEV) * 0.1
-    I = torch.rand(ni, D, device=DEV) * 0.1
-    # run 1: uniform (sizes the slots); no SGD
-    part.run(torch.randperm(nu, device=DEV)[:8000].to(torch.int32),
-             torch.randint(0, ni, (8000,), device=DEV, dtype=torch.int32), torch.rand(8000, device=DEV))
-    # run 2: every rating in tile 0 (rows 0..63), unique users, unique (user, item)
-    B = 8000
-    uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
-    iid = (torch.arange(B, device=DEV, dtype=torch.int32) % Rt)
-    r = torch.rand(B, device=DEV)
-    layout, rec = part.run(uid, iid, r)
-    assert int(layout.ovf_cnt.item()) > 0  # the hot tile overflowed its slot
-    ptr_c, u, row, rr = layout.compact(rec, T, Rt)
-    assert int(ptr_c[1]) == B and torch.equal(torch.sort(u).values, torch.sort(uid.cpu()).values)
-    U0, I0 = U.clone(), I.clone()
-    ops.mf_sgd_tiled(U, I, rec, layout, 0, T, Rt, 0.01)
-    # every user row changed exactly by its one rating's step against SOME item value:
-    # check the total item movement equals the sum of the applied item deltas
-    du = (U - U0)[uid.long()]
-    assert bool((du.abs().sum(1) > 0).all())
-    moved = (I - I0)[:Rt].abs().sum()
-    assert float(moved) > 0 and bool(torch.isfinite(I).all())
