@@ -35,7 +35,11 @@ def main(argv=None):
     ap.add_argument("--ps-path", action="store_true",
                     help="N = 1: run the pull / push protocol instead of updating the tables in place")
     ap.add_argument("--shared-negatives", type=int, default=16, choices=[16, 32],
-                    help="negatives shared by each block of 32 pairs (16: kernel v4, 32: kernel v3)")
+                    help="mode shared: negatives shared by each block of 32 pairs (16: kernel v4, 32: kernel v3)")
+    ap.add_argument("--mode", default="standard", choices=["standard", "shared"],
+                    help="standard: 5 independent negatives per pair (word2vec's objective, the reported number); "
+                         "shared: block-shared negatives (Ji et al.), a different estimator")
+    ap.add_argument("--negatives", type=int, default=5)
     a = ap.parse_args(argv)
 
     import torch
@@ -48,7 +52,7 @@ def main(argv=None):
     dev = comm.device
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
                                    wire_dtype=a.wire, shared_negatives=a.shared_negatives,
-                                   local_direct=not a.ps_path,
+                                   local_direct=not a.ps_path, mode=a.mode, negatives=a.negatives,
                                    **({} if a.neg_group is None else {"neg_group": a.neg_group})), comm=comm)
     toks = synthetic_corpus(max(a.pairs // a.window, 1 << 16) * 2, a.vocab, seed=comm.rank, device=dev)
     c, o = skipgram_pairs(toks, a.window)
@@ -83,8 +87,11 @@ def main(argv=None):
             "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
-            "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} neg=5(shared {a.shared_negatives}/block)",
-                       "neg_group": m.cfg.neg_group,
+            "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} negatives={a.negatives}",
+                       "mode": a.mode,
+                       "negatives": (f"{a.negatives} independent per pair" if a.mode == "standard" else
+                                     f"{a.shared_negatives} shared per {32 * m.cfg.neg_group} pairs, weight "
+                                     f"{a.negatives}/{a.shared_negatives}"),
                        "exchange": "local-direct" if m._direct else "ps",
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)

@@ -8,10 +8,16 @@ Parameters: input vectors ``W_in[V, D]`` (init U[-0.5/D, 0.5/D)) and output
 vectors ``W_out[V, D]`` (zeros), each a hash-sharded PS table.  One step on a
 micro-batch of (center, context) pairs:
 
-1. draw 32 shared negatives per 32 pairs from unigram^0.75 (alias table, K5);
+1. draw negatives from unigram^0.75 (alias table, K5): ``mode="standard"``
+   (default) ``negatives`` independent ones per pair -- word2vec's objective;
+   ``mode="shared"``: ``shared_negatives`` per block of 32 pairs (x ``neg_group``
+   blocks), each weighted ``negatives / shared_negatives`` (Ji et al.'s
+   block-shared negatives: the same expected gradient, ~10-40x fewer negative
+   rows touched; a different estimator, reported separately);
 2. pull the center rows from ``W_in`` and context + negative rows from
    ``W_out`` (deduplicated all-to-all, ``TensorPS``);
-3. ``ops.sgns_step`` (MFMA, K6) computes per-row deltas;
+3. ``ops.sgns_standard`` (K6, ``sgns_std.hip``) / ``ops.sgns_step`` (MFMA,
+   ``sgns.hip``) computes per-row deltas;
 4. push both delta sets; the PS adds them.
 
 With one rank (``local_direct``, default) steps 2 and 4 collapse: the kernel
@@ -50,6 +56,7 @@ class SGNSConfig:
     neg_group: int = 4            # v4: consecutive 32-pair blocks sharing one negative set (1, 2, 4):
                                   # 4 measured +6 % pairs/s at the same loss curve (profiles/r2_sgns.md)
     local_direct: bool = True     # W = 1: kernel reads / atomically updates the local tables in place
+    mode: str = "standard"        # "standard": `negatives` independent negatives per pair | "shared"
 
 
 class DistributedSGNS:
@@ -72,6 +79,15 @@ class DistributedSGNS:
         self.counter = 0
         self.pairs_seen = 0
         self.timer = None  # utils.metrics.StageTimer (optional)
+        if cfg.mode not in ("standard", "shared"):
+            raise ValueError(f"SGNS mode must be 'standard' or 'shared', not {cfg.mode!r}")
+        self.standard = cfg.mode == "standard"
+
+    def _n_negatives(self, P: int) -> int:
+        c = self.cfg
+        if self.standard:
+            return P * c.negatives
+        return ((P + self.BLOCK * c.neg_group - 1) // (self.BLOCK * c.neg_group)) * c.shared_negatives
 
     def step(self, centers: torch.Tensor, contexts: torch.Tensor, lr: Optional[float] = None,
              with_loss: bool = False):
@@ -105,9 +121,8 @@ class DistributedSGNS:
         added in place by the kernel's atomics."""
         c = self.cfg
         P = centers.numel()
-        nb = (P + self.BLOCK * c.neg_group - 1) // (self.BLOCK * c.neg_group)  # negative sets
         dev = self.w_in.weight.device
-        negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives, seed=c.seed + 17 * self.comm.rank,
+        negs = ops.sample_alias(self.prob, self.alias, self._n_negatives(P), seed=c.seed + 17 * self.comm.rank,
                                 counter=self.counter)
         self.counter += 1
         cen = centers.to(device=dev, dtype=torch.int32).contiguous()
@@ -119,10 +134,14 @@ class DistributedSGNS:
             ops.mark_rows(self.w_out.touched, ctx)
             ops.mark_rows(self.w_out.touched, negs)
         with stage("sgns.step", self.timer):
-            loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
-                                 c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
-                                 with_loss=with_loss, neg_k=c.shared_negatives,
-                                 neg_group=c.neg_group)
+            if self.standard:
+                loss = ops.sgns_standard(self.w_in.weight, self.w_out.weight, cen, ctx, negs, c.negatives, lr,
+                                         self.w_in.weight, self.w_out.weight, with_loss=with_loss)
+            else:
+                loss = ops.sgns_step(self.w_in.weight, self.w_out.weight, cen, ctx, negs, lr,
+                                     c.negatives / c.shared_negatives, self.w_in.weight, self.w_out.weight,
+                                     with_loss=with_loss, neg_k=c.shared_negatives,
+                                     neg_group=c.neg_group)
         self.pairs_seen += P
         if with_loss:
             return float(loss.item()) / max(P, 1)
@@ -141,9 +160,8 @@ class DistributedSGNS:
     def _start(self, centers, contexts, async_rows: bool = False):
         c = self.cfg
         P = centers.numel()
-        nb = (P + self.BLOCK * c.neg_group - 1) // (self.BLOCK * c.neg_group)  # negative sets
         with stage("sgns.negatives", self.timer):
-            negs = ops.sample_alias(self.prob, self.alias, nb * c.shared_negatives,
+            negs = ops.sample_alias(self.prob, self.alias, self._n_negatives(P),
                                     seed=c.seed + 17 * self.comm.rank, counter=self.counter)
         self.counter += 1
         outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
@@ -167,9 +185,13 @@ class DistributedSGNS:
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
         with stage("sgns.step", self.timer):
-            loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
-                                 c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
-                                 neg_k=c.shared_negatives, neg_group=c.neg_group)
+            if self.standard:
+                loss = ops.sgns_standard(rows_in.float(), rows_out.float(), plan_in.pos.contiguous(), pos_o, pos_neg,
+                                         c.negatives, lr, d_in, d_out, with_loss=with_loss)
+            else:
+                loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
+                                     c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
+                                     neg_k=c.shared_negatives, neg_group=c.neg_group)
         self.ps_in.push(plan_in, d_in)
         self.ps_out.push(plan_out, d_out)
         self.pairs_seen += P

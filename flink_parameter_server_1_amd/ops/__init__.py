@@ -709,6 +709,36 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
                                      neg_group)])
 
 
+def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d_in, d_out,
+                  with_loss: bool = False):
+    """Standard skip-gram negative sampling (K6, ``kernels/sgns_std.hip``): ``k``
+    independent negatives per pair (``pos_neg[P * k]``), word2vec's objective.
+    ``d_in`` / ``d_out`` receive the deltas (the tables themselves on the local
+    path).  Returns the summed loss (a device / host 1-element tensor) or None.
+    GPU: one wave per 16 pairs, sequential inside a wave's center runs, Hogwild
+    float atomics across waves; CPU: the mini-batch form."""
+    P = pos_c.numel()
+    D = rows_in.shape[1]
+    if pos_neg.numel() != P * k:
+        raise ValueError("sgns_standard: pos_neg needs k rows per pair")
+    if rows_in.is_cuda:
+        for t in (rows_in, rows_out, d_in, d_out):
+            if t.dtype != torch.float32:
+                raise ValueError("sgns_standard: fp32 rows and deltas")
+        if D > 512:
+            raise ValueError("sgns_standard: D <= 512")
+        loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
+        N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
+                                              _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
+                                              _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss),
+                                              N.stream_ptr(rows_in.device)), "sgns_standard")
+        return loss
+    # CPU: the mini-batch form (every pair reads the rows as of the call); the
+    # kernel's exact per-wave order is ``reference.sgns_standard`` (numerics tests)
+    total = R.sgns_standard_batched(rows_in, rows_out, pos_c, pos_o, pos_neg, int(k), lr, d_in, d_out)
+    return torch.tensor([total]) if with_loss else None
+
+
 TOPK_MAX_K = 256
 
 

@@ -464,3 +464,62 @@ def ht_rehash(rowkey, count, tab, rowmap):
             h = (h + 1) & mask
         tb[h] = (1 << 32) | (k & M32)
         rm[h] = r
+
+
+SGNS_STD_CHUNK = 16  # pairs per wave in kernels/sgns_std.hip
+
+
+def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out):
+    """CPU twin of ``fps_sgns_standard`` (sequential; center runs restart at every
+    chunk of ``SGNS_STD_CHUNK`` pairs like the kernel's waves).  Returns the loss."""
+    import math
+
+    P = pos_c.numel()
+    D = rows_in.shape[1]
+    pc, po = pos_c.tolist(), pos_o.tolist()
+    pn = pos_neg.reshape(P, k).tolist() if k else [[] for _ in range(P)]
+    total = 0.0
+    for s0 in range(0, P, SGNS_STD_CHUNK):
+        cur, h, h0 = -1, None, None
+        for p in range(s0, min(P, s0 + SGNS_STD_CHUNK)):
+            c = pc[p]
+            if c != cur:
+                if cur >= 0:
+                    d_in[cur] += (h - h0).to(d_in.dtype)
+                cur = c
+                h = rows_in[c].double().clone()
+                h0 = h.clone()
+            o = po[p]
+            dh = torch.zeros(D, dtype=torch.float64)
+            for x, lab in [(o, 1.0)] + [(n, 0.0) for n in pn[p] if n != o]:
+                xv = rows_out[x].double()
+                s = float(h @ xv)
+                g = lr * (lab - 1.0 / (1.0 + math.exp(-s)))
+                total += math.log1p(math.exp(-s)) if lab > 0 else math.log1p(math.exp(s))
+                d_out[x] += (g * h).to(d_out.dtype)
+                dh += g * xv
+            h = h + dh
+        if cur >= 0:
+            d_in[cur] += (h - h0).to(d_in.dtype)
+    return total
+
+
+def sgns_standard_batched(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out):
+    """Mini-batch form of standard SGNS for CPU runs: every pair of the call reads
+    the rows as they were before the call (the PS path's snapshot semantics),
+    deltas are summed per row.  Returns the loss."""
+    P = pos_c.numel()
+    c, o = pos_c.long(), pos_o.long()
+    x = torch.cat([o.view(P, 1), pos_neg.long().view(P, k)], 1) if k else o.view(P, 1)
+    h = rows_in[c].double()
+    X = rows_out[x].double()                                   # [P, 1+k, D]
+    s = torch.einsum("pd,pjd->pj", h, X)
+    lab = torch.zeros_like(s)
+    lab[:, 0] = 1.0
+    keep = torch.ones_like(s, dtype=torch.bool)
+    keep[:, 1:] = x[:, 1:] != o.view(P, 1)                     # word2vec skips a negative equal to the target
+    g = lr * (lab - torch.sigmoid(s)) * keep
+    loss = torch.where(lab > 0, torch.nn.functional.softplus(-s), torch.nn.functional.softplus(s))[keep].sum()
+    d_out.index_add_(0, x.reshape(-1), (g.unsqueeze(2) * h.unsqueeze(1)).reshape(-1, h.shape[1]).to(d_out.dtype))
+    d_in.index_add_(0, c, torch.einsum("pj,pjd->pd", g, X).to(d_in.dtype))
+    return float(loss)

@@ -147,3 +147,90 @@ def test_sgns_local_direct_matches_ps_path_on_one_rank():
     seen = set(c[:4096].tolist()) | set(o[:4096].tolist())
     assert seen <= res[True][2] and seen <= res[False][2]
     assert len(res[True][2] ^ res[False][2]) <= 0.01 * len(res[False][2])
+
+
+# ----------------------------------------------------------- standard SGNS
+def test_sgns_standard_loop_equals_batched_without_shared_rows():
+    """No center runs, no row shared between pairs: the kernel's sequential order
+    (reference.sgns_standard) and the CPU mini-batch form agree."""
+    torch.manual_seed(0)
+    P, k, D = 40, 5, 12
+    rows_in, rows_out = torch.randn(P, D) * 0.3, torch.randn(P * (k + 1), D) * 0.3
+    pos_c = torch.arange(P, dtype=torch.int32)
+    perm = torch.randperm(P * (k + 1)).to(torch.int32)
+    pos_o, pos_neg = perm[:P], perm[P:]
+    outs = []
+    for fn in (R.sgns_standard, R.sgns_standard_batched):
+        d_in, d_out = torch.zeros(P, D), torch.zeros(P * (k + 1), D)
+        loss = fn(rows_in, rows_out, pos_c, pos_o, pos_neg, k, 0.05, d_in, d_out)
+        outs.append((d_in, d_out, loss))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-7)
+    assert abs(outs[0][2] - outs[1][2]) < 1e-6 * outs[1][2]
+
+
+def test_sgns_standard_skips_negative_equal_to_context():
+    rows_in, rows_out = torch.ones(1, 4), torch.ones(3, 4) * 0.1
+    d_in, d_out = torch.zeros(1, 4), torch.zeros(3, 4)
+    R.sgns_standard_batched(rows_in, rows_out, torch.tensor([0]), torch.tensor([1]), torch.tensor([1, 2]), 2, 0.1,
+                            d_in, d_out)
+    g_o = 0.1 * (1 - torch.sigmoid(torch.tensor(0.4)))
+    torch.testing.assert_close(d_out[1], g_o * torch.ones(4))  # only the positive update on row 1
+
+
+@pytest.mark.parametrize("mode", ["standard", "shared"])
+def test_sgns_modes_learn_on_cpu(mode):
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=2000, dim=16, window=3, learning_rate=0.025, mode=mode))
+    toks = synthetic_corpus(40000, 2000, n_topics=10, seed=1)
+    c, o = skipgram_pairs(toks, 3, torch.Generator().manual_seed(0))
+    first = m.step(c[:2048], o[:2048], with_loss=True)
+    for s in range(0, c.numel() - 1024, 1024):
+        m.step(c[s:s + 1024], o[s:s + 1024])
+    assert m.step(c[:2048], o[:2048], with_loss=True) < 0.8 * first
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [16, 64, 100, 300])
+@pytest.mark.parametrize("runs", [False, True])
+@pytest.mark.parametrize("k", [1, 5, 7])
+def test_sgns_standard_kernel_matches_reference(D, runs, k):
+    """PS-path form (rows read-only, separate delta buffers): the kernel equals the
+    sequential reference, center runs included (float-atomic order aside)."""
+    torch.manual_seed(D + k)
+    Uin, Uout, P = 300, 400, 3000
+    rows_in = torch.randn(Uin, D) * 0.3
+    rows_out = torch.randn(Uout, D) * 0.3
+    pos_c = torch.randint(0, Uin, (P,), dtype=torch.int32)
+    if runs:  # center-major: runs of equal centers, sequential inside a wave's chunk
+        pos_c = torch.sort(torch.randint(0, 60, (P,), dtype=torch.int32)).values
+    pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
+    pos_neg = torch.randint(0, Uout, (P * k,), dtype=torch.int32)
+    d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
+    loss_r = R.sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r)
+    dev = "cuda"
+    d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
+    loss = ops.sgns_standard(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k,
+                             0.05, d_in, d_out, with_loss=True)
+    torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=5e-6)
+    torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=5e-6)
+    assert abs(float(loss) - loss_r) / loss_r < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["standard", "shared"])
+def test_sgns_gpu_modes_reduce_loss(mode):
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=20000, dim=300, window=4, learning_rate=0.01, mode=mode),
+                        comm=Comm(device=torch.device("cuda")))
+    toks = synthetic_corpus(400000, 20000, n_topics=50, seed=1, device="cuda")
+    c, o = skipgram_pairs(toks, 4)
+    first = m.step(c[:8192], o[:8192], with_loss=True)
+    for s in range(0, c.numel() - 8192, 8192):
+        m.step(c[s:s + 8192], o[s:s + 8192])
+    assert m.step(c[:8192], o[:8192], with_loss=True) < 0.8 * first
