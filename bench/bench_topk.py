@@ -38,6 +38,9 @@ def main(argv=None):
     ap.add_argument("--bucket", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--strategy", default="length",
+                    help="LEMP pruning applied per 32-item block on the device: length | coord | lc:T | li:N:T | "
+                         "incr:N (LEMPPruningStrategy.fromString syntax; li / incr run the length bound)")
     a = ap.parse_args(argv)
 
     import torch
@@ -53,7 +56,10 @@ def main(argv=None):
     ids = comm.rank + comm.world * torch.arange(n_local, device=dev)
     scale = torch.rand(n_local, 1, generator=g, device=dev) ** 4  # long-tailed vector lengths
     vecs = torch.randn(n_local, a.dim, generator=g, device=dev) * scale
-    topk = DistributedTopK(ids, vecs, comm, bucket_size=a.bucket)
+    from flink_parameter_server_1_amd.models.mf.pruning import LEMPPruningStrategy
+
+    strategy = LEMPPruningStrategy.from_string(a.strategy)
+    topk = DistributedTopK(ids, vecs, comm, bucket_size=a.bucket, strategy=strategy)
     gq = torch.Generator(device=dev)
     gq.manual_seed(5)  # same query batch on every rank (broadcast users)
     queries = [torch.randn(a.queries, a.dim, generator=gq, device=dev) for _ in range(4)]
@@ -89,7 +95,10 @@ def main(argv=None):
             "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong", "dtype": "fp32", "scorer": _scorer(),
             "data": "synthetic long-tailed item factors, random queries",
             "buckets_scanned_per_query_batch": scanned, "buckets_per_shard": n_buckets, "exact_vs_brute_force": exact,
-            "config": {"items": a.items, "dim": a.dim, "k": a.k, "query_batch": a.queries, "bucket": a.bucket},
+            "coord_block_pairs_scored_skipped": topk.local.coord_stats.tolist()
+            if topk.local.coord_stats is not None else None,
+            "config": {"items": a.items, "dim": a.dim, "k": a.k, "query_batch": a.queries, "bucket": a.bucket,
+                       "strategy": a.strategy},
         }), flush=True)
 
 

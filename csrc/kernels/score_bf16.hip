@@ -49,13 +49,39 @@ __device__ __forceinline__ uint32_t sb_key(float f) {  // order-preserving float
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// LEMP COORD bound of one (query, 32-item block) pair (M/matrix/factorization/
+// pruning/LEMPPruningFunctions.scala:36-49 with the block's longest item as the
+// bucket head): an item x can beat theta > 0 only if its normalised focus
+// coordinate x_f / |x| lies in [lf, uf]; cb holds the min / max of x_c / |x| over
+// the block's items for every coordinate c, so the block is skipped when that range
+// misses [lf, uf] (widened by kCoordSlack for fp32 rounding) -- exact.
+constexpr float kCoordSlack = 1e-4f;
+
+__device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, float qbf, float2 mm) {
+  if (!(theta > 0.f) || !(ql > 0.f)) return true;  // no positive k-th best yet: nothing pruned
+  if (!(bm > 0.f)) return false;                   // zero-length block: every score is 0 < theta
+  const float tbq = fminf(theta / (bm * ql), 1.f);
+  const float a = qbf * tbq;
+  const float b = sqrtf(fmaxf((1.f - tbq * tbq) * (1.f - qbf * qbf), 0.f));
+  const float lfp = a - b, ufp = a + b;
+  const float ratio = qbf != 0.f ? tbq / qbf : INFINITY;
+  const float lf = (qbf >= 0.f || lfp > ratio) ? lfp : -1.f;
+  const float uf = (qbf <= 0.f || ufp < ratio) ? ufp : 1.f;
+  return !(mm.y < lf - kCoordSlack || mm.x > uf + kCoordSlack);
+}
+
 // QB 32-query blocks per wave; a workgroup covers SB_WAVES * QB * 32 queries x
-// SB_ITEMS items.
-template <int D, int QB, bool MASK = false>
+// SB_ITEMS items.  COORD: the LEMP coordinate bound per (32-query block, 32-item
+// block) before the MFMAs (qf / qbf: each query's focus coordinate argmax q_c^2 and
+// q_f / |q|; cb: [N / 32][D] coordinate ranges); stats[0] / [1] count the (query
+// block, item block) pairs scored / skipped.
+template <int D, int QB, bool MASK = false, bool COORD = false>
 __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
-    float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap) {
+    float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
+    const int32_t* __restrict__ qf, const float* __restrict__ qbf, const float2* __restrict__ cb,
+    int32_t* __restrict__ stats) {
   constexpr int S = D / 16;   // k-steps of 16; also 16-B loads per lane per row
   constexpr int HALF = D / 2;
   constexpr int WQ = 32 * QB;
@@ -85,6 +111,8 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
   float theta[QB], ql[QB];
   int qrow[QB];
   uint4 qv[QB][S];
+  int fq[QB];
+  float qb[QB];
   int live = 0;
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
@@ -92,10 +120,16 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     qrow[b] = q;
     theta[b] = INFINITY;  // rows past B never pass
     ql[b] = 0.f;
+    fq[b] = 0;
+    qb[b] = 0.f;
     if (q < B) {
       theta[b] = best_s[(int64_t)q * k + k - 1];
       ql[b] = qlen[q];
       live |= !(theta[b] > -INFINITY && ql[b] * xm * slack <= theta[b]);
+      if (COORD) {
+        fq[b] = qf[q];
+        qb[b] = qbf[q];
+      }
     }
   }
   if (!__syncthreads_or(live)) return;  // uniform
@@ -115,6 +149,7 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
   int lc[QB];
 #pragma unroll
   for (int b = 0; b < QB; ++b) lc[b] = 0;
+  int scored = 0, skipped = 0;
   // software pipeline: block i0 + 32 is requested before block i0's MFMAs
   uint4 xv[S];
   float xl;
@@ -141,6 +176,15 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     }
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
+      if (COORD) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
+        bool pass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
+        if (pass) pass = coord_pass(theta[b], ql[b], bm, qb[b], cb[(int64_t)(i0 / 32) * D + fq[b]]);
+        if (!__any(pass)) {  // wave-uniform
+          ++skipped;
+          continue;
+        }
+        ++scored;
+      }
       floatx16 acc = {0};
 #pragma unroll
       for (int s = 0; s < S; ++s)
@@ -186,6 +230,10 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
         }
       }
     }
+  }
+  if (COORD && stats != nullptr && lane == 0) {
+    atomicAdd(stats, scored);
+    atomicAdd(stats + 1, skipped);
   }
   // flush: both lane halves hold the same query; half 0 reserves for the pair
 #pragma unroll
@@ -257,19 +305,30 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
 // Qb [B, D], Xb [N, D] bf16 (uint16 storage, RNE from the fp32 vectors); qlen [B],
 // xlen [N] the fp32 norms; cand_pos [B, cap] int64 receives item positions (0..N-1),
 // cnt [B] (zeroed by the caller) counts every candidate.  D in {32, 64, 128}.
+// COORD bound (optional, all or none): qf [B] focus coordinates, qbf [B] = q_f / |q|,
+// cb [N / 32][D] float2 coordinate ranges of the 32-item blocks (N a multiple of 32
+// or the last block's range over its items); stats (optional) = 2 counters.
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xlen, float margin, float slack,
-                                  int64_t* cand_pos, int32_t* cnt, int cap, void* stream) {
+                                  int64_t* cand_pos, int32_t* cnt, int cap, const int32_t* qf, const float* qbf,
+                                  const float2* cb, int32_t* stats, void* stream) {
   if (B <= 0 || N <= 0) return 0;
   if (k <= 0 || cap <= 0 || qlen == nullptr || xlen == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nit = (N + SB_ITEMS - 1) / SB_ITEMS;
-#define FPS_SB(D_, QB_, ...)                                                                                \
+  const bool coord = qf != nullptr && qbf != nullptr && cb != nullptr;
+#define FPS_SB(D_, QB_, MASK_)                                                                              \
   {                                                                                                         \
     const int64_t nqt = (B + SB_WAVES * 32 * QB_ - 1) / (SB_WAVES * 32 * QB_);                              \
     if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
-    hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, ##__VA_ARGS__>), dim3((unsigned)(nqt * nit)), dim3(256), 0, s, Qb, \
-                       Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, cap);                 \
+    if (coord)                                                                                              \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true>), dim3((unsigned)(nqt * nit)),    \
+                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
+                         cap, qf, qbf, cb, stats);                                                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false>), dim3((unsigned)(nqt * nit)),   \
+                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
+                         cap, qf, qbf, cb, stats);                                                          \
   }
   // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4
   // blocks with branch or mask epilogues, same-box A/B, profiles/r2_bf16_topk.md)

@@ -34,7 +34,13 @@ from ... import ops
 
 
 class LempTopK:
-    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536):
+    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536, strategy=None):
+        """``strategy`` (a ``pruning`` LEMP strategy; None = LENGTH): the bounds the
+        device scan applies per block of 32 items before scoring.  LENGTH (and LI /
+        INCR, whose incremental per-candidate bound has no work to skip on MFMA
+        tiles): the length bound; COORD (and LC on buckets whose length spread is
+        below its switch threshold): the length and the focus-coordinate bounds.
+        Every bound is exact, so the top-K equals the unpruned scan's."""
         vecs = item_vecs.float().contiguous()
         lengths = torch.linalg.vector_norm(vecs, dim=1)
         order = torch.argsort(lengths, descending=True)
@@ -66,6 +72,11 @@ class LempTopK:
         self.bf16 = (vecs.is_cuda and vecs.shape[1] in ops.BF16_SCORE_DIMS
                      and os.environ.get("FPS_TOPK_BF16", "1") != "0")
         self.vecs_bf = self.vecs.bfloat16() if self.bf16 else None
+        self.strategy = strategy
+        self._cb = None          # LEMP COORD: per-32-item-block coordinate ranges (lazy)
+        self._len_host = None    # lengths on the host (LC's per-bucket switch)
+        #: (32 queries, 32 items) block pairs the COORD scans scored / skipped
+        self.coord_stats = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -77,6 +88,7 @@ class LempTopK:
             self.vecs_bf[pos] = v.bfloat16()
         self.lengths[pos] = torch.linalg.vector_norm(v, dim=1)
         self._suffix = False  # the order is stale: bounds take the max of the tail
+        self._cb = self._len_host = None
 
     def _bound(self, s: int) -> torch.Tensor:
         """max |x| over index positions >= s (a 0-dim tensor)."""
@@ -84,26 +96,34 @@ class LempTopK:
             return self.lengths[s]
         return self.lengths[s:].max()
 
-    def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None):
+    def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None, start: int = 0,
+              state=None):
         """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
-        use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering."""
+        use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering.  ``start`` /
+        ``state = (best_s, best_i)``: continue a scan whose items ``[0, start)`` are
+        already merged into ``state``."""
         Q = Q.float().contiguous()
         B = Q.shape[0]
         dev = Q.device
         qlen = torch.linalg.vector_norm(Q, dim=1)
         N = self.vecs.shape[0]
         fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
-        if fused and self.sync_free and N > self.seed_items:
-            res = self._query_fused(Q, qlen, k)
+        if fused and self.sync_free and N > max(self.seed_items, start):
+            res = self._query_fused(Q, qlen, k, start, None if state is None else (state[0].clone(),
+                                                                                    state[1].clone()))
             if res is not None:
                 return res
             self.overflows += 1  # some query passed more than cap scores: rescan unfused
             fused = False
-        best_s = torch.full((B, k), float("-inf"), device=dev)
-        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+        if state is None:
+            best_s = torch.full((B, k), float("-inf"), device=dev)
+            best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+        else:
+            best_s, best_i = state[0].clone(), state[1].clone()
         # segments: the first ``seed_items`` (longest) items, then the rest of each bucket
-        seed = min(N, self.seed_items) if fused else 0
-        bounds = sorted({0, seed, *range(self.bucket, N, self.bucket), N} - {N}) + [N]
+        seed = min(N, start + self.seed_items) if fused else start
+        bounds = sorted({start, seed, *range(self.bucket, N, self.bucket), N} - {N}) + [N]
+        bounds = [b for b in bounds if b >= start]
         S = None
         cand = None
         for s, e in zip(bounds[:-1], bounds[1:]):
@@ -113,7 +133,7 @@ class LempTopK:
             n = e - s
             if s % self.bucket == 0:
                 self.buckets_scanned += 1
-            if fused and s > 0:
+            if fused and s > start:
                 # scoring fused with the k-th-best filter: only the few passing scores
                 # leave the kernel (no [B, n] score matrix)
                 if cand is None:
@@ -140,26 +160,35 @@ class LempTopK:
                 best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
         return best_s, best_i
 
-    def _query_fused(self, Q, qlen, k):
+    def _query_fused(self, Q, qlen, k, start: int = 0, state=None):
         """GPU scan without a host sync per segment: seed segment scored + merged,
         then per segment the fused 128 x 128 scorer (tiles that cannot beat any of
         their queries' k-th best skip themselves) and the candidate merge, which
         flags overflowing rows on the device.  One sync per ``break_check``
-        segments (early exit) and one at the end (overflow -> ``None``: rescan)."""
+        segments (early exit) and one at the end (overflow -> ``None``: rescan).
+        ``start`` / ``state``: continue from a partial scan (the seed segment then
+        runs from ``start`` to the next 32-item boundary, or is skipped)."""
         B, dev = Q.shape[0], Q.device
         N = self.vecs.shape[0]
-        best_s = torch.full((B, k), float("-inf"), device=dev)
-        best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
-        seed = self.seed_items
-        S = ops.score_gemm(Q, self.vecs[:seed])
-        ops.topk_merge(S, self.ids[:seed], best_s, best_i)
-        del S
-        self.buckets_scanned += 1
+        if state is None:
+            best_s = torch.full((B, k), float("-inf"), device=dev)
+            best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
+            seed = self.seed_items
+        else:
+            best_s, best_i = state
+            seed = min(N, -(-start // 32) * 32)  # fused segments start on 32-item blocks
+        if seed > start:
+            S = ops.score_gemm(Q, self.vecs[start:seed])
+            ops.topk_merge(S, self.ids[start:seed], best_s, best_i)
+            del S
+            self.buckets_scanned += 1
+        if seed >= N:
+            return best_s, best_i
         # segments grow geometrically up to the bucket size: a segment of n items after
         # s scanned ones passes ~k ln(1 + n / s) scores per query, so doubling keeps
         # every merge on the small rank path (one 4096 -> 65536 step passed ~1100)
-        cuts = {*range(self.bucket, N, self.bucket)}
-        c = seed if self.geometric else N
+        cuts = {seed, *(b for b in range(self.bucket, N, self.bucket) if b > seed)}
+        c = max(seed, self.seed_items) if self.geometric else N
         while c < min(N, self.bucket):
             cuts.add(c)
             c *= 2
@@ -170,6 +199,7 @@ class LempTopK:
         cnt = torch.empty(B, dtype=torch.int32, device=dev)
         ovf = torch.zeros(1, dtype=torch.int32, device=dev)
         Qb = Q.bfloat16() if self.bf16 else None
+        coord = self._coord_inputs(Q, qlen, bounds) if self.bf16 else None
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
@@ -178,7 +208,12 @@ class LempTopK:
                 self.buckets_scanned += 1
             cnt.zero_()
             if self.bf16:
-                ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e])
+                seg_coord = None
+                if coord is not None and self._coord_segment(s, e):
+                    qf, qbf = coord
+                    seg_coord = (qf, qbf, self._cb[s // 32: -(-e // 32)])
+                ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e],
+                                      coord=seg_coord, stats=self.coord_stats if seg_coord is not None else None)
                 # (re-score fused into the rank merge, one query per workgroup: 59 us against
                 # 22 + 27 us for the two kernels -- profiles/r2_bf16_topk.md)
                 ops.cand_rescore(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt)
@@ -189,6 +224,32 @@ class LempTopK:
         if int(ovf.item()):
             return None
         return best_s, best_i
+
+
+    def _coord_inputs(self, Q, qlen, bounds):
+        """``(focus coordinate int32[B], q_f / |q|)`` when the strategy uses COORD
+        on some segment (segments start on 32-item blocks), else None."""
+        from .pruning import COORD, LC
+
+        if not isinstance(self.strategy, (COORD, LC)) or any(b % 32 for b in bounds[:-1]):
+            return None
+        if self._cb is None:
+            self._cb = ops.coord_block_bounds(self.vecs, self.lengths)
+        f = torch.argmax(Q * Q, dim=1)
+        qbf = Q.gather(1, f.view(-1, 1)).view(-1) / qlen.clamp_min(1e-30)
+        return f.to(torch.int32).contiguous(), qbf.contiguous()
+
+    def _coord_segment(self, s: int, e: int) -> bool:
+        """COORD on this segment?  LC switches to LENGTH where the segment's lengths
+        spread more than its threshold (``head > last * t``, the reference's choice
+        per bucket, ``M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:82-96``)."""
+        from .pruning import LC
+
+        if not isinstance(self.strategy, LC):
+            return True
+        if self._len_host is None:
+            self._len_host = self.lengths.cpu()
+        return not (float(self._len_host[s]) > float(self._len_host[e - 1]) * self.strategy.algorithm_switch_threshold)
 
 
 def merge_top_k(scores: torch.Tensor, ids: torch.Tensor, k: int, exclude_ids: Optional[torch.Tensor] = None):
@@ -206,11 +267,12 @@ def merge_top_k(scores: torch.Tensor, ids: torch.Tensor, k: int, exclude_ids: Op
 class DistributedTopK:
     """Item shards per rank, broadcast queries, all-gather + merge."""
 
-    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, comm=None, bucket_size: int = 65536):
+    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, comm=None, bucket_size: int = 65536,
+                 strategy=None):
         from ...parallel.comm import Comm
 
         self.comm = comm or Comm()
-        self.local = LempTopK(item_ids, item_vecs, bucket_size)
+        self.local = LempTopK(item_ids, item_vecs, bucket_size, strategy=strategy)
 
     def query(self, Q: torch.Tensor, K: int, worker_k: Optional[int] = None,
               exclude_ids: Optional[torch.Tensor] = None):

@@ -227,11 +227,28 @@ def lemp_candidate_mask(Q: torch.Tensor, qlen: torch.Tensor, theta: torch.Tensor
 
 
 class PrunedLempTopK(LempTopK):
-    """``LempTopK`` whose buckets are filtered by a LEMP strategy's candidate mask
-    before the merge (statistics in ``pruned`` / ``scored``)."""
+    """LEMP top-K with a pruning strategy (``M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:35-114``).
+
+    The reference prunes with ``theta = 0`` until a query holds ``workerK``
+    candidates (``if (topK.length < K) 0.0 else topK.head._1``), which can drop
+    negative-score items; once every query's k-th best is positive its bounds are
+    exact.  So the scan runs the reference's bucket loop with the strategy's masks
+    (torch, one host check per bucket) only until every query's k-th best is
+    positive -- the first bucket on real data -- and continues with the device scan
+    (``LempTopK(strategy=...)``): the length bound and, for COORD / LC, the
+    focus-coordinate bound per block of 32 items inside the bf16 scorer, no host
+    sync per bucket.  ``reference_quirks`` (inexact LENGTH / INCR bounds, SURVEY
+    B6 / B7) keeps the mask loop for the whole scan (bit parity only).  ``pruned``
+    / ``scored`` count the mask loop's candidates, ``coord_stats`` the device
+    scan's (32 x 32) block pairs."""
+
+    #: device scan segments (the reference's ``bucketSize`` is an algorithmic knob of
+    #: its per-item loop; on MFMA tiles it only sizes the launches)
+    DEVICE_BUCKET = 65536
 
     def __init__(self, item_ids, item_vecs, bucket_size: int = 4096, strategy=None, reference_quirks=False):
-        super().__init__(item_ids, item_vecs, bucket_size)
+        super().__init__(item_ids, item_vecs, max(bucket_size, self.DEVICE_BUCKET), strategy=strategy)
+        self.ref_bucket = int(bucket_size)
         self.strategy, self.quirks = strategy, reference_quirks
         self.pruned = 0
         self.scored = 0
@@ -240,17 +257,27 @@ class PrunedLempTopK(LempTopK):
         if self.strategy is None:
             return super().query(Q, k)
         Q = Q.float().contiguous()
+        best_s, best_i, s0 = self._mask_scan(Q, k, settle=not self.quirks)
+        if s0 < self.vecs.shape[0]:
+            best_s, best_i = super().query(Q, k, start=s0, state=(best_s, best_i))
+        best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
+        return best_s, best_i
+
+    def _mask_scan(self, Q: torch.Tensor, k: int, settle: bool):
+        """The reference's bucket loop with the strategy's masks; with ``settle`` it
+        stops after the first bucket that leaves every query's k-th best positive.
+        Returns ``(best_s, best_i, next item position)``."""
         B, dev = Q.shape[0], Q.device
         qlen = torch.linalg.vector_norm(Q, dim=1)
         best_s = torch.full((B, k), float("-inf"), device=dev)
         best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
         N = self.vecs.shape[0]
-        for s in range(0, N, self.bucket):
-            e = min(N, s + self.bucket)
+        for s in range(0, N, self.ref_bucket):
+            e = min(N, s + self.ref_bucket)
             theta = _theta(best_s)
             full = torch.isfinite(best_s[:, -1])
             if s > 0 and bool((full & (qlen * self.lengths[s] <= theta)).all()):
-                break
+                return best_s, best_i, N
             self.buckets_scanned += 1
             X, xl = self.vecs[s:e], self.lengths[s:e]
             S = ops.score_gemm(Q, X) if dev.type == "cuda" else Q @ X.t()
@@ -268,8 +295,9 @@ class PrunedLempTopK(LempTopK):
                 ts, tj = torch.topk(cs, min(k, cs.shape[1]), dim=1)
                 ci = torch.cat([best_i, self.ids[s:e].expand(B, e - s)], 1)
                 best_s, best_i = ts, torch.gather(ci, 1, tj)
-        best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
-        return best_s, best_i
+            if settle and bool((best_s[:, -1] > 0).all()):
+                return best_s, best_i, e
+        return best_s, best_i, N
 
 
 # ------------------------------------------------------------------ merging

@@ -817,13 +817,31 @@ def bf16_score_margin(D: int) -> float:
     return (2 * u + u * u + 2 * D * 2.0 ** -24) * 1.001
 
 
+def coord_block_bounds(X: torch.Tensor, xlen: torch.Tensor) -> torch.Tensor:
+    """``[ceil(n / 32), D, 2]`` min / max of the normalised coordinates ``x_c / |x|``
+    over every block of 32 consecutive items (the last block over its own items):
+    the per-block table of the LEMP COORD bound in ``score_filter_bf16``."""
+    n, D = X.shape
+    xn = X.float() / xlen.float().clamp_min(1e-30).view(-1, 1)
+    nb = -(-n // 32)
+    pad = nb * 32 - n
+    if pad:
+        xn = torch.cat([xn, xn[-1:].expand(pad, D)], 0)
+    xn = xn.view(nb, 32, D)
+    return torch.stack([xn.amin(1), xn.amax(1)], 2).contiguous()
+
+
 def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, cand_pos: torch.Tensor,
-                      cnt: torch.Tensor, qlen: torch.Tensor, xlen: torch.Tensor) -> None:
+                      cnt: torch.Tensor, qlen: torch.Tensor, xlen: torch.Tensor, coord=None,
+                      stats: Optional[torch.Tensor] = None) -> None:
     """Candidate filter on bf16 MFMA (GPU only, K8 fast path): every item ``i`` whose bf16
     score can exceed ``best_s[b, -1]`` (margin ``bf16_score_margin(D) |q_b| max|x|``) gets
     its position appended to row ``b`` of ``cand_pos`` ``[B, cap]`` (int64); ``cnt[b]``
     (zeroed by the caller) counts them all.  ``cand_rescore`` turns the list into exact
-    (key, id) candidates for ``topk_merge_cand``."""
+    (key, id) candidates for ``topk_merge_cand``.  ``coord = (qf int32[B], qbf[B], cb)``
+    turns on the LEMP COORD + length bounds per (32 queries, 32 items) block pair
+    (``cb`` = ``coord_block_bounds`` of these items); ``stats`` (int32[2]) counts the
+    block pairs scored / skipped."""
     B, D = Qb.shape
     n = Xb.shape[0]
     cap = cand_pos.shape[1]
@@ -832,11 +850,20 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     if best_s.shape[0] != B or cnt.numel() != B or cand_pos.dtype != torch.int64 or qlen.numel() != B \
             or xlen.numel() != n:
         raise ValueError("score_filter_bf16: shape mismatch")
+    qf = qbf = cb = None
+    if coord is not None:
+        qf, qbf, cb = coord
+        if qf.dtype != torch.int32 or qf.numel() != B or qbf.numel() != B or tuple(cb.shape) != (-(-n // 32), D, 2):
+            raise ValueError("score_filter_bf16: coord = (int32 qf[B], qbf[B], cb[ceil(n/32), D, 2])")
+        if DEBUG:
+            check_index(qf, D, "score_filter_bf16 qf")
+        qf, qbf, cb = _c(qf), _c(qbf.float()), _c(cb.float())
     slack = 1.0 + 1e-4 + D * 2.4e-7
     N.check(N.require().fps_score_filter_bf16(
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
         _c(qlen.float()).data_ptr(), _c(xlen.float()).data_ptr(), bf16_score_margin(D), slack,
-        _c(cand_pos).data_ptr(), _c(cnt).data_ptr(), cap, N.stream_ptr(Qb.device)), "score_filter_bf16")
+        _c(cand_pos).data_ptr(), _c(cnt).data_ptr(), cap, N.ptr(qf), N.ptr(qbf), N.ptr(cb), N.ptr(stats),
+        N.stream_ptr(Qb.device)), "score_filter_bf16")
 
 
 def cand_rescore(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, cand_key: torch.Tensor,

@@ -160,3 +160,54 @@ def test_bf16_filter_tight_margin_worst_case():
     ck, ci, raw, ids = _run_filter(Q, X, theta)
     assert int(raw.min()) == n
     _check_exact(Q, X, theta, ck, ci, raw, ids)
+
+
+@pytest.mark.parametrize("strategy", ["coord", "lc:1.05", "li:3:1.05", "length"])
+def test_lemp_device_coord_bound_exact_and_skips(strategy):
+    """LEMP COORD per (32 queries, 32 items) block inside the bf16 scorer: on
+    axis-dominated items (each item mostly one coordinate) the bound skips block
+    pairs, and the top-K still equals brute force (the bound is exact)."""
+    from flink_parameter_server_1_amd.models.mf.pruning import LEMPPruningStrategy
+    from flink_parameter_server_1_amd.models.mf.topk_fast import LempTopK
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    N, D, B, k = 200_000, 64, 512, 50
+    axis = torch.randint(0, D, (N,), generator=g, device="cuda")
+    X = torch.randn(N, D, generator=g, device="cuda") * 0.05
+    X[torch.arange(N, device="cuda"), axis] += 1.0
+    X *= torch.rand(N, 1, generator=g, device="cuda") ** 2 + 0.05
+    qa = torch.randint(0, D, (B,), generator=g, device="cuda")
+    Q = torch.randn(B, D, generator=g, device="cuda") * 0.05
+    Q[torch.arange(B, device="cuda"), qa] += 1.0
+    ids = torch.arange(N, device="cuda") * 3 + 1
+    idx = LempTopK(ids, X, 65536, strategy=LEMPPruningStrategy.from_string(strategy))
+    s, i = idx.query(Q, k)
+    ref = torch.topk(Q @ X.t(), k, dim=1)
+    torch.testing.assert_close(s, ref.values, rtol=1e-5, atol=1e-5)
+    assert torch.equal(i, ids[ref.indices])
+    scored, skipped = idx.coord_stats.tolist()
+    if strategy in ("coord", "lc:1.05"):
+        assert skipped > 0 and scored > 0, (scored, skipped)
+    else:
+        assert scored == 0 and skipped == 0
+
+
+@pytest.mark.parametrize("strategy", ["coord", "lc:1.2", "li:3:1.2", "incr:3", "length"])
+def test_pruned_lemp_gpu_equals_reference_semantics(strategy):
+    """PrunedLempTopK (reference theta = 0 prefix, then the device scan) == the mask
+    loop over the whole scan (the reference's semantics, exact strategies)."""
+    from flink_parameter_server_1_amd.models.mf.pruning import LEMPPruningStrategy
+    from flink_parameter_server_1_amd.models.mf.topk_tensor import PrunedLempTopK
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    N, D, B, k = 30_000, 64, 256, 20
+    X = torch.randn(N, D, generator=g, device="cuda") * torch.rand(N, 1, generator=g, device="cuda") ** 3
+    Q = torch.randn(B, D, generator=g, device="cuda")
+    ids = torch.arange(N, device="cuda")
+    st = LEMPPruningStrategy.from_string(strategy)
+    a = PrunedLempTopK(ids, X, 100, st)
+    sa, ia = a.query(Q, k)
+    b = PrunedLempTopK(ids, X, 100, st)
+    sb, ib, _ = b._mask_scan(Q.float().contiguous(), k, settle=False)
+    torch.testing.assert_close(sa, sb, rtol=0, atol=0)
+    assert torch.equal(ia, ib)

@@ -31,8 +31,37 @@ def test_pruned_lemp_is_exact(strategy):
     ts, tj = torch.topk(S, k, dim=1)
     torch.testing.assert_close(s, ts, rtol=1e-5, atol=1e-5)
     assert torch.equal(i, ids[tj])
-    if strategy is not None:
-        assert idx.pruned > 0  # the masks did skip candidates
+
+
+@pytest.mark.parametrize("strategy", [LENGTH(), COORD(), INCR(3), LC(1.3), LI(3, 1.3)])
+def test_lemp_masks_keep_every_top_k_item_and_prune(strategy):
+    """The strategies' candidate masks (LEMPPruningFunctions) are exact bounds: with the
+    final k-th best as theta no true top-K item of a bucket is masked, and the masks
+    do reject candidates; ``reference_quirks`` runs them bucket by bucket."""
+    from flink_parameter_server_1_amd.models.mf.topk_tensor import lemp_candidate_mask
+
+    g = torch.Generator().manual_seed(1)
+    N, D, B, k = 2000, 12, 30, 10
+    X = torch.randn(N, D, generator=g) * torch.rand(N, 1, generator=g)
+    X = X[torch.argsort(X.norm(dim=1), descending=True)]
+    Q = torch.randn(B, D, generator=g)
+    S = Q @ X.t()
+    ts, tj = torch.topk(S, k, dim=1)
+    theta = ts[:, -1] * (1 - 1e-6)
+    qlen = Q.norm(dim=1)
+    pruned = 0
+    for s0 in range(0, N, 256):
+        xs = X[s0:s0 + 256]
+        keep = lemp_candidate_mask(Q, qlen, theta, xs, xs.norm(dim=1), strategy)
+        in_top = (tj >= s0) & (tj < s0 + xs.shape[0])
+        for b in range(B):
+            cols = (tj[b][in_top[b]] - s0).long()
+            assert bool(keep[b, cols].all()), (s0, b)
+        pruned += int((~keep).sum())
+    assert pruned > 0
+    idx = PrunedLempTopK(torch.arange(N), X, bucket_size=256, strategy=strategy, reference_quirks=True)
+    idx.query(Q, k)
+    assert idx.pruned > 0
 
 
 @pytest.mark.parametrize("num_users", [None, 5])  # sorted keys / dense per-user rings
