@@ -70,6 +70,37 @@ class PulledBatch:
         return self.keys.numel()
 
 
+class MaskedPair:
+    """A ``(ids, values)`` output pair restricted to the rows where ``mask`` holds,
+    compacted on first access.  Lets a worker emit a masked selection (e.g. the
+    predictions of the unlabelled examples of a mixed micro-batch) without a host
+    sync on the step: the consumer pays the compaction when it reads the output.
+    Unpacks, indexes and iterates like the 2-tuple it stands for."""
+
+    __slots__ = ("_ids", "_values", "_mask", "_pair")
+
+    def __init__(self, ids: torch.Tensor, values: torch.Tensor, mask: torch.Tensor):
+        self._ids, self._values, self._mask, self._pair = ids, values, mask, None
+
+    def pair(self) -> tuple:
+        if self._pair is None:
+            self._pair = (self._ids[self._mask], self._values[self._mask])
+            self._ids = self._values = self._mask = None
+        return self._pair
+
+    def __iter__(self):
+        return iter(self.pair())
+
+    def __getitem__(self, i):
+        return self.pair()[i]
+
+    def __len__(self) -> int:
+        return 2
+
+    def __repr__(self) -> str:
+        return f"MaskedPair{self.pair()!r}"
+
+
 class BatchedPSClient:
     """The worker's handle inside the tensor engine (see module docstring)."""
 

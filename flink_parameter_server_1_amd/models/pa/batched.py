@@ -8,7 +8,8 @@ every example on the pulled weights (K10-K12: ``ops.pa_binary`` /
 ``ops.pa_multi``, one wave per example, per-feature deltas summed per unique
 feature in the kernel) and pushes the summed deltas (``push_unique``).
 Unlabelled examples (binary label 0, multiclass -1) are predicted and emitted as
-``Left((example ids, labels))``; the PS logic (range partitioned
+``Left((example ids, labels))`` (an ``api.batched.MaskedPair``: compacted when
+read, so the step issues no host sync); the PS logic (range partitioned
 ``RangePSLogicWithClose`` or hash ``SimplePSLogicWithClose``, ``:262-281``) dumps
 the model at close as ``Right((feature ids, weights))``.
 
@@ -23,7 +24,7 @@ from typing import Iterable, Optional
 import torch
 
 from ... import ops
-from ...api.batched import BatchedWorkerLogic
+from ...api.batched import BatchedWorkerLogic, MaskedPair
 from ...core.tensor_engine import TensorRuntime
 from ...parallel.comm import Comm
 from ...ps.device_logics import DeviceRangePSLogicWithClose, DeviceSimplePSLogicWithClose
@@ -68,9 +69,8 @@ class PAWorker(BatchedWorkerLogic):
         if ids is None:
             ids = torch.arange(self._seen, self._seen + B, device=labels.device)
         self._seen += B
-        unl = labels == (0 if self.kind == "binary" else -1)
-        if self.emit_predictions and bool(unl.any()):
-            ps.output((ids[unl], pred[unl]))
+        if self.emit_predictions:  # the unlabelled examples' predictions, compacted by the consumer (no sync)
+            ps.output(MaskedPair(ids, pred, labels == (0 if self.kind == "binary" else -1)))
         self.examples += B
         self.last = (pred, loss)
 

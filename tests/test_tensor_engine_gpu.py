@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from flink_parameter_server_1_amd import ops
-from flink_parameter_server_1_amd.core.messages import Right
+from flink_parameter_server_1_amd.core.messages import Left, Right
 from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime, fold_outputs
 from flink_parameter_server_1_amd.models.mf.apps import ps_online_mf
 from flink_parameter_server_1_amd.models.mf.core import Rating
@@ -76,6 +76,37 @@ def test_pipelined_engine_issues_no_implicit_sync():
     rt.finish()
     ps = rt.ps_logic.ps
     assert ps.stats["steps"] == 24 and ps.stats["pulls"] == 24 * B
+
+
+def test_pipelined_pa_worker_issues_no_implicit_sync():
+    """PAWorker on the pipelined engine (staleness 1): labelled and unlabelled
+    examples mixed in every micro-batch, predictions emitted as MaskedPairs --
+    no implicit device->host sync in the loop; the outputs compact when read."""
+    from flink_parameter_server_1_amd.models.pa.batched import PAWorker
+    from flink_parameter_server_1_amd.models.pa.fast import synthetic_sparse_batch
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceRangePSLogicWithClose
+
+    F, B = 100_000, 2048
+    batches = []
+    for s in range(24):
+        ip, idx, val, lab = synthetic_sparse_batch(B, 16, F, seed=1, step=s, device=DEV)
+        lab = torch.where(torch.arange(B, device=DEV) % 4 == 0, torch.zeros_like(lab), lab)  # 1/4 unlabelled
+        batches.append((ip, idx, val, lab))
+    rt = TensorRuntime(Comm(device=DEV), staleness=1)
+    rt.start(PAWorker("binary", 1, "PA", 1.0), DeviceRangePSLogicWithClose(F, 1, init=("zeros",)))
+    for b in batches[:4]:  # warm-up: workspaces allocated
+        rt.submit(b)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for b in batches[4:]:
+            rt.submit(b)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    out = rt.finish()
+    preds = [e.value for e in out if isinstance(e, Left)]
+    assert len(preds) == 24 and all(ids.numel() == B // 4 for ids, _ in preds)
 
 
 def test_add_renorm_kernel_matches_reference():
