@@ -40,6 +40,7 @@ from typing import List, Optional
 import torch
 
 from .. import ops
+from ..api.batched import MaskedPair
 from ..utils.tracing import stage
 from .comm import Comm
 from .table import ShardedTable
@@ -240,8 +241,12 @@ class TensorPS:
             else:
                 self.table.apply_rows(recv_keys, recv, lr=lr, op=opt)
         if return_updated:
-            k = recv_keys[recv_keys >= 0] if self.masked_push else recv_keys
-            return self.table.global_ids(k), self.table.weight[k.long()]
+            if not sum(plan.recv_splits):  # nothing arrived at this shard (host-known sizes)
+                return None
+            if self.masked_push:  # rows the push skipped drop out when the consumer reads (no sync here)
+                k = recv_keys.long().clamp_min(0)
+                return MaskedPair(self.table.global_ids(k), self.table.weight[k], recv_keys >= 0)
+            return self.table.global_ids(recv_keys), self.table.weight[recv_keys.long()]
         return None
 
     @staticmethod

@@ -146,8 +146,8 @@ class DevicePSLogic:
 
     def after_push(self, updated) -> List[Any]:
         """PS outputs of one applied push: ``(global ids, new rows)`` on this shard."""
-        if self.emit == "push" and updated is not None and updated[0].numel():
-            return [updated]
+        if self.emit == "push" and updated is not None:
+            return [updated]  # (ids, rows) or a MaskedPair; no emptiness test (that would sync)
         return []
 
     def close(self) -> List[Any]:

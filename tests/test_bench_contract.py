@@ -7,6 +7,14 @@ import sys
 
 import pytest
 
+
+def _free_port() -> str:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return str(sk.getsockname()[1])
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
@@ -38,7 +46,7 @@ def test_bench_single_rank_json_line():
 @pytest.mark.parametrize("exchange", ["rotate", "ps"])
 def test_bench_two_ranks_gloo(exchange):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", "29671" if exchange == "rotate" else "29672",
+           "127.0.0.1", "--master-port", _free_port(),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--exchange", exchange] + TINY
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -96,7 +104,7 @@ def test_bench_metrics_jsonl(tmp_path):
 def test_secondary_benches_two_ranks_gloo(script, args, metric_key):
     """The secondary benches run end to end at world size 2 (gloo) and report the
     whole job from rank 0 only."""
-    port = {"bench/bench_mf_topk.py": "29681", "bench/bench_w2v.py": "29682", "bench/bench_pa.py": "29683"}[script]
+    port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", port, os.path.join(ROOT, script)] + args
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
