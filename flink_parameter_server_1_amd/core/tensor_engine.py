@@ -216,6 +216,8 @@ class TensorRuntime:
         if ps_logic.locking:
             self.pipe = None
         else:
+            # world 1 on the GPU: static plans, so no micro-batch waits on the device
+            ps_logic.ps.static = c.world == 1 and self.device.type == "cuda"
             self.pipe = BoundedStalenessPipeline(ps_logic.ps, self._compute, self.staleness,
                                                  lookahead=self.lookahead)
         self._started = True

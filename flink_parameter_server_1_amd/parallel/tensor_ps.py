@@ -56,6 +56,8 @@ class PullPlan:
     peer_flags: List[int] = field(default_factory=list)  # flag each rank sent with this plan
     n_requests: int = 0
     recv_rows: Optional[torch.Tensor] = None  # rows of recv_keys in the shard (cached by serve)
+    #: static plans (world 1): n_unique is an upper bound; valid[j] marks the real unique keys
+    valid: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -69,6 +71,8 @@ class PendingPlan:
                              # world 1: int32[1], the count alone (the flag never leaves the rank)
     event: Optional[object]  # torch.cuda.Event or None (host tensors: already complete)
     flag: int = 0
+    valid: Optional[torch.Tensor] = None  # static plan: [n_bound] bool
+    n_bound: int = 0
 
 
 class TensorPS:
@@ -88,6 +92,10 @@ class TensorPS:
         #: per-push output instead of being applied as zero deltas
         self.masked_push = False
         self._pinned = table.device.type == "cuda"
+        #: world 1, dense shard: plans whose sizes need no device->host copy -- the
+        #: unique keys are padded to ``min(n, key space)`` rows (padding gathers row 0
+        #: and is never applied), so a micro-batch issues no host sync at all
+        self.static = False
 
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0) -> PendingPlan:
@@ -100,6 +108,11 @@ class TensorPS:
         with stage("ps.dedup", self.timer):
             counts, prefix, uniq, pos = self.dedup.run(keys)
         W = self.comm.world
+        if W == 1 and self.static and not getattr(self.table, "sparse", False):
+            nb = min(n, int(self.table.key_space))
+            valid = torch.arange(nb, device=keys.device) < prefix[1]
+            gkeys = torch.where(valid, uniq[:nb], torch.zeros_like(uniq[:nb]))
+            return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb)
         # the workspace is reused by the next plan_begin: this plan keeps copies
         counts = counts.clone()
         uniq = uniq[:n].clone()
@@ -129,6 +142,12 @@ class TensorPS:
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
+        if pp.valid is not None:  # static world-1 plan: sizes known on the host, nothing to wait for
+            self.stats["pulls"] += pp.n
+            self.stats["unique"] += pp.n_bound
+            self.stats["steps"] += 1
+            return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
+                            valid=pp.valid)
         if pp.event is not None:
             if not pp.event.query():
                 self.stats["host_stalls"] += 1
@@ -208,6 +227,8 @@ class TensorPS:
         else:  # a push without a pull (push_keys, model load)
             rows, fresh = self.table.rows_for(plan.recv_keys, push=True)
         recv_keys = rows
+        if plan.valid is not None:  # static plan: the padding rows are never applied
+            recv_keys = torch.where(plan.valid, recv_keys, torch.full_like(recv_keys, -1))
         if self.masked_push:
             valid = recv[:, D] > 0.5
             recv = recv[:, :D].contiguous()
