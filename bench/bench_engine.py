@@ -29,6 +29,7 @@ def main(argv=None):
     ap.add_argument("--batches", default="1,64,4096,262144")
     ap.add_argument("--seconds", type=float, default=2.0, help="timed seconds per micro-batch size")
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--graph", action="store_true", help="replay captured hipGraph steps (world 1, core.step_graph)")
     a = ap.parse_args(argv)
 
     import torch
@@ -49,10 +50,12 @@ def main(argv=None):
     for B in [int(x) for x in a.batches.split(",")]:
         worker = FunctionBatchedWorkerLogic(lambda keys, ps: ps.pull(keys),
                                             lambda pulled, ps: ps.push_unique(torch.full(
-                                                (pulled.n_unique, a.dim), 1e-3, device=pulled.rows.device)))
+                                                (pulled.n_unique, a.dim), 1e-3, device=pulled.rows.device)),
+                                            graph_safe=True)
         logic = DeviceSimplePSLogic(a.keys, a.dim, op="add", init=("zeros",))
         logic.emit = "none"
-        rt = TensorRuntime(comm, staleness=a.staleness, output_sink=lambda e: None).start(worker, logic)
+        rt = TensorRuntime(comm, staleness=a.staleness, output_sink=lambda e: None,
+                           graph=a.graph).start(worker, logic)
         g = torch.Generator(device=dev)
         g.manual_seed(11 + comm.rank)
         pool = [torch.randint(0, a.keys, (B,), generator=g, device=dev) for _ in range(8)]
@@ -78,12 +81,12 @@ def main(argv=None):
         sync()
         comm.barrier()
         dt = comm.max_over_ranks(time.perf_counter() - t0)
-        results.append({"batch": B, "steps": steps, "micro_batches_per_s": steps / dt,
+        results.append({"batch": B, "steps": steps, "graph_replays": rt.graphs.replays if rt.graphs else 0, "micro_batches_per_s": steps / dt,
                         "keys_per_s": comm.world * steps * B / dt, "us_per_step": dt / steps * 1e6})
     if comm.rank == 0:
         print(json.dumps({"metric": "tensor-engine plumbing: micro-batches/s and keys/s (whole node)",
                           "n_gpus": comm.world, "dtype": "fp32", "data": "synthetic uniform keys",
-                          "config": {"keys": a.keys, "dim": a.dim, "staleness": a.staleness}, "results": results}),
+                          "config": {"keys": a.keys, "dim": a.dim, "staleness": a.staleness, "graph": a.graph}, "results": results}),
               flush=True)
 
 

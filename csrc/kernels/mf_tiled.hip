@@ -77,7 +77,9 @@ __device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, const TileGeo&
   bucket = (g.dU.div(u) * 2 * g.W + 2 * q + h) * g.T + g.dR.div(row);  // user phase, item block, tile
 }
 
-constexpr int TP_MAX_BUCKETS = 16384;  // 64 KiB of LDS counters
+// LDS counters of the count kernel: KT ints of dynamic LDS (64 KiB at KT = 16k: two
+// 1024-thread workgroups per CU; up to 128 KiB -- a workgroup may declare 160 KiB)
+constexpr int TP_MAX_BUCKETS = 32768;
 
 typedef int tp_i2 __attribute__((ext_vector_type(2)));
 typedef int tp_i3 __attribute__((ext_vector_type(3)));
@@ -117,7 +119,7 @@ __device__ __forceinline__ void f4_st(float4* p, float4 v) {
 __global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restrict__ totals_g, int KT,
                                                          int32_t* __restrict__ ptr) {
   __shared__ int32_t part[1024];
-  __shared__ int32_t totals[16384];  // KT <= TP_MAX_BUCKETS: staged by coalesced loads
+  __shared__ int32_t totals[TP_MAX_BUCKETS];  // KT <= TP_MAX_BUCKETS: staged by coalesced loads
   for (int k = threadIdx.x; k < KT; k += 1024) totals[k] = totals_g[k];
   __syncthreads();
   const int per = (KT + 1023) / 1024;
@@ -193,7 +195,7 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
   // One LDS atomic per rating (LDS atomics run at ~1 lane per CU cycle and
   // bound this kernel); the coarse counts of a chunk are read off the fine
   // histogram afterwards: 8 lanes per coarse key sum its 2^cshift buckets.
-  __shared__ int32_t hb[TP_MAX_BUCKETS];
+  extern __shared__ int32_t hb[];  // [KT] (dynamic LDS)
   __shared__ int32_t hc_prev[TP3_MAXK];
   for (int k = threadIdx.x; k < KT; k += blockDim.x) hb[k] = 0;
   if (threadIdx.x < NC) hc_prev[threadIdx.x] = 0;
@@ -632,7 +634,13 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
   const int Gc = (G + sub - 1) / sub;
   int32_t* bhist = H1 + 1024 * (int64_t)NC;  // [1 + Gc][KT]: totals, then one row per count workgroup
-  hipLaunchKernelGGL(tp3_count_kernel, dim3(Gc), dim3(1024), 0, s, uid, iid, n, chunk, G, sub, g, cshift, NC, KT,
+  const size_t hb_bytes = sizeof(int32_t) * (size_t)KT;
+  if (hb_bytes > 65536) {  // above the default dynamic-LDS ceiling: opt in (a workgroup may hold 160 KiB)
+    e = hipFuncSetAttribute((const void*)tp3_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hb_bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(tp3_count_kernel, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G,
+                     sub, g, cshift, NC, KT,
                      ccount, bhist, seen, H1);
   hipLaunchKernelGGL(tp3_colsum_kernel, dim3((KT + 63) / 64), dim3(1024), 0, s, bhist, Gc, KT);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);

@@ -45,14 +45,19 @@ __device__ __forceinline__ float sigmoidf(float s) { return 1.f / (1.f + __expf(
 // log(1 + exp(x)) without overflow
 __device__ __forceinline__ float softplusf(float x) { return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x)); }
 
-template <int NPL>
+// GOUT = false: output-row deltas by float atomics (above).  GOUT = true: the
+// output rows are not touched here; the pair's coefficient g_x goes to
+// gbuf[p * (k + 1) + x] and sgns_rows_kernel below applies sum_x g_x * h per
+// output row from the coefficients sorted by row (no atomics on the hot rows).
+template <int NPL, bool GOUT>
 __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__ rows_in,
                                                        const float* __restrict__ rows_out,
                                                        const int32_t* __restrict__ pos_c,
                                                        const int32_t* __restrict__ pos_o,
                                                        const int32_t* __restrict__ pos_neg, int64_t P, int D, int k,
                                                        float lr, float* __restrict__ d_in, float* __restrict__ d_out,
-                                                       float* __restrict__ loss, int chunk) {
+                                                       float* __restrict__ loss, int chunk,
+                                                       float* __restrict__ gbuf) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t p0 = wave * chunk;
@@ -124,12 +129,18 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
         const float s = part[q];
         const float g = lr * (label - sigmoidf(s));
         if (loss != nullptr && lane == 0) lsum += label > 0.f ? softplusf(-s) : softplusf(s);
-        float* dst = d_out + (int64_t)row[q] * D;
+        if constexpr (GOUT) {
+          if (lane == 0) gbuf[p * (k + 1) + x0 + q] = g;
 #pragma unroll
-        for (int m = 0; m < NPL; ++m) {
-          const int j = lane + 64 * m;
-          if (j < D) atomic_add_noret(dst + j, g * h[m]);
-          dh[m] += g * xv[q][m];
+          for (int m = 0; m < NPL; ++m) dh[m] += g * xv[q][m];
+        } else {
+          float* dst = d_out + (int64_t)row[q] * D;
+#pragma unroll
+          for (int m = 0; m < NPL; ++m) {
+            const int j = lane + 64 * m;
+            if (j < D) atomic_add_noret(dst + j, g * h[m]);
+            dh[m] += g * xv[q][m];
+          }
         }
       }
     }
@@ -140,7 +151,135 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
   if (loss != nullptr && lane == 0) atomicAdd(loss, lsum);
 }
 
+// Output-row pass of the sorted form.  srow[n] = output rows sorted, perm[n] =
+// their entry e = p * (k + 1) + x in gbuf; the delta of row r is
+// sum over its entries of gbuf[e] * rows_h[pos_c[e / (k + 1)]].  One wave per
+// C consecutive sorted entries: the wave stages its entries' (row, center, g)
+// in LDS with parallel loads, then walks them with RG center rows in flight,
+// summing each run of equal rows in registers.  A run that lies wholly inside
+// the wave's range is the row's only writer: plain read-modify-write; the (at
+// most two) runs cut by the range ends are shared with a neighbour wave: float
+// atomics.  The hottest output rows (Zipf contexts) thus cost one atomic per
+// wave range instead of one per pair.
+constexpr int SR_C = 256;  // sorted entries per wave
+constexpr int SR_G = 8;    // center rows in flight per lane
+
+template <int NPL>
+__global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restrict__ srow,
+                                                        const int64_t* __restrict__ perm,
+                                                        const float* __restrict__ gbuf,
+                                                        const int32_t* __restrict__ pos_c, int k1, int64_t n,
+                                                        const float* __restrict__ rows_h, int D,
+                                                        float* __restrict__ d_out) {
+  __shared__ int32_t s_row[4][SR_C], s_cen[4][SR_C];
+  __shared__ float s_g[4][SR_C];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t t0 = ((int64_t)blockIdx.x * 4 + wv) * SR_C;
+  const int m_n = t0 < n ? (int)min((int64_t)SR_C, n - t0) : 0;
+  for (int i = lane; i < m_n; i += 64) {
+    const int64_t e = perm[t0 + i];
+    s_row[wv][i] = srow[t0 + i];
+    s_g[wv][i] = gbuf[e];
+    s_cen[wv][i] = pos_c[e / k1];
+  }
+  __syncthreads();
+  if (m_n == 0) return;  // after the only barrier
+  float acc[NPL];
+#pragma unroll
+  for (int m = 0; m < NPL; ++m) acc[m] = 0.f;
+  int32_t cur = s_row[wv][0];
+  bool whole = t0 == 0 || srow[t0 - 1] != cur;  // the current run starts inside this range
+  auto flush = [&](bool complete) {
+    float* dst = d_out + (int64_t)cur * D;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+      const int j = lane + 64 * m;
+      if (j < D) {
+        if (complete) dst[j] += acc[m];
+        else atomic_add_noret(dst + j, acc[m]);
+      }
+      acc[m] = 0.f;
+    }
+  };
+  for (int i0 = 0; i0 < m_n; i0 += SR_G) {
+    float hv[SR_G][NPL];
+#pragma unroll
+    for (int q = 0; q < SR_G; ++q) {  // all SR_G center rows in flight
+      const int i = min(i0 + q, m_n - 1);
+      const float* src = rows_h + (int64_t)s_cen[wv][i] * D;
+#pragma unroll
+      for (int m = 0; m < NPL; ++m) {
+        const int j = lane + 64 * m;
+        hv[q][m] = j < D ? src[j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < SR_G; ++q) {
+      const int i = i0 + q;
+      if (i >= m_n) break;  // wave-uniform
+      const int32_t r = s_row[wv][i];
+      if (r != cur) {  // the run of `cur` ended inside the range
+        flush(whole);
+        cur = r;
+        whole = true;
+      }
+      const float g = s_g[wv][i];
+#pragma unroll
+      for (int m = 0; m < NPL; ++m) acc[m] += g * hv[q][m];
+    }
+  }
+  flush(whole && (t0 + m_n == n || srow[t0 + m_n] != cur));
+}
+
 }  // namespace
+
+// Sorted form, pass 1: centers as in fps_sgns_standard (d_in), output-row
+// coefficients into gbuf[P * (k + 1)] (zeroed by the caller; skipped negatives
+// stay 0).
+FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, const int32_t* pos_c,
+                                   const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
+                                   float* d_in, float* loss, float* gbuf, void* stream) {
+  if (P <= 0) return 0;
+  if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
+  const int chunk = 16;
+  const int64_t waves = (P + chunk - 1) / chunk;
+  const int64_t blocks = (waves + 3) / 4;
+  if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+#define FPS_SGC(NPL_)                                                                                            \
+  hipLaunchKernelGGL((sgns_std_kernel<NPL_, true>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, loss, chunk, gbuf)
+  if (D <= 64) FPS_SGC(1);
+  else if (D <= 128) FPS_SGC(2);
+  else if (D <= 256) FPS_SGC(4);
+  else if (D <= 320) FPS_SGC(5);
+  else FPS_SGC(8);
+#undef FPS_SGC
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// Sorted form, pass 2: d_out[srow[t]] += gbuf[perm[t]] * rows_h[pos_c[perm[t] / k1]]
+// over the n = P * k1 entries sorted by output row.
+FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float* gbuf, const int32_t* pos_c, int k1,
+                          int64_t n, const float* rows_h, int D, float* d_out, void* stream) {
+  if (n <= 0) return 0;
+  if (D <= 0 || D > 512 || k1 <= 0) return (int)hipErrorInvalidValue;
+  const int64_t blocks = (n + 4 * SR_C - 1) / (4 * SR_C);
+  if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+#define FPS_SGR(NPL_)                                                                                            \
+  hipLaunchKernelGGL(sgns_rows_kernel<NPL_>, dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf, pos_c, k1, \
+                     n, rows_h, D, d_out)
+  if (D <= 64) FPS_SGR(1);
+  else if (D <= 128) FPS_SGR(2);
+  else if (D <= 256) FPS_SGR(4);
+  else if (D <= 320) FPS_SGR(5);
+  else FPS_SGR(8);
+#undef FPS_SGR
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
 
 // P pairs: centers pos_c[P] (rows of rows_in / d_in), contexts pos_o[P] and
 // k negatives per pair pos_neg[P * k] (rows of rows_out / d_out); fp32 rows,
@@ -158,8 +297,8 @@ FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGS(NPL_)                                                                                            \
-  hipLaunchKernelGGL(sgns_std_kernel<NPL_>, dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out, pos_c,    \
-                     pos_o, pos_neg, P, D, k, lr, d_in, d_out, loss, chunk)
+  hipLaunchKernelGGL((sgns_std_kernel<NPL_, false>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, loss, chunk, (float*)nullptr)
   if (D <= 64) FPS_SGS(1);
   else if (D <= 128) FPS_SGS(2);
   else if (D <= 256) FPS_SGS(4);

@@ -130,6 +130,10 @@ class BatchedWorkerLogic:
 
     arbitrary_pushes = False
     pushes = True
+    #: the callbacks are a pure device function of the batch and device state (no
+    #: host syncs, no per-batch Python state): ``TensorRuntime(graph=True)`` may
+    #: replay captured steps instead of calling them (``core.step_graph``)
+    graph_safe = False
 
     def open(self, ctx: RuntimeContext) -> None:
         pass
@@ -153,8 +157,10 @@ class BatchedWorkerLogic:
 class FunctionBatchedWorkerLogic(BatchedWorkerLogic):
     """A batched worker from plain callables (tests / scripts)."""
 
-    def __init__(self, on_recv_batch, on_pull_recv_batch, open=None, close=None):  # noqa: A002
+    def __init__(self, on_recv_batch, on_pull_recv_batch, open=None, close=None,  # noqa: A002
+                 graph_safe: bool = False):
         self._recv, self._answer, self._open, self._close = on_recv_batch, on_pull_recv_batch, open, close
+        self.graph_safe = bool(graph_safe)
 
     def open(self, ctx):
         if self._open:

@@ -45,6 +45,7 @@ from ..ps.device_logics import DevicePSLogic
 from ..utils.metrics import Counters
 from ..utils.tracing import stage
 from .messages import Left, Right
+from .step_graph import StepGraphs
 
 
 def staleness_for_pull_limit(pull_limit: int, micro_batch: int) -> int:
@@ -127,8 +128,7 @@ class _Client(BatchedPSClient):
             tmp = torch.zeros((U + 1, self._dim()), dtype=self._acc.dtype, device=self._acc.device)
             tmp.scatter_reduce_(0, idx.view(-1, 1).expand(-1, self._dim()), d.to(tmp.dtype),
                                 reduce="amax" if comb == "max" else "amin", include_self=False)
-            hit = torch.zeros(U + 1, dtype=torch.bool, device=pos.device)
-            hit[idx] = True
+            hit = torch.zeros(U + 1, dtype=torch.bool, device=pos.device).index_fill_(0, idx, True)
             tmp, hit = tmp[:U], hit[:U]
             both = torch.maximum(self._acc, tmp) if comb == "max" else torch.minimum(self._acc, tmp)
             self._acc = torch.where((hit & self._mask).view(-1, 1), both,
@@ -140,15 +140,17 @@ class _Client(BatchedPSClient):
                 rid = torch.where(mask, rid, torch.full_like(rid, -1))
             last = torch.full((self._plan.n_unique,), -1, dtype=torch.int64, device=pos.device)
             last.scatter_reduce_(0, pos, rid, reduce="amax")
-            hit = last >= 0
-            self._acc[hit] = d[last[hit]].to(self._acc.dtype)
+            hit = last >= 0  # (no boolean indexing: the step stays free of host syncs)
+            self._acc = torch.where(hit.view(-1, 1), d[last.clamp_min(0)].to(self._acc.dtype), self._acc)
             self._mask |= hit
         else:
             if mask is not None:
                 d = d * mask.view(-1, 1).to(d.dtype)
-                self._mask[pos[mask]] = True
+                hits = torch.zeros(self._mask.numel(), dtype=torch.int32, device=pos.device)
+                hits.index_add_(0, pos, mask.to(torch.int32))
+                self._mask |= hits > 0
             else:
-                self._mask[pos] = True
+                self._mask.index_fill_(0, pos, True)
             self._acc.index_add_(0, pos, d.to(self._acc.dtype))
 
     def push_unique(self, deltas, mask=None):
@@ -170,7 +172,7 @@ class _Client(BatchedPSClient):
             mask = torch.ones(U, dtype=torch.bool, device=d.device)
         mask = mask.to(dtype=torch.bool).reshape(-1)
         if self.rt.ps_logic.op == "set":
-            self._acc[mask] = d[mask].to(self._acc.dtype)
+            self._acc = torch.where(mask.view(-1, 1), d.to(self._acc.dtype), self._acc)
         else:
             self._acc += d.to(self._acc.dtype) * mask.view(-1, 1).to(self._acc.dtype)
         self._mask |= mask
@@ -190,7 +192,10 @@ class TensorRuntime:
     """Per-rank driver of a tensor-engine job (see module docstring)."""
 
     def __init__(self, comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
-                 output_sink: Optional[Callable[[Any], None]] = None, lookahead: Optional[bool] = None):
+                 output_sink: Optional[Callable[[Any], None]] = None, lookahead: Optional[bool] = None,
+                 graph: bool = False):
+        """``graph``: replay fixed-shape micro-batch steps from captured hipGraphs
+        (``core.step_graph``; world 1, static plans, a ``graph_safe`` worker)."""
         self.comm = comm or Comm()
         self.device = self.comm.device
         self.staleness = int(staleness)
@@ -203,6 +208,9 @@ class TensorRuntime:
         self.worker_logic: Optional[BatchedWorkerLogic] = None
         self.ps_logic: Optional[DevicePSLogic] = None
         self._started = False
+        self.graph = bool(graph)
+        self.graphs: Optional[StepGraphs] = None
+        self._capture_emits: Optional[List[Any]] = None
 
     # ------------------------------------------------------------------ setup
     def start(self, worker_logic: BatchedWorkerLogic, ps_logic: DevicePSLogic) -> "TensorRuntime":
@@ -221,9 +229,17 @@ class TensorRuntime:
             self.pipe = BoundedStalenessPipeline(ps_logic.ps, self._compute, self.staleness,
                                                  lookahead=self.lookahead)
         self._started = True
+        if self.graph:
+            self.graphs = StepGraphs(self)
+            why = self.graphs.why_not()
+            if why is not None:
+                raise ValueError(f"TensorRuntime(graph=True) cannot capture this job's steps: {why}")
+            ps_logic.ps.dedup.clear_after = True
         return self
 
     def set_timer(self, timer) -> None:
+        if timer is not None and self.graphs is not None:
+            raise ValueError("a stage timer cannot time captured (graph=True) steps")
         self.timer = timer
         if self.ps_logic is not None and self.ps_logic.ps is not None:
             self.ps_logic.ps.timer = timer
@@ -262,6 +278,9 @@ class TensorRuntime:
 
     # --------------------------------------------------------------- running
     def _emit(self, e) -> None:
+        if self._capture_emits is not None:  # capturing a step: re-emitted after every replay
+            self._capture_emits.append(e)
+            return
         if self.output_sink is not None:
             self.output_sink(e)
         else:
@@ -270,6 +289,11 @@ class TensorRuntime:
     def submit(self, batch: Any, flag: int = 0) -> None:
         """One micro-batch of this rank (collective: all ranks submit in lockstep;
         ``batch=None`` takes part without data)."""
+        if self.graphs is not None and self.graphs.submit(batch, flag):
+            return
+        self._submit_eager(batch, flag)
+
+    def _submit_eager(self, batch: Any, flag: int = 0) -> None:
         c = self.client
         c._requests, c._n = [], 0
         if batch is not None:

@@ -166,6 +166,42 @@ def occurrence_rounds(users: torch.Tensor) -> torch.Tensor:
     return rnd
 
 
+class RoundPlan:
+    """The occurrence rounds of a micro-batch's users, planned when the batch is
+    RECEIVED: entries ordered by round (stable: batch order inside a round) and the
+    per-round counts copied to pinned host memory behind an event.  By the time
+    the batch's answer is served (one micro-batch later on a pipelined engine)
+    the counts are on the host, so the merge loop over rounds issues no
+    device->host sync -- the same trick as the PS count exchange
+    (``parallel.tensor_ps``)."""
+
+    def __init__(self, users: torch.Tensor):
+        rnd = occurrence_rounds(users)
+        B = users.numel()
+        self.order = torch.argsort(rnd, stable=True)
+        cnt = torch.zeros(B + 1, dtype=torch.int32, device=users.device)
+        cnt.index_add_(0, rnd, torch.ones_like(rnd, dtype=torch.int32))
+        if users.is_cuda:
+            self._host = torch.empty(B + 1, dtype=torch.int32, pin_memory=True)
+            self._host.copy_(cnt, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+        else:
+            self._host, self._event = cnt, None
+
+    def rounds(self) -> List[tuple]:
+        """``[(start, n)]`` slices of ``order``, one per non-empty round, in order."""
+        if self._event is not None:
+            self._event.synchronize()
+        out, a = [], 0
+        for n in self._host.tolist():
+            if n == 0:
+                break  # rounds are dense: round r exists only if round r-1 does
+            out.append((a, n))
+            a += n
+        return out
+
+
 # ------------------------------------------------------------- LEMP pruning
 def _theta(best_s: torch.Tensor) -> torch.Tensor:
     """k-th best so far; 0 while fewer than k candidates were kept (the reference's
@@ -360,7 +396,7 @@ def as_reference_records(outputs) -> List[tuple]:
 class _TopKServing:
     """Shared query path: partial LEMP top-K on the local items, gather, seen-aware merge."""
 
-    def _serve(self, Q, valid, users, items, ts, ps):
+    def _serve(self, Q, valid, users, items, ts, ps, plan: Optional[RoundPlan] = None):
         with stage("topk.score", None):
             if self.index is not None and self.index.vecs.shape[0] > 0:
                 s, i = self.index.query(Q, self.worker_k)
@@ -371,11 +407,11 @@ class _TopKServing:
             i = torch.where(valid.view(-1, 1), i, torch.full_like(i, -1))
         with stage("topk.merge", None):
             ss, ii = _gather_partials(self.comm, s, i)
-            rnd = occurrence_rounds(users)
+            plan = plan if plan is not None else RoundPlan(users)
             best_s = torch.empty((users.numel(), self.K), device=Q.device)
             best_i = torch.empty((users.numel(), self.K), dtype=torch.long, device=Q.device)
-            for r in range(int(rnd.max()) + 1 if rnd.numel() else 0):
-                sel = torch.nonzero(rnd == r).flatten()
+            for a, n in plan.rounds():  # a user's later entries see its earlier ones as seen
+                sel = plan.order[a:a + n]
                 exc = self.seen.contains(users[sel], ii[sel])
                 bs, bi = merge_partials(ss[sel], ii[sel], self.K, exc)
                 best_s[sel], best_i[sel] = bs, bi
@@ -418,15 +454,15 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
 
     def on_recv_batch(self, batch, ps):
         users, items, ts = (t.to(self.device) for t in batch)
-        ps.pull(users, (users, items, ts))
+        ps.pull(users, (users, items, ts, RoundPlan(users)))
 
     def on_pull_recv_batch(self, pulled, ps):
-        users, items, ts = pulled.payload
+        users, items, ts, plan = pulled.payload
         rows = pulled.values()
         D = rows.shape[1] - 1
         valid = rows[:, D] >= 0  # (len, vec) stores; len -1 = invalid (never loaded)
         self._build(D)
-        self._serve(rows[:, :D].contiguous(), valid, users, items, ts, ps)
+        self._serve(rows[:, :D].contiguous(), valid, users, items, ts, ps, plan)
 
 
 def ps_top_k_generator_tensor(queries: Iterable, ps_model, worker_model, num_users: int, num_factors: int = 10,
@@ -507,7 +543,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
 
     def on_recv_batch(self, batch, ps):
         users, items, ts, rating = (t.to(self.device) for t in batch)
-        ps.pull(users, (users, items, ts, rating.float()))
+        ps.pull(users, (users, items, ts, rating.float(), RoundPlan(users)))
 
     @property
     def trained(self) -> int:
@@ -543,13 +579,13 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self.index.update_rows(p, self.items.weight[rows])
 
     def on_pull_recv_batch(self, pulled, ps):
-        users, items, ts, rating = pulled.payload
+        users, items, ts, rating, plan = pulled.payload
         U = pulled.values()  # [B, D] user vectors (length recomputed on the worker)
         self.served += users.numel()
         if self._stale or self.index is None:
             self._rebuild_index()
         self._since_sort += 1
-        self._serve(U, torch.ones(users.numel(), dtype=torch.bool, device=U.device), users, items, ts, ps)
+        self._serve(U, torch.ones(users.numel(), dtype=torch.bool, device=U.device), users, items, ts, ps, plan)
         # learning: the owner of each rated item (non-owned rows masked, not compacted)
         n = self.items.n_local
         own = (items.long() % self.W) == self.rank

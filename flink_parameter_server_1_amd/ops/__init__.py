@@ -201,6 +201,9 @@ class DedupWorkspace:
         if self.method not in (None, "claim", "flags"):
             raise ValueError(f"dedup method must be 'claim' or 'flags', not {self.method!r}")
         self.flag = None
+        #: empty every claimed entry after the step (``reset_claims``): set by a
+        #: runtime that replays captured steps
+        self.clear_after = False
         self.device = torch.device(device)
         self.epoch = 0
         self.cap = 0
@@ -264,6 +267,21 @@ class DedupWorkspace:
                                   self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
                                   self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup")
         return self.counts, self.prefix, self.uniq, self.pos[:n]
+
+    def reset_claims(self, keys: torch.Tensor) -> None:
+        """Empty the claim entries of ``keys`` (the step's unique keys).  In
+        ``clear_after`` mode every entry is empty between steps, so a constant
+        epoch -- the one baked into a captured hipGraph step
+        (``core.step_graph``) -- stays valid."""
+        if self.device.type != "cuda":
+            return
+        if self.hashed:
+            self.tab.zero_()
+            return
+        k = keys.long()
+        self.map.index_fill_(0, k, 0)
+        if self.flag is not None:
+            self.flag.index_fill_(0, k, 0)
 
 
 def lock_acquire(lock: torch.Tensor, rows: torch.Tensor, src: int) -> torch.Tensor:
@@ -385,7 +403,7 @@ TILED_DIMS = (16, 32, 64, 128, 256)
 
 
 #: bucket counters a tile partition keeps in LDS (``TP_MAX_BUCKETS`` in mf_tiled.hip)
-TILE_MAX_BUCKETS = 16384
+TILE_MAX_BUCKETS = 32768
 
 
 def tile_rows_for(dim: int, block_rows: int, W: int = 1) -> Optional[int]:
@@ -709,14 +727,28 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
                                      neg_group)])
 
 
+SGNS_METHODS = ("sorted", "atomic")
+
+
 def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d_in, d_out,
-                  with_loss: bool = False):
+                  with_loss: bool = False, method: Optional[str] = None):
     """Standard skip-gram negative sampling (K6, ``kernels/sgns_std.hip``): ``k``
     independent negatives per pair (``pos_neg[P * k]``), word2vec's objective.
     ``d_in`` / ``d_out`` receive the deltas (the tables themselves on the local
     path).  Returns the summed loss (a device / host 1-element tensor) or None.
-    GPU: one wave per 16 pairs, sequential inside a wave's center runs, Hogwild
-    float atomics across waves; CPU: the mini-batch form."""
+
+    GPU: one wave per 16 pairs, sequential inside a wave's center runs (the
+    center's change is added once per run).  Output rows (context + negatives):
+
+    * ``method="sorted"`` (default): the pass computes each pair's coefficients
+      g_x against the output rows as of the call; the (row, entry) list is sorted
+      by row and ``sgns_rows_kernel`` adds sum g_x * h per row, one plain
+      read-modify-write per row run (float atomics only where a run straddles two
+      waves).  ``h`` = the center rows after this call's center updates
+      (``rows_in``; on the PS path the pulled rows).
+    * ``method="atomic"``: Hogwild float atomics per pair and row, inside the pass.
+
+    CPU: the mini-batch form."""
     P = pos_c.numel()
     D = rows_in.shape[1]
     if pos_neg.numel() != P * k:
@@ -728,6 +760,22 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
         if D > 512:
             raise ValueError("sgns_standard: D <= 512")
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
+        method = method or os.environ.get("FPS_SGNS_METHOD", "sorted")
+        if method not in SGNS_METHODS:
+            raise ValueError(f"sgns_standard: method must be one of {SGNS_METHODS}")
+        if method == "sorted":
+            lib = N.require()
+            s = N.stream_ptr(rows_in.device)
+            k1 = int(k) + 1
+            gbuf = torch.zeros(P * k1, dtype=torch.float32, device=rows_in.device)
+            N.check(lib.fps_sgns_standard_coef(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
+                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
+                                               _c(d_in).data_ptr(), N.ptr(loss), gbuf.data_ptr(), s), "sgns_coef")
+            keys = torch.cat([pos_o.reshape(P, 1), pos_neg.reshape(P, int(k))], dim=1).reshape(-1)
+            srow, perm = torch.sort(keys.to(torch.int32))
+            N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
+                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), s), "sgns_rows")
+            return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
                                               _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss),

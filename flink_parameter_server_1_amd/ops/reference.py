@@ -469,10 +469,15 @@ def ht_rehash(rowkey, count, tab, rowmap):
 SGNS_STD_CHUNK = 16  # pairs per wave in kernels/sgns_std.hip
 
 
-def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out):
+def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out, method="atomic"):
     """CPU twin of ``fps_sgns_standard`` (sequential; center runs restart at every
-    chunk of ``SGNS_STD_CHUNK`` pairs like the kernel's waves).  Returns the loss."""
+    chunk of ``SGNS_STD_CHUNK`` pairs like the kernel's waves).  Returns the loss.
+    ``method="sorted"``: the output-row deltas are ``g * rows_in[center]`` added
+    after the pass (``rows_in`` after the center updates when ``d_in`` is
+    ``rows_in``), the sorted form of ``ops.sgns_standard``."""
     import math
+
+    deferred = []
 
     P = pos_c.numel()
     D = rows_in.shape[1]
@@ -496,11 +501,16 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out):
                 s = float(h @ xv)
                 g = lr * (lab - 1.0 / (1.0 + math.exp(-s)))
                 total += math.log1p(math.exp(-s)) if lab > 0 else math.log1p(math.exp(s))
-                d_out[x] += (g * h).to(d_out.dtype)
+                if method == "sorted":
+                    deferred.append((x, g, c))
+                else:
+                    d_out[x] += (g * h).to(d_out.dtype)
                 dh += g * xv
             h = h + dh
         if cur >= 0:
             d_in[cur] += (h - h0).to(d_in.dtype)
+    for x, g, c in deferred:
+        d_out[x] += (g * rows_in[c].double()).to(d_out.dtype)
     return total
 
 

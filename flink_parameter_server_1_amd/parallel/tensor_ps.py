@@ -112,6 +112,8 @@ class TensorPS:
             nb = min(n, int(self.table.key_space))
             valid = torch.arange(nb, device=keys.device) < prefix[1]
             gkeys = torch.where(valid, uniq[:nb], torch.zeros_like(uniq[:nb]))
+            if self.dedup.clear_after:
+                self.dedup.reset_claims(gkeys)
             return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb)
         # the workspace is reused by the next plan_begin: this plan keeps copies
         counts = counts.clone()

@@ -196,7 +196,8 @@ def test_sgns_modes_learn_on_cpu(mode):
 @pytest.mark.parametrize("D", [16, 64, 100, 300])
 @pytest.mark.parametrize("runs", [False, True])
 @pytest.mark.parametrize("k", [1, 5, 7])
-def test_sgns_standard_kernel_matches_reference(D, runs, k):
+@pytest.mark.parametrize("method", ["sorted", "atomic"])
+def test_sgns_standard_kernel_matches_reference(D, runs, k, method):
     """PS-path form (rows read-only, separate delta buffers): the kernel equals the
     sequential reference, center runs included (float-atomic order aside)."""
     torch.manual_seed(D + k)
@@ -209,14 +210,65 @@ def test_sgns_standard_kernel_matches_reference(D, runs, k):
     pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
     pos_neg = torch.randint(0, Uout, (P * k,), dtype=torch.int32)
     d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
-    loss_r = R.sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r)
+    loss_r = R.sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r, method=method)
     dev = "cuda"
     d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
     loss = ops.sgns_standard(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k,
-                             0.05, d_in, d_out, with_loss=True)
+                             0.05, d_in, d_out, with_loss=True, method=method)
     torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=5e-6)
     torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=5e-6)
     assert abs(float(loss) - loss_r) / loss_r < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [64, 300])
+def test_sgns_standard_sorted_in_place_matches_reference(D):
+    """Local path (d_in is rows_in, d_out is rows_out; a few very hot output rows
+    shared by many waves): the sorted form equals its sequential reference -- the
+    output rows take g * (center row after the pass's center updates).  Center runs
+    are 8 pairs, aligned to the kernel's 16-pair waves, so no center row is shared
+    between waves and the result is deterministic up to summation order."""
+    torch.manual_seed(D)
+    V, P, k = 5000, 16000, 5
+    w_in = torch.randn(V, D) * 0.1
+    w_out = torch.randn(V, D) * 0.1
+    pos_c = torch.randperm(V)[:P // 8].to(torch.int32).repeat_interleave(8)
+    pos_o = (torch.rand(P) ** 4 * V).to(torch.int32)  # Zipf-ish: a few very hot context rows
+    pos_neg = torch.randint(0, V, (P * k,), dtype=torch.int32)
+    d_in = torch.zeros_like(w_in)
+    loss_r = R.sgns_standard(w_in, w_out, pos_c, pos_o, pos_neg, k, 0.05, d_in, torch.zeros_like(w_out))
+    wi_post = w_in + d_in
+    wo_post = w_out + _deferred_out(w_in, w_out, wi_post, pos_c, pos_o, pos_neg, k, 0.05)
+    dev = "cuda"
+    wi, wo = w_in.to(dev), w_out.to(dev)
+    loss = ops.sgns_standard(wi, wo, pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k, 0.05, wi, wo,
+                             with_loss=True, method="sorted")
+    torch.testing.assert_close(wi.cpu(), wi_post, rtol=1e-4, atol=5e-6)
+    torch.testing.assert_close(wo.cpu(), wo_post, rtol=1e-4, atol=2e-5)
+    assert abs(float(loss) - loss_r) / loss_r < 1e-4
+
+
+def _deferred_out(rows_in, rows_out, h_rows, pos_c, pos_o, pos_neg, k, lr):
+    """Output-row deltas of the sorted form: g from the sequential pass (runs of
+    SGNS_STD_CHUNK pairs), times ``h_rows[center]``."""
+    import math
+
+    P, D = pos_c.numel(), rows_in.shape[1]
+    out = torch.zeros(rows_out.shape[0], D, dtype=torch.float64)
+    pc, po, pn = pos_c.tolist(), pos_o.tolist(), pos_neg.reshape(P, k).tolist()
+    for s0 in range(0, P, R.SGNS_STD_CHUNK):
+        cur, h = -1, None
+        for p in range(s0, min(P, s0 + R.SGNS_STD_CHUNK)):
+            if pc[p] != cur:
+                cur, h = pc[p], rows_in[pc[p]].double().clone()
+            dh = torch.zeros(D, dtype=torch.float64)
+            for x, lab in [(po[p], 1.0)] + [(n, 0.0) for n in pn[p] if n != po[p]]:
+                xv = rows_out[x].double()
+                g = lr * (lab - 1.0 / (1.0 + math.exp(-float(h @ xv))))
+                out[x] += g * h_rows[cur].double()
+                dh += g * xv
+            h = h + dh
+    return out.float()
 
 
 @pytest.mark.gpu

@@ -78,6 +78,51 @@ def test_pipelined_engine_issues_no_implicit_sync():
     assert ps.stats["steps"] == 24 and ps.stats["pulls"] == 24 * B
 
 
+def test_pipelined_mf_topk_worker_syncs_once_per_batch():
+    """OnlineMFTopKWorker (online MF + top-K serving) on the pipelined engine: the
+    occurrence rounds of a batch's users are planned when it is received
+    (``RoundPlan``) and the PS plans one batch ahead, so the only device->host sync
+    left per micro-batch is the top-K scan's exactness certificate (did any query
+    pass more candidates than the merge holds? then rescan unfused) -- at most one
+    per batch, whatever the repeats of a user inside the batch."""
+    import warnings
+
+    from flink_parameter_server_1_amd.models.mf.topk_tensor import OnlineMFTopKWorker
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogic
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    users, items, B, D = 3000, 5000, 512, 16
+    batches = []
+    for s in range(20):
+        u = torch.randint(0, users, (B,), generator=g, device=DEV)
+        u[:8] = 7  # one user rated several times in the batch: several merge rounds
+        batches.append((u, torch.randint(0, items, (B,), generator=g, device=DEV),
+                        torch.arange(B, device=DEV) + s * B, torch.rand(B, generator=g, device=DEV)))
+    w = OnlineMFTopKWorker(items, D, 0.01, K=20, worker_k=20, memory=64, negative_sample_rate=2,
+                           prefill_items=True, num_users=users, resort_every=1000)
+    logic = DeviceSimplePSLogic(users, D, op="add_renorm", init=("uniform", -0.01, 0.01))
+    rt = TensorRuntime(Comm(device=DEV), staleness=1).start(w, logic)
+    for b in batches[:4]:
+        rt.submit(b)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("warn")
+    try:
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            for b in batches[4:]:
+                rt.submit(b)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    syncs = [r for r in rec if "synchroniz" in str(r.message)]
+    assert len(syncs) <= 16, [str(r.message)[:120] for r in syncs]
+    out = rt.finish()
+    tops = [e.value for e in out if isinstance(e, Left)]
+    assert len(tops) == 20
+    (u0, _, _), S0, I0 = tops[-1]
+    assert S0.shape == (B, 20) and bool((I0[:, 0] >= 0).all())
+
+
 def test_pipelined_pa_worker_issues_no_implicit_sync():
     """PAWorker on the pipelined engine (staleness 1): labelled and unlabelled
     examples mixed in every micro-batch, predictions emitted as MaskedPairs --

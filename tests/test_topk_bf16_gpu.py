@@ -184,7 +184,11 @@ def test_lemp_device_coord_bound_exact_and_skips(strategy):
     s, i = idx.query(Q, k)
     ref = torch.topk(Q @ X.t(), k, dim=1)
     torch.testing.assert_close(s, ref.values, rtol=1e-5, atol=1e-5)
-    assert torch.equal(i, ids[ref.indices])
+    # ids: equal to brute force up to near-ties (axis-dominated items tie closely); every
+    # returned item really has the score reported for it
+    assert (i == ids[ref.indices]).float().mean() > 0.99
+    mine = (Q.double().unsqueeze(1) * X.double()[(i - 1) // 3]).sum(-1)
+    torch.testing.assert_close(mine.float(), ref.values, rtol=1e-5, atol=1e-5)
     scored, skipped = idx.coord_stats.tolist()
     if strategy in ("coord", "lc:1.05"):
         assert skipped > 0 and scored > 0, (scored, skipped)
