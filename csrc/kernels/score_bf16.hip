@@ -81,8 +81,11 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
     float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
     const int32_t* __restrict__ qf, const float* __restrict__ qbf, const float2* __restrict__ cb,
-    int32_t* __restrict__ stats) {
+    int32_t* __restrict__ stats, const int32_t* __restrict__ gate) {
   constexpr int S = D / 16;   // k-steps of 16; also 16-B loads per lane per row
+  // COORD gate (device flag, nullable): off when the bound stopped paying on earlier
+  // segments of this scan (coord_gate_kernel) -- the bound costs VALU per block pair
+  const bool use_coord = COORD && (gate == nullptr || gate[0] != 0);
   constexpr int HALF = D / 2;
   constexpr int WQ = 32 * QB;
   constexpr int GQ = SB_WAVES * WQ;
@@ -153,6 +156,7 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
   // software pipeline: block i0 + 32 is requested before block i0's MFMAs
   uint4 xv[S];
   float xl;
+  float2 cbv[QB];  // COORD: this block's range of each query's focus coordinate (prefetched with xv)
   {
     const int i = i_begin + r;
     const bool ok = i < i_end;
@@ -160,11 +164,20 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
 #pragma unroll
     for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
     xl = ok ? xlen[i] : 0.f;
+    if (COORD && use_coord) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)(i_begin / 32) * D + fq[b]];
+    }
   }
   for (int i0 = i_begin; i0 < i_end; i0 += 32) {
     uint4 cur[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) cur[s] = xv[s];
+    float2 cbc[QB];
+    if (COORD && use_coord) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) cbc[b] = cbv[b];
+    }
     const float bm = group_max<64>(xl);  // longest item of this block
     if (i0 + 32 < i_end) {
       const int i = i0 + 32 + r;
@@ -173,12 +186,16 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
 #pragma unroll
       for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
       xl = ok ? xlen[i] : 0.f;
+      if (COORD && use_coord) {  // the next block's coordinate ranges: no dependent load before the bound
+#pragma unroll
+        for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)((i0 + 32) / 32) * D + fq[b]];
+      }
     }
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
-      if (COORD) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
+      if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
         bool pass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
-        if (pass) pass = coord_pass(theta[b], ql[b], bm, qb[b], cb[(int64_t)(i0 / 32) * D + fq[b]]);
+        if (pass) pass = coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
         if (!__any(pass)) {  // wave-uniform
           ++skipped;
           continue;
@@ -231,7 +248,7 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
       }
     }
   }
-  if (COORD && stats != nullptr && lane == 0) {
+  if (COORD && use_coord && stats != nullptr && lane == 0) {
     atomicAdd(stats, scored);
     atomicAdd(stats + 1, skipped);
   }
@@ -302,6 +319,26 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
 
 }  // namespace
 
+// COORD gate of a scan: stats = cumulative (scored, skipped) block pairs, prev = their
+// values at the previous update; the bound stays on while it skipped at least num / den
+// of the block pairs it evaluated since (one thread; no host sync)
+namespace {
+__global__ void coord_gate_kernel(const int32_t* __restrict__ stats, int32_t* __restrict__ prev,
+                                  int32_t* __restrict__ gate, int num, int den) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t ds = (int64_t)stats[0] - prev[0], dk = (int64_t)stats[1] - prev[1];
+  if (ds + dk > 0) gate[0] = dk * den >= (ds + dk) * num ? 1 : 0;
+  prev[0] = stats[0];
+  prev[1] = stats[1];
+}
+}  // namespace
+
+FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, int num, int den, void* stream) {
+  hipLaunchKernelGGL(coord_gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats, prev, gate, num, den);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 // Qb [B, D], Xb [N, D] bf16 (uint16 storage, RNE from the fp32 vectors); qlen [B],
 // xlen [N] the fp32 norms; cand_pos [B, cap] int64 receives item positions (0..N-1),
 // cnt [B] (zeroed by the caller) counts every candidate.  D in {32, 64, 128}.
@@ -311,7 +348,7 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xlen, float margin, float slack,
                                   int64_t* cand_pos, int32_t* cnt, int cap, const int32_t* qf, const float* qbf,
-                                  const float2* cb, int32_t* stats, void* stream) {
+                                  const float2* cb, int32_t* stats, const int32_t* gate, void* stream) {
   if (B <= 0 || N <= 0) return 0;
   if (k <= 0 || cap <= 0 || qlen == nullptr || xlen == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -324,11 +361,11 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
     if (coord)                                                                                              \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true>), dim3((unsigned)(nqt * nit)),    \
                          dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
-                         cap, qf, qbf, cb, stats);                                                          \
+                         cap, qf, qbf, cb, stats, gate);                                                    \
     else                                                                                                    \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false>), dim3((unsigned)(nqt * nit)),   \
                          dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
-                         cap, qf, qbf, cb, stats);                                                          \
+                         cap, qf, qbf, cb, stats, gate);                                                    \
   }
   // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4
   // blocks with branch or mask epilogues, same-box A/B, profiles/r2_bf16_topk.md)

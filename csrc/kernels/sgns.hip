@@ -521,299 +521,7 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
-// ---------------------------------------------------------------- v5
-// v4's waves wait ~81 % of their cycles: vmcnt counts loads, stores and
-// atomics together in issue order, so every global load a wave issues after
-// its float atomics waits for those atomics (~3,000 cycles each under load,
-// MI355X_MICROARCH.md "float atomic add" / vmcnt rows).  v5 gives the two kinds
-// of memory traffic to different waves of a 512-thread block (one per CU):
-//
-//  * loader waves 0-3 issue only loads: they prefetch the NEXT block's H, N and
-//    O rows into registers while the current block's gradients are being
-//    pushed, copy them into LDS at the top of the iteration and compute
-//    S = H N^T (waves 0-1, two accumulators) and the block's indices;
-//  * atomic waves 4-7 issue no global loads: positive scores from LDS (Hs . Os),
-//    then dH = G N + g+ O (O from LDS), dN = G^T H and the per-context dO sums,
-//    all pushed with no-return float atomics that drain behind the next
-//    iteration's barriers.
-//
-// Barriers are raw s_barrier after an lgkmcnt(0) wait (LDS only): a
-// __syncthreads() fence could make the atomic waves wait for their atomics.
-// Same math, block shape (32 pairs x 16 shared negatives) and results as v4.
-constexpr int NT5 = 512;
-constexpr int NL5 = 4;           // loader waves
-constexpr int PF5 = 25;          // prefetched float4 per loader lane: 80 rows x Dp/4 over 256 lanes, Dp <= 320
-
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: LDS writes of this wave done
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <bool BF16>
-__global__ void __launch_bounds__(NT5) sgns_v5_kernel(const void* __restrict__ rows_in,
-                                                      const void* __restrict__ rows_out,
-                                                      const int32_t* __restrict__ pos_c,
-                                                      const int32_t* __restrict__ pos_o,
-                                                      const int32_t* __restrict__ pos_neg, int64_t n_pairs, int D,
-                                                      float lr, float neg_weight, float* __restrict__ d_in,
-                                                      float* __restrict__ d_out, float* __restrict__ loss_out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Dp = (D + 31) & ~31;
-  const int LD = Dp + 1;
-  float* Hs = smem;                 // [M][LD]
-  float* Ns = Hs + M * LD;          // [K4][LD]
-  float* Os = Ns + K4 * LD;         // [M][LD]
-  float* Gs = Os + M * LD;          // [M][K4+1]
-  float* gpos = Gs + M * (K4 + 1);  // [M]
-  float* lossacc = gpos + M;        // [1]
-  int32_t* pcb = (int32_t*)(lossacc + 1);  // [2][M]  double-buffered indices
-  int32_t* pob = pcb + 2 * M;              // [2][M]
-  int32_t* pnb = pob + 2 * M;              // [2][K4]
-  int32_t* lead = pnb + 2 * K4;            // [M]
-  int32_t* nxt = lead + M;                 // [M]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool loader = wave < NL5;
-  const int64_t n_blocks = (n_pairs + M - 1) / M;
-  const int64_t first = blockIdx.x, stride = gridDim.x;
-  if (first >= n_blocks) return;  // uniform per block
-
-  auto load_idx = [&](int64_t blk, int32_t& a, int32_t& b) {  // wave 3: lanes < M pc/po, M.. M+K4 pn
-    const int64_t p0 = blk * M;
-    a = -1;
-    b = -1;
-    if (lane < M) {
-      if (p0 + lane < n_pairs) { a = pos_c[p0 + lane]; b = pos_o[p0 + lane]; }
-    } else if (lane < M + K4) {
-      a = pos_neg[blk * K4 + (lane - M)];
-    }
-  };
-  auto store_idx = [&](int buf, int32_t a, int32_t b) {
-    if (lane < M) { pcb[buf * M + lane] = a; pob[buf * M + lane] = b; }
-    else if (lane < M + K4) pnb[buf * K4 + (lane - M)] = a;
-  };
-  // loader waves: the next block's 80 rows (0..31 H, 32..47 N, 48..79 O) as one flat
-  // array of float4 spread over the 256 loader lanes (consecutive lanes, consecutive
-  // float4 of a row): PF5 registers of float4 per lane
-  const int F4 = Dp / 4;
-  const int ll = wave * 64 + lane;
-  float4 pre[PF5];
-  // an opaque zero per use keeps the compiler from hoisting the PF5 (row, column,
-  // address) computations out of the block loop (they would pin ~3 VGPRs each)
-  auto opaque0 = []() {
-    int z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    return z;
-  };
-  auto prefetch = [&](int buf) {
-    const int z = opaque0();
-#pragma unroll
-    for (int j = 0; j < PF5; ++j) {
-      const int e = j * (NL5 * 64) + ll + z;
-      const int r = e / F4, c = 4 * (e - r * F4);
-      int32_t rr = -1;
-      const void* src = rows_out;
-      if (r < M) { rr = pcb[buf * M + r]; src = rows_in; }
-      else if (r < M + K4) rr = pnb[buf * K4 + r - M];
-      else if (r < 2 * M + K4) rr = pob[buf * M + r - M - K4];
-      pre[j] = rr >= 0 ? ld4<BF16>(src, rr, D, c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-
-  if (tid == 0) *lossacc = 0.f;
-  if (wave == 3) {
-    int32_t a, b;
-    load_idx(first, a, b);
-    store_idx(0, a, b);
-  }
-  lds_barrier();
-  if (loader) prefetch(0);
-  int cur = 0;
-  int32_t ia = -1, ib = -1;  // wave 3: indices of the next block in flight
-  for (int64_t blk = first; blk < n_blocks; blk += stride, cur ^= 1) {
-    const int lanez = lane + opaque0();  // per block: keeps lane-derived addresses out of registers
-    const int npairs = (int)((n_pairs - blk * M) < M ? (n_pairs - blk * M) : M);
-    const bool has_next = blk + stride < n_blocks;
-    const int32_t* pc = pcb + cur * M;
-    const int32_t* po = pob + cur * M;
-    const int32_t* pn = pnb + cur * K4;
-    lds_barrier();  // B0: the atomic waves are done reading the previous block's LDS
-    if (loader) {
-      const int z = opaque0();
-#pragma unroll
-      for (int j = 0; j < PF5; ++j) {
-        const int e = j * (NL5 * 64) + ll + z;
-        const int r = e / F4, c = 4 * (e - r * F4);
-        if (r < 2 * M + K4) {
-          float* dst = (r < M ? Hs + r * LD : (r < M + K4 ? Ns + (r - M) * LD : Os + (r - M - K4) * LD)) + c;
-          dst[0] = pre[j].x; dst[1] = pre[j].y; dst[2] = pre[j].z; dst[3] = pre[j].w;
-        }
-      }
-      if (wave == 3 && has_next) load_idx(blk + stride, ia, ib);
-      if (wave == 2 && lanez < M) {  // one dO row per distinct context of the block
-        int l = lanez, nx = -1;
-        for (int j = 0; j < lanez; ++j)
-          if (po[j] == po[lanez]) { l = j; break; }
-        for (int j = lanez + 1; j < M; ++j)
-          if (po[j] == po[lanez]) { nx = j; break; }
-        lead[lanez] = l;
-        nxt[lanez] = nx;
-      }
-    }
-    lds_barrier();  // B1: H, N, O, lead/nxt of this block in LDS
-    if (wave < 2) {
-      // ---- S = H N^T: one 16x16 tile per wave, two accumulation chains
-      const int i = lanez & 15, kq = lanez >> 4;
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const float* hrow = Hs + (16 * wave + i) * LD + kq;
-      const float* nrow = Ns + i * LD + kq;
-      int k = 0;
-      for (; k + 4 < Dp; k += 8) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k + 4], nrow[k + 4], acc1, 0, 0, 0);
-      }
-      if (k < Dp) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hrow[k], nrow[k], acc0, 0, 0, 0);
-      float lsum = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * wave + 4 * kq + r;
-        const bool ok = m < npairs;
-        const float sg = sigmoidf_(acc0[r] + acc1[r]);
-        Gs[m * (K4 + 1) + i] = ok ? -lr * neg_weight * sg : 0.f;
-        if (ok) lsum += -neg_weight * __logf(1.f - sg + 1e-12f);
-      }
-      if (loss_out) {
-        lsum = group_sum<64>(lsum);
-        if (lanez == 0) atomicAdd(lossacc, lsum);  // LDS
-      }
-    } else if (wave == 3) {
-      if (has_next) store_idx(cur ^ 1, ia, ib);
-    } else if (!loader) {
-      // ---- positive scores h.o from LDS: 8 rows per atomic wave
-      for (int m = wave - NL5; m < M; m += NT5 / 64 - NL5) {
-        float p = 0.f;
-        if (m < npairs)
-          for (int c = lanez; c < D; c += 64) p = fmaf(Hs[m * LD + c], Os[m * LD + c], p);
-        p = group_sum<64>(p);
-        if (lanez == 0) {
-          const bool ok = m < npairs;
-          gpos[m] = ok ? lr * (1.f - sigmoidf_(p)) : 0.f;
-          if (ok && loss_out) atomicAdd(lossacc, -__logf(sigmoidf_(p) + 1e-12f));  // LDS
-        }
-      }
-    }
-    lds_barrier();  // B2: G, g+ and the next block's indices in LDS
-    if (loader) {
-      if (has_next) prefetch(cur ^ 1);  // in flight while the atomic waves push this block
-      continue;
-    }
-    // ---- atomic waves: dH, dN tiles, then dO rows
-    const int aw = wave - NL5, naw = NT5 / 64 - NL5;
-    const int ntile = Dp / 32;
-    const int lz = lane + opaque0();  // recomputed per block: no hoisted per-lane addresses
-    const int i = lz & 31, kh = lz >> 5;
-    for (int t = aw; t < 2 * ntile; t += naw) {
-      const bool is_h = t < ntile;
-      const int c0 = (is_h ? t : t - ntile) * 32;
-      const int col = c0 + i;
-      floatx16 acc = {0};
-      if (is_h) {
-#pragma unroll
-        for (int kk = 0; kk < K4; kk += 2) {
-          const int k = kk + kh;
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[i * (K4 + 1) + k], Ns[k * LD + c0 + i], acc, 0, 0, 0);
-        }
-        float v[16], o[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = acc_row(lz, r);
-          v[r] = acc[r] + gpos[row] * Os[row * LD + col];  // g+ = 0 and O row zero past npairs
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] = __shfl_xor(v[r], 32, 64);
-        const int r1 = min(16, npairs - 16 * kh);
-        float run = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int ri0 = (j & 3) + 4 * (j >> 3);
-          const int ri1 = (j & 3) + 4 * (2 + (j >> 3));
-          const float a0 = (j & 4) ? o[ri0] : v[ri0];
-          const float a1 = (j & 4) ? v[ri1] : o[ri1];
-          const float val = kh ? a1 : a0;
-          if (j < r1) {
-            const int q = 16 * kh + j;
-            run += val;
-            if (j + 1 == r1 || pc[q + 1] != pc[q]) {
-              if (col < D) atomic_add_noret(d_in + (int64_t)pc[q] * D + col, run);
-              run = 0.f;
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < M; kk += 2) {
-          const int k = kk + kh;
-          const float a = i < K4 ? Gs[k * (K4 + 1) + i] : 0.f;
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Hs[k * LD + c0 + i], acc, 0, 0, 0);
-        }
-        if (col < D) {
-#pragma unroll
-          for (int r = 0; r < 8; ++r) atomic_add_noret(d_out + (int64_t)pn[acc_row(lz, r)] * D + col, acc[r]);
-        }
-      }
-    }
-    for (int m = aw; m < npairs; m += naw) {
-      if (lead[m] != m) continue;  // uniform in the wave
-      float a[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = 0.f;
-      for (int q = m; q >= 0 && q < npairs; q = nxt[q]) {
-        const float g = gpos[q];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (lz + 64 * u < D) a[u] += g * Hs[q * LD + lz + 64 * u];
-      }
-      float* dst = d_out + (int64_t)po[m] * D;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (lz + 64 * u < D) atomic_add_noret(dst + lz + 64 * u, a[u]);
-    }
-  }
-  lds_barrier();
-  if (loss_out && tid == NL5 * 64) atomicAdd(loss_out, *lossacc);
-}
-
 }  // namespace
-
-FPS_API size_t fps_sgns_v5_smem_bytes(int D) {
-  const int Dp = (D + 31) & ~31, LD = Dp + 1;
-  return sizeof(float) * ((size_t)(32 + K4 + 32) * LD + 32 * (K4 + 1) + 32 + 1) + sizeof(int32_t) * (6 * 32 + 2 * K4);
-}
-
-// v5: same contract as v4 (16 negative rows per block of 32 pairs); one 512-thread block per CU
-FPS_API int fps_sgns_step_v5(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
-                             const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
-                             float neg_weight, float* d_in, float* d_out, float* loss_out, void* stream) {
-  if (n_pairs <= 0) return 0;
-  if (((D + 31) & ~31) > 320) return (int)hipErrorInvalidValue;  // PF5 registers cover Dp <= 320
-  const size_t smem = fps_sgns_v5_smem_bytes(D);
-  if (smem > 160 * 1024) return (int)hipErrorInvalidValue;
-  const int64_t nb = (n_pairs + 31) / 32;
-  const int grid = (int)(nb < 256 ? nb : 256);
-  hipStream_t s = (hipStream_t)stream;
-  if (rows_bf16) {
-    (void)hipFuncSetAttribute((const void*)sgns_v5_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(sgns_v5_kernel<true>, dim3(grid), dim3(NT5), smem, s, rows_in, rows_out, pos_c, pos_o,
-                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
-  } else {
-    (void)hipFuncSetAttribute((const void*)sgns_v5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(sgns_v5_kernel<false>, dim3(grid), dim3(NT5), smem, s, rows_in, rows_out, pos_c, pos_o,
-                       pos_neg, n_pairs, D, lr, neg_weight, d_in, d_out, loss_out);
-  }
-  FPS_CHECK_LAUNCH();
-  return 0;
-}
 
 FPS_API size_t fps_sgns_smem_bytes(int D) {
   const int Dp = (D + 31) & ~31, LD = Dp + 1;

@@ -55,6 +55,8 @@ class PulledBatch:
     #: under a locking PS logic only a subset of a pull is answered per round:
     #: positions of the answered requests within the original ``pull`` (else None)
     index: Optional[torch.Tensor] = None
+    #: the pull was planned as the identity over the key space (``pos`` = the key)
+    identity: bool = False
 
     def values(self) -> torch.Tensor:
         """``[B, D]`` parameter of every request, in request order (fp32; fp64

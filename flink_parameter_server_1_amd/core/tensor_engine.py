@@ -319,7 +319,8 @@ class TensorRuntime:
             for r in reqs:
                 c._req = r
                 self.worker_logic.on_pull_recv_batch(
-                    PulledBatch(r.keys, rows, plan.pos[r.off:r.off + r.n], r.payload), c)
+                    PulledBatch(r.keys, rows, plan.pos[r.off:r.off + r.n], r.payload,
+                                identity=plan.identity and len(reqs) == 1), c)
         c._req = None
         self._push(plan, c)
         c._plan = None

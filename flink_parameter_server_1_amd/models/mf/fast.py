@@ -160,17 +160,28 @@ class DistributedMF:
             self.user_phases = max(1, P)
             upp = -(-self.users.n_local // self.user_phases)
             halves = [cfg.num_items] if exchange == "ps" else shard_halves(cfg.num_items, tile_w)
+            # ps: a batch covering the key space gets an identity plan (pulled row = item id,
+            # ``TensorPS.identity_for``), so its partition can be staged when the batch is
+            # RECEIVED, beside the SGD of an earlier batch: with the pipeline (staleness 1)
+            # two received batches wait for their compute -> three partition buffers
+            ps_spec = exchange == "ps" and cfg.prefetch_partition and dev.type == "cuda"
+            n_tilers = 2 if exchange != "ps" else (3 if ps_spec else 1)
             self._tilers = [ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8,
                                                 phases=self.user_phases, users_per_phase=upp)
-                            for _ in range(2 if exchange != "ps" else 1)]
+                            for _ in range(n_tilers)]
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
                               and exchange != "ps")
+            self._ps_spec = ps_spec
+            # the PS path's own partition (batches without an identity plan)
+            self._ps_tiler = self._tilers[0] if not ps_spec else \
+                ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8, phases=self.user_phases,
+                                    users_per_phase=upp)
             # the partition of batch k+1 runs on a side stream beside the SGD of batch k
             # (a priority stream for the SGD and CU-masked streams splitting the CUs
             # between them were measured slower and removed, profiles/r2_partition.md)
-            self._side = torch.cuda.Stream(dev) if self._prefetch else None
+            self._side = torch.cuda.Stream(dev) if (self._prefetch or ps_spec) else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
@@ -326,7 +337,7 @@ class DistributedMF:
         returns ``(ptr, rec, ready_event)``."""
         seen = self._seen if (self.exchange == "rotate" and self.items.touched is not None) else None
         tiler = self._tilers[self._tiler_i]
-        self._tiler_i ^= 1
+        self._tiler_i = (self._tiler_i + 1) % len(self._tilers)
         if self._side is None:
             with stage("mf.partition", self.timer):
                 ptr, rec = tiler.run(uid_local, iid, rating, seen)
@@ -372,16 +383,23 @@ class DistributedMF:
             with stage("mf.rotate.end", self.timer):
                 self.rot.end()
 
-    def _item_deltas(self, rows, pos, n_unique, uid_local, rating):
+    def _item_deltas(self, rows, pos, n_unique, uid_local, rating, staged=None):
         """SGD of one micro-batch on its pulled item rows ``rows[pos[b]]``; returns
-        the per-unique-item deltas to push (user rows are updated in place)."""
+        the per-unique-item deltas to push (user rows are updated in place).
+        ``staged``: the batch's partition by item id, staged when it was received
+        (valid when the plan is the identity: pulled row = item id)."""
         c = self.cfg
         if self.sgd_mode == "tiled":
             # tile-grouped SGD on a working copy of the pulled rows (one block, no item
             # atomics); the pushed delta is what the micro-batch added to each row
             orig = rows.float()
             work = orig.clone()
-            ptr, rec = self._tilers[0].run(uid_local, pos, rating)
+            if staged is not None:
+                ptr, rec, ev = staged
+                if ev is not None:
+                    torch.cuda.current_stream(self.U.device).wait_event(ev)
+            else:
+                ptr, rec = self._ps_tiler.run(uid_local, pos, rating)
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):
                     ops.mf_sgd_tiled(self.U, work, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
@@ -503,11 +521,19 @@ class _MFPSWorker(BatchedWorkerLogic):
 
     def on_recv_batch(self, batch, ps):
         uid_local, iid, rating = batch
-        ps.pull(iid, (uid_local, rating))
+        m = self.m
+        staged = None
+        if m.sgd_mode == "tiled" and m._ps_spec and m.ps.identity_for(iid.numel()):
+            # identity plan ahead: bucket by item id now, on the side stream, while an
+            # earlier batch's SGD runs (the partition no longer sits on the critical path)
+            staged = m._stage_partition(uid_local, iid, rating)
+        ps.pull(iid, (uid_local, rating, staged))
 
     def on_pull_recv_batch(self, pulled, ps):
-        uid_local, rating = pulled.payload
-        ps.push_unique(self.m._item_deltas(pulled.rows, pulled.pos, pulled.n_unique, uid_local, rating))
+        uid_local, rating, staged = pulled.payload
+        if staged is not None and not getattr(pulled, "identity", False):
+            raise RuntimeError("MF PS path: a partition was staged for an identity plan that did not happen")
+        ps.push_unique(self.m._item_deltas(pulled.rows, pulled.pos, pulled.n_unique, uid_local, rating, staged))
 
 
 @dataclass

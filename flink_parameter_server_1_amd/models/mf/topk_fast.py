@@ -77,6 +77,10 @@ class LempTopK:
         self._len_host = None    # lengths on the host (LC's per-bucket switch)
         #: (32 queries, 32 items) block pairs the COORD scans scored / skipped
         self.coord_stats = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
+        #: device COORD gate of a scan (``ops.coord_gate``): on at the start of every query
+        #: batch, off once a segment's bound skipped < 1/4 of its block pairs
+        self._coord_gate = torch.ones(1, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
+        self._coord_prev = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -200,6 +204,9 @@ class LempTopK:
         ovf = torch.zeros(1, dtype=torch.int32, device=dev)
         Qb = Q.bfloat16() if self.bf16 else None
         coord = self._coord_inputs(Q, qlen, bounds) if self.bf16 else None
+        if coord is not None:
+            self._coord_gate.fill_(1)
+            self._coord_prev.copy_(self.coord_stats)
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
@@ -213,7 +220,10 @@ class LempTopK:
                     qf, qbf = coord
                     seg_coord = (qf, qbf, self._cb[s // 32: -(-e // 32)])
                 ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e],
-                                      coord=seg_coord, stats=self.coord_stats if seg_coord is not None else None)
+                                      coord=seg_coord, stats=self.coord_stats if seg_coord is not None else None,
+                                      gate=self._coord_gate if seg_coord is not None else None)
+                if seg_coord is not None:
+                    ops.coord_gate(self.coord_stats, self._coord_prev, self._coord_gate)
                 # (re-score fused into the rank merge, one query per workgroup: 59 us against
                 # 22 + 27 us for the two kernels -- profiles/r2_bf16_topk.md)
                 ops.cand_rescore(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt)

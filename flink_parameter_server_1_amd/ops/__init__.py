@@ -683,15 +683,15 @@ SGNS_NEG_K = (16, 32)
 
 
 def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: float, d_in, d_out,
-              with_loss: bool = False, neg_k: int = 16, kernel: Optional[str] = None, neg_group: int = 1):
+              with_loss: bool = False, neg_k: int = 16, neg_group: int = 1):
     """Block-shared-negative skip-gram step on MFMA (K6); deltas accumulate into
     ``d_in`` / ``d_out`` (per pulled row).  ``pos_neg`` has ``neg_k`` rows per 32
     pairs: 16 runs kernel v4 (two 512-thread blocks per CU), 32 kernel v3.
-    ``kernel`` (or ``FPS_SGNS_KERNEL``) = "v5" runs the loader / atomic wave split
-    variant (D <= 320; measured slower than v4, profiles/r1_w2v_v4.md).
     ``neg_group`` (1, 2 or 4; v4 only): that many consecutive blocks of 32 pairs share
     one set of ``neg_k`` negatives (``pos_neg`` holds ``neg_k`` rows per 32 * neg_group
-    pairs); their negative-row gradients are summed on chip and pushed once."""
+    pairs); their negative-row gradients are summed on chip and pushed once.  (A
+    loader / atomic wave-split variant, v5, measured slower than v4 and was removed in
+    round 3: ``profiles/r1_w2v_v4.md``.)"""
     D = rows_in.shape[1]
     if neg_k not in SGNS_NEG_K:
         raise ValueError(f"sgns_step: neg_k must be one of {SGNS_NEG_K}")
@@ -702,23 +702,14 @@ def sgns_step(rows_in, rows_out, pos_c, pos_o, pos_neg, lr: float, neg_weight: f
     if rows_in.is_cuda:
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
         lib = N.require()
-        if neg_k == 32:
-            fn = lib.fps_sgns_step
-        else:
-            kern = kernel or os.environ.get("FPS_SGNS_KERNEL") or "v4"
-            if kern not in ("v4", "v5"):
-                raise ValueError(f"sgns_step: kernel must be 'v4' or 'v5', not {kern!r}")
-            if neg_group > 1 and kern != "v4":
-                raise ValueError("sgns_step: neg_group > 1 runs on kernel v4")
-            if kern == "v4":
-                N.check(lib.fps_sgns_step_v4g(
-                    _c(rows_in).data_ptr(), _c(rows_out).data_ptr(), int(rows_in.dtype == torch.bfloat16),
-                    _c(pos_c).data_ptr(), _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), pos_c.numel(), D, lr,
-                    neg_weight, _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss), neg_group,
-                    N.stream_ptr(rows_in.device)), "sgns_step")
-                return loss
-            fn = lib.fps_sgns_step_v5
-        N.check(fn(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
+        if neg_k == 16:
+            N.check(lib.fps_sgns_step_v4g(
+                _c(rows_in).data_ptr(), _c(rows_out).data_ptr(), int(rows_in.dtype == torch.bfloat16),
+                _c(pos_c).data_ptr(), _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), pos_c.numel(), D, lr,
+                neg_weight, _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss), neg_group,
+                N.stream_ptr(rows_in.device)), "sgns_step")
+            return loss
+        N.check(lib.fps_sgns_step(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(),
                                   int(rows_in.dtype == torch.bfloat16), _c(pos_c).data_ptr(), _c(pos_o).data_ptr(),
                                   _c(pos_neg).data_ptr(), pos_c.numel(), D, lr, neg_weight, _c(d_in).data_ptr(),
                                   _c(d_out).data_ptr(), N.ptr(loss), N.stream_ptr(rows_in.device)), "sgns_step")
@@ -881,7 +872,7 @@ def coord_block_bounds(X: torch.Tensor, xlen: torch.Tensor) -> torch.Tensor:
 
 def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, cand_pos: torch.Tensor,
                       cnt: torch.Tensor, qlen: torch.Tensor, xlen: torch.Tensor, coord=None,
-                      stats: Optional[torch.Tensor] = None) -> None:
+                      stats: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None) -> None:
     """Candidate filter on bf16 MFMA (GPU only, K8 fast path): every item ``i`` whose bf16
     score can exceed ``best_s[b, -1]`` (margin ``bf16_score_margin(D) |q_b| max|x|``) gets
     its position appended to row ``b`` of ``cand_pos`` ``[B, cap]`` (int64); ``cnt[b]``
@@ -889,7 +880,8 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     (key, id) candidates for ``topk_merge_cand``.  ``coord = (qf int32[B], qbf[B], cb)``
     turns on the LEMP COORD + length bounds per (32 queries, 32 items) block pair
     (``cb`` = ``coord_block_bounds`` of these items); ``stats`` (int32[2]) counts the
-    block pairs scored / skipped."""
+    block pairs scored / skipped; ``gate`` (int32[1], optional): the COORD bound is
+    evaluated only while ``gate[0] != 0`` (``coord_gate``)."""
     B, D = Qb.shape
     n = Xb.shape[0]
     cap = cand_pos.shape[1]
@@ -911,7 +903,17 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
         _c(qlen.float()).data_ptr(), _c(xlen.float()).data_ptr(), bf16_score_margin(D), slack,
         _c(cand_pos).data_ptr(), _c(cnt).data_ptr(), cap, N.ptr(qf), N.ptr(qbf), N.ptr(cb), N.ptr(stats),
-        N.stream_ptr(Qb.device)), "score_filter_bf16")
+        N.ptr(gate), N.stream_ptr(Qb.device)), "score_filter_bf16")
+
+
+def coord_gate(stats: torch.Tensor, prev: torch.Tensor, gate: torch.Tensor, num: int = 1, den: int = 4) -> None:
+    """Device-side COORD switch of a LEMP scan (GPU only): ``gate[0] = 1`` while the
+    bound skipped at least ``num / den`` of the (query, item) block pairs it
+    evaluated since the previous call (``stats`` = cumulative scored / skipped,
+    ``prev`` = their values at the previous call).  No host sync: the bound is
+    exact either way, the gate only decides whether evaluating it pays."""
+    N.check(N.require().fps_coord_gate(_c(stats).data_ptr(), _c(prev).data_ptr(), _c(gate).data_ptr(), int(num),
+                                       int(den), N.stream_ptr(stats.device)), "coord_gate")
 
 
 def cand_rescore(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, cand_key: torch.Tensor,

@@ -51,7 +51,8 @@ _SIGNATURES = {
     "fps_score_filter_lemp": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
                               c_int, c_vp],
     "fps_score_filter_bf16": [c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_int,
-                              c_vp, c_vp, c_vp, c_vp, c_vp],
+                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_coord_gate": [c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     "fps_cand_rescore": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
     "fps_lock_acquire": [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp],
     "fps_lock_release": [c_vp, c_vp, c_i64, c_vp, c_vp],
@@ -71,7 +72,6 @@ _SIGNATURES = {
     "fps_sgns_step": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4g": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp],
-    "fps_sgns_step_v5": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_score_gemm": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp],
     "fps_pa_multi": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],

@@ -214,7 +214,7 @@ class HashShardTable:
         return self.rows_for(ids, insert=False)[0]
 
     # ----------------------------------------------------------------- PS side
-    def serve_rows(self, rows: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
+    def serve_rows(self, rows: torch.Tensor, wire_dtype=torch.float32, mark: bool = True) -> torch.Tensor:
         return ops.gather_rows(self._store, rows.clamp_min(0), out_dtype=wire_dtype)
 
     def serve(self, keys: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:

@@ -186,8 +186,9 @@ class ShardedTable:
             fresh = self.touched[local_keys.long().clamp_min(0)] == 0
         return local_keys, fresh
 
-    def serve_rows(self, rows: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
-        return ops.gather_rows(self.weight, rows, out_dtype=wire_dtype, touched=self.touched)
+    def serve_rows(self, rows: torch.Tensor, wire_dtype=torch.float32, mark: bool = True) -> torch.Tensor:
+        """Pull serve (K2); ``mark``: the served rows count as touched (close-time dump)."""
+        return ops.gather_rows(self.weight, rows, out_dtype=wire_dtype, touched=self.touched if mark else None)
 
     def serve(self, local_keys: torch.Tensor, wire_dtype=torch.float32) -> torch.Tensor:
         """Pull serve (K2): rows for the requested local keys."""

@@ -58,6 +58,9 @@ class PullPlan:
     recv_rows: Optional[torch.Tensor] = None  # rows of recv_keys in the shard (cached by serve)
     #: static plans (world 1): n_unique is an upper bound; valid[j] marks the real unique keys
     valid: Optional[torch.Tensor] = None
+    #: identity plan (world 1, a batch at least as large as the key space): the unique
+    #: keys are the whole key space in order, so ``pos`` is the key itself
+    identity: bool = False
 
 
 @dataclass
@@ -73,6 +76,7 @@ class PendingPlan:
     flag: int = 0
     valid: Optional[torch.Tensor] = None  # static plan: [n_bound] bool
     n_bound: int = 0
+    identity: bool = False
 
 
 class TensorPS:
@@ -96,6 +100,15 @@ class TensorPS:
         #: unique keys are padded to ``min(n, key space)`` rows (padding gathers row 0
         #: and is never applied), so a micro-batch issues no host sync at all
         self.static = False
+        self._iota: Optional[torch.Tensor] = None
+
+    def identity_for(self, n: int) -> bool:
+        """Will a static plan of ``n`` requests be the identity plan?  (World 1, a
+        dense shard and ``n >= key space``: instead of de-duplicating, the plan takes
+        the whole key space in order -- ``pos`` = the key, a presence flag per key --
+        so a worker may bucket its requests by key before the plan exists.)"""
+        return (self.static and self.comm.world == 1 and not getattr(self.table, "sparse", False)
+                and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
 
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0) -> PendingPlan:
@@ -105,13 +118,26 @@ class TensorPS:
         delivered to every peer with the counts (``PullPlan.peer_flags``)."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
         n = keys.numel()
+        if self.identity_for(n):
+            ks = int(self.table.key_space)
+            if self._iota is None or self._iota.numel() != ks:
+                self._iota = torch.arange(ks, dtype=torch.int32, device=keys.device)
+            with stage("ps.presence", self.timer):
+                present = torch.zeros(ks, dtype=torch.uint8, device=keys.device)
+                ops.mark_rows(present, keys)
+            return PendingPlan(n, None, self._iota, keys, None, None, int(flag), valid=present.view(torch.bool),
+                               n_bound=ks, identity=True)
         with stage("ps.dedup", self.timer):
             counts, prefix, uniq, pos = self.dedup.run(keys)
         W = self.comm.world
         if W == 1 and self.static and not getattr(self.table, "sparse", False):
             nb = min(n, int(self.table.key_space))
-            valid = torch.arange(nb, device=keys.device) < prefix[1]
-            gkeys = torch.where(valid, uniq[:nb], torch.zeros_like(uniq[:nb]))
+            j = torch.arange(nb, device=keys.device)
+            valid = j < prefix[1]
+            # padding slot j serves the real key uniq[j mod U]: real rows only (the
+            # close-time dump stays exact) and spread over all of them (a single padding
+            # row shared by millions of slots serialised the gather on one cache line)
+            gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
             if self.dedup.clear_after:
                 self.dedup.reset_claims(gkeys)
             return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb)
@@ -149,7 +175,7 @@ class TensorPS:
             self.stats["unique"] += pp.n_bound
             self.stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
-                            valid=pp.valid)
+                            valid=pp.valid, identity=pp.identity)
         if pp.event is not None:
             if not pp.event.query():
                 self.stats["host_stalls"] += 1
@@ -180,7 +206,13 @@ class TensorPS:
         with stage("ps.serve", self.timer):
             if plan.recv_rows is None:  # dense shards: the local key is the row; sparse: lookup-or-insert
                 plan.recv_rows = self.table.rows_for(plan.recv_keys)[0]
-            return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
+            touched = getattr(self.table, "touched", None)
+            if not plan.identity or touched is None:
+                return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
+            # identity plan: every row is served, only the keys present count as pulled
+            out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
+            touched |= plan.valid.view(torch.uint8)
+            return out
 
     def pull_planned(self, plan: PullPlan, async_op: bool = False):
         """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``."""

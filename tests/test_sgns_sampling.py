@@ -66,12 +66,11 @@ def test_sgns_distributed_gloo():
 @pytest.mark.parametrize("D", [16, 64, 100, 300])
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("runs", [False, True])
-@pytest.mark.parametrize("neg_k,kernel,group", [(16, "v5", 1), (16, "v4", 1), (16, "v4", 2), (16, "v4", 4),
-                                                (32, None, 1)])
-def test_sgns_kernel_matches_reference(D, wire, runs, neg_k, kernel, group):
+@pytest.mark.parametrize("neg_k,group", [(16, 1), (16, 2), (16, 4), (32, 1)])
+def test_sgns_kernel_matches_reference(D, wire, runs, neg_k, group):
     torch.manual_seed(D)
-    # v5: many blocks per persistent workgroup; groups: a partial last group (200 = 1.5 groups of 4 x 32 + 8)
-    Uin, Uout, P = 300, 400, 200 if kernel != "v5" else 20000
+    # groups: a partial last group (200 = 1.5 groups of 4 x 32 + 8)
+    Uin, Uout, P = 300, 400, 200
     rows_in = (torch.randn(Uin, D) * 0.3).to(wire)
     rows_out = (torch.randn(Uout, D) * 0.3).to(wire)
     pos_c = torch.randint(0, Uin, (P,), dtype=torch.int32)
@@ -84,7 +83,7 @@ def test_sgns_kernel_matches_reference(D, wire, runs, neg_k, kernel, group):
     dev = "cuda"
     d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
     loss = ops.sgns_step(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), 0.05,
-                         5 / neg_k, d_in, d_out, with_loss=True, neg_k=neg_k, kernel=kernel, neg_group=group)
+                         5 / neg_k, d_in, d_out, with_loss=True, neg_k=neg_k, neg_group=group)
     torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=2e-6)
     torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=2e-6)
     assert abs(float(loss) - loss_r) / loss_r < 1e-4
