@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
   constexpr int S = D / 16;   // k-steps of 16; also 16-B loads per lane per row
   // COORD gate (device flag, nullable): off when the bound stopped paying on earlier
   // segments of this scan (coord_gate_kernel) -- the bound costs VALU per block pair
-  const bool use_coord = COORD && (gate == nullptr || gate[0] != 0);
+  const bool use_coord = COORD && (gate == nullptr || gate[0] > 0);
   constexpr int HALF = D / 2;
   constexpr int WQ = 32 * QB;
   constexpr int GQ = SB_WAVES * WQ;
@@ -319,22 +319,28 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
 
 }  // namespace
 
-// COORD gate of a scan: stats = cumulative (scored, skipped) block pairs, prev = their
-// values at the previous update; the bound stays on while it skipped at least num / den
-// of the block pairs it evaluated since (one thread; no host sync)
+// COORD gate of a scan (evaluated while gate > 0): stats = cumulative (scored,
+// skipped) block pairs, prev = their values at the previous update.  After a segment
+// that evaluated the bound: on (1) if it skipped at least num / den of the block pairs,
+// else off for the next `rest` segments (gate = -rest + 1 .. 0), after which the bound
+// is probed again -- later LEMP buckets hold shorter items, where it prunes more.
+// One thread; no host sync.
 namespace {
 __global__ void coord_gate_kernel(const int32_t* __restrict__ stats, int32_t* __restrict__ prev,
-                                  int32_t* __restrict__ gate, int num, int den) {
+                                  int32_t* __restrict__ gate, int num, int den, int rest) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int64_t ds = (int64_t)stats[0] - prev[0], dk = (int64_t)stats[1] - prev[1];
-  if (ds + dk > 0) gate[0] = dk * den >= (ds + dk) * num ? 1 : 0;
+  if (ds + dk > 0) gate[0] = dk * den >= (ds + dk) * num ? 1 : 1 - rest;
+  else gate[0] += 1;
   prev[0] = stats[0];
   prev[1] = stats[1];
 }
 }  // namespace
 
-FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, int num, int den, void* stream) {
-  hipLaunchKernelGGL(coord_gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats, prev, gate, num, den);
+FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, int num, int den, int rest,
+                           void* stream) {
+  hipLaunchKernelGGL(coord_gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats, prev, gate, num, den,
+                     rest);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -184,23 +184,33 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
   }
   __syncthreads();
   if (m_n == 0) return;  // after the only barrier
-  float acc[NPL];
-#pragma unroll
-  for (int m = 0; m < NPL; ++m) acc[m] = 0.f;
+  // A run that starts inside the range loads its row when it starts (the load hides
+  // behind the run's gathers) and stores row + sum when it ends; a run cut by a range
+  // end adds its sum with atomics instead.
+  float acc[NPL], base[NPL];
   int32_t cur = s_row[wv][0];
   bool whole = t0 == 0 || srow[t0 - 1] != cur;  // the current run starts inside this range
+  auto start = [&]() {
+    const float* dst = d_out + (int64_t)cur * D;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+      const int j = lane + 64 * m;
+      acc[m] = 0.f;
+      base[m] = (whole && j < D) ? dst[j] : 0.f;
+    }
+  };
   auto flush = [&](bool complete) {
     float* dst = d_out + (int64_t)cur * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
       if (j < D) {
-        if (complete) dst[j] += acc[m];
+        if (complete) dst[j] = base[m] + acc[m];
         else atomic_add_noret(dst + j, acc[m]);
       }
-      acc[m] = 0.f;
     }
   };
+  start();
   for (int i0 = 0; i0 < m_n; i0 += SR_G) {
     float hv[SR_G][NPL];
 #pragma unroll
@@ -222,6 +232,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
         flush(whole);
         cur = r;
         whole = true;
+        start();
       }
       const float g = s_g[wv][i];
 #pragma unroll

@@ -133,8 +133,9 @@ class BatchedWorkerLogic:
     arbitrary_pushes = False
     pushes = True
     #: the callbacks are a pure device function of the batch and device state (no
-    #: host syncs, no per-batch Python state): ``TensorRuntime(graph=True)`` may
-    #: replay captured steps instead of calling them (``core.step_graph``)
+    #: host syncs, no per-batch Python state, no buffer re-allocated after the first
+    #: micro-batches of a shape): ``TensorRuntime(graph=True)`` may replay captured
+    #: steps instead of calling them (``core.step_graph``)
     graph_safe = False
 
     def open(self, ctx: RuntimeContext) -> None:

@@ -78,7 +78,8 @@ class LempTopK:
         #: (32 queries, 32 items) block pairs the COORD scans scored / skipped
         self.coord_stats = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
         #: device COORD gate of a scan (``ops.coord_gate``): on at the start of every query
-        #: batch, off once a segment's bound skipped < 1/4 of its block pairs
+        #: batch, off for 3 segments after a segment whose bound skipped < 1/4 of its block
+        #: pairs, then probed again
         self._coord_gate = torch.ones(1, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
         self._coord_prev = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
 

@@ -906,14 +906,16 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
         N.ptr(gate), N.stream_ptr(Qb.device)), "score_filter_bf16")
 
 
-def coord_gate(stats: torch.Tensor, prev: torch.Tensor, gate: torch.Tensor, num: int = 1, den: int = 4) -> None:
-    """Device-side COORD switch of a LEMP scan (GPU only): ``gate[0] = 1`` while the
-    bound skipped at least ``num / den`` of the (query, item) block pairs it
-    evaluated since the previous call (``stats`` = cumulative scored / skipped,
-    ``prev`` = their values at the previous call).  No host sync: the bound is
-    exact either way, the gate only decides whether evaluating it pays."""
+def coord_gate(stats: torch.Tensor, prev: torch.Tensor, gate: torch.Tensor, num: int = 1, den: int = 4,
+               rest: int = 3) -> None:
+    """Device-side COORD switch of a LEMP scan (GPU only; the scorer evaluates the
+    bound while ``gate[0] > 0``).  After a segment that evaluated it: on if it skipped
+    at least ``num / den`` of the (query, item) block pairs (``stats`` = cumulative
+    scored / skipped, ``prev`` = their values at the previous call), else off for the
+    next ``rest`` segments, then probed again.  No host sync: the bound is exact
+    either way, the gate only decides whether evaluating it pays."""
     N.check(N.require().fps_coord_gate(_c(stats).data_ptr(), _c(prev).data_ptr(), _c(gate).data_ptr(), int(num),
-                                       int(den), N.stream_ptr(stats.device)), "coord_gate")
+                                       int(den), int(rest), N.stream_ptr(stats.device)), "coord_gate")
 
 
 def cand_rescore(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, cand_key: torch.Tensor,
