@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Probe: random vs key-sorted row access into a 1B-row fp32 table (the PA PS path's
+gather / apply over 4M unique features), and the cost of sorting the keys.
+
+    python bench/probe_sorted_gather.py [--features 1000000000] [--n 4194304]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--features", type=int, default=1_000_000_000)
+    ap.add_argument("--n", type=int, default=1 << 22)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args(argv)
+    import torch
+
+    from flink_parameter_server_1_amd import ops
+
+    dev = torch.device("cuda", 0)
+    table = torch.zeros(a.features, 1, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    u = torch.rand(a.n, generator=g, device=dev)
+    keys = torch.clamp((u ** 2 * a.features).long(), max=a.features - 1).to(torch.int32)
+    uk = torch.unique(keys)  # sorted unique
+    perm = torch.randperm(uk.numel(), generator=g, device=dev)
+    rk = uk[perm].contiguous()  # the same keys in random order
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / a.reps * 1e3  # us
+
+    out = {"n_requests": a.n, "n_unique": uk.numel()}
+    for name, k in (("random", rk), ("sorted", uk)):
+        rows = torch.empty(k.numel(), 1, device=dev)
+        d = torch.full((k.numel(), 1), 1e-6, device=dev)
+        out[f"gather_{name}_us"] = timeit(lambda: ops.gather_rows(table, k, out=rows))
+        out[f"apply_add_unique_{name}_us"] = timeit(lambda: ops.apply_rows(table, k, d, op="add_unique"))
+    v = torch.arange(rk.numel(), device=dev, dtype=torch.int32)
+    out["sort_pairs_int32_us"] = timeit(lambda: torch.sort(rk))
+    out["sort_keys_with_perm_us"] = timeit(lambda: torch.sort(rk.long()))
+    out["keys_sort_stable_int32_us"] = timeit(lambda: torch.sort(rk, stable=True))
+    del v
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

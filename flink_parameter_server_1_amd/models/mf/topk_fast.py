@@ -114,8 +114,21 @@ class LempTopK:
         N = self.vecs.shape[0]
         fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
         if fused and self.sync_free and N > max(self.seed_items, start):
-            res = self._query_fused(Q, qlen, k, start, None if state is None else (state[0].clone(),
-                                                                                    state[1].clone()))
+            st = None if state is None else (state[0].clone(), state[1].clone())
+            perm = self._focus_order(Q) if self.bf16 else None
+            if perm is not None:
+                # the COORD bound is evaluated per 32-query block and skips a block pair only
+                # when it holds for all 32 queries: queries grouped by focus coordinate share
+                # one coordinate range per block (random order mixes ~32 coordinates in a
+                # block, and a block pair almost never passes them all)
+                res = self._query_fused(Q[perm], qlen[perm], k, start,
+                                        None if st is None else (st[0][perm], st[1][perm]))
+                if res is not None:
+                    inv = torch.empty_like(perm)
+                    inv[perm] = torch.arange(perm.numel(), device=perm.device)
+                    res = (res[0][inv], res[1][inv])
+            else:
+                res = self._query_fused(Q, qlen, k, start, st)
             if res is not None:
                 return res
             self.overflows += 1  # some query passed more than cap scores: rescan unfused
@@ -249,6 +262,17 @@ class LempTopK:
         f = torch.argmax(Q * Q, dim=1)
         qbf = Q.gather(1, f.view(-1, 1)).view(-1) / qlen.clamp_min(1e-30)
         return f.to(torch.int32).contiguous(), qbf.contiguous()
+
+    def _focus_order(self, Q: torch.Tensor) -> Optional[torch.Tensor]:
+        """Query order grouping equal focus coordinates (``argmax q_c^2``) when the
+        strategy evaluates COORD on the device and the batch spans several 32-query
+        blocks; None otherwise (the order does not change any result: each query's
+        top-K is its own)."""
+        from .pruning import COORD, LC
+
+        if not isinstance(self.strategy, (COORD, LC)) or Q.shape[0] <= 32:
+            return None
+        return torch.argsort(torch.argmax(Q * Q, dim=1), stable=True)
 
     def _coord_segment(self, s: int, e: int) -> bool:
         """COORD on this segment?  LC switches to LENGTH where the segment's lengths

@@ -176,7 +176,10 @@ def test_lemp_device_coord_bound_exact_and_skips(strategy):
     X = torch.randn(N, D, generator=g, device="cuda") * 0.05
     X[torch.arange(N, device="cuda"), axis] += 1.0
     X *= torch.rand(N, 1, generator=g, device="cuda") ** 2 + 0.05
-    qa = torch.randint(0, D, (B,), generator=g, device="cuda")
+    # queries in random order over 8 focus coordinates: the scan groups them by focus
+    # coordinate, so each 32-query block shares one and COORD skips item blocks that
+    # hold no item dominated by it (with 64 coordinates mixed in a block, it would not)
+    qa = torch.randint(0, 8, (B,), generator=g, device="cuda")
     Q = torch.randn(B, D, generator=g, device="cuda") * 0.05
     Q[torch.arange(B, device="cuda"), qa] += 1.0
     ids = torch.arange(N, device="cuda") * 3 + 1
