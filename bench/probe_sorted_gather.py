@@ -51,6 +51,18 @@ def main(argv=None):
         d = torch.full((k.numel(), 1), 1e-6, device=dev)
         out[f"gather_{name}_us"] = timeit(lambda: ops.gather_rows(table, k, out=rows))
         out[f"apply_add_unique_{name}_us"] = timeit(lambda: ops.apply_rows(table, k, d, op="add_unique"))
+    touched = torch.zeros(a.features, dtype=torch.uint8, device=dev)
+    rows = torch.empty(rk.numel(), 1, device=dev)
+    d = torch.full((rk.numel(), 1), 1e-6, device=dev)
+    out["gather_random_touched_us"] = timeit(lambda: ops.gather_rows(table, rk, out=rows, touched=touched))
+    out["apply_random_touched_us"] = timeit(lambda: ops.apply_rows(table, rk, d, op="add_unique", touched=touched))
+    out["mark_rows_random_us"] = timeit(lambda: ops.mark_rows(touched, rk))
+    # de-duplication of the 4M requests over the 1B-id space: hashed claim map vs dense claim map
+    for name, hashed in (("hashed", True), ("dense_claim", False)):
+        ws = ops.DedupWorkspace(a.features, 1, 0, 1, dev, hashed=hashed)
+        out[f"dedup_{name}_us"] = timeit(lambda: ws.run(keys))
+        del ws
+        torch.cuda.empty_cache()
     v = torch.arange(rk.numel(), device=dev, dtype=torch.int32)
     out["sort_pairs_int32_us"] = timeit(lambda: torch.sort(rk))
     out["sort_keys_with_perm_us"] = timeit(lambda: torch.sort(rk.long()))

@@ -125,28 +125,64 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
 // older epochs count as empty, so nothing is cleared between steps.  The
 // capacity (power of two, >= 2n) bounds every probe sequence.  The request
 // whose CAS writes the key owns it; owner_slot is then indexed by hash slot.
+//
+// HU requests per thread are in flight together (their key loads, slot loads and
+// first CASes issue back to back): with one request per iteration the dependent
+// key -> slot -> CAS chain left the kernel latency-bound (202 us per 4M keys,
+// profiles/r3_pa_ps_path_kernel_stats.csv).  The rare requests whose first slot
+// is taken by another key finish with the serial probe loop.
+constexpr int DEDUP_HU = 4;
+
+__device__ __forceinline__ bool hash_probe(unsigned long long* __restrict__ tab, uint32_t mask, uint32_t epoch,
+                                           unsigned long long mine, uint32_t& h, unsigned long long cur) {
+  for (;;) {  // cur = tab[h] as last seen; returns whether this request inserted the key
+    if ((uint32_t)(cur >> 32) != epoch) {
+      const unsigned long long old = atomicCAS(tab + h, cur, mine);
+      if (old == cur) return true;  // claimed the empty slot: this request owns the key
+      cur = old;                    // somebody else wrote it first: re-examine
+      if ((uint32_t)(cur >> 32) != epoch) continue;
+    }
+    if (cur == mine) return false;  // our key already lives here
+    h = (h + 1) & mask;
+    cur = tab[h];
+  }
+}
+
 __global__ void dedup_hash_insert_kernel(const int32_t* __restrict__ keys, int64_t n,
                                          unsigned long long* __restrict__ tab, uint32_t mask, uint32_t epoch,
                                          int32_t* __restrict__ hslot) {
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t k = (uint32_t)keys[b];
-    const unsigned long long mine = ((unsigned long long)epoch << 32) | k;
-    uint32_t h = fmix32(k ^ 0x5bd1e995u) & mask;
-    bool own = false;
-    for (;;) {
-      unsigned long long cur = tab[h];
-      if ((uint32_t)(cur >> 32) != epoch) {
-        const unsigned long long old = atomicCAS(tab + h, cur, mine);
-        if (old == cur) { own = true; break; }  // claimed the empty slot: this request owns the key
-        cur = old;               // somebody else wrote it first: re-examine
-        if ((uint32_t)(cur >> 32) != epoch) continue;
-      }
-      if (cur == mine) break;    // our key already lives here
-      h = (h + 1) & mask;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b0 < n; b0 += DEDUP_HU * stride) {
+    unsigned long long mine[DEDUP_HU], cur[DEDUP_HU];
+    uint32_t h[DEDUP_HU];
+    bool act[DEDUP_HU], own[DEDUP_HU];
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {
+      const int64_t b = b0 + u * stride;
+      act[u] = b < n;
+      const uint32_t k = act[u] ? (uint32_t)keys[b] : 0u;
+      mine[u] = ((unsigned long long)epoch << 32) | k;
+      h[u] = fmix32(k ^ 0x5bd1e995u) & mask;
+      own[u] = false;
     }
-    // bit 31 marks the key's owner (the CAS winner: exactly one per key), so no
-    // separate claim pass is needed on the hashed path; cap <= 2^31 keeps h < 2^31
-    hslot[b] = (int32_t)(h | (own ? 0x80000000u : 0u));
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) cur[u] = act[u] ? tab[h[u]] : 0ull;
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {  // first attempt of every request: independent CASes
+      if (act[u] && (uint32_t)(cur[u] >> 32) != epoch) {
+        const unsigned long long old = atomicCAS(tab + h[u], cur[u], mine[u]);
+        if (old == cur[u]) { own[u] = true; act[u] = false; }
+        else cur[u] = old;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {
+      if (act[u]) own[u] = hash_probe(tab, mask, epoch, mine[u], h[u], cur[u]);
+      // bit 31 marks the key's owner (the CAS winner: exactly one per key), so no
+      // separate claim pass is needed on the hashed path; cap <= 2^31 keeps h < 2^31
+      const int64_t b = b0 + u * stride;
+      if (b < n) hslot[b] = (int32_t)(h[u] | (own[u] ? 0x80000000u : 0u));
+    }
   }
 }
 
@@ -222,7 +258,7 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
       int32_t local;
       key_dest(k, W, part_kind, block, d, local);
       if (HASHED) {
-        own = hslot[b] < 0;
+        own = hslot == nullptr || hslot[b] < 0;  // no hslot: every request owns its own slot b
       } else {
         const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
         own = owner == (uint32_t)b;
@@ -240,7 +276,7 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
     if (dd[it] < 0) continue;
     const int64_t b = base + (int64_t)it * blockDim.x + threadIdx.x;
     // dense: indexed by the owner's request index; hashed: by the key's hash slot
-    owner_slot[HASHED ? (int64_t)(hslot[b] & 0x7fffffff) : b] = lds_base[dd[it]] + slot_l[it];
+    owner_slot[HASHED && hslot != nullptr ? (int64_t)(hslot[b] & 0x7fffffff) : b] = lds_base[dd[it]] + slot_l[it];
   }
 }
 
@@ -261,24 +297,37 @@ __global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, const int
                                      int W, int part_kind, int64_t block, const int32_t* __restrict__ prefix,
                                      const int32_t* __restrict__ owner_slot, int32_t* __restrict__ uniq,
                                      int32_t* __restrict__ pos) {
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t k = keys[b];
-    int d; int32_t local;
-    key_dest(k, W, part_kind, block, d, local);
-    int64_t at;
-    bool own;
-    if (HASHED) {
-      const int32_t hs = hslot[b];
-      at = hs & 0x7fffffff;
-      own = hs < 0;
-    } else {
-      const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
-      at = owner;
-      own = owner == (uint32_t)b;
+  // DEDUP_HU requests per thread in flight (the owner-slot loads are random)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b0 < n; b0 += DEDUP_HU * stride) {
+    int32_t local[DEDUP_HU], p[DEDUP_HU];
+    int64_t at[DEDUP_HU];
+    bool own[DEDUP_HU], act[DEDUP_HU];
+    int d[DEDUP_HU];
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {
+      const int64_t b = b0 + u * stride;
+      act[u] = b < n;
+      const int32_t k = act[u] ? keys[b] : 0;
+      key_dest(k, W, part_kind, block, d[u], local[u]);
+      if (HASHED) {
+        const int32_t hs = !act[u] ? 0 : (hslot != nullptr ? hslot[b] : (int32_t)((uint32_t)b | 0x80000000u));
+        at[u] = hs & 0x7fffffff;
+        own[u] = hs < 0;
+      } else {
+        const uint32_t owner = act[u] ? 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull) : 0u;
+        at[u] = owner;
+        own[u] = owner == (uint32_t)b;
+      }
     }
-    const int32_t p = prefix[d] + owner_slot[at];
-    pos[b] = p;
-    if (own) uniq[p] = local;
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) p[u] = act[u] ? prefix[d[u]] + owner_slot[at[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {
+      if (!act[u]) continue;
+      pos[b0 + u * stride] = p[u];
+      if (own[u]) uniq[p[u]] = local[u];
+    }
   }
 }
 
@@ -611,6 +660,18 @@ FPS_API int fps_dedup_hashed(const int32_t* keys, int64_t n, unsigned long long*
   }
   return launch_dedup<true>(keys, hslot, n, nullptr, epoch, W, part_kind, block, counts, prefix, owner_slot, uniq,
                             pos, s);
+}
+
+// Requests grouped by destination shard WITHOUT de-duplication (request plans of
+// key spaces far larger than the batch, where repeats are rare and the dedup pass
+// costs more than the rows it saves): every request is its own "unique key" --
+// the hashed pipeline with an identity slot map (no insert kernel).  pos[b] =
+// the request's position in the shard-major uniq[n]; owner_slot has n entries.
+FPS_API int fps_route_requests(const int32_t* keys, int64_t n, int W, int part_kind, int64_t block, int32_t* counts,
+                               int32_t* prefix, int32_t* owner_slot, int32_t* uniq, int32_t* pos, void* stream) {
+  if (n >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  return launch_dedup<true>(keys, nullptr, n, nullptr, 0u, W, part_kind, block, counts, prefix, owner_slot, uniq, pos,
+                            (hipStream_t)stream);
 }
 
 namespace {

@@ -268,6 +268,21 @@ class DedupWorkspace:
                                   self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup")
         return self.counts, self.prefix, self.uniq, self.pos[:n]
 
+    def route(self, keys: torch.Tensor):
+        """Like ``run`` but WITHOUT de-duplication: every request is its own entry of
+        ``uniq`` (grouped by owning shard), ``pos`` a permutation of the requests.
+        Same return layout as ``run``."""
+        if self.device.type != "cuda":
+            return R.route(keys, self.W, self.part_kind, self.block)
+        n = keys.numel()
+        self._grow(max(n, 1))
+        self.counts.zero_()
+        N.check(N.require().fps_route_requests(_c(keys).data_ptr(), n, self.W, self.part_kind, self.block,
+                                               self.counts.data_ptr(), self.prefix.data_ptr(),
+                                               self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(),
+                                               N.stream_ptr(self.device)), "route_requests")
+        return self.counts, self.prefix, self.uniq, self.pos[:n]
+
     def reset_claims(self, keys: torch.Tensor) -> None:
         """Empty the claim entries of ``keys`` (the step's unique keys).  In
         ``clear_after`` mode every entry is empty between steps, so a constant

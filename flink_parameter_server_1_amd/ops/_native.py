@@ -36,6 +36,7 @@ _SIGNATURES = {
     "fps_gather_rows": [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_int, c_vp, c_vp],
     "fps_apply_rows": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_f32, c_f32, c_vp, c_vp],
     "fps_dedup": [c_vp, c_i64, c_vp, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_route_requests": [c_vp, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_dedup_hashed": [c_vp, c_i64, c_vp, c_i64, c_u32, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                          c_vp],
     "fps_pair_sgd_pulled": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_int, c_vp, c_vp],

@@ -110,6 +110,20 @@ def dedup(keys: torch.Tensor, W: int, part_kind: int, block: int):
     return counts.to(torch.int32), prefix, uniq, pos
 
 
+def route(keys: torch.Tensor, W: int, part_kind: int, block: int):
+    """``dedup``'s layout without de-duplication: every request is an entry of
+    ``uniq`` (shard-major, request order inside a shard), ``pos`` a permutation."""
+    keys = keys.long()
+    dest, local = shard_of(keys, W, part_kind, block)
+    counts = torch.bincount(dest, minlength=W)
+    order = torch.argsort(dest, stable=True)
+    pos = torch.empty_like(order)
+    pos[order] = torch.arange(order.numel(), device=keys.device)
+    prefix = torch.zeros(W + 1, dtype=torch.int32, device=keys.device)
+    prefix[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return counts.to(torch.int32), prefix, local[order].to(torch.int32), pos.to(torch.int32)
+
+
 def _unique_first(keys):
     uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
     first = torch.full((uniq.numel(),), keys.numel(), dtype=torch.long)

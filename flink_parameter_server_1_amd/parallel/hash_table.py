@@ -221,7 +221,7 @@ class HashShardTable:
         return self.serve_rows(self.rows_for(keys)[0], wire_dtype)
 
     def apply_rows(self, rows: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
-                   fresh: Optional[torch.Tensor] = None) -> None:
+                   fresh: Optional[torch.Tensor] = None, mark: bool = True) -> None:
         op = op or self.optimizer
         if op == "fn":
             fn_apply(self._store, self.scratch_row, rows, deltas, self.update_fn, self.global_ids, fresh)

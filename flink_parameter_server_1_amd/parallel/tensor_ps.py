@@ -61,6 +61,9 @@ class PullPlan:
     #: identity plan (world 1, a batch at least as large as the key space): the unique
     #: keys are the whole key space in order, so ``pos`` is the key itself
     identity: bool = False
+    #: False: a request plan (no de-duplication) -- keys may repeat, so pushes apply
+    #: with atomics instead of the unique-key read-modify-write
+    unique: bool = True
 
 
 @dataclass
@@ -77,6 +80,8 @@ class PendingPlan:
     valid: Optional[torch.Tensor] = None  # static plan: [n_bound] bool
     n_bound: int = 0
     identity: bool = False
+    unique: bool = True
+    static: bool = False  # sizes known on the host (world 1): nothing to wait for
 
 
 class TensorPS:
@@ -101,6 +106,28 @@ class TensorPS:
         #: and is never applied), so a micro-batch issues no host sync at all
         self.static = False
         self._iota: Optional[torch.Tensor] = None
+        #: de-duplicate each micro-batch's keys (True), ship every request (False: a
+        #: request plan), or decide per batch size (None): requests go undeduplicated
+        #: when the key space is at least ``REQUEST_PLAN_RATIO`` times the batch (repeats
+        #: are then rare, so the dedup pass costs more than the rows it saves: PA over 1B
+        #: features repeats ~8 % of 4M keys) and the rule is additive (atomic apply)
+        self.dedup_mode: Optional[bool] = None
+        self._req_iota: Optional[torch.Tensor] = None
+
+    #: key space / batch ratio above which ``dedup_mode = None`` ships requests undeduplicated
+    REQUEST_PLAN_RATIO = 64
+
+    def dedups(self, n: int) -> bool:
+        """Does a micro-batch of ``n`` requests get a de-duplicating plan?"""
+        if self.dedup_mode is not None:
+            return bool(self.dedup_mode) or not self._request_plans_ok()
+        return not (self._request_plans_ok() and n > 0 and int(self.table.key_space) >= self.REQUEST_PLAN_RATIO * n)
+
+    def _request_plans_ok(self) -> bool:
+        """Request plans need an additive rule (repeated keys apply atomically) and a
+        dense shard (the sparse hash shard and lookup partitions resolve keys once)."""
+        return (getattr(self.table, "optimizer", "") in ("add", "sgd") and not self.masked_push
+                and not getattr(self.table, "sparse", False) and getattr(self.table, "partition", "") != "lookup")
 
     def identity_for(self, n: int) -> bool:
         """Will a static plan of ``n`` requests be the identity plan?  (World 1, a
@@ -111,11 +138,12 @@ class TensorPS:
                 and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
 
     # ----------------------------------------------------------------- planning
-    def plan_begin(self, keys: torch.Tensor, flag: int = 0) -> PendingPlan:
+    def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None) -> PendingPlan:
         """Stage A: dedup + count exchange, counts copied to pinned host memory
         asynchronously.  Collective: every rank calls it once per micro-batch
         (with empty ``keys`` when it has nothing to pull).  ``flag`` (an int) is
-        delivered to every peer with the counts (``PullPlan.peer_flags``)."""
+        delivered to every peer with the counts (``PullPlan.peer_flags``).  ``dedup``:
+        force (True) the de-duplicating plan instead of ``dedups(n)``'s choice."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
         n = keys.numel()
         if self.identity_for(n):
@@ -126,10 +154,19 @@ class TensorPS:
                 present = torch.zeros(ks, dtype=torch.uint8, device=keys.device)
                 ops.mark_rows(present, keys)
             return PendingPlan(n, None, self._iota, keys, None, None, int(flag), valid=present.view(torch.bool),
-                               n_bound=ks, identity=True)
+                               n_bound=ks, identity=True, static=True)
+        W = self.comm.world
+        if not (dedup or self.dedups(n)):
+            if W == 1 and self.static:  # every request is its own row: nothing to compute
+                if self._req_iota is None or self._req_iota.numel() < n:
+                    self._req_iota = torch.arange(max(n, 1), dtype=torch.int32, device=keys.device)
+                return PendingPlan(n, None, keys, self._req_iota[:n], None, None, int(flag), n_bound=n,
+                                   unique=False, static=True)
+            with stage("ps.route", self.timer):
+                counts, prefix, uniq, pos = self.dedup.route(keys)
+            return self._pending(n, counts, uniq, pos, flag, unique=False)
         with stage("ps.dedup", self.timer):
             counts, prefix, uniq, pos = self.dedup.run(keys)
-        W = self.comm.world
         if W == 1 and self.static and not getattr(self.table, "sparse", False):
             nb = min(n, int(self.table.key_space))
             j = torch.arange(nb, device=keys.device)
@@ -140,7 +177,13 @@ class TensorPS:
             gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
             if self.dedup.clear_after:
                 self.dedup.reset_claims(gkeys)
-            return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb)
+            return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb,
+                               static=True)
+        return self._pending(n, counts, uniq, pos, flag)
+
+    def _pending(self, n, counts, uniq, pos, flag, unique: bool = True) -> PendingPlan:
+        """Stage A's count exchange of a computed (de-duplicated or request) plan."""
+        W = self.comm.world
         # the workspace is reused by the next plan_begin: this plan keeps copies
         counts = counts.clone()
         uniq = uniq[:n].clone()
@@ -153,7 +196,7 @@ class TensorPS:
                 ev.record()
             else:
                 host, ev = counts[:1].to("cpu", torch.int32), None
-            return PendingPlan(n, counts, uniq, pos, host, ev, int(flag))
+            return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique)
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
         send = torch.cat([counts.view(W, 1).to(torch.int32), flags], dim=1).contiguous()  # [W, 2]
         with stage("ps.count-a2a", self.timer):
@@ -166,16 +209,16 @@ class TensorPS:
             ev.record()
         else:
             host, ev = both.to("cpu"), None
-        return PendingPlan(n, counts, uniq, pos, host, ev, int(flag))
+        return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique)
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
-        if pp.valid is not None:  # static world-1 plan: sizes known on the host, nothing to wait for
+        if pp.static:  # static world-1 plan: sizes known on the host, nothing to wait for
             self.stats["pulls"] += pp.n
             self.stats["unique"] += pp.n_bound
             self.stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
-                            valid=pp.valid, identity=pp.identity)
+                            valid=pp.valid, identity=pp.identity, unique=pp.unique)
         if pp.event is not None:
             if not pp.event.query():
                 self.stats["host_stalls"] += 1
@@ -194,12 +237,13 @@ class TensorPS:
         self.stats["pulls"] += pp.n
         self.stats["unique"] += n_unique
         self.stats["steps"] += 1
-        return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n)
+        return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n, unique=pp.unique)
 
-    def plan(self, keys: torch.Tensor, persistent: bool = False, flag: int = 0) -> PullPlan:
+    def plan(self, keys: torch.Tensor, persistent: bool = False, flag: int = 0,
+             dedup: Optional[bool] = None) -> PullPlan:
         """Stages A + B back to back (the host waits on this micro-batch's counts).
         Plans never alias the dedup workspace, so ``persistent`` is implied."""
-        return self.plan_end(self.plan_begin(keys, flag))
+        return self.plan_end(self.plan_begin(keys, flag, dedup))
 
     # --------------------------------------------------------------------- pull
     def serve(self, plan: PullPlan) -> torch.Tensor:
@@ -256,7 +300,9 @@ class TensorPS:
         with stage("ps.push-a2a", self.timer):
             recv = self.comm.all_to_all(wire.contiguous(), plan.send_splits, plan.recv_splits)
         fresh = None
-        if plan.recv_rows is not None:  # served by this plan: the rows exist
+        # served by this plan: the rows exist and were marked touched when served
+        mark = plan.recv_rows is None
+        if plan.recv_rows is not None:
             rows = plan.recv_rows
         else:  # a push without a pull (push_keys, model load)
             rows, fresh = self.table.rows_for(plan.recv_keys, push=True)
@@ -270,7 +316,8 @@ class TensorPS:
         opt = op or self.table.optimizer
         self.stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
-            seg_add = opt == "add" and len(plan.recv_splits) <= 16
+            # (a request plan repeats keys inside a segment: atomic add)
+            seg_add = opt == "add" and len(plan.recv_splits) <= 16 and plan.unique
             if opt == "fn":  # user rule: sequential over the source segments (keys repeat across them)
                 if fresh is not None:  # the id is absent only for its first push, in segment order
                     fresh = self._first_fresh(recv_keys, fresh)
@@ -291,10 +338,10 @@ class TensorPS:
                 for n in plan.recv_splits:
                     if n:
                         self.table.apply_rows(recv_keys[off:off + n], recv[off:off + n], lr=lr,
-                                              op="add_unique" if seg_add else opt)
+                                              op="add_unique" if seg_add else opt, mark=mark)
                     off += n
             else:
-                self.table.apply_rows(recv_keys, recv, lr=lr, op=opt)
+                self.table.apply_rows(recv_keys, recv, lr=lr, op=opt, mark=mark)
         if return_updated:
             if not sum(plan.recv_splits):  # nothing arrived at this shard (host-known sizes)
                 return None
@@ -349,8 +396,9 @@ class TensorPS:
     def push_keys(self, keys: torch.Tensor, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
                   return_updated: bool = False):
         """Push to arbitrary keys (not a pulled plan): plans them (host waits on
-        the counts), pre-reduces duplicates and applies."""
-        plan = self.plan(keys)
+        the counts), pre-reduces duplicates and applies (always a de-duplicating plan:
+        ``set`` needs one value per key)."""
+        plan = self.plan(keys, dedup=True)
         opt = op or self.table.optimizer
         red = self.reduce_requests(plan, deltas, "set" if opt == "set" else "add")
         return self.push(plan, red, lr=lr, op=opt, return_updated=return_updated)

@@ -89,12 +89,14 @@ class DevicePSLogic:
                  lr: float = 0.0, dtype=torch.float32, track_touched: bool = True,
                  table: Optional[ShardedTable] = None, ps: Optional[TensorPS] = None, sparse: bool = False,
                  capacity: int = 1 << 14, init_fn: Optional[Callable] = None, update_fn: Optional[Callable] = None,
-                 combine: str = "sum"):
+                 combine: str = "sum", dedup: Optional[bool] = None):
         """``table`` / ``ps``: serve an existing shard (and its PS front) instead of
         allocating one at ``open`` -- how the model classes (``DistributedMF``,
         ``DistributedPA``) run their PS path through this engine.  ``sparse``: a
         device hash-table shard (``num_ids`` may be None, ``capacity`` = initial
-        rows per shard; it grows)."""
+        rows per shard; it grows).  ``dedup``: de-duplicate each micro-batch's pulled
+        keys (True), ship every request (False), or let the PS decide by batch size
+        (None, ``TensorPS.dedups``); additive rules only ship requests."""
         if op not in OPS:
             raise ValueError(f"op must be one of {OPS}, not {op!r}")
         if combine not in COMBINE:
@@ -114,6 +116,7 @@ class DevicePSLogic:
         self.track_touched = track_touched
         self.sparse, self.capacity = bool(sparse), int(capacity)
         self.init_fn, self.update_fn, self.combine = init_fn, update_fn, combine
+        self.dedup = dedup
         self.table: Optional[ShardedTable] = None
         self.ps: Optional[TensorPS] = None
 
@@ -139,6 +142,8 @@ class DevicePSLogic:
         # set-rules, user rules and per-push outputs must tell pushed keys from
         # merely pulled ones (a user rule need not map a zero delta to a no-op)
         self.ps.masked_push = self.op in ("set", "fn") or self.emit == "push" or self.combine != "sum"
+        if self.dedup is not None:
+            self.ps.dedup_mode = self.dedup
 
     @property
     def needs_mask(self) -> bool:

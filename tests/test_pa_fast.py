@@ -118,13 +118,16 @@ def test_pa_multi_kernel_matches_reference(mode, L):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("direct", [False, True])
-def test_pa_fast_gpu_learns_and_hashed_dedup(direct):
+@pytest.mark.parametrize("direct,dedup", [(False, None), (False, True), (True, None)])
+def test_pa_fast_gpu_learns_and_hashed_dedup(direct, dedup):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    F = 1 << 29  # above the dense-map limit: exercises the hashed dedup (PS path)
+    F = 1 << 29  # above the dense-map limit: the hashed dedup (PS path, dedup=True)
     m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=direct), Comm(device=torch.device("cuda")))
+    m.ps.dedup_mode = dedup
     assert m.ps.dedup.hashed and m._direct == direct
+    # 2^29 features >= 64 x the 131k requests of a batch: the automatic choice ships requests
+    assert m.ps.dedups(4096 * 32) == bool(dedup)
     # zipf 1: at heavier skew one batch sums thousands of PA steps on the hot features
     # and overshoots (the same happens on the CPU path: batch-synchronous PA semantics)
     batches = [synthetic_sparse_batch(4096, 32, F, seed=1, step=s, device="cuda", zipf=1.0) for s in range(4)]
@@ -135,3 +138,28 @@ def test_pa_fast_gpu_learns_and_hashed_dedup(direct):
     ip, idx, val, lab = batches[0]
     acc = float((m.predict(ip, idx, val).to(torch.int8) == lab).float().mean())
     assert acc > 0.8, acc
+
+
+@pytest.mark.gpu
+def test_pa_request_plan_matches_dedup_plan_gpu():
+    """PA through the PS path with request plans (every feature request shipped,
+    deltas applied with atomics) == with de-duplicated plans (deltas summed per
+    feature): the same touched features and weights up to fp32 summation order."""
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    F = 1 << 24
+    batches = [synthetic_sparse_batch(2048, 32, F, seed=3, step=s, device="cuda", zipf=1.0) for s in range(3)]
+    dumps = []
+    for dedup in (True, False):
+        m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=False),
+                          Comm(device=torch.device("cuda")))
+        m.ps.dedup_mode = dedup
+        for s in range(6):
+            m.train_step(*batches[s % 3])
+        ids, w = m.dump()
+        o = torch.argsort(ids)
+        dumps.append((ids[o], w[o].reshape(-1)))
+        if not dedup:
+            assert m.ps.stats["unique"] == m.ps.stats["pulls"]
+    assert torch.equal(dumps[0][0], dumps[1][0])
+    torch.testing.assert_close(dumps[0][1], dumps[1][1], rtol=1e-4, atol=1e-6)

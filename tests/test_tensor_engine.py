@@ -85,7 +85,7 @@ class _CountWorker(BatchedWorkerLogic):
         ps.output((pulled.keys, pulled.values()))
 
 
-def _model_load(rank, world, n_params, staleness):
+def _model_load(rank, world, n_params, staleness, dedup=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     comm = Comm()
@@ -95,15 +95,22 @@ def _model_load(rank, world, n_params, staleness):
     mine = keys[rank::world]
     batches = [torch.tensor(mine[s:s + 7]) for s in range(0, len(mine), 7)]
     rt = TensorRuntime(comm, staleness=staleness)
-    out = rt.execute(batches, _CountWorker(), DeviceSimplePSLogicWithClose(n_params, 1, op="add"), model=model)
+    logic = DeviceSimplePSLogicWithClose(n_params, 1, op="add", dedup=dedup)
+    out = rt.execute(batches, _CountWorker(), logic, model=model)
+    if dedup is False:  # request plans: every pull of the run shipped its key as is
+        assert logic.ps.stats["unique"] == logic.ps.stats["pulls"]
     return [(e.value[0], e.value[1]) for e in out if isinstance(e, Right)]
 
 
-@pytest.mark.parametrize("world,staleness", [(1, 0), (3, 0), (4, 2)])
-def test_tensor_model_load_exact(world, staleness):
+@pytest.mark.parametrize("world,staleness,dedup", [(1, 0, None), (3, 0, None), (4, 2, None), (1, 0, False),
+                                                   (3, 0, False), (2, 1, False)])
+def test_tensor_model_load_exact(world, staleness, dedup):
     """FlinkSimpleStackTest 'model load': 50 params loaded as 10*i, pulled and
-    pushed +1 three times each -> the close-time dump is exactly 10*i + 3."""
-    res = run_ranks(_model_load, world, 50, staleness) if world > 1 else [_model_load(0, 1, 50, staleness)]
+    pushed +1 three times each -> the close-time dump is exactly 10*i + 3.  With
+    ``dedup=False`` (request plans) keys repeat inside micro-batches and their +1s
+    are applied one by one (atomic adds)."""
+    res = run_ranks(_model_load, world, 50, staleness, dedup) if world > 1 else \
+        [_model_load(0, 1, 50, staleness, dedup)]
     dump = {}
     for r in res:
         for ids, vals in r:

@@ -123,7 +123,8 @@ def test_pipelined_mf_topk_worker_syncs_once_per_batch():
     assert S0.shape == (B, 20) and bool((I0[:, 0] >= 0).all())
 
 
-def test_pipelined_pa_worker_issues_no_implicit_sync():
+@pytest.mark.parametrize("dedup", [None, False])
+def test_pipelined_pa_worker_issues_no_implicit_sync(dedup):
     """PAWorker on the pipelined engine (staleness 1): labelled and unlabelled
     examples mixed in every micro-batch, predictions emitted as MaskedPairs --
     no implicit device->host sync in the loop; the outputs compact when read."""
@@ -139,7 +140,7 @@ def test_pipelined_pa_worker_issues_no_implicit_sync():
         lab = torch.where(torch.arange(B, device=DEV) % 4 == 0, torch.zeros_like(lab), lab)  # 1/4 unlabelled
         batches.append((ip, idx, val, lab))
     rt = TensorRuntime(Comm(device=DEV), staleness=1)
-    rt.start(PAWorker("binary", 1, "PA", 1.0), DeviceRangePSLogicWithClose(F, 1, init=("zeros",)))
+    rt.start(PAWorker("binary", 1, "PA", 1.0), DeviceRangePSLogicWithClose(F, 1, init=("zeros",), dedup=dedup))
     for b in batches[:4]:  # warm-up: workspaces allocated
         rt.submit(b)
     torch.cuda.synchronize()
