@@ -301,7 +301,12 @@ class TensorRuntime:
                 self.worker_logic.on_recv_batch(batch, c)
         reqs, c._requests = c._requests, None
         if reqs:
-            keys = torch.cat([r.keys.to(device=self.device, dtype=torch.int64) for r in reqs])
+            # one key tensor as the worker gave it (no int64 round trip when every
+            # request is int32: at 4M keys per micro-batch the conversions and the
+            # copy cost ~40 us, profiles/r3_pa_ps_path_kernel_stats.csv)
+            kd = torch.int32 if all(r.keys.dtype == torch.int32 for r in reqs) else torch.int64
+            keys = reqs[0].keys.to(device=self.device, dtype=kd) if len(reqs) == 1 else \
+                torch.cat([r.keys.to(device=self.device, dtype=kd) for r in reqs])
         else:
             keys = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.counters.add("micro_batches", 1 if batch is not None else 0)
