@@ -89,6 +89,33 @@ def test_dedup(W, kind, hashed, num_ids, method):
             keys = keys[torch.randint(0, 5000, (keys.numel(),))]
 
 
+@pytest.mark.parametrize("W,kind", [(1, 0), (3, 0), (4, 1), (5, 2)])
+@pytest.mark.parametrize("hashed", [False, True])
+def test_route_requests(W, kind, hashed):
+    """Request plans (``DedupWorkspace.route``): every request is an entry of the
+    shard-major ``uniq`` (no de-duplication), ``pos`` a permutation of the requests,
+    the shard counts those of the reference grouping."""
+    num_ids = 1 << 30 if hashed else 100_000
+    block = -(-num_ids // W)
+    ws = ops.DedupWorkspace(num_ids, W, kind, block, DEV, hashed=hashed)
+    for n in (50000, 20000, 120000):  # the third call grows the workspace
+        keys = torch.randint(0, num_ids, (n,), dtype=torch.int32)
+        keys[: n // 4] = keys[n // 4: n // 2]  # repeated keys stay separate entries
+        counts, prefix, uniq, pos = ws.route(keys.to(DEV))
+        c_ref, p_ref, u_ref, _ = R.route(keys, W, kind, block)
+        assert counts.cpu().tolist() == c_ref.tolist()
+        assert prefix.cpu().tolist() == p_ref.tolist()
+        assert int(prefix[-1]) == n
+        p = pos.cpu().long()
+        assert torch.equal(torch.sort(p).values, torch.arange(n))  # a permutation
+        _, local = R.shard_of(keys, W, kind, block)
+        assert torch.equal(uniq[:n].cpu()[p].long(), local)
+        for d in range(W):  # every request sits in its owner's group
+            a, b = int(p_ref[d]), int(p_ref[d + 1])
+            dest, _ = R.shard_of(keys, W, kind, block)
+            assert bool(((p >= a) & (p < b) == (dest == d)).all())
+
+
 @pytest.mark.parametrize("D", [8, 15, 64, 128])
 def test_mf_sgd_local_unique_rows(D):
     """Unique users/items per batch -> the Hogwild kernel is deterministic."""

@@ -100,3 +100,29 @@ def test_w2v_pipelined_multirank_on_one_gpu():
     res = run_ranks(_w2v, 2)
     for first, last in res:
         assert last < 0.97 * first, (first, last)  # learning (not a convergence test)
+
+
+def _pa_plans(rank, world):
+    """PA through the PS path with request plans (the routing kernel at W > 1) and with
+    de-duplicating plans: the same model, on real kernels."""
+    from flink_parameter_server_1_amd.models.pa.fast import DistributedPA, PAConfig, synthetic_sparse_batch
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    F = 1 << 26
+    out = []
+    for dedup in (True, False):
+        m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=False),
+                          Comm(device=torch.device("cuda", 0)))
+        m.ps.dedup_mode = dedup
+        for s in range(8):
+            m.train_step(*synthetic_sparse_batch(2048, 32, F, seed=rank + 3, step=s % 4, device="cuda"))
+        ids, w = m.dump()
+        o = torch.argsort(ids)
+        out.append((ids[o].cpu(), w[o].reshape(-1).cpu()))
+    return out
+
+
+def test_pa_request_plans_multirank_on_one_gpu():
+    for (ia, wa), (ib, wb) in run_ranks(_pa_plans, 2):
+        assert torch.equal(ia, ib)
+        torch.testing.assert_close(wa, wb, rtol=2e-3, atol=1e-5)  # fp32 summation order (tests/test_pa_fast.py)
