@@ -134,7 +134,9 @@ WATCHDOG_SCRIPT = textwrap.dedent("""
     from flink_parameter_server_1_amd.utils.watchdog import Watchdog
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo", rank=rank, world_size=2)
-    wd = Watchdog(2.0, name="test").start()
+    # only rank 0 watches: a watchdog on the hung rank would end it too, and rank 0's
+    # blocked collective would then fail on the closed connection instead (a race)
+    wd = Watchdog(2.0 if rank == 0 else 600.0, name="test").start()
     t = torch.ones(1)
     for step in range(3):
         dist.all_reduce(t)
@@ -158,7 +160,7 @@ def test_watchdog_ends_a_rank_stuck_on_a_hung_peer(tmp_path):
                                       stderr=subprocess.PIPE, text=True))
     t0 = time.monotonic()
     try:
-        out0, err0 = procs[0].communicate(timeout=90)
+        out0, err0 = procs[0].communicate(timeout=150)
         elapsed = time.monotonic() - t0
     finally:
         for p in procs:
@@ -169,4 +171,6 @@ def test_watchdog_ends_a_rank_stuck_on_a_hung_peer(tmp_path):
 
     assert procs[0].returncode == WATCHDOG_EXIT, (procs[0].returncode, err0[-2000:])
     assert "watchdog: no progress" in err0 and "unreachable" not in out0
-    assert elapsed < 60
+    # well before the peer's 120 s sleep ends (generous: two fresh interpreters import
+    # torch and rendezvous on a CPU box that may be running other test workers)
+    assert elapsed < 110
