@@ -15,3 +15,6 @@ timeout -k 10 300 python bench.py --gpus 4 --steps 3 --warmup 1 --batch 2097152 
 tail -1 gpurun_out/rehearse/share4.log | cut -c1-400
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench/bench_mf_topk.py --users 100000 --items 200000 --batch 1024 --steps 3 --warmup 1 > gpurun_out/rehearse/mftopk2.log 2>&1 || { tail -30 gpurun_out/rehearse/mftopk2.log; exit 1; }
 tail -1 gpurun_out/rehearse/mftopk2.log | cut -c1-300
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29543 bench/bench_pa.py --steps 4 --warmup 1 > gpurun_out/rehearse/pa2.log 2>&1 || { tail -30 gpurun_out/rehearse/pa2.log; exit 1; }
+tail -1 gpurun_out/rehearse/pa2.log | cut -c1-300
+echo ALLDONE
