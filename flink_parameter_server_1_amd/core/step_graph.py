@@ -35,6 +35,7 @@ disables graphs for the runtime with a warning and runs the batch eagerly.
 """
 from __future__ import annotations
 
+import gc
 import traceback
 import warnings
 from typing import Any, Dict, List, Optional, Tuple
@@ -206,6 +207,12 @@ class StepGraphs:
         sub0 = rt.pipe.submitted
         g = torch.cuda.CUDAGraph()
         rt._capture_emits = emits
+        # no automatic garbage collection while capturing: a collected pinned host tensor
+        # or event of an earlier eager step would be freed on the capturing thread, and
+        # the host allocator's stream bookkeeping is illegal there (process abort);
+        # torch.cuda.graph collects once before the capture starts
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
         try:
             # thread_local: only this thread's calls are checked (a helper thread of the
             # process, e.g. a watchdog, must not invalidate the capture)
@@ -223,6 +230,8 @@ class StepGraphs:
             return None
         finally:
             rt._capture_emits = None
+            if gc_was_enabled:
+                gc.enable()
         dc = {k: v - c0.get(k, 0.0) for k, v in rt.counters.c.items() if v != c0.get(k, 0.0)}
         ds = {k: v - s0.get(k, 0) for k, v in rt.ps_logic.ps.stats.items() if v != s0.get(k, 0)}
         # the capture itself executed nothing: undo its host-side increments (replay adds them)
