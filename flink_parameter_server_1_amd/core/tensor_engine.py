@@ -135,6 +135,8 @@ class _Client(BatchedPSClient):
                                     torch.where(hit.view(-1, 1), tmp, self._acc))
             self._mask |= hit
         elif self.rt.ps_logic.op == "set" or comb == "last":  # last writer wins, in request order
+            if pos.numel() == 0:  # an empty request: nothing to write (d may be [0, D] with U > 0)
+                return
             rid = torch.arange(pos.numel(), device=pos.device)
             if mask is not None:
                 rid = torch.where(mask, rid, torch.full_like(rid, -1))

@@ -15,7 +15,10 @@ micro-batch of (center, context) pairs:
    block-shared negatives: the same expected gradient, ~10-40x fewer negative
    rows touched; a different estimator, reported separately);
 2. pull the center rows from ``W_in`` and context + negative rows from
-   ``W_out`` (deduplicated all-to-all, ``TensorPS``);
+   ``W_out`` (deduplicated all-to-all, ``TensorPS``); both tables' plans share
+   one count exchange, made one micro-batch ahead
+   (``BoundedStalenessPipeline`` over both tables), so the host never waits
+   for split sizes in steady state;
 3. ``ops.sgns_standard`` (K6, ``sgns_std.hip``) / ``ops.sgns_step`` (MFMA,
    ``sgns.hip``) computes per-row deltas;
 4. push both delta sets; the PS adds them.
@@ -35,6 +38,7 @@ import torch
 from ... import ops
 from ...parallel.comm import Comm
 from ...parallel.table import ShardedTable
+from ...parallel.staleness import BoundedStalenessPipeline
 from ...parallel.tensor_ps import TensorPS
 from ...utils.tracing import stage
 
@@ -72,6 +76,16 @@ class DistributedSGNS:
         wire = _WIRE[cfg.wire_dtype]
         self.ps_in = TensorPS(self.w_in, self.comm, wire)
         self.ps_out = TensorPS(self.w_out, self.comm, wire)
+        # the kernels find "negative == context" and center runs by comparing plan
+        # positions: request plans (one position per request) would silently break
+        # both, so the SGNS tables always de-duplicate
+        self.ps_in.dedup_mode = True
+        self.ps_out.dedup_mode = True
+        # PS path: both tables planned together (one count exchange per micro-batch),
+        # one micro-batch ahead (lookahead): the host reads counts enqueued a step
+        # earlier and never idles the device; staleness 1 when pipelined
+        self.pipe = BoundedStalenessPipeline([self.ps_in, self.ps_out], self._compute,
+                                             staleness=1 if cfg.pipeline else 0)
         if counts is None:  # Zipf-like default frequency profile
             counts = 1.0 / torch.arange(1, cfg.vocab_size + 1, dtype=torch.float64)
         prob, alias = ops.build_alias_table((counts.double() ** cfg.unigram_power).numpy())
@@ -99,16 +113,23 @@ class DistributedSGNS:
         lr = c.learning_rate if lr is None else lr
         if self._direct:
             return self._direct_step(centers, contexts, lr, with_loss)
-        if with_loss:
-            self.flush()
-            return self._finish(self._start(centers, contexts), lr, True)
-        pending = self._start(centers, contexts, async_rows=self._pipelined)
-        if self._pipelined:
-            prev, self._pending = self._pending, (pending, lr)
-            if prev is not None:
-                self._finish(prev[0], prev[1], False)
-        else:
-            self._finish(pending, lr, False)
+        P = centers.numel()
+        with stage("sgns.negatives", self.timer):
+            negs = ops.sample_alias(self.prob, self.alias, self._n_negatives(P),
+                                    seed=c.seed + 17 * self.comm.rank, counter=self.counter)
+        self.counter += 1
+        outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
+        keys = (centers, outs)
+        if with_loss:  # synchronous: every earlier batch applied, this one computed now
+            self.pipe.drain()
+            st, la = self.pipe.staleness, self.pipe.lookahead
+            self.pipe.staleness, self.pipe.lookahead = 0, False
+            try:
+                res = self.pipe.submit(keys, (P, lr, True))
+            finally:
+                self.pipe.staleness, self.pipe.lookahead = st, la
+            return res[0]
+        self.pipe.submit(keys, (P, lr, False))
         return None
 
     @property
@@ -149,36 +170,18 @@ class DistributedSGNS:
 
     @property
     def _pipelined(self) -> bool:
-        return self.cfg.pipeline and self.comm.world > 1
+        return self.cfg.pipeline and not self._direct
 
     def flush(self):
-        p = getattr(self, "_pending", None)
-        self._pending = None
-        if p is not None:
-            self._finish(p[0], p[1], False)
+        self.pipe.drain()
 
-    def _start(self, centers, contexts, async_rows: bool = False):
+    def _compute(self, rows, plans, payload):
+        """The SGNS kernel on one micro-batch's pulled rows: per-unique-row deltas of
+        both tables (pushed by the pipeline) and, on request, the summed loss."""
         c = self.cfg
-        P = centers.numel()
-        with stage("sgns.negatives", self.timer):
-            negs = ops.sample_alias(self.prob, self.alias, self._n_negatives(P),
-                                    seed=c.seed + 17 * self.comm.rank, counter=self.counter)
-        self.counter += 1
-        outs = torch.cat([contexts.to(device=negs.device, dtype=torch.int32), negs])
-        if async_rows:
-            rin, win, plan_in = self.ps_in.pull_async(centers)
-            rout, wout, plan_out = self.ps_out.pull_async(outs)
-            return P, (rin, win, plan_in), (rout, wout, plan_out)
-        rin, plan_in = self.ps_in.pull(centers)
-        rout, plan_out = self.ps_out.pull(outs)
-        return P, (rin, None, plan_in), (rout, None, plan_out)
-
-    def _finish(self, pending, lr, with_loss):
-        c = self.cfg
-        P, (rows_in, w_in, plan_in), (rows_out, w_out, plan_out) = pending
-        for w in (w_in, w_out):
-            if w is not None:
-                w.wait()
+        P, lr, with_loss = payload
+        rows_in, rows_out = rows
+        plan_in, plan_out = plans
         dev = rows_in.device
         d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
         d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
@@ -192,12 +195,8 @@ class DistributedSGNS:
                 loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
                                      c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
                                      neg_k=c.shared_negatives, neg_group=c.neg_group)
-        self.ps_in.push(plan_in, d_in)
-        self.ps_out.push(plan_out, d_out)
         self.pairs_seen += P
-        if with_loss:
-            return float(loss.item()) / max(P, 1)
-        return None
+        return [d_in, d_out], (float(loss.item()) / max(P, 1) if with_loss else None)
 
     def embeddings(self, only_touched: bool = True):
         self.flush()

@@ -24,6 +24,11 @@ the device on split sizes.  Everything is stream-ordered on the device, so the
 bound is exact: the gather of batch ``k`` is enqueued after the apply of batch
 ``k-s-1``.
 
+Several tables: ``ps`` may be a list of ``TensorPS`` (SGNS pulls input and output
+rows per micro-batch); ``submit`` then takes one key tensor per table, their
+plans share ONE count exchange (``TensorPS.plan_begin_multi``), and ``compute``
+receives / returns lists (rows, plans, deltas) in table order.
+
 End of input: every ``submit`` carries a ``flag`` that reaches all peers with
 the counts; ``all_flagged`` turns True on every rank at the same micro-batch once
 every rank flagged it (the ``FlinkEOF`` barrier, ``M/utils/FlinkEOF.scala:97-107``,
@@ -43,7 +48,7 @@ ComputeFn = Callable[[torch.Tensor, PullPlan, Any], Tuple[Optional[torch.Tensor]
 
 
 class BoundedStalenessPipeline:
-    def __init__(self, ps: TensorPS, compute: ComputeFn, staleness: int = 1, lr: float = 0.0,
+    def __init__(self, ps, compute: ComputeFn, staleness: int = 1, lr: float = 0.0,
                  lookahead: Optional[bool] = None):
         """``lookahead`` (default: ``staleness > 0``): stage B of a batch waits for
         the next ``submit``, so its counts are never waited for on an idle device.
@@ -51,6 +56,8 @@ class BoundedStalenessPipeline:
         batch is pulled, computed and pushed inside its own ``submit``."""
         if staleness < 0:
             raise ValueError("staleness must be >= 0")
+        self.multi = isinstance(ps, (list, tuple))
+        self.pss: List[TensorPS] = list(ps) if self.multi else [ps]
         self.ps, self.compute, self.staleness, self.lr = ps, compute, int(staleness), lr
         self.lookahead = staleness > 0 if lookahead is None else bool(lookahead)
         self._planned: deque = deque()  # (pending plan, payload) after stage A
@@ -63,7 +70,10 @@ class BoundedStalenessPipeline:
         """Begin the pull of a new micro-batch; finish (compute + push) every
         batch that would otherwise exceed the staleness bound.  Returns the
         results of the batches finished by this call, oldest first."""
-        self._planned.append((self.ps.plan_begin(keys, flag), payload))
+        if self.multi:
+            self._planned.append((TensorPS.plan_begin_multi(self.pss, keys, flag), payload))
+        else:
+            self._planned.append((self.ps.plan_begin(keys, flag), payload))
         self.submitted += 1
         out: List[Any] = []
         while len(self._planned) > (1 if self.lookahead else 0):
@@ -93,19 +103,28 @@ class BoundedStalenessPipeline:
         return len(self._planned)
 
     def _pull_next(self):
-        pp, payload = self._planned.popleft()
-        plan = self.ps.plan_end(pp)
-        if plan.peer_flags and all(f != 0 for f in plan.peer_flags):
+        pps, payload = self._planned.popleft()
+        if not self.multi:
+            pps = [pps]
+        plans = [ps.plan_end(pp) for ps, pp in zip(self.pss, pps)]
+        if plans[0].peer_flags and all(f != 0 for f in plans[0].peer_flags):
             self.all_flagged = True
-        rows, work = self.ps.pull_planned(plan, async_op=True)
+        pulled = [ps.pull_planned(plan, async_op=True) for ps, plan in zip(self.pss, plans)]
         self.max_observed = max(self.max_observed, len(self._pulled))
-        self._pulled.append((rows, work, plan, payload))
+        self._pulled.append(([r for r, _ in pulled], [w for _, w in pulled], plans, payload))
 
     def _finish(self, item) -> Any:
-        rows, work, plan, payload = item
-        if work is not None:
-            work.wait()
-        deltas, result = self.compute(rows, plan, payload)
+        rows, works, plans, payload = item
+        for w in works:
+            if w is not None:
+                w.wait()
+        if self.multi:
+            deltas, result = self.compute(rows, plans, payload)
+            for ps, plan, d in zip(self.pss, plans, deltas or [None] * len(plans)):
+                if d is not None:
+                    ps.push(plan, d, lr=self.lr)
+            return result
+        deltas, result = self.compute(rows[0], plans[0], payload)
         if deltas is not None:
-            self.ps.push(plan, deltas, lr=self.lr)
+            self.ps.push(plans[0], deltas, lr=self.lr)
         return result

@@ -35,7 +35,7 @@ micro-batches so pull ``k`` is served before the pushes of ``k-s .. k-1``
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import torch
 
@@ -82,6 +82,11 @@ class PendingPlan:
     identity: bool = False
     unique: bool = True
     static: bool = False  # sizes known on the host (world 1): nothing to wait for
+    #: ``TensorPS._plan_seq`` when the counts' event was recorded
+    seq: int = 0
+    #: columns of ``host`` holding (sent count, sent flag, recv count, recv flag): several
+    #: tables planned together (``plan_begin_multi``) share one exchange and one host copy
+    cols: tuple = (0, 1, 2, 3)
 
 
 class TensorPS:
@@ -92,9 +97,12 @@ class TensorPS:
         # sparse-id tables (parallel.hash_table) dedup through the per-batch hashed claim map
         self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device,
                                         hashed=True if getattr(table, "sparse", False) else None)
-        #: pulls = requests, unique = unique keys, steps = plans; host_stalls = plan_end
-        #: calls whose counts had not reached the host yet (the host waited on the device)
-        self.stats = {"pulls": 0, "unique": 0, "steps": 0, "host_stalls": 0, "pushes": 0}
+        self._stats = {"pulls": 0, "unique": 0, "steps": 0, "host_waits": 0, "host_stalls": 0, "pushes": 0}
+        #: plans whose counts went to the host through an event (``PendingPlan.seq``)
+        self._plan_seq = 0
+        #: static plans pad their unique keys to a bound: the exact counts accumulate on
+        #: the device (no per-step sync) and are folded in when ``stats`` is read
+        self._lazy: dict = {}
         self.timer = None  # utils.metrics.StageTimer (optional)
         #: pushes carry a validity column (set by the device PS logic on every rank
         #: alike): rows a worker did not push are skipped by the apply and by the
@@ -113,6 +121,35 @@ class TensorPS:
         #: features repeats ~8 % of 4M keys) and the rule is additive (atomic apply)
         self.dedup_mode: Optional[bool] = None
         self._req_iota: Optional[torch.Tensor] = None
+        #: static request / identity plans reference the caller's key tensor (``uniq`` /
+        #: ``pos`` = the keys) until the batch is served and pushed, which with a
+        #: pipeline is one or more submits later: they keep a copy unless the owner
+        #: guarantees its key tensors are never rewritten (``keys_stable``)
+        self.keys_stable = False
+
+    @property
+    def stats(self) -> dict:
+        """pulls = requests, unique = unique keys planned (exact also for padded static
+        plans), steps = plans, pushes = unique keys applied; host_waits = ``plan_end``
+        calls that found their counts not yet on the host (the host waited: with a
+        device-bound pipeline that is plain back-pressure), host_stalls = the subset
+        where nothing had been enqueued after those counts -- the device drains and
+        idles while the host waits (``plan()`` back to back, or a pipeline without
+        lookahead)."""
+        if self._lazy:
+            for k, t in self._lazy.items():
+                self._stats[k] += int(t.item())
+            self._lazy = {}
+        return self._stats
+
+    def _count_lazy(self, key: str, valid: torch.Tensor) -> None:
+        if valid.is_cuda and torch.cuda.is_current_stream_capturing():
+            # a captured step (core.step_graph) replays its host-side increments: count the
+            # bound there (a device counter inside the graph would not be read per replay)
+            self._stats[key] += valid.numel()
+            return
+        n = valid.sum()
+        self._lazy[key] = n if key not in self._lazy else self._lazy[key] + n
 
     #: key space / batch ratio above which ``dedup_mode = None`` ships requests undeduplicated
     REQUEST_PLAN_RATIO = 64
@@ -144,6 +181,14 @@ class TensorPS:
         (with empty ``keys`` when it has nothing to pull).  ``flag`` (an int) is
         delivered to every peer with the counts (``PullPlan.peer_flags``).  ``dedup``:
         force (True) the de-duplicating plan instead of ``dedups(n)``'s choice."""
+        a = self._stage_a(keys, flag, dedup)
+        if isinstance(a, PendingPlan):
+            return a
+        return self._pending(*a, flag=flag)
+
+    def _stage_a(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None):
+        """The device part of stage A: a finished (static) ``PendingPlan``, or
+        ``(n, counts, uniq, pos, unique)`` still needing the count exchange."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
         n = keys.numel()
         if self.identity_for(n):
@@ -153,6 +198,8 @@ class TensorPS:
             with stage("ps.presence", self.timer):
                 present = torch.zeros(ks, dtype=torch.uint8, device=keys.device)
                 ops.mark_rows(present, keys)
+            if not self.keys_stable:
+                keys = keys.clone()
             return PendingPlan(n, None, self._iota, keys, None, None, int(flag), valid=present.view(torch.bool),
                                n_bound=ks, identity=True, static=True)
         W = self.comm.world
@@ -160,11 +207,12 @@ class TensorPS:
             if W == 1 and self.static:  # every request is its own row: nothing to compute
                 if self._req_iota is None or self._req_iota.numel() < n:
                     self._req_iota = torch.arange(max(n, 1), dtype=torch.int32, device=keys.device)
-                return PendingPlan(n, None, keys, self._req_iota[:n], None, None, int(flag), n_bound=n,
+                return PendingPlan(n, None, keys if self.keys_stable else keys.clone(), self._req_iota[:n], None,
+                                   None, int(flag), n_bound=n,
                                    unique=False, static=True)
             with stage("ps.route", self.timer):
                 counts, prefix, uniq, pos = self.dedup.route(keys)
-            return self._pending(n, counts, uniq, pos, flag, unique=False)
+            return n, counts, uniq, pos, False
         with stage("ps.dedup", self.timer):
             counts, prefix, uniq, pos = self.dedup.run(keys)
         if W == 1 and self.static and not getattr(self.table, "sparse", False):
@@ -179,9 +227,9 @@ class TensorPS:
                 self.dedup.reset_claims(gkeys)
             return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb,
                                static=True)
-        return self._pending(n, counts, uniq, pos, flag)
+        return n, counts, uniq, pos, True
 
-    def _pending(self, n, counts, uniq, pos, flag, unique: bool = True) -> PendingPlan:
+    def _pending(self, n, counts, uniq, pos, unique: bool = True, flag: int = 0) -> PendingPlan:
         """Stage A's count exchange of a computed (de-duplicated or request) plan."""
         W = self.comm.world
         # the workspace is reused by the next plan_begin: this plan keeps copies
@@ -196,7 +244,8 @@ class TensorPS:
                 ev.record()
             else:
                 host, ev = counts[:1].to("cpu", torch.int32), None
-            return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique)
+            self._plan_seq += 1
+            return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
         send = torch.cat([counts.view(W, 1).to(torch.int32), flags], dim=1).contiguous()  # [W, 2]
         with stage("ps.count-a2a", self.timer):
@@ -209,35 +258,86 @@ class TensorPS:
             ev.record()
         else:
             host, ev = both.to("cpu"), None
-        return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique)
+        self._plan_seq += 1
+        return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
         if pp.static:  # static world-1 plan: sizes known on the host, nothing to wait for
-            self.stats["pulls"] += pp.n
-            self.stats["unique"] += pp.n_bound
-            self.stats["steps"] += 1
+            self._stats["pulls"] += pp.n
+            if pp.valid is not None:
+                self._count_lazy("unique", pp.valid)
+            else:
+                self._stats["unique"] += pp.n_bound
+            self._stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
                             valid=pp.valid, identity=pp.identity, unique=pp.unique)
         if pp.event is not None:
             if not pp.event.query():
-                self.stats["host_stalls"] += 1
+                self._stats["host_waits"] += 1
+                if pp.seq == self._plan_seq:  # no later plan was enqueued behind these counts
+                    self._stats["host_stalls"] += 1
             pp.event.synchronize()
+        sc, _, rc, rf = pp.cols
         if pp.host.dim() == 1:  # world 1
-            c = int(pp.host[0])
-            h = [[c, pp.flag, c, pp.flag]]
+            c = int(pp.host[sc])
+            send_splits, recv_splits, peer_flags = [c], [c], [pp.flag]
         else:
             h = pp.host.tolist()
-        send_splits = [int(r[0]) for r in h]
-        recv_splits = [int(r[2]) for r in h]
-        peer_flags = [int(r[3]) for r in h]
+            send_splits = [int(r[sc]) for r in h]
+            recv_splits = [int(r[rc]) for r in h]
+            peer_flags = [int(r[rf]) for r in h]
         n_unique = int(sum(send_splits))
         with stage("ps.key-a2a", self.timer):
             recv_keys = self.comm.all_to_all(pp.uniq[:n_unique], send_splits, recv_splits)
-        self.stats["pulls"] += pp.n
-        self.stats["unique"] += n_unique
-        self.stats["steps"] += 1
+        self._stats["pulls"] += pp.n
+        self._stats["unique"] += n_unique
+        self._stats["steps"] += 1
         return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n, unique=pp.unique)
+
+    @staticmethod
+    def plan_begin_multi(pss: Sequence["TensorPS"], keys_list: Sequence[torch.Tensor], flag: int = 0,
+                         dedup: Optional[bool] = None) -> List[PendingPlan]:
+        """Stage A of one micro-batch's plans on several tables (same ranks and
+        device) with ONE count exchange and ONE device->host copy: the counts of
+        every table and the flag travel as the columns of one ``[W, T + 1]``
+        message (SGNS pulls from two tables per micro-batch: two exchanges and two
+        host copies otherwise)."""
+        if len(pss) != len(keys_list):
+            raise ValueError("one key tensor per table")
+        staged = [ps._stage_a(k, flag, dedup) for ps, k in zip(pss, keys_list)]
+        comm = pss[0].comm
+        dyn = [j for j, a in enumerate(staged) if not isinstance(a, PendingPlan)]
+        out: List[PendingPlan] = [a if isinstance(a, PendingPlan) else None for a in staged]
+        if not dyn:
+            return out
+        T, W = len(dyn), comm.world
+        dev = staged[dyn[0]][1].device
+        counts = [staged[j][1].clone() for j in dyn]  # the workspaces are reused by the next plan
+        if W == 1:
+            send = torch.cat([c[:1].to(torch.int32) for c in counts])  # [T]
+            both = send
+        else:
+            cols = [c.view(W, 1).to(torch.int32) for c in counts]
+            cols.append(torch.full((W, 1), int(flag), dtype=torch.int32, device=dev))
+            send = torch.cat(cols, dim=1).contiguous()  # [W, T + 1]
+            with stage("ps.count-a2a", pss[0].timer):
+                recv = comm.exchange_counts(send)
+            both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 2T + 2]
+        if dev.type == "cuda":
+            host = torch.empty(tuple(both.shape), dtype=torch.int32, pin_memory=True)
+            host.copy_(both, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = both.to("cpu"), None
+        for t, j in enumerate(dyn):
+            n, _, uniq, pos, unique = staged[j]
+            cols = (t, T, t, T) if W == 1 else (t, T, T + 1 + t, 2 * T + 1)
+            pss[j]._plan_seq += 1
+            out[j] = PendingPlan(n, counts[t], uniq[:n].clone(), pos.clone(), host, ev, int(flag), unique=unique,
+                                 cols=cols, seq=pss[j]._plan_seq)
+        return out
 
     def plan(self, keys: torch.Tensor, persistent: bool = False, flag: int = 0,
              dedup: Optional[bool] = None) -> PullPlan:
@@ -314,7 +414,10 @@ class TensorPS:
             recv = recv[:, :D].contiguous()
             recv_keys = torch.where(valid, recv_keys, torch.full_like(recv_keys, -1))
         opt = op or self.table.optimizer
-        self.stats["pushes"] += plan.n_unique
+        if plan.valid is not None:
+            self._count_lazy("pushes", plan.valid)
+        else:
+            self._stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
             # (a request plan repeats keys inside a segment: atomic add)
             seg_add = opt == "add" and len(plan.recv_splits) <= 16 and plan.unique

@@ -285,3 +285,86 @@ def test_sgns_gpu_modes_reduce_loss(mode):
     for s in range(0, c.numel() - 8192, 8192):
         m.step(c[s:s + 8192], o[s:s + 8192])
     assert m.step(c[:8192], o[:8192], with_loss=True) < 0.8 * first
+
+
+# ----------------------------------------------------------- SGNS PS path: planning
+def test_sgns_ps_plans_always_deduplicate_at_large_vocab_ratio():
+    """The kernels find "negative == context" and center runs by comparing plan
+    positions, so SGNS tables never get request plans -- even at a vocab / batch
+    ratio far above TensorPS.REQUEST_PLAN_RATIO."""
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig
+
+    V, P = 200_000, 256
+    m = DistributedSGNS(SGNSConfig(vocab_size=V, dim=16, learning_rate=0.01, local_direct=False))
+    assert V >= m.ps_in.REQUEST_PLAN_RATIO * P * (1 + m.cfg.negatives)
+    assert m.ps_in.dedups(P) and m.ps_out.dedups(P * (1 + m.cfg.negatives))
+    g = torch.Generator().manual_seed(0)
+    c = torch.randint(0, 50, (P,), generator=g, dtype=torch.int32)  # repeated centers: runs must merge
+    o = torch.randint(0, V, (P,), generator=g, dtype=torch.int32)
+    for _ in range(3):
+        m.step(c, o)
+    m.flush()
+    st = m.ps_in.stats
+    assert st["unique"] <= 50 * st["steps"] < st["pulls"]
+
+
+def test_sgns_ps_path_both_tables_share_one_plan_exchange():
+    """Both tables are planned by one ``plan_begin_multi`` (one count exchange, one
+    host copy) one micro-batch ahead: the pipelined steps equal the synchronous ones
+    up to the staleness of one batch, and the last flush applies everything."""
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.tensor_ps import TensorPS
+
+    calls = []
+    orig = TensorPS.plan_begin_multi
+
+    def spy(pss, keys, flag=0, dedup=None):
+        calls.append(len(pss))
+        return orig(pss, keys, flag, dedup)
+
+    TensorPS.plan_begin_multi = staticmethod(spy)
+    try:
+        m = DistributedSGNS(SGNSConfig(vocab_size=3000, dim=16, learning_rate=0.01, local_direct=False))
+        c, o = skipgram_pairs(synthetic_corpus(20000, 3000, seed=2), 4)
+        l0 = m.step(c[:2048], o[:2048], with_loss=True)
+        for i in range(30):
+            s = (i * 2048) % (c.numel() - 2048)
+            m.step(c[s:s + 2048], o[s:s + 2048])
+        assert m.pipe.in_flight + m.pipe.planned >= 1  # one batch still in the pipeline
+        l1 = m.step(c[:2048], o[:2048], with_loss=True)  # drains first
+    finally:
+        TensorPS.plan_begin_multi = staticmethod(orig)
+    assert calls and all(n == 2 for n in calls) and len(calls) == 32
+    assert l1 < l0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_sgns_ps_path_steady_state_never_idles_the_device_on_counts(pipeline):
+    """Pipelined: every plan_end finds later work enqueued behind its counts (zero
+    device-idling host stalls); synchronous (pipeline=False): each step's counts are
+    the newest work on the stream, so the host drains the device every step."""
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=100_000, dim=128, learning_rate=0.01, local_direct=False,
+                                   pipeline=pipeline), comm=Comm(device=torch.device("cuda")))
+    c, o = skipgram_pairs(synthetic_corpus(400_000, 100_000, seed=1, device="cuda"), 4)
+    P = 1 << 16
+    for i in range(4):  # warm-up
+        m.step(c[i * P:(i + 1) * P], o[i * P:(i + 1) * P])
+    m.flush()
+    torch.cuda.synchronize()
+    s0 = dict(m.ps_in.stats), dict(m.ps_out.stats)
+    for i in range(20):
+        s = ((i + 4) * P) % (c.numel() - P)
+        m.step(c[s:s + P], o[s:s + P])
+    m.flush()
+    torch.cuda.synchronize()
+    stalls = [ps.stats["host_stalls"] - s["host_stalls"] for ps, s in zip((m.ps_in, m.ps_out), s0)]
+    if pipeline:
+        assert stalls == [0, 0], stalls
+    else:
+        assert min(stalls) >= 10, stalls

@@ -1,0 +1,184 @@
+"""The virtual N-rank world (``parallel/vworld.py``) on CPU: collective semantics,
+desync detection, and the N > 1 model paths against gloo / the sequential replay.
+
+On CPU every transfer completes when it is matched (no streams), so these tests pin
+the matching rules and the data movement; tests/test_vworld_gpu.py runs the same
+paths with RCCL's stream semantics and injected delays."""
+import pytest
+import torch
+import torch.distributed as dist
+
+from dist_utils import run_ranks
+from flink_parameter_server_1_amd.parallel.vworld import VirtualWorldAborted, run_virtual
+
+
+def _collectives(comm):
+    W, r = comm.world, comm.rank
+    send = torch.arange(sum(range(1, W + 1)), dtype=torch.float32) + 100 * r
+    ss = list(range(1, W + 1))  # rank r sends p+1 rows to rank p
+    rs = [r + 1] * W
+    out = comm.all_to_all(send, ss, rs)
+    out2, work = comm.all_to_all_async(send * 2, ss, rs)
+    work.wait()
+    counts = comm.exchange_counts(torch.tensor([[10 * r + p, r] for p in range(W)], dtype=torch.int32))
+    s, mx = torch.tensor([float(r + 1)]), torch.tensor([float(r + 1)])
+    comm.all_reduce(s)
+    comm.all_reduce(mx, op=dist.ReduceOp.MAX)
+    g = [int(x) for x in comm.all_gather(torch.tensor([r * r]))]
+    return out, out2, counts, float(s), float(mx), g, comm.max_over_ranks(r), comm.sum_over_ranks(1.0), \
+        comm.gather_floats(r * 0.5)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_collectives_move_the_right_rows(world):
+    res = run_virtual(_collectives, world)
+    for p, (out, out2, counts, s, mx, g, m, n, gf) in enumerate(res):
+        want = []
+        for r in range(world):
+            off = sum(range(1, p + 1))
+            want += [off + k + 100 * r for k in range(p + 1)]
+        assert out.tolist() == want and out2.tolist() == [2 * x for x in want]
+        assert counts.tolist() == [[10 * r + p, r] for r in range(world)]
+        assert s == world * (world + 1) / 2 and mx == world
+        assert g == [r * r for r in range(world)] and m == world - 1 and n == world
+        assert gf == [r * 0.5 for r in range(world)]
+
+
+def test_p2p_matches_fifo_per_channel():
+    def f(comm):
+        W, r = comm.world, comm.rank
+        nxt, prv = (r + 1) % W, (r - 1) % W
+        bufs = [torch.empty(3) for _ in range(3)]
+        works = []
+        for k in range(3):  # three messages on the same channel, posted before any wait
+            works += comm.p2p([(torch.full((3,), 10.0 * r + k), nxt)], [(bufs[k], prv)])
+        for w in works:
+            w.wait()
+        return [b.tolist() for b in bufs], comm.peer_bytes
+
+    for p, (bufs, peer_bytes) in enumerate(run_virtual(f, 4)):
+        prv = (p - 1) % 4
+        assert bufs == [[10.0 * prv + k] * 3 for k in range(3)]
+        assert peer_bytes[(p + 1) % 4] == 3 * 12
+
+
+def test_desync_and_mismatch_abort_every_rank():
+    def desync(comm):
+        if comm.rank == 0:
+            comm.all_reduce(torch.ones(1))
+        else:
+            comm.all_gather(torch.ones(1))
+
+    with pytest.raises(VirtualWorldAborted, match="desync"):
+        run_virtual(desync, 2, timeout_s=10)
+
+    def bad_splits(comm):
+        comm.all_to_all(torch.zeros(4), [2, 2], [1, 3] if comm.rank == 0 else [2, 2])
+
+    with pytest.raises(VirtualWorldAborted, match="expects"):
+        run_virtual(bad_splits, 2, timeout_s=10)
+
+    def unmatched(comm):
+        if comm.rank == 0:
+            for w in comm.p2p([(torch.ones(2), 1)], []):
+                w.wait()
+
+    with pytest.raises(VirtualWorldAborted, match="never matched"):
+        run_virtual(unmatched, 2, timeout_s=2)
+
+    def boom(comm):
+        if comm.rank == 1:
+            raise KeyError("rank 1 failed")
+        comm.barrier()
+
+    with pytest.raises(KeyError):
+        run_virtual(boom, 3, timeout_s=10)
+
+
+NU, NI, D, B, STEPS = 700, 301, 8, 500, 3
+
+
+def _mf(comm, world, schedule, exchange):
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+
+    cfg = MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.1, range_min=0.0, range_max=0.3,
+                   rotation=schedule, exchange=exchange)
+    m = DistributedMF(cfg, comm)
+    data = SyntheticRatings(NU, NI, B * STEPS, comm.rank, world, seed=3)
+    for s in range(STEPS):
+        m.step(*data.batch(s, B))
+    se = m.sq_err(*data.batch(0, B))
+    ids, vals = m.item_vectors(only_touched=True)
+    o = torch.argsort(ids)
+    return ids[o], vals[o], m.U.clone(), se
+
+
+def _mf_gloo(rank, world, schedule, exchange):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    return _mf(Comm(), world, schedule, exchange)
+
+
+@pytest.mark.parametrize("world,schedule", [(2, "bidir"), (3, "ring"), (4, "bidir")])
+def test_rotation_in_virtual_world_equals_sequential_replay(world, schedule):
+    import test_rotation as T
+
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        res = run_virtual(_mf, world, world, schedule, "rotate")
+        users, items, seen = T._emulate(world, STEPS, schedule=schedule)
+    finally:
+        torch.set_num_threads(nt)
+    ids = torch.cat([x[0] for x in res])
+    assert torch.equal(torch.sort(ids).values, torch.nonzero(seen).flatten())
+    torch.testing.assert_close(torch.cat([x[1] for x in res]), items[ids], rtol=1e-6, atol=1e-7)
+    for r in range(world):
+        torch.testing.assert_close(res[r][2], users[r].weight, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("exchange", ["ps", "rotate"])
+def test_virtual_world_equals_gloo_bitwise(exchange):
+    """Same model, same data: N threads over the virtual transport == N gloo processes."""
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        v = run_virtual(_mf, 2, 2, "bidir", exchange)
+    finally:
+        torch.set_num_threads(nt)
+    g = run_ranks(_mf_gloo, 2, "bidir", exchange)
+    for a, b in zip(v, g):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+        assert a[3] == b[3]
+
+
+def _sgns(comm, world):
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    m = DistributedSGNS(SGNSConfig(vocab_size=3000, dim=16, window=3, learning_rate=0.01), comm=comm)
+    c, o = skipgram_pairs(synthetic_corpus(20000, 3000, seed=comm.rank), 3, torch.Generator().manual_seed(1))
+    for i in range(6):
+        m.step(c[i * 1024:(i + 1) * 1024], o[i * 1024:(i + 1) * 1024])
+    loss = m.step(c[:1024], o[:1024], with_loss=True)
+    ids, w = m.embeddings()
+    o_ = torch.argsort(ids)
+    return ids[o_], w[o_], loss
+
+
+def _sgns_gloo(rank, world):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    return _sgns(Comm(), world)
+
+
+def test_sgns_pipeline_in_virtual_world_equals_gloo_bitwise():
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        v = run_virtual(_sgns, 2, 2)
+    finally:
+        torch.set_num_threads(nt)
+    g = run_ranks(_sgns_gloo, 2)
+    for a, b in zip(v, g):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and a[2] == b[2]
