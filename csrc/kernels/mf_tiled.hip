@@ -187,6 +187,25 @@ __device__ __forceinline__ void tp3_scan(const int32_t* cnt, int32_t* off, int n
 // <= 512 fine histograms are written however many level-1 chunks there are.
 // (Flushing the fine histogram with global atomics cost 16M atomics per step
 // at KT = 15.6k buckets and 65k-rating chunks, 4M with 256 workgroups.)
+//
+// H16: two 16-bit counters per LDS word (KT / 2 words: 62.5 KiB instead of 125 KiB
+// at the N = 8 layout's 31k buckets, so a count workgroup leaves room for two
+// tile-SGD workgroups on its CU -- the partition of batch k+1 runs beside the SGD
+// of batch k, profiles/r3_emulate8_timeline.md).  Overflow-safe: the ratings are
+// counted in sub-batches of H16_SB per workgroup; a counter that reaches 2^15 sets a
+// flag, and at the next sub-batch boundary the whole histogram is flushed into the
+// workgroup's global row (which then accumulates) and zeroed.  A counter is below
+// 2^15 at the start of every sub-batch and grows by at most H16_SB = 2^15 in it,
+// so it never exceeds 2^16 - 1.  Uniform keys never flush (~8 counts per bucket).
+constexpr int H16_SB = 32768;
+
+template <bool H16>
+__device__ __forceinline__ int32_t hb_get(const int32_t* hb, int b) {
+  if constexpr (H16) return (int32_t)(((uint32_t)hb[b >> 1] >> ((b & 1) << 4)) & 0xffffu);
+  else return hb[b];
+}
+
+template <bool H16>
 __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restrict__ uid,
                                                          const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
                                                          int G, int sub, TileGeo g, int cshift, int NC, int KT,
@@ -195,56 +214,89 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
   // One LDS atomic per rating (LDS atomics run at ~1 lane per CU cycle and
   // bound this kernel); the coarse counts of a chunk are read off the fine
   // histogram afterwards: 8 lanes per coarse key sum its 2^cshift buckets.
-  extern __shared__ int32_t hb[];  // [KT] (dynamic LDS)
-  __shared__ int32_t hc_prev[TP3_MAXK];
-  for (int k = threadIdx.x; k < KT; k += blockDim.x) hb[k] = 0;
-  if (threadIdx.x < NC) hc_prev[threadIdx.x] = 0;
+  extern __shared__ int32_t hb[];  // [KT] ints, or [ceil(KT / 2)] words of two 16-bit counters (dynamic LDS)
+  __shared__ int32_t hc_prev[TP3_MAXK], hc_acc[TP3_MAXK];
+  __shared__ int32_t s_ovf, s_flushed;
+  const int KW = H16 ? (KT + 1) / 2 : KT;
+  for (int k = threadIdx.x; k < KW; k += blockDim.x) hb[k] = 0;
+  if (threadIdx.x < NC) { hc_prev[threadIdx.x] = 0; hc_acc[threadIdx.x] = 0; }
+  if (threadIdx.x == 0) { s_ovf = 0; s_flushed = 0; }
   __syncthreads();
+  int32_t* Hf = bcount + (int64_t)(blockIdx.x + 1) * KT;  // row 0 = the totals (tp3_colsum_kernel)
   const int span = 1 << cshift;
   const int per = (span + 7) / 8;
   const int ck = threadIdx.x >> 3, cl = threadIdx.x & 7;  // coarse key, lane in its group of 8
+  // coarse key ck's count now (summed by its 8 lanes; every lane gets the total)
+  auto coarse_now = [&]() {
+    int32_t tot = 0;
+    if (ck < NC)
+      for (int q = 0; q < per; ++q) {
+        const int b = (ck << cshift) + cl * per + q;
+        if (cl * per + q < span && b < KT) tot += hb_get<H16>(hb, b);
+      }
+    tot += __shfl_xor(tot, 1, 64);
+    tot += __shfl_xor(tot, 2, 64);
+    tot += __shfl_xor(tot, 4, 64);
+    return tot;
+  };
   const int c0 = blockIdx.x * sub, c1 = min(G, c0 + sub);
   for (int c = c0; c < c1; ++c) {
     const int64_t lo = (int64_t)c * chunk, hi = min(n, lo + chunk);
     constexpr int U4 = 8;  // loads in flight per thread (a lone dependent load pair per
                            // iteration left the kernel latency-bound at ~1.7 TB/s)
-    for (int64_t x0 = lo + threadIdx.x; x0 < hi; x0 += U4 * blockDim.x) {
-      int32_t iv[U4], uv[U4];
+    const int64_t step = (int64_t)U4 * blockDim.x;
+    for (int64_t s0 = lo; s0 < hi; s0 += (H16 ? H16_SB : hi - lo)) {
+      const int64_t s1 = H16 ? min(hi, s0 + H16_SB) : hi;
+      for (int64_t x0 = s0 + threadIdx.x; x0 < s1; x0 += step) {
+        int32_t iv[U4], uv[U4];
 #pragma unroll
-      for (int j = 0; j < U4; ++j) {
-        const int64_t x = x0 + (int64_t)j * blockDim.x;
-        iv[j] = x < hi ? iid[x] : -1;
-        uv[j] = x < hi ? uid[x] : 0;
+        for (int j = 0; j < U4; ++j) {
+          const int64_t x = x0 + (int64_t)j * blockDim.x;
+          iv[j] = x < s1 ? iid[x] : -1;
+          uv[j] = x < s1 ? uid[x] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < U4; ++j) {
+          if (iv[j] < 0) continue;
+          int bk; int32_t row;
+          tile_bucket(iv[j], uv[j], g, bk, row);
+          if constexpr (H16) {
+            const int sh = (bk & 1) << 4;
+            const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(hb) + (bk >> 1), 1u << sh);
+            if (((old >> sh) & 0xffffu) >= 32767u) s_ovf = 1;  // this counter reached 2^15
+          } else {
+            atomicAdd(hb + bk, 1);
+          }
+          if (seen != nullptr) seen[iv[j]] = 1;
+        }
       }
-#pragma unroll
-      for (int j = 0; j < U4; ++j) {
-        if (iv[j] < 0) continue;
-        int bk; int32_t row;
-        tile_bucket(iv[j], uv[j], g, bk, row);
-        atomicAdd(hb + bk, 1);
-        if (seen != nullptr) seen[iv[j]] = 1;
+      if constexpr (H16) {
+        __syncthreads();
+        if (s_ovf) {  // uniform: flush the histogram into the global row and restart it at zero
+          const int32_t tot = coarse_now();
+          if (ck < NC && cl == 0) { hc_acc[ck] += tot - hc_prev[ck]; hc_prev[ck] = 0; }
+          const bool first = !s_flushed;
+          for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = (first ? 0 : Hf[k]) + hb_get<true>(hb, k);
+          __syncthreads();
+          for (int k = threadIdx.x; k < KW; k += blockDim.x) hb[k] = 0;
+          if (threadIdx.x == 0) { s_ovf = 0; s_flushed = 1; }
+          __syncthreads();
+        }
       }
     }
     __syncthreads();
-    int32_t tot = 0;
-    if (ck < NC)
-      for (int q = 0; q < per; ++q) {
-        const int b = (ck << cshift) + cl * per + q;
-        if (cl * per + q < span && b < KT) tot += hb[b];
-      }
-    tot += __shfl_xor(tot, 1, 64);
-    tot += __shfl_xor(tot, 2, 64);
-    tot += __shfl_xor(tot, 4, 64);
+    const int32_t tot = coarse_now();
     if (ck < NC && cl == 0) {
-      const int32_t v = tot - hc_prev[ck];
+      const int32_t v = hc_acc[ck] + tot - hc_prev[ck];
       hc_prev[ck] = tot;
+      hc_acc[ck] = 0;
       if (v) atomicAdd(ccount + ck, v);
       H1[(int64_t)c * NC + ck] = v;
     }
     __syncthreads();  // hb is read above before the next chunk adds to it
   }
-  int32_t* Hf = bcount + (int64_t)(blockIdx.x + 1) * KT;  // row 0 = the totals (tp3_colsum_kernel)
-  for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = hb[k];
+  const bool flushed = s_flushed;
+  for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = (flushed ? Hf[k] : 0) + hb_get<H16>(hb, k);
 }
 
 // bcount[k] = sum of the count workgroups' rows bcount[1 + g][k]: 64 columns x 16
@@ -447,13 +499,23 @@ __device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int6
 // tiles [T0, grid) block I1 (offsets ptr1) -- two blocks with disjoint item rows
 // need no ordering, and one launch instead of two halves the tail of partly filled
 // waves (the local layout's two halves; the bidirectional rotation's two rings).
-template <int TPR, int V, int PF, bool REC8>
+//
+// DELTA (the PS path, one block): the item rows I are READ-ONLY (the pulled rows)
+// and the kernel writes the micro-batch's delta of every row of the block to Dl --
+// what the PS then adds (SimplePSLogic's vector sum).  With dl_init every row of
+// every tile is written in its tile's first chunk (zero when the chunk has none of
+// its ratings, the whole tile when the tile has no ratings); a later chunk of the
+// tile -- or a later launch without dl_init (the next user phase) -- starts from
+// I + Dl (the row as the earlier work left it) and adds its sum to Dl.  Replaces a working copy of the pulled rows and a subtraction pass
+// (round 3: clone + SGD + sub_, 1.3 GB of extra traffic at 1M x 64 rows).
+template <int TPR, int V, int PF, bool REC8, bool DELTA>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
                                                                int64_t block_rows, float lr, float lambda,
                                                                float* __restrict__ I1, int64_t block_rows1, int T0,
-                                                               const int32_t* __restrict__ ptr1) {
+                                                               const int32_t* __restrict__ ptr1,
+                                                               float* __restrict__ Dl, int dl_init) {
   using Rec = typename RecT<REC8>::type;
   constexpr int TG_CAP = tg_cap<REC8>();
   const Rec* __restrict__ rec = reinterpret_cast<const Rec*>(rec_);
@@ -474,7 +536,16 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
   const int grp = wave * GPW + lane / TPR, j = lane % TPR;
   float4* Ig = reinterpret_cast<float4*>(I) + r0 * D4;
   float4* Ug = reinterpret_cast<float4*>(U);
+  float4* Dg = DELTA ? reinterpret_cast<float4*>(Dl) + r0 * D4 : nullptr;
+  if (DELTA && dl_init && beg == end) {  // no ratings in this tile: its rows' deltas are zero
+    for (int k = threadIdx.x; k < nr * D4; k += blockDim.x) f4_st<true>(Dg + k, make_float4(0.f, 0.f, 0.f, 0.f));
+    return;
+  }
   for (int32_t c0 = beg; c0 < end; c0 += TG_CAP) {
+    // first: Dl of this tile holds nothing yet (its first chunk of a launch that
+    // initialises Dl); else every row continues from I + Dl (an earlier chunk, or an
+    // earlier launch over the same rows -- the user phases)
+    const bool first = DELTA && dl_init && c0 == beg;
     const int nc = min(TG_CAP, end - c0);
     for (int k = threadIdx.x; k <= nr; k += blockDim.x) cnt[k] = 0;
     __syncthreads();
@@ -517,12 +588,21 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
     __syncthreads();
     for (int row = grp; row < nr; row += ngroups) {
       const int a = start[row], b = start[row + 1];
-      if (a == b) continue;  // uniform in the lane group
-      float4 iv[V], acc[V];
+      if (a == b) {  // uniform in the lane group
+        if (DELTA && first)
+#pragma unroll
+          for (int v = 0; v < V; ++v) f4_st<true>(Dg + (int64_t)row * D4 + j + v * TPR, make_float4(0.f, 0.f, 0.f, 0.f));
+        continue;
+      }
+      float4 iv[V], acc[V], dv[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         iv[v] = f4_ld<true>(Ig + (int64_t)row * D4 + j + v * TPR);
         acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (DELTA && !first) {  // the earlier chunks' sum: the row continues from I + Dl
+          dv[v] = f4_ld<true>(Dg + (int64_t)row * D4 + j + v * TPR);
+          iv[v].x += dv[v].x; iv[v].y += dv[v].y; iv[v].z += dv[v].z; iv[v].w += dv[v].w;
+        }
       }
       // float4 offsets of the user rows: 32-bit for 8-B records (user < 2^24, D4 <= 64),
       // 14 fewer live VGPRs than 64-bit offsets
@@ -565,9 +645,15 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        float4 o = iv[v];
-        o.x += acc[v].x; o.y += acc[v].y; o.z += acc[v].z; o.w += acc[v].w;
-        f4_st<true>(Ig + (int64_t)row * D4 + j + v * TPR, o);
+        if constexpr (DELTA) {
+          float4 o = acc[v];
+          if (!first) { o.x += dv[v].x; o.y += dv[v].y; o.z += dv[v].z; o.w += dv[v].w; }
+          f4_st<true>(Dg + (int64_t)row * D4 + j + v * TPR, o);
+        } else {
+          float4 o = iv[v];
+          o.x += acc[v].x; o.y += acc[v].y; o.z += acc[v].z; o.w += acc[v].w;
+          f4_st<true>(Ig + (int64_t)row * D4 + j + v * TPR, o);
+        }
       }
     }
     __syncthreads();  // LDS reused by the next chunk
@@ -634,14 +720,17 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
   const int Gc = (G + sub - 1) / sub;
   int32_t* bhist = H1 + 1024 * (int64_t)NC;  // [1 + Gc][KT]: totals, then one row per count workgroup
-  const size_t hb_bytes = sizeof(int32_t) * (size_t)KT;
-  if (hb_bytes > 65536) {  // above the default dynamic-LDS ceiling: opt in (a workgroup may hold 160 KiB)
-    e = hipFuncSetAttribute((const void*)tp3_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hb_bytes);
-    if (e != hipSuccess) return (int)e;
+  // more than 16k buckets: 16-bit LDS counters (<= 64 KiB, the default dynamic-LDS
+  // ceiling, and room on the CU for two SGD workgroups beside the count workgroup)
+  const bool h16 = KT > 16384;
+  const size_t hb_bytes = sizeof(int32_t) * (size_t)(h16 ? (KT + 1) / 2 : KT);
+  if (h16) {
+    hipLaunchKernelGGL(tp3_count_kernel<true>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
+                       cshift, NC, KT, ccount, bhist, seen, H1);
+  } else {
+    hipLaunchKernelGGL(tp3_count_kernel<false>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
+                       cshift, NC, KT, ccount, bhist, seen, H1);
   }
-  hipLaunchKernelGGL(tp3_count_kernel, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G,
-                     sub, g, cshift, NC, KT,
-                     ccount, bhist, seen, H1);
   hipLaunchKernelGGL(tp3_colsum_kernel, dim3((KT + 63) / 64), dim3(1024), 0, s, bhist, Gc, KT);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)bhist, KT, ptr);
@@ -666,21 +755,27 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // Tiled SGD over one or two item blocks: block 0 = rows I0[rows0, D] with tile
 // offsets ptr0[T+1], block 1 (nblk = 2) = I1[rows1, D] with ptr1[T+1]; T tiles of
 // R (<= 256) rows each.  D must be 16, 32, 64, 128 or 256.
+// delta0 != nullptr (nblk = 1): DELTA mode -- I0 read-only, the block's deltas written
+// to delta0 (delta_init) or added to it (a later user phase over the same rows).
 FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, const int32_t* ptr0, int T, int R,
                              int64_t rows0, float* I1, const int32_t* ptr1, int64_t rows1, int nblk, int D, float lr,
-                             float lambda, void* stream) {
+                             float lambda, float* delta0, int delta_init, void* stream) {
   if (T <= 0) return 0;
   if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
+  if (delta0 != nullptr && nblk != 1) return (int)hipErrorInvalidValue;
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   if (nblk == 1) { I1 = I0; ptr1 = ptr0; rows1 = rows0; }
   const int grid = nblk * T;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
-#define FPS_TILED(TPR_, V_)                                                                                    \
-  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true>), dim3(grid), dim3(512), 0, s, U, I0,  \
-                               rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1);                            \
-  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false>), dim3(grid), dim3(512), 0, s, U, I0, rec, \
-                          ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1)
+#define FPS_TILED_(TPR_, V_, DL_)                                                                              \
+  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_>), dim3(grid), dim3(512), 0, s, U,  \
+                               I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init);    \
+  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_>), dim3(grid), dim3(512), 0, s, U, I0, \
+                          rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init)
+#define FPS_TILED(TPR_, V_)                      \
+  if (delta0 != nullptr) { FPS_TILED_(TPR_, V_, true); } \
+  else { FPS_TILED_(TPR_, V_, false); }
   switch (D) {
     case 16: FPS_TILED(4, 1); break;
     case 32: FPS_TILED(8, 1); break;
@@ -690,6 +785,7 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
     default: return (int)hipErrorInvalidValue;
   }
 #undef FPS_TILED
+#undef FPS_TILED_
   FPS_CHECK_LAUNCH();
   return 0;
 }

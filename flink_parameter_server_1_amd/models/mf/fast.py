@@ -390,10 +390,11 @@ class DistributedMF:
         (valid when the plan is the identity: pulled row = item id)."""
         c = self.cfg
         if self.sgd_mode == "tiled":
-            # tile-grouped SGD on a working copy of the pulled rows (one block, no item
-            # atomics); the pushed delta is what the micro-batch added to each row
-            orig = rows.float()
-            work = orig.clone()
+            # tile-grouped SGD on the pulled rows (one block, no item atomics) in the
+            # kernel's delta mode: the rows stay as pulled and the kernel writes what
+            # the micro-batch added to each row -- the pushed delta -- directly
+            rows = rows if rows.dtype == torch.float32 else rows.float()
+            delta = torch.empty_like(rows)  # every row written by the first phase's launch
             if staged is not None:
                 ptr, rec, ev = staged
                 if ev is not None:
@@ -402,9 +403,9 @@ class DistributedMF:
                 ptr, rec = self._ps_tiler.run(uid_local, pos, rating)
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):
-                    ops.mf_sgd_tiled(self.U, work, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
-                                     c.lam)
-            return work.sub_(orig)
+                    ops.mf_sgd_tiled(self.U, rows, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
+                                     c.lam, delta=delta, delta_init=p == 0)
+            return delta
         with stage("mf.sgd", self.timer):
             if self.sgd_mode == "grouped":
                 ptr, order = self.grouper.run(pos, n_unique)

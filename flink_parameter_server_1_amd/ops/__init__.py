@@ -518,20 +518,33 @@ class TilePartitioner:
         return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
-def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0):
+def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
+                 delta: Optional[torch.Tensor] = None, delta_init: bool = True):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
     records from ``TilePartitioner``): one workgroup per tile, every item row owned
-    by one lane group (registers), item deltas summed per row -- no item atomics."""
+    by one lane group (registers), item deltas summed per row -- no item atomics.
+    ``delta`` (same shape as ``I_block``): leave ``I_block`` unchanged and write
+    every row's summed item delta there instead (the PS path's push);
+    ``delta_init=False`` adds to the deltas of an earlier launch over the same rows
+    (the rows then continue from ``I_block + delta``)."""
+    if delta is not None and (delta.shape != I_block.shape or delta.dtype != torch.float32):
+        raise ValueError("mf_sgd_tiled: delta must be an fp32 tensor shaped like the item block")
     if _on_gpu(U):
         lib = N.require()
         p0 = _c(ptr).data_ptr() + 4 * block * T
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), p0, T, tile_rows, I_block.shape[0], None, None, 0, 1,
-                                     U.shape[1], lr, lam, N.stream_ptr(U.device)), "mf_sgd_tiled")
+                                     U.shape[1], lr, lam, None if delta is None else _c(delta).data_ptr(),
+                                     int(delta_init), N.stream_ptr(U.device)), "mf_sgd_tiled")
         return
     uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
-    R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
+    if delta is None:
+        R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
+        return
+    work = I_block.clone() if delta_init else I_block + delta
+    R.mf_sgd_local(U, work, uid[a:b], row[a:b], r[a:b], lr, lam)
+    torch.sub(work, I_block, out=delta)
 
 
 def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
@@ -547,7 +560,7 @@ def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, l
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), base + 4 * block * T, T, tile_rows, I0.shape[0],
                                      _c(I1).data_ptr(), base + 4 * block1 * T, I1.shape[0], 2, U.shape[1], lr, lam,
-                                     N.stream_ptr(U.device)), "mf_sgd_tiled_pair")
+                                     None, 1, N.stream_ptr(U.device)), "mf_sgd_tiled_pair")
         return
     mf_sgd_tiled(U, I0, rec, ptr, block, T, tile_rows, lr, lam)
     mf_sgd_tiled(U, I1, rec, ptr, block1, T, tile_rows, lr, lam)

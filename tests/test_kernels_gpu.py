@@ -215,8 +215,10 @@ def test_mf_sgd_local_seg_matches_slice():
 @pytest.mark.parametrize("rec8", [False, True])
 @pytest.mark.parametrize("phases", [1, 3])
 @pytest.mark.parametrize("skew", [False, True])
-@pytest.mark.parametrize("W,R", [(1, 128), (2, 64), (8, 64), (1, 256)])
+@pytest.mark.parametrize("W,R", [(1, 128), (2, 64), (8, 64), (1, 256), (1, 16)])
 def test_tile_partition_matches_reference(W, R, rec8, skew, phases):
+    """(1, 16): 25k+ buckets -- the count kernel's 16-bit LDS counters; with skew,
+    one workgroup counts ~60k ratings of a hot item (overflow-safe flushes)."""
     from flink_parameter_server_1_amd.parallel.rotation import block_rows, shard_halves
 
     NI, n = 200_003, 500_000
@@ -252,6 +254,28 @@ def test_tile_partition_matches_reference(W, R, rec8, skew, phases):
 
 def R_tile(*a):
     return R.tile_partition(*a)
+
+
+def test_tile_partition_16bit_counters_survive_one_hot_bucket():
+    """Every rating on ONE item: one bucket gets all n = 1M counts, four times the
+    16-bit range per count workgroup -- the flushes must keep the counts exact."""
+    NI, R, n = 200_003, 16, 1 << 20
+    T = -(-NI // R)
+    assert ops.TILE_MAX_BUCKETS >= 2 * T > 16384  # the 16-bit counter path
+    uid = torch.randint(0, 5000, (n,), dtype=torch.int32)
+    iid = torch.full((n,), 12345, dtype=torch.int32)
+    iid[::97] = torch.randint(0, NI, (iid[::97].numel(),), dtype=torch.int32)
+    r = torch.rand(n)
+    half_t = torch.tensor([NI], dtype=torch.int32)
+    p_ref, u_ref, row_ref, r_ref = R_tile(uid, iid, r, 1, half_t, R, T, 1, 5000)
+    part = ops.TilePartitioner(1, [NI], R, T, DEV, rec8=True, phases=1, users_per_phase=5000)
+    ptr, rec = part.run(uid.to(DEV), iid.to(DEV), r.to(DEV))
+    assert torch.equal(ptr.cpu(), p_ref)
+    u, row, rr = part.unpack(rec, ptr)
+    bucket = torch.repeat_interleave(torch.arange(p_ref.numel() - 1), (p_ref[1:] - p_ref[:-1]).long())
+    got = sorted(zip(bucket.tolist(), u.cpu().tolist(), row.cpu().tolist(), rr.cpu().tolist()))
+    want = sorted(zip(bucket.tolist(), u_ref.tolist(), row_ref.tolist(), r_ref.tolist()))
+    assert got == want
 
 
 @pytest.mark.parametrize("rec8", [False, True])
@@ -342,3 +366,38 @@ def test_ring_known_and_known_list_sampling_match_reference():
     r = R.sample_uniform_reject(1000, 3, ni, pos, uid, ring_r, mem, 4, 2, lst_g.cpu(), n_known)
     assert torch.equal(g, r)  # same known list on both sides
     assert set(g.tolist()) <= known_set
+
+
+@pytest.mark.parametrize("phases", [1, 3])
+@pytest.mark.parametrize("rec8", [False, True])
+def test_mf_sgd_tiled_delta_mode_equals_in_place(phases, rec8):
+    """The PS path's delta mode (item rows read-only, the summed deltas written to a
+    separate buffer, later user phases accumulating) == the in-place kernel's row
+    change.  Unique users (no Hogwild race); items repeat ~60x, so tiles span several
+    LDS chunks and some tiles and rows get no ratings at all."""
+    D, nu, ni, B = 64, 400_000, 6000, 200_000
+    U0 = torch.rand(nu, D, device=DEV) * 0.1
+    I0 = torch.rand(ni, D, device=DEV) * 0.1
+    uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
+    iid = torch.randint(0, ni - 700, (B,), device=DEV, dtype=torch.int32)  # the last tiles stay empty
+    iid[iid % 7 == 3] = 11  # a hot row: many chunks in its tile
+    r = torch.rand(B, device=DEV)
+    Rt = ops.tile_rows_for(D, ni, 1)
+    T = -(-ni // Rt)
+    upp = -(-nu // phases)
+    part = ops.TilePartitioner(1, [ni], Rt, T, DEV, rec8=rec8, phases=phases, users_per_phase=upp)
+    ptr, rec = part.run(uid, iid, r)
+    assert int((ptr[1:T + 1] - ptr[:T]).max()) > 2 * 4608  # a multi-chunk tile
+    U1, I1 = U0.clone(), I0.clone()
+    for p in range(phases):
+        ops.mf_sgd_tiled(U1, I1, rec, ptr, 2 * p, T, Rt, 0.05, 0.01)
+    U2, I2 = U0.clone(), I0.clone()
+    delta = torch.full_like(I2, float("nan"))  # every row must be written
+    for p in range(phases):
+        ops.mf_sgd_tiled(U2, I2, rec, ptr, 2 * p, T, Rt, 0.05, 0.01, delta=delta, delta_init=p == 0)
+    torch.cuda.synchronize()
+    assert torch.equal(I2, I0)  # read-only
+    assert not torch.isnan(delta).any()
+    assert torch.equal(delta[ni - 600:], torch.zeros_like(delta[ni - 600:]))
+    torch.testing.assert_close(U2, U1, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(I0 + delta, I1, rtol=1e-6, atol=1e-6)
