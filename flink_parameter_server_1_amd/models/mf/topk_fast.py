@@ -82,6 +82,14 @@ class LempTopK:
         #: pairs, then probed again
         self._coord_gate = torch.ones(1, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
         self._coord_prev = torch.zeros(2, dtype=torch.int32, device=vecs.device) if vecs.is_cuda else None
+        #: COORD / LC self-disable across query batches: a batch whose COORD bound skipped
+        #: less than ``COORD_MIN_SKIP`` of the block pairs it evaluated switches COORD off
+        #: -- no query grouping, no bound inputs, no gate launches: the LENGTH scan --
+        #: for the next ``COORD_REPROBE`` batches, then it is probed again.  Read with the
+        #: scan's one end-of-batch sync.  (The device gate above only skips evaluating the
+        #: bound inside a scan; the grouping and the per-segment launches stayed.)
+        self.coord_off_batches = 0
+        self.coord_batches = {"on": 0, "off": 0}
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -115,6 +123,12 @@ class LempTopK:
         fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
         if fused and self.sync_free and N > max(self.seed_items, start):
             st = None if state is None else (state[0].clone(), state[1].clone())
+            if self._uses_coord():
+                if self.coord_off_batches > 0:
+                    self.coord_off_batches -= 1
+                    self.coord_batches["off"] += 1
+                else:
+                    self.coord_batches["on"] += 1
             perm = self._focus_order(Q) if self.bf16 else None
             if perm is not None:
                 # the COORD bound is evaluated per 32-query block and skips a block pair only
@@ -221,6 +235,7 @@ class LempTopK:
         if coord is not None:
             self._coord_gate.fill_(1)
             self._coord_prev.copy_(self.coord_stats)
+            stats0 = self.coord_stats.clone()
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
@@ -245,17 +260,33 @@ class LempTopK:
                 ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen,
                                       self.lengths[s:e])
             ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf)
-        if int(ovf.item()):
+        if coord is not None:  # one sync: overflow flag + this batch's COORD block pairs
+            o, scored, skipped = torch.cat([ovf, self.coord_stats - stats0]).tolist()
+            if scored + skipped and skipped < self.COORD_MIN_SKIP * (scored + skipped):
+                self.coord_off_batches = self.COORD_REPROBE
+        else:
+            o = int(ovf.item())
+        if o:
             return None
         return best_s, best_i
+
+    #: COORD self-disable (see ``coord_off_batches``)
+    COORD_MIN_SKIP = 0.25
+    COORD_REPROBE = 64
+
+    def _uses_coord(self) -> bool:
+        from .pruning import COORD, LC
+
+        return isinstance(self.strategy, (COORD, LC))
+
+    def _coord_active(self) -> bool:
+        return self._uses_coord() and self.coord_off_batches == 0
 
 
     def _coord_inputs(self, Q, qlen, bounds):
         """``(focus coordinate int32[B], q_f / |q|)`` when the strategy uses COORD
         on some segment (segments start on 32-item blocks), else None."""
-        from .pruning import COORD, LC
-
-        if not isinstance(self.strategy, (COORD, LC)) or any(b % 32 for b in bounds[:-1]):
+        if not self._coord_active() or any(b % 32 for b in bounds[:-1]):
             return None
         if self._cb is None:
             self._cb = ops.coord_block_bounds(self.vecs, self.lengths)
@@ -268,9 +299,7 @@ class LempTopK:
         strategy evaluates COORD on the device and the batch spans several 32-query
         blocks; None otherwise (the order does not change any result: each query's
         top-K is its own)."""
-        from .pruning import COORD, LC
-
-        if not isinstance(self.strategy, (COORD, LC)) or Q.shape[0] <= 32:
+        if not self._coord_active() or Q.shape[0] <= 32:
             return None
         return torch.argsort(torch.argmax(Q * Q, dim=1), stable=True)
 

@@ -5,6 +5,8 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4d
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k "tile_partition or delta_mode" --timeout 150 --timeout-method thread > gpurun_out/r4d/partition_tests.log 2>&1 || { tail -30 gpurun_out/r4d/partition_tests.log; exit 1; }
 tail -1 gpurun_out/r4d/partition_tests.log
+timeout -k 10 300 python -u -m pytest tests/test_topk_bf16_gpu.py -m gpu -x -q -k "coord" --timeout 150 --timeout-method thread > gpurun_out/r4d/coord_tests.log 2>&1 || { tail -30 gpurun_out/r4d/coord_tests.log; exit 1; }
+tail -1 gpurun_out/r4d/coord_tests.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/r4d/gpu_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/r4d/gpu_tests.log
 [ $rc -eq 0 ] || exit 1
@@ -28,4 +30,11 @@ tail -1 gpurun_out/r4d/w2v_ps.log | cut -c1-200
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4d/prof_w2vps -- python bench/bench_w2v.py --mode standard --ps-path --steps 5 --warmup 2 > gpurun_out/r4d/prof_w2vps.log 2>&1 || { tail -20 gpurun_out/r4d/prof_w2vps.log; exit 1; }
 timeout -k 10 600 python bench/bench_emulate_world.py --ws 1,8 --steps 10 --warmup 3 > gpurun_out/r4d/emulate.log 2>&1 || { tail -20 gpurun_out/r4d/emulate.log; exit 1; }
 tail -3 gpurun_out/r4d/emulate.log
+for st in length coord lc:1.3; do
+  timeout -k 10 300 python bench/bench_topk.py --strategy $st > gpurun_out/r4d/topk_$st.log 2>&1 || { tail -20 gpurun_out/r4d/topk_$st.log; exit 1; }
+  echo "topk $st $(tail -1 gpurun_out/r4d/topk_$st.log | cut -c1-150)"
+done
+timeout -k 10 300 python bench/bench_pa.py --ps-path > gpurun_out/r4d/pa_ps.log 2>&1 || { tail -20 gpurun_out/r4d/pa_ps.log; exit 1; }
+tail -1 gpurun_out/r4d/pa_ps.log | cut -c1-200
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4d/prof_pa -- python bench/bench_pa.py --ps-path --steps 5 --warmup 1 > gpurun_out/r4d/prof_pa.log 2>&1 || { tail -20 gpurun_out/r4d/prof_pa.log; exit 1; }
 echo ALLDONE

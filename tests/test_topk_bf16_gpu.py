@@ -195,10 +195,35 @@ def test_lemp_device_coord_bound_exact_and_skips(strategy):
     scored, skipped = idx.coord_stats.tolist()
     if strategy == "coord":
         assert skipped > 0 and scored > 0, (scored, skipped)
+        assert idx.coord_off_batches == 0  # the bound pays here: COORD stays on
     elif strategy == "lc:1.05":  # COORD only where a segment's lengths spread < 1.05x
         assert scored + skipped > 0, (scored, skipped)
     else:
         assert scored == 0 and skipped == 0
+
+
+def test_lemp_coord_switches_itself_off_where_it_skips_nothing():
+    """Random directions (the COORD bound holds for ~no block pair): after one batch
+    COORD stops being evaluated -- no query grouping, no bound inputs -- for
+    ``COORD_REPROBE`` batches, so the strategy runs the LENGTH scan; on axis-dominated
+    data it stays on.  Results are exact either way."""
+    from flink_parameter_server_1_amd.models.mf.pruning import LEMPPruningStrategy
+    from flink_parameter_server_1_amd.models.mf.topk_fast import LempTopK
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    N, D, B, k = 100_000, 64, 256, 20
+    X = torch.randn(N, D, generator=g, device="cuda") * (torch.rand(N, 1, generator=g, device="cuda") + 0.1)
+    idx = LempTopK(torch.arange(N, device="cuda"), X, 65536, strategy=LEMPPruningStrategy.from_string("coord"))
+    for b in range(3):
+        Q = torch.randn(B, D, generator=g, device="cuda")
+        s, _ = idx.query(Q, k)
+        torch.testing.assert_close(s, torch.topk(Q @ X.t(), k, dim=1).values, rtol=1e-5, atol=1e-5)
+        if b == 0:
+            after_first = idx.coord_stats.clone()
+            assert idx.coord_off_batches == idx.COORD_REPROBE
+    assert torch.equal(idx.coord_stats, after_first)  # batches 2, 3: COORD not evaluated
+    assert idx.coord_batches == {"on": 1, "off": 2}
+    assert idx.coord_off_batches == idx.COORD_REPROBE - 2
 
 
 @pytest.mark.parametrize("strategy", ["coord", "lc:1.2", "li:3:1.2", "incr:3", "length"])
