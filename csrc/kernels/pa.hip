@@ -35,7 +35,8 @@ __global__ void __launch_bounds__(256) pa_binary_kernel(const int64_t* __restric
                                                         const int32_t* __restrict__ pos,
                                                         const float* __restrict__ w, const int8_t* __restrict__ y,
                                                         int64_t B, int variant, float C, float* __restrict__ delta,
-                                                        int8_t* __restrict__ pred, float* __restrict__ loss_out) {
+                                                        int8_t* __restrict__ pred, float* __restrict__ loss_out,
+                                                        float* __restrict__ flip) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -44,7 +45,11 @@ __global__ void __launch_bounds__(256) pa_binary_kernel(const int64_t* __restric
     float m = 0.f, n2 = 0.f;
     for (int64_t j = s + lane; j < e; j += 64) {
       const float x = xval[j];
-      m = fmaf(x, w[pos[j]], m);
+      const float wv = w[pos[j]];
+      // in place (flip = the table): a feature's first pull turns its -0.0 "untouched"
+      // sentinel into +0.0 (table_ops.hip gather_rows_kernel), no byte-mark pass
+      if (flip != nullptr && __float_as_uint(wv) == 0x80000000u) flip[pos[j]] = 0.f;
+      m = fmaf(x, wv, m);
       n2 = fmaf(x, x, n2);
     }
     m = group_sum<64>(m);
@@ -68,7 +73,7 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
                                                        int L, const int32_t* __restrict__ y, int64_t B, int mode,
                                                        int variant, float C, const float* __restrict__ cost,
                                                        float* __restrict__ delta, int32_t* __restrict__ pred,
-                                                       float* __restrict__ loss_out) {
+                                                       float* __restrict__ loss_out, float* __restrict__ flip) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -78,7 +83,12 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
     float d = 0.f, n2 = 0.f;
     for (int64_t j = s; j < e; ++j) {  // lanes = classes; row read is L contiguous floats
       const float x = xval[j];
-      if (cl) d = fmaf(x, W[(int64_t)pos[j] * L + lane], d);
+      if (cl) {
+        const int64_t o = (int64_t)pos[j] * L + lane;
+        const float wv = W[o];
+        if (flip != nullptr && __float_as_uint(wv) == 0x80000000u) flip[o] = 0.f;  // first pull (see binary)
+        d = fmaf(x, wv, d);
+      }
       n2 = fmaf(x, x, n2);
     }
     // argmax over classes (ties -> lowest class, like Breeze argmax)
@@ -128,23 +138,25 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
 
 }  // namespace
 
+// flip != nullptr (the in-place path: flip = the table = delta): first pulls turn the
+// table's untouched sentinel -0.0 into +0.0 (ShardedTable touch_sentinel).
 FPS_API int fps_pa_binary(const int64_t* indptr, const float* xval, const int32_t* pos, const float* w,
                           const int8_t* y, int64_t B, int variant, float C, float* delta, int8_t* pred,
-                          float* loss_out, void* stream) {
+                          float* loss_out, float* flip, void* stream) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(pa_binary_kernel, dim3(grid_for(B, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, indptr,
-                     xval, pos, w, y, B, variant, C, delta, pred, loss_out);
+                     xval, pos, w, y, B, variant, C, delta, pred, loss_out, flip);
   FPS_CHECK_LAUNCH();
   return 0;
 }
 
 FPS_API int fps_pa_multi(const int64_t* indptr, const float* xval, const int32_t* pos, const float* W, int L,
                          const int32_t* y, int64_t B, int mode, int variant, float C, const float* cost,
-                         float* delta, int32_t* pred, float* loss_out, void* stream) {
+                         float* delta, int32_t* pred, float* loss_out, float* flip, void* stream) {
   if (B <= 0) return 0;
   if (L < 1 || L > 64) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pa_multi_kernel, dim3(grid_for(B, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, indptr,
-                     xval, pos, W, L, y, B, mode, variant, C, cost, delta, pred, loss_out);
+                     xval, pos, W, L, y, B, mode, variant, C, cost, delta, pred, loss_out, flip);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -40,21 +40,29 @@ __global__ void __launch_bounds__(256) init_rows_kernel(float* __restrict__ tabl
   }
 }
 
+// Untouched-row sentinel (tables with ``touch_sentinel``: zero init, additive rules):
+// a row that was never pulled or pushed holds -0.0 (bits 0x80000000) and reads as
+// zero; the first serve of it stores +0.0 back (``flip``), and every apply adds
+// deltas with -0.0 mapped to +0.0 (``pos0``), so "touched" = "not the sentinel" and
+// the close-time dump needs no per-request byte marks -- the flip is a conditional
+// store to the cache line the gather just read, and only on a row's first touch.
+constexpr uint32_t NEG0_BITS = 0x80000000u;
+__device__ __forceinline__ float pos0(float x) { return x == 0.f ? 0.f : x; }  // -0.0 -> +0.0
+
 template <int TPR, bool OUT_BF16, typename IDX>
 __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, const IDX* __restrict__ idx,
                                                           int64_t n, int D, void* __restrict__ out,
-                                                          uint8_t* __restrict__ touched) {
+                                                          uint8_t* __restrict__ touched, float* __restrict__ flip) {
   int64_t r, step; int j0;
   row_coords<TPR>(r, step, j0);
   for (; r < n; r += step) {
     const int64_t row = (int64_t)idx[r];
     const float* src = table + row * D;
-    if (OUT_BF16) {
-      uint16_t* dst = (uint16_t*)out + r * D;
-      for (int j = j0; j < D; j += TPR) dst[j] = f32_to_bf16(src[j]);
-    } else {
-      float* dst = (float*)out + r * D;
-      for (int j = j0; j < D; j += TPR) dst[j] = src[j];
+    for (int j = j0; j < D; j += TPR) {
+      const float v = src[j];
+      if (OUT_BF16) ((uint16_t*)out)[r * D + j] = f32_to_bf16(v);
+      else ((float*)out)[r * D + j] = v;
+      if (flip != nullptr && __float_as_uint(v) == NEG0_BITS) flip[row * D + j] = 0.f;
     }
     if (touched != nullptr && j0 == 0) touched[row] = 1;
   }
@@ -80,7 +88,8 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
     float* dst = table + row * D;
     float ss = 0.f;
     for (int j = j0; j < D; j += TPR) {
-      float g = IN_BF16 ? bf16_to_f32(((const uint16_t*)delta)[r * D + j]) : ((const float*)delta)[r * D + j];
+      // pos0: a -0.0 delta must not keep an untouched row's -0.0 sentinel (see gather_rows_kernel)
+      float g = pos0(IN_BF16 ? bf16_to_f32(((const uint16_t*)delta)[r * D + j]) : ((const float*)delta)[r * D + j]);
       if (OP == 5) {
         const float v = dst[j] + g;
         dst[j] = v;
@@ -90,14 +99,14 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
       } else if (OP == 1) {
         dst[j] = g;
       } else if (OP == 2) {
-        atomic_add_noret(dst + j, -lr * g);
+        atomic_add_noret(dst + j, pos0(-lr * g));
       } else if (OP == 4) {
         dst[j] += g;  // keys unique within the launch: plain read-modify-write
       } else {
         float* acc = state + row * D + j;
         float a = *acc + g * g;
         *acc = a;
-        dst[j] -= lr * g * rsqrtf(a + eps);
+        dst[j] += pos0(-lr * g * rsqrtf(a + eps));
       }
     }
     if (OP == 5) {  // the lane group of the row (TPR lanes, all active together) sums the squares
@@ -564,17 +573,18 @@ FPS_API int fps_init_rows(float* table, int64_t n_rows, int D, int64_t id_base, 
 }
 
 FPS_API int fps_gather_rows(const float* table, const void* idx, int idx_is_64, int64_t n, int D, void* out,
-                            int out_bf16, uint8_t* touched, void* stream) {
+                            int out_bf16, uint8_t* touched, int flip_sentinel, void* stream) {
+  float* flip = flip_sentinel ? const_cast<float*>(table) : nullptr;
   if (n <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   TPR_SWITCH(D, {
     const int g = rows_grid(n, TPR);
     if (idx_is_64) {
-      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched);
-      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched);
+      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched, flip);
+      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, D, out, touched, flip);
     } else {
-      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched);
-      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched);
+      if (out_bf16) hipLaunchKernelGGL((gather_rows_kernel<TPR, true, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched, flip);
+      else hipLaunchKernelGGL((gather_rows_kernel<TPR, false, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, D, out, touched, flip);
     }
   });
   FPS_CHECK_LAUNCH();

@@ -49,8 +49,10 @@ class DistributedPA:
         if self.L > 64:
             raise ValueError("multiclass kernels keep the classes on the 64 lanes: label_count <= 64")
         W, r, dev = self.comm.world, self.comm.rank, self.comm.device
+        # untouched features hold the -0.0 sentinel (ShardedTable touch_sentinel): the
+        # close-time dump of touched features needs no byte-mark pass per micro-batch
         self.table = ShardedTable(cfg.feature_count, self.L, r, W, cfg.partition, ("zeros",), 0, dev,
-                                  optimizer="add")
+                                  optimizer="add", touch_sentinel=True)
         self.ps = TensorPS(self.table, self.comm, _WIRE[cfg.wire_dtype])
         if cfg.kind in ("pb", "ml"):
             if cost is None:
@@ -83,15 +85,17 @@ class DistributedPA:
             # reference's per-feature pull / push interleaving)
             w = self.table.weight
             idx = indices.to(device=w.device, dtype=torch.int32).contiguous()
-            if train and self.table.touched is not None:
-                ops.mark_rows(self.table.touched, idx)
+            # train steps pull (the reference creates a feature's entry on its first pull):
+            # the kernel flips the -0.0 sentinel of first-pulled features as it reads them
+            flip = w if train else None
             with stage("pa.step", self.timer):
                 if c.kind == "binary":
                     pred, loss = ops.pa_binary(indptr, values, idx, w.view(-1), labels, c.variant,
-                                               c.aggressiveness, w.view(-1), with_loss)
+                                               c.aggressiveness, w.view(-1), with_loss,
+                                               flip=None if flip is None else flip.view(-1))
                 else:
                     pred, loss = ops.pa_multi(indptr, values, idx, w, labels, c.kind, c.variant, c.aggressiveness,
-                                              self.cost, w, with_loss)
+                                              self.cost, w, with_loss, flip=flip)
             if train:
                 self.examples += indptr.numel() - 1
             return pred, loss

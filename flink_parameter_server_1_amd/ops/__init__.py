@@ -81,10 +81,12 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
 
 
 def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
-                touched: torch.Tensor = None) -> torch.Tensor:
+                touched: torch.Tensor = None, flip: bool = False) -> torch.Tensor:
     """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2).
     The HIP kernel serves fp32 tables; fp64 tables (the bit-parity configuration
-    against the per-record engine's doubles) take the torch twin on any device."""
+    against the per-record engine's doubles) take the torch twin on any device.
+    ``flip``: served entries holding the untouched sentinel -0.0 become +0.0 in the
+    table (``ShardedTable(touch_sentinel=True)``)."""
     n = idx.numel()
     if DEBUG:
         check_index(idx, table.shape[0], "gather_rows")
@@ -94,10 +96,12 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None
     if _on_gpu(table) and table.dtype == torch.float32 and out.dtype in (torch.float32, torch.bfloat16):
         lib = N.require()
         N.check(lib.fps_gather_rows(_c(table).data_ptr(), _c(idx).data_ptr(), int(idx.dtype == torch.int64), n, d,
-                                    _c(out).data_ptr(), int(out.dtype == torch.bfloat16), N.ptr(touched),
+                                    _c(out).data_ptr(), int(out.dtype == torch.bfloat16), N.ptr(touched), int(flip),
                                     N.stream_ptr(table.device)), "gather_rows")
         return out
     out.copy_(R.gather_rows(table, idx, out.dtype, touched))
+    if flip:
+        flip_sentinel(table, idx)
     return out
 
 
@@ -997,33 +1001,50 @@ PA_VARIANTS = {"PA": 0, "PA-I": 1, "PA-II": 2}
 PA_MODES = {"ova": 0, "pb": 1, "ml": 2}
 
 
-def pa_binary(indptr, xval, pos, w, y, variant: str, C: float, delta, with_loss: bool = False):
-    """Binary PA on a CSR micro-batch (K10); returns ``(pred int8[B], loss or None)``."""
+def flip_sentinel(table: torch.Tensor, rows: torch.Tensor) -> None:
+    """Torch twin of the kernels' untouched-row sentinel flip: entries of ``table[rows]``
+    holding -0.0 become +0.0 (``ShardedTable(touch_sentinel=True)``)."""
+    r = rows.long()
+    x = table[r]
+    table[r] = torch.where((x == 0) & torch.signbit(x), torch.zeros_like(x), x)
+
+
+def pa_binary(indptr, xval, pos, w, y, variant: str, C: float, delta, with_loss: bool = False,
+              flip: Optional[torch.Tensor] = None):
+    """Binary PA on a CSR micro-batch (K10); returns ``(pred int8[B], loss or None)``.
+    ``flip`` (the in-place path: the table itself): the first pull of a feature turns
+    its untouched sentinel -0.0 into +0.0."""
     B = indptr.numel() - 1
+    if flip is not None and not xval.is_cuda:
+        flip_sentinel(flip.view(-1, 1), pos)
     if xval.is_cuda:
         pred = torch.empty(B, dtype=torch.int8, device=xval.device)
         loss = torch.zeros(1, device=xval.device) if with_loss else None
         lib = N.require()
         N.check(lib.fps_pa_binary(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(w).data_ptr(),
                                   _c(y).data_ptr(), B, PA_VARIANTS[variant], C, _c(delta).data_ptr(),
-                                  pred.data_ptr(), N.ptr(loss), N.stream_ptr(xval.device)), "pa_binary")
+                                  pred.data_ptr(), N.ptr(loss), N.ptr(flip), N.stream_ptr(xval.device)), "pa_binary")
         return pred, loss
     pred, loss = R.pa_binary(indptr, xval, pos, w, y, PA_VARIANTS[variant], C, delta)
     return pred, torch.tensor([loss])
 
 
-def pa_multi(indptr, xval, pos, W, y, mode: str, variant: str, C: float, cost, delta, with_loss: bool = False):
-    """Multiclass PA (OVA / cost PB / cost ML) on a CSR micro-batch (K11/K12); L <= 64."""
+def pa_multi(indptr, xval, pos, W, y, mode: str, variant: str, C: float, cost, delta, with_loss: bool = False,
+             flip: Optional[torch.Tensor] = None):
+    """Multiclass PA (OVA / cost PB / cost ML) on a CSR micro-batch (K11/K12); L <= 64.
+    ``flip``: as ``pa_binary``."""
     B = indptr.numel() - 1
     L = W.shape[1]
+    if flip is not None and not xval.is_cuda:
+        flip_sentinel(flip, pos)
     if xval.is_cuda:
         pred = torch.empty(B, dtype=torch.int32, device=xval.device)
         loss = torch.zeros(1, device=xval.device) if with_loss else None
         lib = N.require()
         N.check(lib.fps_pa_multi(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(W).data_ptr(), L,
                                  _c(y).data_ptr(), B, PA_MODES[mode], PA_VARIANTS[variant], C, N.ptr(cost),
-                                 _c(delta).data_ptr(), pred.data_ptr(), N.ptr(loss), N.stream_ptr(xval.device)),
-                "pa_multi")
+                                 _c(delta).data_ptr(), pred.data_ptr(), N.ptr(loss), N.ptr(flip),
+                                 N.stream_ptr(xval.device)), "pa_multi")
         return pred, loss
     pred, loss = R.pa_multi(indptr, xval, pos, W, y, PA_MODES[mode], PA_VARIANTS[variant], C, cost, delta)
     return pred, torch.tensor([loss])

@@ -58,6 +58,8 @@ def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touch
     idx = idx.long()
     keep = idx >= 0
     idx, delta = idx[keep], delta[keep].to(table.dtype)
+    # -0.0 deltas add as +0.0 (the kernels' pos0): an untouched row's -0.0 sentinel flips
+    delta = torch.where(delta == 0, torch.zeros_like(delta), delta)
     if touched is not None:
         touched[idx] = 1
     if op in ("add", "add_unique"):

@@ -73,12 +73,20 @@ class ShardedTable:
     def __init__(self, num_ids: int, dim: int, rank: int = 0, world: int = 1, partition: str = "hash",
                  init: Tuple = ("uniform", -0.01, 0.01), seed: int = 0, device="cpu", optimizer: str = "add",
                  track_touched: bool = True, dtype=torch.float32, owner: Optional[torch.Tensor] = None,
-                 init_fn: Optional[Callable] = None, update_fn: Optional[Callable] = None):
+                 init_fn: Optional[Callable] = None, update_fn: Optional[Callable] = None,
+                 touch_sentinel: bool = False):
         """``partition="lookup"`` takes ``owner[num_ids]`` (id -> shard): an arbitrary
         assignment, addressed through virtual keys (``LookupPartitioner``).
         ``optimizer="fn"``: user rules -- ``init_fn(global ids) -> rows`` (applied to
         the whole shard at construction: deterministic-by-id rules then equal
-        init-on-first-pull) and ``update_fn(old, delta[, ids]) -> new`` (``fn_apply``)."""
+        init-on-first-pull) and ``update_fn(old, delta[, ids]) -> new`` (``fn_apply``).
+
+        ``touch_sentinel`` (zero init, additive rule, fp32): instead of a byte of
+        "touched" marks per row, untouched rows hold -0.0 (which reads as zero); the
+        first serve of a row, and any push to it, leave +0.0 or a value there
+        (``csrc/kernels/table_ops.hip``), so the close-time dump keeps exactly the rows
+        that were pulled or pushed without a mark pass per micro-batch (PA's 1B-feature
+        shards: ~100 us of random byte stores per 4M requests, and 1 GB of marks)."""
         if partition not in self.PART_KIND:
             raise ValueError(partition)
         self.num_ids, self.dim, self.rank, self.world = int(num_ids), int(dim), rank, world
@@ -101,6 +109,13 @@ class ShardedTable:
         self.init_fn, self.update_fn = init_fn, update_fn
         if optimizer == "fn" and update_fn is None:
             raise ValueError("optimizer='fn' needs update_fn")
+        self.sentinel = bool(touch_sentinel)
+        if self.sentinel and (init[0] != "zeros" or optimizer not in ("add", "sgd") or dtype != torch.float32
+                              or partition == "lookup"):
+            raise ValueError("touch_sentinel needs zero init, an additive rule (add / sgd), fp32 rows and a "
+                             "hash / range partition")
+        if self.sentinel:
+            track_touched = False
         # function rules get one scratch row past the shard (masked apply entries)
         self._store = torch.empty((self.n_local + (optimizer == "fn"), self.dim), dtype=dtype, device=self.device)
         self.weight = self._store[:self.n_local]
@@ -167,7 +182,7 @@ class ShardedTable:
             _, lo, hi = self.init_spec
             ops.init_rows(self.weight, self.id_base, self.id_stride, float(lo), float(hi), self.seed)
         elif kind == "zeros":
-            self.weight.zero_()
+            self.weight.fill_(-0.0 if getattr(self, "sentinel", False) else 0.0)
         elif kind == "const":
             self.weight.fill_(float(self.init_spec[1]))
         else:
@@ -191,7 +206,7 @@ class ShardedTable:
         The marks are a separate pass: fused into the narrow-row gather, the random byte
         stores cost 170 us per 3.8M rows of a 1B-row table, on their own 63 us
         (``bench/probe_sorted_gather.py``)."""
-        out = ops.gather_rows(self.weight, rows, out_dtype=wire_dtype)
+        out = ops.gather_rows(self.weight, rows, out_dtype=wire_dtype, flip=mark and self.sentinel)
         if mark and self.touched is not None:
             ops.mark_rows(self.touched, rows)
         return out
@@ -233,16 +248,27 @@ class ShardedTable:
         ids = ids.to(self.device).long()
         mine = self.part.shard_tensor(ids) == self.rank
         loc = self.local_of(ids[mine]).to(torch.int32)
-        ops.apply_rows(self.weight, loc, values.to(self.device)[mine].to(torch.float32).contiguous(), "set",
-                       touched=self.touched)
+        vals = values.to(self.device)[mine].to(torch.float32).contiguous()
+        if self.sentinel:  # raw copy: a snapshot's untouched rows keep their -0.0 sentinel
+            self.weight[loc.long()] = vals.reshape(loc.numel(), self.dim)
+            return
+        ops.apply_rows(self.weight, loc, vals, "set", touched=self.touched)
 
     def dump(self, only_touched: bool = True):
         """(global ids, values) of this shard -- the close-time model output."""
-        if only_touched and self.touched is not None:
+        if only_touched and self.sentinel:
+            loc = torch.nonzero(self.touched_mask(), as_tuple=False).flatten()
+        elif only_touched and self.touched is not None:
             loc = torch.nonzero(self.touched, as_tuple=False).flatten()
         else:
             loc = torch.arange(self.n_local, device=self.device)
         return self.global_ids(loc), self.weight[loc]
+
+    def touched_mask(self) -> Optional[torch.Tensor]:
+        """bool[n_local]: rows pulled or pushed so far (None: not tracked)."""
+        if self.sentinel:
+            return (self.weight.view(torch.int32) != -(1 << 31)).any(dim=1)
+        return None if self.touched is None else self.touched.bool()
 
     def nbytes(self) -> int:
         n = self.weight.numel() * self.weight.element_size()

@@ -172,7 +172,8 @@ class TensorPS:
         the whole key space in order -- ``pos`` = the key, a presence flag per key --
         so a worker may bucket its requests by key before the plan exists.)"""
         return (self.static and self.comm.world == 1 and not getattr(self.table, "sparse", False)
-                and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
+                and getattr(self.table, "partition", "") != "lookup" and not getattr(self.table, "sentinel", False)
+                and n >= int(self.table.key_space))
 
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None) -> PendingPlan:

@@ -542,7 +542,7 @@ def run_virtual(fn: Callable[..., Any], world: int, *args, device=None, mode: st
     threads = [threading.Thread(target=body, args=(r,), name=f"vrank{r}", daemon=True) for r in range(world)]
     for t in threads:
         t.start()
-    deadline = time.time() + timeout_s
+    deadline = time.time() + timeout_s + 10.0  # past the waits' own timeout: they report what hung
     for t in threads:
         t.join(max(0.0, deadline - time.time()))
     if any(t.is_alive() for t in threads):

@@ -134,10 +134,15 @@ class DevicePSLogic:
             partition, owner = self.partition, None
             if not isinstance(partition, str):
                 owner, partition = owner_table(partition, self.num_ids, comm.world), "lookup"
+            track = self.track_touched or self.emit == "close" or self.op == "fn"
+            # zero-init additive fp32 shards track touched rows by the -0.0 sentinel
+            # (ShardedTable touch_sentinel: no byte-mark pass per micro-batch)
+            sentinel = (track and tuple(self.init) == ("zeros",) and self.op in ("add", "sgd")
+                        and self.dtype == torch.float32 and partition != "lookup" and self.init_fn is None)
             self.table = ShardedTable(self.num_ids, self.dim, comm.rank, comm.world, partition, self.init,
-                                      self.seed, comm.device, optimizer=self.op,
-                                      track_touched=self.track_touched or self.emit == "close" or self.op == "fn",
-                                      dtype=self.dtype, owner=owner, init_fn=self.init_fn, update_fn=self.update_fn)
+                                      self.seed, comm.device, optimizer=self.op, track_touched=track,
+                                      dtype=self.dtype, owner=owner, init_fn=self.init_fn, update_fn=self.update_fn,
+                                      touch_sentinel=sentinel)
         self.ps = ps if ps is not None else TensorPS(self.table, comm, self.wire_dtype)
         # set-rules, user rules and per-push outputs must tell pushed keys from
         # merely pulled ones (a user rule need not map a zero delta to a no-op)
