@@ -74,7 +74,8 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 // SB_ITEMS items.  COORD: the LEMP coordinate bound per (32-query block, 32-item
 // block) before the MFMAs (qf / qbf: each query's focus coordinate argmax q_c^2 and
 // q_f / |q|; cb: [N / 32][D] coordinate ranges); stats[0] / [1] count the (query
-// block, item block) pairs scored / skipped.
+// block, item block) pairs scored / skipped by the coordinate bound (pairs the length
+// bound skips by itself are in neither).
 template <int D, int QB, bool MASK = false, bool COORD = false>
 __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
@@ -194,10 +195,13 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
-        bool pass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
-        if (pass) pass = coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
+        const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
+        const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
         if (!__any(pass)) {  // wave-uniform
-          ++skipped;
+          // counted only when the length bound alone would have scored the pair: the
+          // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
+          // adds over LENGTH, not what the length bound skips anyway
+          if (__any(lpass)) ++skipped;
           continue;
         }
         ++scored;

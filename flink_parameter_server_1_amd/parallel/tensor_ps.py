@@ -172,8 +172,7 @@ class TensorPS:
         the whole key space in order -- ``pos`` = the key, a presence flag per key --
         so a worker may bucket its requests by key before the plan exists.)"""
         return (self.static and self.comm.world == 1 and not getattr(self.table, "sparse", False)
-                and getattr(self.table, "partition", "") != "lookup" and not getattr(self.table, "sentinel", False)
-                and n >= int(self.table.key_space))
+                and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
 
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None) -> PendingPlan:
@@ -352,11 +351,16 @@ class TensorPS:
             if plan.recv_rows is None:  # dense shards: the local key is the row; sparse: lookup-or-insert
                 plan.recv_rows = self.table.rows_for(plan.recv_keys)[0]
             touched = getattr(self.table, "touched", None)
-            if not plan.identity or touched is None:
+            sentinel = getattr(self.table, "sentinel", False)
+            if not plan.identity or (touched is None and not sentinel):
                 return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
             # identity plan: every row is served, only the keys present count as pulled
             out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
-            touched |= plan.valid.view(torch.uint8)
+            if sentinel:  # flip the untouched sentinel of the present rows only
+                w = self.table.weight
+                w.masked_fill_((w == 0) & torch.signbit(w) & plan.valid.view(-1, 1), 0.0)
+            else:
+                touched |= plan.valid.view(torch.uint8)
             return out
 
     def pull_planned(self, plan: PullPlan, async_op: bool = False):

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4d
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_touch_sentinel.py -m gpu -x -q -k "tile_partition or delta_mode or sentinel or pulled_features" --timeout 150 --timeout-method thread > gpurun_out/r4d/partition_tests.log 2>&1 || { tail -30 gpurun_out/r4d/partition_tests.log; exit 1; }
 tail -1 gpurun_out/r4d/partition_tests.log
-timeout -k 10 300 python -u -m pytest tests/test_topk_bf16_gpu.py -m gpu -x -q -k "coord" --timeout 150 --timeout-method thread > gpurun_out/r4d/coord_tests.log 2>&1 || { tail -30 gpurun_out/r4d/coord_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_topk_bf16_gpu.py tests/test_sgns_sampling.py -m gpu -x -q -k "coord or steady_state" --timeout 150 --timeout-method thread > gpurun_out/r4d/coord_tests.log 2>&1 || { tail -30 gpurun_out/r4d/coord_tests.log; exit 1; }
 tail -1 gpurun_out/r4d/coord_tests.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/r4d/gpu_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/r4d/gpu_tests.log

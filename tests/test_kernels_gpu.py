@@ -389,15 +389,16 @@ def test_mf_sgd_tiled_delta_mode_equals_in_place(phases, rec8):
     ptr, rec = part.run(uid, iid, r)
     assert int((ptr[1:T + 1] - ptr[:T]).max()) > 2 * 4608  # a multi-chunk tile
     U1, I1 = U0.clone(), I0.clone()
+    lr = 1e-3  # the hot row sums ~28k ratings' deltas: a small step keeps it bounded
     for p in range(phases):
-        ops.mf_sgd_tiled(U1, I1, rec, ptr, 2 * p, T, Rt, 0.05, 0.01)
+        ops.mf_sgd_tiled(U1, I1, rec, ptr, 2 * p, T, Rt, lr, 0.01)
     U2, I2 = U0.clone(), I0.clone()
     delta = torch.full_like(I2, float("nan"))  # every row must be written
     for p in range(phases):
-        ops.mf_sgd_tiled(U2, I2, rec, ptr, 2 * p, T, Rt, 0.05, 0.01, delta=delta, delta_init=p == 0)
+        ops.mf_sgd_tiled(U2, I2, rec, ptr, 2 * p, T, Rt, lr, 0.01, delta=delta, delta_init=p == 0)
     torch.cuda.synchronize()
     assert torch.equal(I2, I0)  # read-only
     assert not torch.isnan(delta).any()
     assert torch.equal(delta[ni - 600:], torch.zeros_like(delta[ni - 600:]))
-    torch.testing.assert_close(U2, U1, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(I0 + delta, I1, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(U2, U1, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(I0 + delta, I1, rtol=1e-5, atol=1e-5)

@@ -214,6 +214,7 @@ def test_lemp_coord_switches_itself_off_where_it_skips_nothing():
     N, D, B, k = 100_000, 64, 256, 20
     X = torch.randn(N, D, generator=g, device="cuda") * (torch.rand(N, 1, generator=g, device="cuda") + 0.1)
     idx = LempTopK(torch.arange(N, device="cuda"), X, 65536, strategy=LEMPPruningStrategy.from_string("coord"))
+    assert idx.bf16
     for b in range(3):
         Q = torch.randn(B, D, generator=g, device="cuda")
         s, _ = idx.query(Q, k)
