@@ -96,7 +96,9 @@ def main(argv=None):
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="tiled SGD: partition each batch on the main stream instead of prefetching it")
-    ap.add_argument("--user-update", default="store", choices=["store", "atomic"])
+    ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"],
+                    help="store: Hogwild user rows (plain accesses); sc1: write-through user rows (about half the lost "
+                         "user updates); atomic: float-atomic user updates, flat kernel (none lost)")
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--user-phases", type=int, default=0,

@@ -41,7 +41,13 @@ def main(argv=None):
     ap.add_argument("--exchange", default="rotate", choices=["rotate", "ps"])
     ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
     ap.add_argument("--mode", default="async", choices=["async", "sync"])
+    ap.add_argument("--traceback-s", type=float, default=0.0,
+                    help="dump every thread's Python stack to stderr every this many seconds (hang diagnosis)")
     a = ap.parse_args(argv)
+    if a.traceback_s > 0:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(a.traceback_s, repeat=True, file=sys.stderr)
 
     import torch
 
@@ -69,8 +75,10 @@ def main(argv=None):
         sync(True)
         barrier.wait()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for k in range(a.steps):
             m.step(*batch)
+            if comm.rank == 0:
+                print(f"[vworld] rank 0 enqueued step {k}", file=sys.stderr, flush=True)
         m.flush()
         sync()
         barrier.wait()

@@ -11,8 +11,9 @@ start at 0 and the learning rate is tiny, so to first order each rating adds
 ``lr * r * item`` to its user row and leaves the item rows alone.  A user's row after
 one step must then equal ``lr * sum_k r_k item_k`` (to ~1e-5 relative); a user whose
 row misses by more than a fraction of one rating's share lost an update.  Reports
-the fraction of users and of ratings affected at the given density (the headline:
-64M ratings over 10M users = 6.4 ratings per user per step, 4 user phases).
+the fraction of users affected and the fraction of rating updates lost (least squares
+per user: ``lost_update_count``) at the given density (the headline: 64M ratings over
+10M users = 6.4 ratings per user per step, 4 user phases).
 """
 from __future__ import annotations
 
@@ -24,7 +25,40 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int = 0, lr: float = 1e-4) -> dict:
+def lost_update_count(U, uid, v, users: int, nmax: int = 24, chunk: int = 200_000):
+    """Updates missing from each user's row: the row must be ``sum_k c_k v_k`` with
+    every ``c_k = 1`` (``v_k`` = rating k's contribution); ``c`` by least squares per
+    user (<= ``nmax`` ratings, 64 dims), a lost update shows as ``c_k ~ 0``.  Returns
+    ``(lost updates, ratings checked)``."""
+    import torch
+
+    dev = U.device
+    order = torch.argsort(uid.long(), stable=True)
+    su = uid.long()[order]
+    cnt = torch.bincount(su, minlength=users)
+    start = torch.cumsum(cnt, 0) - cnt
+    rank = torch.arange(su.numel(), device=dev) - start[su]
+    lost, checked = 0.0, 0
+    for a in range(0, users, chunk):
+        b = min(users, a + chunk)
+        lo, hi = int(start[a]), int(start[b - 1] + cnt[b - 1])
+        u_ = su[lo:hi] - a
+        k_ = rank[lo:hi]
+        ok = (k_ < nmax) & (cnt[su[lo:hi]] <= nmax)
+        V = torch.zeros((b - a, nmax, v.shape[1]), dtype=torch.float64, device=dev)
+        V[u_[ok], k_[ok]] = v[order[lo:hi][ok]].double()
+        pad = torch.arange(nmax, device=dev).view(1, -1) >= cnt[a:b].view(-1, 1)
+        G = V @ V.transpose(1, 2) + torch.diag_embed(pad.double())
+        rhs = (V @ U[a:b].double().unsqueeze(-1)).squeeze(-1)
+        c = torch.linalg.solve(G, rhs)
+        real = ~pad & (cnt[a:b] <= nmax).view(-1, 1)
+        lost += float(((1.0 - c.clamp(0.0, 1.0)) * real).sum())
+        checked += int(real.sum())
+    return lost, checked
+
+
+def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int = 0, lr: float = 1e-4,
+                 count_updates: bool = True, user_update: str = "store") -> dict:
     import torch
 
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig
@@ -32,9 +66,9 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
 
     dev = torch.device("cuda", 0)
     cfg = MFConfig(num_users=users, num_items=items, dim=64, learning_rate=lr, user_phases=phases,
-                   prefetch_partition=False)
+                   prefetch_partition=False, user_update=user_update)
     m = DistributedMF(cfg, Comm(device=dev))
-    assert m.sgd_mode == "tiled"
+    assert m.sgd_mode == ("flat" if user_update == "atomic" else "tiled")
     g = torch.Generator(device=dev).manual_seed(seed)
     with torch.no_grad():
         m.U.zero_()
@@ -47,16 +81,21 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
     m.step(uid, iid, r)
     m.flush()
     torch.cuda.synchronize()
-    want = torch.zeros_like(m.U).index_add_(0, uid.long(), lr * r.view(-1, 1) * I0[iid.long()])
+    v = lr * r.view(-1, 1) * I0[iid.long()]  # rating k's contribution to its user's row
+    want = torch.zeros_like(m.U).index_add_(0, uid.long(), v)
     cnt = torch.bincount(uid.long(), minlength=users)
     err = (m.U - want).norm(dim=1)
     share = want.norm(dim=1) / cnt.clamp_min(1)  # ~ one rating's contribution
     lost = (err > 0.2 * share) & (cnt > 1)
     rated = cnt > 0
-    return {"users": users, "items": items, "ratings": n, "ratings_per_user": per_user, "phases": m.user_phases,
-            "tile_rows": m.tile_R, "users_with_lost_update": int(lost.sum()), "rated_users": int(rated.sum()),
-            "lost_user_fraction": float(lost.sum()) / max(int(rated.sum()), 1),
-            "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())}
+    out = {"users": users, "items": items, "ratings": n, "ratings_per_user": per_user,
+           "phases": getattr(m, "user_phases", None), "tile_rows": getattr(m, "tile_R", None), "user_update": cfg.user_update, "users_with_lost_update": int(lost.sum()),
+           "rated_users": int(rated.sum()), "lost_user_fraction": float(lost.sum()) / max(int(rated.sum()), 1),
+           "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())}
+    if count_updates:
+        nl, nc = lost_update_count(m.U, uid, v, users)
+        out.update({"lost_updates": nl, "updates_checked": nc, "lost_update_fraction": nl / max(nc, 1)})
+    return out
 
 
 def main(argv=None):
@@ -65,9 +104,12 @@ def main(argv=None):
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--per-user", type=float, default=6.4)
     ap.add_argument("--phases", default="1,4")
+    ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"])
+    ap.add_argument("--no-count", action="store_true", help="skip the per-update least-squares count")
     a = ap.parse_args(argv)
     for p in [int(x) for x in a.phases.split(",")]:
-        print(json.dumps(lost_updates(a.users, a.items, a.per_user, p)), flush=True)
+        print(json.dumps(lost_updates(a.users, a.items, a.per_user, p, count_updates=not a.no_count,
+                                      user_update=a.user_update)), flush=True)
 
 
 if __name__ == "__main__":

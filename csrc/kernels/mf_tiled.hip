@@ -508,14 +508,20 @@ __device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int6
 // tile -- or a later launch without dl_init (the next user phase) -- starts from
 // I + Dl (the row as the earlier work left it) and adds its sum to Dl.  Replaces a working copy of the pulled rows and a subtraction pass
 // (round 3: clone + SGD + sub_, 1.3 GB of extra traffic at 1M x 64 rows).
-template <int TPR, int V, int PF, bool REC8, bool DELTA>
+// USC1: user rows loaded and stored write-through (`sc1`: loads bypass the CU's L1,
+// stores drop the line from the writing XCD's L2), so a user row updated on another CU
+// or XCD is not re-read from a stale cached copy (the Hogwild race on user rows,
+// profiles/r4_hogwild.md).  Buffer addressing: the table must be < 4 GiB.
+typedef unsigned int tg_u4 __attribute__((ext_vector_type(4)));
+
+template <int TPR, int V, int PF, bool REC8, bool DELTA, bool USC1>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
                                                                int64_t block_rows, float lr, float lambda,
                                                                float* __restrict__ I1, int64_t block_rows1, int T0,
                                                                const int32_t* __restrict__ ptr1,
-                                                               float* __restrict__ Dl, int dl_init) {
+                                                               float* __restrict__ Dl, int dl_init, uint32_t ubytes) {
   using Rec = typename RecT<REC8>::type;
   constexpr int TG_CAP = tg_cap<REC8>();
   const Rec* __restrict__ rec = reinterpret_cast<const Rec*>(rec_);
@@ -537,6 +543,8 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
   float4* Ig = reinterpret_cast<float4*>(I) + r0 * D4;
   float4* Ug = reinterpret_cast<float4*>(U);
   float4* Dg = DELTA ? reinterpret_cast<float4*>(Dl) + r0 * D4 : nullptr;
+  __amdgpu_buffer_rsrc_t urs;
+  if constexpr (USC1) urs = __builtin_amdgcn_make_buffer_rsrc(U, (short)0, (int)ubytes, 0x00020000);
   if (DELTA && dl_init && beg == end) {  // no ratings in this tile: its rows' deltas are zero
     for (int k = threadIdx.x; k < nr * D4; k += blockDim.x) f4_st<true>(Dg + k, make_float4(0.f, 0.f, 0.f, 0.f));
     return;
@@ -617,7 +625,13 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
           get_rec<REC8>(srec[min(k0 + q, b - 1)], r0, u, rw, rv[q]);
           ur[q] = (Off)u * D4;
 #pragma unroll
-          for (int v = 0; v < V; ++v) uv[q][v] = Ug[ur[q] + j + v * TPR];
+          for (int v = 0; v < V; ++v) {
+            if constexpr (USC1)
+              uv[q][v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        urs, (int)((uint32_t)(ur[q] + j + v * TPR) * 16u), 0, 16));
+            else
+              uv[q][v] = Ug[ur[q] + j + v * TPR];
+          }
         }
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
@@ -635,7 +649,11 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
             nu.y = u.y + lr * (e * i.y - lambda * u.y);
             nu.z = u.z + lr * (e * i.z - lambda * u.z);
             nu.w = u.w + lr * (e * i.w - lambda * u.w);
-            Ug[ur[q] + j + v * TPR] = nu;
+            if constexpr (USC1)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tg_u4, nu), urs,
+                                                     (int)((uint32_t)(ur[q] + j + v * TPR) * 16u), 0, 16);
+            else
+              Ug[ur[q] + j + v * TPR] = nu;
             acc[v].x += lr * (e * u.x - lambda * i.x);
             acc[v].y += lr * (e * u.y - lambda * i.y);
             acc[v].z += lr * (e * u.z - lambda * i.z);
@@ -759,7 +777,8 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // to delta0 (delta_init) or added to it (a later user phase over the same rows).
 FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, const int32_t* ptr0, int T, int R,
                              int64_t rows0, float* I1, const int32_t* ptr1, int64_t rows1, int nblk, int D, float lr,
-                             float lambda, float* delta0, int delta_init, void* stream) {
+                             float lambda, float* delta0, int delta_init, int64_t users_bytes, int user_sc1,
+                             void* stream) {
   if (T <= 0) return 0;
   if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
   if (delta0 != nullptr && nblk != 1) return (int)hipErrorInvalidValue;
@@ -768,11 +787,20 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
   const int grid = nblk * T;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
-#define FPS_TILED_(TPR_, V_, DL_)                                                                              \
-  if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_>), dim3(grid), dim3(512), 0, s, U,  \
-                               I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init);    \
-  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_>), dim3(grid), dim3(512), 0, s, U, I0, \
-                          rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init)
+  // user-row cache policy (user_sc1: write-through sc1, see USC1); 8-B records address
+  // users with 32-bit offsets, the buffer descriptor needs the table < 4 GiB
+  if (user_sc1 && !(rec8 && users_bytes > 0 && users_bytes < (int64_t)0xFFFFFFFF)) return (int)hipErrorInvalidValue;
+  const bool usc1 = user_sc1 != 0;
+  const uint32_t ubytes = (uint32_t)(usc1 ? users_bytes : 0);
+#define FPS_TILED_(TPR_, V_, DL_)                                                                               \
+  if (rec8 && usc1) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, true>), dim3(grid),       \
+                                       dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, \
+                                       delta0, delta_init, ubytes);                                              \
+  else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, false>), dim3(grid),          \
+                                    dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1,    \
+                                    delta0, delta_init, ubytes);                                                 \
+  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_, false>), dim3(grid), dim3(512), 0, s, \
+                          U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init, ubytes)
 #define FPS_TILED(TPR_, V_)                      \
   if (delta0 != nullptr) { FPS_TILED_(TPR_, V_, true); } \
   else { FPS_TILED_(TPR_, V_, false); }

@@ -62,7 +62,9 @@ class MFConfig:
     range_min: float = -0.01
     range_max: float = 0.01
     seed: int = 0
-    user_update: str = "store"        # "store" (Hogwild) | "atomic"
+    user_update: str = "store"        # "store" (Hogwild, plain accesses) | "sc1" (Hogwild, write-through user
+                                      # rows: ~half the lost user updates, profiles/r4_hogwild.md) | "atomic"
+                                      # (no lost update: float atomics, flat kernel)
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
@@ -113,7 +115,10 @@ class DistributedMF:
         # PS item shard
         self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.item_seed(), dev, optimizer="add")
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
+        if cfg.user_update not in ("store", "sc1", "atomic"):
+            raise ValueError(f"user_update must be 'store', 'sc1' or 'atomic', not {cfg.user_update!r}")
         self.user_atomic = cfg.user_update == "atomic"
+        self.user_sc1 = cfg.user_update == "sc1" and dev.type == "cuda"
         exchange = cfg.exchange
         if exchange == "auto":
             exchange = "ps" if cfg.force_ps_path else ("rotate" if Wn > 1 else "local")
@@ -150,6 +155,9 @@ class DistributedMF:
             # side stream while batch k's SGD runs (one micro-batch of latency, flush()
             # completes it; same SGD order)
             rec8 = self.users.n_local < (1 << 24)  # 8-B rating records (user index in 24 bits)
+            if self.user_sc1 and not (rec8 and self.U.numel() * 4 < 0xFFFFFFFF):
+                raise ValueError("user_update='sc1' addresses the user shard with 32-bit byte offsets: "
+                                 "< 2^24 users and < 4 GiB per shard")
             # user phases: ratings also bucketed by local user range, each phase's
             # launches touch ~2.5M user rows (640 MB) instead of all of them --
             # measured 1.67 ms x 4 vs 7.34 ms of SGD per 64M ratings at 10M users
@@ -363,7 +371,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):  # both item blocks of a phase in one launch
                     ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
-                                          c.learning_rate, c.lam)
+                                          c.learning_rate, c.lam, user_sc1=self.user_sc1)
             return
         nb = 2 * self.rot_w  # item blocks per user phase in the partition layout
         for _ in range(self.rot.K):
@@ -375,11 +383,11 @@ class DistributedMF:
                     if len(act) == 2:  # one block of each ring: disjoint items, one launch
                         (g0, b0), (g1, b1) = act
                         ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                              c.learning_rate, c.lam, block1=p * nb + g1)
+                                              c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1)
                     else:
                         (g0, b0), = act
                         ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                         c.learning_rate, c.lam)
+                                         c.learning_rate, c.lam, user_sc1=self.user_sc1)
             with stage("mf.rotate.end", self.timer):
                 self.rot.end()
 
@@ -404,7 +412,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):
                     ops.mf_sgd_tiled(self.U, rows, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
-                                     c.lam, delta=delta, delta_init=p == 0)
+                                     c.lam, delta=delta, delta_init=p == 0, user_sc1=self.user_sc1)
             return delta
         with stage("mf.sgd", self.timer):
             if self.sgd_mode == "grouped":

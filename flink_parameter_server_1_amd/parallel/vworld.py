@@ -22,9 +22,15 @@ its own model instance, and talks through a ``VirtualComm`` -- a drop-in
   posting a different collective (or different split sizes) than its peers
   aborts the world with a desync report instead of hanging;
 * a matched transfer runs on a dedicated LINK stream after waiting for both
-  sides' post events, after an injectable delay (``torch.cuda._sleep``) that
-  models the xGMI time of the message (``latency_us + bytes / link_gbps``,
-  scaled by ``dilate``);
+  sides' post events, after an injectable delay that models the xGMI time of
+  the message (``latency_us + bytes / link_gbps``, scaled by ``dilate``; one
+  message at a time per link).  ``delay_model="host"`` (default): a link thread
+  watches the post events and issues the copy once the data has been ready for
+  the modelled time -- the delay occupies no compute unit, so it does not
+  compete with the ranks' kernels; ``"kernel"``: a ``torch.cuda._sleep`` on the
+  link stream before the copy (needs a free CU slot to start: under a
+  GPU-filling grid it queues behind the compute, which overstates the exposed
+  wait);
 * ``Work.wait()`` makes the CALLER's current stream wait for the transfer's
   completion event (the host blocks only until the peer has posted its side,
   i.e. until the transfer exists) -- exactly ``ProcessGroupNCCL``'s contract:
@@ -152,9 +158,12 @@ class VirtualWorld:
     """The shared transport of ``world`` rank threads on ``device``."""
 
     def __init__(self, world: int, device=None, mode: str = "async", link_gbps: float = 50.0,
-                 latency_us: float = 5.0, dilate: float = 1.0, delay: bool = True, timeout_s: float = 300.0):
+                 latency_us: float = 5.0, dilate: float = 1.0, delay: bool = True, timeout_s: float = 300.0,
+                 delay_model: str = "host"):
         if mode not in ("async", "sync"):
             raise ValueError("mode must be 'async' (RCCL semantics) or 'sync' (host-synchronous reference)")
+        if delay_model not in ("host", "kernel"):
+            raise ValueError("delay_model must be 'host' or 'kernel'")
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else \
                 torch.device("cpu")
@@ -177,8 +186,16 @@ class VirtualWorld:
         self.link_us: Dict[Tuple[int, int], float] = defaultdict(float)
         self.link_bytes: Dict[Tuple[int, int], int] = defaultdict(int)
         self.transfers = 0
-        if self.delay:
+        self.delay_model = delay_model
+        self._pending: deque = deque()     # host-timed transfers not issued yet
+        self._link_busy: Dict[Tuple[int, int], float] = defaultdict(float)
+        self._link_thread: Optional[threading.Thread] = None
+        self._closed = False
+        if self.delay and delay_model == "kernel":
             _Sleep.calibrate(self.device)
+        if self.delay and delay_model == "host":
+            self._link_thread = threading.Thread(target=self._link_loop, name="vworld-links", daemon=True)
+            self._link_thread.start()
 
     # ------------------------------------------------------------------ plumbing
     def comm(self, rank: int) -> "VirtualComm":
@@ -239,12 +256,23 @@ class VirtualWorld:
             for w in works:
                 w.pending -= 1
             return
+        if self.delay and self.delay_model == "host" and src_rank != dst_rank:
+            us = self._delay_us(nbytes)
+            self.link_us[(src_rank, dst_rank)] += us
+            self._pending.append([src_rank, dst_rank, dst, src, evs, works, us, None])
+            self.cv.notify_all()
+            return
+        self._issue(src_rank, dst_rank, dst, src, evs, works)
+
+    def _issue(self, src_rank: int, dst_rank: int, dst: torch.Tensor, src: torch.Tensor, evs, works) -> None:
+        """Enqueue the copy of a transfer on its link stream (called with ``cv`` held)."""
+        nbytes = src.numel() * src.element_size()
         s = self._link(src_rank, dst_rank)
         with torch.cuda.stream(s):
             for ev in evs:
                 if ev is not None:
                     s.wait_event(ev)
-            if self.delay and src_rank != dst_rank:
+            if self.delay and self.delay_model == "kernel" and src_rank != dst_rank:
                 us = self._delay_us(nbytes)
                 self.link_us[(src_rank, dst_rank)] += us
                 _Sleep.us(self.device, us)
@@ -258,6 +286,41 @@ class VirtualWorld:
         for w in works:
             w.events.append(done)
             w.pending -= 1
+
+    def _link_loop(self) -> None:
+        """Host-timed links: a transfer starts when both sides' post events have
+        completed (and its link finished the previous message), and is issued to the
+        device once its modelled duration has passed."""
+        torch.cuda.set_device(self.device)
+        while True:
+            with self.cv:
+                if self._closed or self.error is not None:
+                    return
+                now = time.perf_counter()
+                issued = False
+                for item in list(self._pending):
+                    src_rank, dst_rank, dst, src, evs, works, us, t_start = item
+                    key = (src_rank, dst_rank)
+                    if t_start is None:
+                        if all(ev is None or ev.query() for ev in evs):
+                            item[7] = t_start = max(now, self._link_busy[key])
+                            self._link_busy[key] = t_start + us * 1e-6
+                        continue
+                    if now >= t_start + us * 1e-6:
+                        self._pending.remove(item)
+                        self._issue(src_rank, dst_rank, dst, src, evs, works)
+                        issued = True
+                if issued:
+                    self.cv.notify_all()
+                wait_s = 2e-5 if self._pending else 1e-3
+                self.cv.wait(timeout=wait_s)
+
+    def close(self) -> None:
+        with self.cv:
+            self._closed = True
+            self.cv.notify_all()
+        if self._link_thread is not None:
+            self._link_thread.join(5.0)
 
     # ------------------------------------------------------------------ point-to-point
     def post_p2p(self, rank: int, sends: Sequence, recvs: Sequence) -> List[VWork]:
@@ -394,7 +457,7 @@ class VirtualWorld:
         with torch.cuda.stream(s):
             for ev in evs:
                 s.wait_event(ev)
-            if self.delay:
+            if self.delay and self.delay_model == "kernel":  # (host-timed links model point-to-point traffic)
                 _Sleep.us(self.device, self._delay_us(ts[0].numel() * ts[0].element_size() * 2))
             run()
             done = torch.cuda.Event()
@@ -516,12 +579,12 @@ class VirtualComm(Comm):
 
 def run_virtual(fn: Callable[..., Any], world: int, *args, device=None, mode: str = "async",
                 link_gbps: float = 50.0, latency_us: float = 5.0, dilate: float = 1.0, delay: bool = True,
-                timeout_s: float = 300.0, return_world: bool = False, **kwargs):
+                timeout_s: float = 300.0, return_world: bool = False, delay_model: str = "host", **kwargs):
     """Run ``fn(comm, *args, **kwargs)`` on ``world`` rank threads of one
     ``VirtualWorld``; each thread gets its own current stream.  Returns the list of
     results (and the world when ``return_world``); re-raises the first rank's error."""
     vw = VirtualWorld(world, device, mode=mode, link_gbps=link_gbps, latency_us=latency_us, dilate=dilate,
-                      delay=delay, timeout_s=timeout_s)
+                      delay=delay, timeout_s=timeout_s, delay_model=delay_model)
     results: List[Any] = [None] * world
     errors: List[Optional[BaseException]] = [None] * world
 
@@ -545,6 +608,7 @@ def run_virtual(fn: Callable[..., Any], world: int, *args, device=None, mode: st
     deadline = time.time() + timeout_s + 10.0  # past the waits' own timeout: they report what hung
     for t in threads:
         t.join(max(0.0, deadline - time.time()))
+    vw.close()
     if any(t.is_alive() for t in threads):
         vw._abort("virtual world timed out")
         for t in threads:
