@@ -107,6 +107,8 @@ def main(argv=None):
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     ap.add_argument("--watchdog-s", type=float, default=0.0,
                     help="fail fast: end this rank (exit 17) when a step makes no progress for this long (0 = off)")
+    ap.add_argument("--no-hogwild-probe", action="store_true",
+                    help="skip the side probe of lost user updates (run after the timed loop, reported in config)")
     ap.add_argument("--metrics-jsonl", default=None,
                     help="append per-step stage timings (HIP events) and counters of rank 0 to this JSON-lines file")
     a = ap.parse_args(argv)
@@ -181,6 +183,24 @@ def main(argv=None):
     bytes_per_rank = comm.gather_floats(sent)
     import torch.distributed as dist
 
+    # side probe (outside the timed region): the Hogwild user-row race of the tiled SGD
+    # measured on this rank's geometry -- users per GPU, the same batch and user phases
+    # (bench/probe_hogwild.py: user rows from 0, tiny step, every lost contribution
+    # counted by least squares per user); rank 0 only, the others wait at the barrier
+    hog = None
+    if (not a.no_hogwild_probe and dev.type == "cuda" and model.sgd_mode == "tiled" and model.exchange != "ps"
+            and comm.rank == 0):
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
+        from probe_hogwild import lost_updates
+
+        del data
+        torch.cuda.empty_cache()
+        n_loc = model.users.n_local
+        hog = lost_updates(n_loc, a.items, a.batch / n_loc, getattr(model, "user_phases", 1),
+                           user_update=a.user_update)
+        torch.cuda.empty_cache()
+    comm.barrier()
+
     world_seen = dist.get_world_size() if dist.is_initialized() else 1
     backend = dist.get_backend() if dist.is_initialized() else "none (single process)"
     total_updates = a.batch * a.steps * n
@@ -222,6 +242,11 @@ def main(argv=None):
                 "users_per_rank": [int(x) for x in n_local],
                 "bytes_sent_per_rank": bytes_per_rank,
                 "bytes_per_peer_rank0": list(comm.peer_bytes),
+                "user_update": a.user_update,
+                # Hogwild race of the user rows (side probe on rank 0's geometry, not timed):
+                # fraction of rated users that lost >= 1 update, fraction of rating updates lost
+                "lost_user_fraction": None if hog is None else hog["lost_user_fraction"],
+                "lost_user_update_fraction": None if hog is None else hog.get("lost_update_fraction"),
             },
         }
         print(json.dumps(out), flush=True)

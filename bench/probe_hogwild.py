@@ -48,7 +48,14 @@ def lost_update_count(U, uid, v, users: int, nmax: int = 24, chunk: int = 200_00
         V = torch.zeros((b - a, nmax, v.shape[1]), dtype=torch.float64, device=dev)
         V[u_[ok], k_[ok]] = v[order[lo:hi][ok]].double()
         pad = torch.arange(nmax, device=dev).view(1, -1) >= cnt[a:b].view(-1, 1)
-        G = V @ V.transpose(1, 2) + torch.diag_embed(pad.double())
+        G = V @ V.transpose(1, 2)
+        # scale of this user's contributions; padded slots get it on the diagonal, and a
+        # ridge of 1e-9 of it keeps a user who rated one item twice (parallel
+        # contributions) solvable
+        real_n = (~pad).sum(1, keepdim=True).clamp_min(1)
+        scale = (G.diagonal(dim1=1, dim2=2) * (~pad)).sum(1, keepdim=True) / real_n
+        scale = torch.where(scale > 0, scale, torch.ones_like(scale))
+        G = G + torch.diag_embed(pad.double() * scale + 1e-9 * scale)
         rhs = (V @ U[a:b].double().unsqueeze(-1)).squeeze(-1)
         c = torch.linalg.solve(G, rhs)
         real = ~pad & (cnt[a:b] <= nmax).view(-1, 1)
@@ -67,7 +74,7 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
     dev = torch.device("cuda", 0)
     cfg = MFConfig(num_users=users, num_items=items, dim=64, learning_rate=lr, user_phases=phases,
                    prefetch_partition=False, user_update=user_update)
-    m = DistributedMF(cfg, Comm(device=dev))
+    m = DistributedMF(cfg, Comm(device=dev, local=True))
     assert m.sgd_mode == ("flat" if user_update == "atomic" else "tiled")
     g = torch.Generator(device=dev).manual_seed(seed)
     with torch.no_grad():

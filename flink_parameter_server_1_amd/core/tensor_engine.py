@@ -55,10 +55,11 @@ def staleness_for_pull_limit(pull_limit: int, micro_batch: int) -> int:
 
 
 class _Request:
-    __slots__ = ("keys", "payload", "off", "n")
+    __slots__ = ("keys", "payload", "off", "n", "presence")
 
-    def __init__(self, keys, payload, off, n):
+    def __init__(self, keys, payload, off, n, presence=None):
         self.keys, self.payload, self.off, self.n = keys, payload, off, n
+        self.presence = presence
 
 
 class _Client(BatchedPSClient):
@@ -79,11 +80,15 @@ class _Client(BatchedPSClient):
         self._arb_vals: List[torch.Tensor] = []
 
     # --------------------------------------------------------------- pulls
-    def pull(self, keys, payload=None):
+    def pull(self, keys, payload=None, presence=None):
+        """``presence`` (optional, a hint): ``(flags uint8[key space], ready event)`` -- which
+        keys of the table occur in ``keys``, computed by the worker anyway (e.g. by its
+        partition pass); a plan over the whole key space (identity plan) then skips its
+        own marking pass.  Used only when this is the micro-batch's only request."""
         if self._requests is None:
             raise RuntimeError("pull() is only valid inside on_recv_batch")
         keys = torch.as_tensor(keys).reshape(-1)
-        self._requests.append(_Request(keys, payload, self._n, keys.numel()))
+        self._requests.append(_Request(keys, payload, self._n, keys.numel(), presence))
         self._n += keys.numel()
 
     # --------------------------------------------------------------- pushes
@@ -316,7 +321,8 @@ class TensorRuntime:
         if self.pipe is None:
             self._locked_step(keys, reqs, flag)
         else:
-            self.pipe.submit(keys, reqs, flag)
+            hint = reqs[0].presence if len(reqs) == 1 else None
+            self.pipe.submit(keys, reqs, flag, presence=hint)
 
     def _compute(self, rows, plan, reqs):
         c = self.client

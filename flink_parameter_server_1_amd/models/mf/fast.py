@@ -177,6 +177,11 @@ class DistributedMF:
             self._tilers = [ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8,
                                                 phases=self.user_phases, users_per_phase=upp)
                             for _ in range(n_tilers)]
+            # PS path, identity plans: the partition's count pass marks the items a batch
+            # rates (one flag array per partition buffer) -- the plan's presence flags, so
+            # the PS needs no marking pass over the 64M keys of its own
+            self._presence = [torch.zeros(cfg.num_items, dtype=torch.uint8, device=dev) for _ in range(n_tilers)] \
+                if ps_spec else None
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
@@ -215,6 +220,12 @@ class DistributedMF:
             from ...ps.device_logics import DeviceSimplePSLogicWithClose
 
             logic = DeviceSimplePSLogicWithClose(cfg.num_items, cfg.dim, table=self.items, ps=self.ps)
+            if self.sgd_mode == "tiled" and self._ps_spec:
+                # the delta-mode SGD only reads the pulled rows, and the staged partition
+                # (not the plan's positions) addresses them: the world-1 identity plan may
+                # serve the shard itself and keep the batch's key tensor as is
+                self.ps.zero_copy_identity = True
+                self.ps.keys_stable = True
             self.runtime = TensorRuntime(self.comm, staleness=1 if self.pipeline else 0)
             self.runtime.start(_MFPSWorker(self), logic)
         if cfg.negative_sample_rate > 0:
@@ -342,10 +353,14 @@ class DistributedMF:
 
     def _stage_partition(self, uid_local, iid, rating):
         """Tile partition of one batch into the next of the two partition buffers;
-        returns ``(ptr, rec, ready_event)``."""
+        returns ``(ptr, rec, ready_event)`` (PS path, identity plans: the count pass also
+        marks the batch's items in this buffer's presence flags, ``self._presence[i]``)."""
         seen = self._seen if (self.exchange == "rotate" and self.items.touched is not None) else None
-        tiler = self._tilers[self._tiler_i]
+        i = self._tiler_i
+        tiler = self._tilers[i]
         self._tiler_i = (self._tiler_i + 1) % len(self._tilers)
+        if self._presence is not None:
+            seen = self._presence[i]
         if self._side is None:
             with stage("mf.partition", self.timer):
                 ptr, rec = tiler.run(uid_local, iid, rating, seen)
@@ -353,6 +368,8 @@ class DistributedMF:
         main = torch.cuda.current_stream(self.U.device)
         self._side.wait_stream(main)  # inputs written, and this buffer's previous SGD done
         with torch.cuda.stream(self._side):
+            if self._presence is not None:
+                seen.zero_()
             with stage("mf.partition", self.timer):  # timed on the side stream
                 ptr, rec = tiler.run(uid_local, iid, rating, seen)
             ev = torch.cuda.Event()
@@ -536,6 +553,10 @@ class _MFPSWorker(BatchedWorkerLogic):
             # identity plan ahead: bucket by item id now, on the side stream, while an
             # earlier batch's SGD runs (the partition no longer sits on the critical path)
             staged = m._stage_partition(uid_local, iid, rating)
+            # the partition marked the rated items: the identity plan's presence flags
+            ps.pull(iid, (uid_local, rating, staged), presence=(m._presence[(m._tiler_i - 1) % len(m._tilers)],
+                                                                 staged[2]))
+            return
         ps.pull(iid, (uid_local, rating, staged))
 
     def on_pull_recv_batch(self, pulled, ps):

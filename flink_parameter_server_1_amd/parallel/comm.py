@@ -30,9 +30,10 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, local: bool = False):
+        """``local``: a world of one even inside a process group (side computations)."""
         self.group = group
-        if dist.is_available() and dist.is_initialized():
+        if not local and dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
             self.backend = dist.get_backend(group)

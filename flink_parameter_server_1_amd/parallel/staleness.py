@@ -66,14 +66,15 @@ class BoundedStalenessPipeline:
         self.all_flagged = False
         self.submitted = 0
 
-    def submit(self, keys: torch.Tensor, payload: Any = None, flag: int = 0) -> List[Any]:
+    def submit(self, keys: torch.Tensor, payload: Any = None, flag: int = 0, presence=None) -> List[Any]:
         """Begin the pull of a new micro-batch; finish (compute + push) every
         batch that would otherwise exceed the staleness bound.  Returns the
-        results of the batches finished by this call, oldest first."""
+        results of the batches finished by this call, oldest first.  ``presence``:
+        the single-table plan's key-presence hint (``TensorPS.plan_begin``)."""
         if self.multi:
             self._planned.append((TensorPS.plan_begin_multi(self.pss, keys, flag), payload))
         else:
-            self._planned.append((self.ps.plan_begin(keys, flag), payload))
+            self._planned.append((self.ps.plan_begin(keys, flag, presence=presence), payload))
         self.submitted += 1
         out: List[Any] = []
         while len(self._planned) > (1 if self.lookahead else 0):

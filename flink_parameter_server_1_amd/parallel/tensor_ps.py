@@ -64,6 +64,7 @@ class PullPlan:
     #: False: a request plan (no de-duplication) -- keys may repeat, so pushes apply
     #: with atomics instead of the unique-key read-modify-write
     unique: bool = True
+    ready: Optional[object] = None  # event to wait for before the plan's device data is read
 
 
 @dataclass
@@ -82,6 +83,7 @@ class PendingPlan:
     identity: bool = False
     unique: bool = True
     static: bool = False  # sizes known on the host (world 1): nothing to wait for
+    ready: Optional[object] = None  # event the plan's inputs (a presence hint) are ready behind
     #: ``TensorPS._plan_seq`` when the counts' event was recorded
     seq: int = 0
     #: columns of ``host`` holding (sent count, sent flag, recv count, recv flag): several
@@ -126,6 +128,10 @@ class TensorPS:
         #: pipeline is one or more submits later: they keep a copy unless the owner
         #: guarantees its key tensors are never rewritten (``keys_stable``)
         self.keys_stable = False
+        #: world-1 identity plans serve the shard itself instead of a copy (the pulled
+        #: rows are the table): for owners whose workers only READ the pulled rows and
+        #: accept reading them fresher than served (never staler: the bound still holds)
+        self.zero_copy_identity = False
 
     @property
     def stats(self) -> dict:
@@ -175,18 +181,21 @@ class TensorPS:
                 and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
 
     # ----------------------------------------------------------------- planning
-    def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None) -> PendingPlan:
+    def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None,
+                   presence=None) -> PendingPlan:
         """Stage A: dedup + count exchange, counts copied to pinned host memory
         asynchronously.  Collective: every rank calls it once per micro-batch
         (with empty ``keys`` when it has nothing to pull).  ``flag`` (an int) is
         delivered to every peer with the counts (``PullPlan.peer_flags``).  ``dedup``:
-        force (True) the de-duplicating plan instead of ``dedups(n)``'s choice."""
-        a = self._stage_a(keys, flag, dedup)
+        force (True) the de-duplicating plan instead of ``dedups(n)``'s choice.
+        ``presence``: ``(uint8 flags [key space], event)`` of the keys, computed by the
+        caller (an identity plan then skips its marking pass; other plans ignore it)."""
+        a = self._stage_a(keys, flag, dedup, presence)
         if isinstance(a, PendingPlan):
             return a
         return self._pending(*a, flag=flag)
 
-    def _stage_a(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None):
+    def _stage_a(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None, presence=None):
         """The device part of stage A: a finished (static) ``PendingPlan``, or
         ``(n, counts, uniq, pos, unique)`` still needing the count exchange."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
@@ -195,13 +204,17 @@ class TensorPS:
             ks = int(self.table.key_space)
             if self._iota is None or self._iota.numel() != ks:
                 self._iota = torch.arange(ks, dtype=torch.int32, device=keys.device)
-            with stage("ps.presence", self.timer):
-                present = torch.zeros(ks, dtype=torch.uint8, device=keys.device)
-                ops.mark_rows(present, keys)
+            ready = None
+            if presence is not None and presence[0].numel() == ks:
+                present, ready = presence  # the caller's flags (e.g. from its partition pass)
+            else:
+                with stage("ps.presence", self.timer):
+                    present = torch.zeros(ks, dtype=torch.uint8, device=keys.device)
+                    ops.mark_rows(present, keys)
             if not self.keys_stable:
                 keys = keys.clone()
             return PendingPlan(n, None, self._iota, keys, None, None, int(flag), valid=present.view(torch.bool),
-                               n_bound=ks, identity=True, static=True)
+                               n_bound=ks, identity=True, static=True, ready=ready)
         W = self.comm.world
         if not (dedup or self.dedups(n)):
             if W == 1 and self.static:  # every request is its own row: nothing to compute
@@ -264,6 +277,8 @@ class TensorPS:
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
         if pp.static:  # static world-1 plan: sizes known on the host, nothing to wait for
+            if pp.ready is not None and self.table.device.type == "cuda":
+                torch.cuda.current_stream(self.table.device).wait_event(pp.ready)
             self._stats["pulls"] += pp.n
             if pp.valid is not None:
                 self._count_lazy("unique", pp.valid)
@@ -271,7 +286,7 @@ class TensorPS:
                 self._stats["unique"] += pp.n_bound
             self._stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
-                            valid=pp.valid, identity=pp.identity, unique=pp.unique)
+                            valid=pp.valid, identity=pp.identity, unique=pp.unique, ready=pp.ready)
         if pp.event is not None:
             if not pp.event.query():
                 self._stats["host_waits"] += 1
@@ -355,7 +370,10 @@ class TensorPS:
             if not plan.identity or (touched is None and not sentinel):
                 return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
             # identity plan: every row is served, only the keys present count as pulled
-            out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
+            if self.zero_copy_identity and self.wire_dtype == self.table.weight.dtype:
+                out = self.table.weight  # the pulled rows ARE the shard (read-only consumer)
+            else:
+                out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
             if sentinel:  # flip the untouched sentinel of the present rows only
                 w = self.table.weight
                 w.masked_fill_((w == 0) & torch.signbit(w) & plan.valid.view(-1, 1), 0.0)

@@ -603,12 +603,20 @@ def run_virtual(fn: Callable[..., Any], world: int, *args, device=None, mode: st
             vw._abort(f"rank {r} raised {type(e).__name__}: {e}")
 
     threads = [threading.Thread(target=body, args=(r,), name=f"vrank{r}", daemon=True) for r in range(world)]
+    # N rank threads and the link thread share one interpreter: a short GIL switch
+    # interval keeps a thread that just became runnable (a transfer to issue, a wait
+    # that matched) from queueing behind the default 5 ms time slice of another
+    import sys
+
+    switch = sys.getswitchinterval()
+    sys.setswitchinterval(5e-5)
     for t in threads:
         t.start()
     deadline = time.time() + timeout_s + 10.0  # past the waits' own timeout: they report what hung
     for t in threads:
         t.join(max(0.0, deadline - time.time()))
     vw.close()
+    sys.setswitchinterval(switch)
     if any(t.is_alive() for t in threads):
         vw._abort("virtual world timed out")
         for t in threads:
