@@ -41,6 +41,8 @@ def main(argv=None):
     ap.add_argument("--exchange", default="rotate", choices=["rotate", "ps"])
     ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
     ap.add_argument("--mode", default="async", choices=["async", "sync"])
+    ap.add_argument("--no-delay", action="store_true",
+                    help="control run: transfers as soon as both sides posted (what remains is rank skew)")
     ap.add_argument("--traceback-s", type=float, default=0.0,
                     help="dump every thread's Python stack to stderr every this many seconds (hang diagnosis)")
     a = ap.parse_args(argv)
@@ -90,14 +92,14 @@ def main(argv=None):
                 "a2a_bytes_sent": comm.bytes_sent, "sgd_mode": m.sgd_mode}
 
     res, vw = run_virtual(rank_main, a.world, mode=a.mode, link_gbps=a.link_gbps, latency_us=a.latency_us,
-                          dilate=dilate, return_world=True, timeout_s=1000)
+                          dilate=dilate, return_world=True, timeout_s=1000, delay=not a.no_delay)
     step = max(r["ms_per_step"] for r in res)
     waits = [r["comm_wait_ms_per_step"] for r in res]
     link_ms = sum(vw.link_us.values()) / 1e3 / max(len(vw.link_us), 1) / (a.steps + a.warmup)
     out = {
         "bench": "vworld", "world": a.world, "exchange": a.exchange, "rotation": a.rotation, "mode": a.mode,
         "batch_per_rank": a.batch, "users": a.users, "items": a.items, "dim": a.dim, "steps": a.steps,
-        "link_gbps": a.link_gbps, "latency_us": a.latency_us, "dilate": dilate,
+        "link_gbps": a.link_gbps, "latency_us": a.latency_us, "dilate": dilate, "delay": not a.no_delay,
         "ms_per_step_all_ranks_one_gpu": step,
         "comm_wait_ms_per_step_per_rank": waits,
         "exposed_wait_fraction_max": max(waits) / step if step else None,

@@ -25,6 +25,7 @@ _lib = None
 _err = None
 
 c_int, c_i64, c_f32, c_u32, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32, ctypes.c_void_p
+c_u64 = ctypes.c_uint64
 
 _SIGNATURES = {
     "fps_abi_version": [],
@@ -46,7 +47,7 @@ _SIGNATURES = {
     "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                            c_int, c_vp, c_vp],
     "fps_mf_sgd_tiled": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_f32,
-                         c_f32, c_vp, c_int, c_i64, c_int, c_vp],
+                         c_f32, c_vp, c_int, c_i64, c_int, c_vp, c_u64, c_int, c_vp],
     "fps_score_filter": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_topk_merge_cand": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp],
     "fps_score_filter_lemp": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
