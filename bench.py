@@ -103,8 +103,6 @@ def main(argv=None):
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--user-phases", type=int, default=0,
                     help="tiled SGD: user-range phases per step (0 = auto, ~2.5M users per phase)")
-    ap.add_argument("--persistent-sgd", action="store_true",
-                    help="tiled SGD: persistent launches taking tiles from a device counter (no tail round)")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
     ap.add_argument("--watchdog-s", type=float, default=0.0,
@@ -130,7 +128,7 @@ def main(argv=None):
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
-                   user_phases=a.user_phases, rotation=a.rotation, persistent_sgd=a.persistent_sgd)
+                   user_phases=a.user_phases, rotation=a.rotation)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
     dev = comm.device

@@ -37,7 +37,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
-    ap.add_argument("--persistent-sgd", action="store_true")
     a = ap.parse_args()
 
     import torch
@@ -50,8 +49,7 @@ def main():
     base = None
     for W in [int(x) for x in a.ws.split(",")]:
         cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
-                       exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0,
-                       persistent_sgd=a.persistent_sgd)
+                       exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0)
         m = DistributedMF(cfg, comm)
         data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
         s = 0

@@ -684,12 +684,10 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
   }
 }
 
-// One workgroup per tile (grid = tiles), or -- ``ctr`` != nullptr -- a persistent grid
-// whose workgroups take tiles from a 64-bit counter (tile = fetched - base) until it runs
-// past ntiles: no tail of a last, partly filled round of workgroups (16 launches of
-// ~2k tiles per step at N = 8: two rounds each).  Every workgroup makes exactly one
-// fetch past the end, so a launch advances the counter by ntiles + grid (the host's
-// next base).
+// One workgroup per tile.  (A persistent grid taking tiles from a device counter, to
+// drop the tail round of the 16 small launches per step at N = 8, was measured slower:
+// 9.58e9 vs 9.87e9 updates/s at N = 1, 7.64 vs 7.45 ms emulated N = 8 --
+// profiles/r4_persistent_sgd_ab.txt; removed.)
 template <int TPR, int V, int PF, bool REC8, bool DELTA, bool USC1>
 __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
@@ -697,26 +695,10 @@ __global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict
                                                                int64_t block_rows, float lr, float lambda,
                                                                float* __restrict__ I1, int64_t block_rows1, int T0,
                                                                const int32_t* __restrict__ ptr1,
-                                                               float* __restrict__ Dl, int dl_init, uint32_t ubytes,
-                                                               unsigned long long* __restrict__ ctr,
-                                                               unsigned long long base, int ntiles) {
+                                                               float* __restrict__ Dl, int dl_init, uint32_t ubytes) {
   __shared__ TgShared<REC8> sh;
-  if (ctr == nullptr) {
-    tilegroup_tile<TPR, V, PF, REC8, DELTA, USC1>(sh, blockIdx.x, U, I, rec_, ptr, R, block_rows, lr, lambda, I1,
-                                                  block_rows1, T0, ptr1, Dl, dl_init, ubytes);
-    return;
-  }
-  __shared__ int s_t;
-  for (;;) {
-    if (threadIdx.x == 0) s_t = (int)min(atomicAdd(ctr, 1ull) - base, (unsigned long long)ntiles);
-    __syncthreads();
-    const int t = s_t;
-    __syncthreads();  // every thread read s_t before thread 0 fetches the next tile
-    if (t >= ntiles) break;  // uniform: every wave leaves
-    tilegroup_tile<TPR, V, PF, REC8, DELTA, USC1>(sh, t, U, I, rec_, ptr, R, block_rows, lr, lambda, I1,
-                                                  block_rows1, T0, ptr1, Dl, dl_init, ubytes);
-    __syncthreads();  // the tile's LDS reads are done before the next tile's writes
-  }
+  tilegroup_tile<TPR, V, PF, REC8, DELTA, USC1>(sh, blockIdx.x, U, I, rec_, ptr, R, block_rows, lr, lambda, I1,
+                                                block_rows1, T0, ptr1, Dl, dl_init, ubytes);
 }
 
 }  // namespace
@@ -816,12 +798,9 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // R (<= 256) rows each.  D must be 16, 32, 64, 128 or 256.
 // delta0 != nullptr (nblk = 1): DELTA mode -- I0 read-only, the block's deltas written
 // to delta0 (delta_init) or added to it (a later user phase over the same rows).
-// ctr != nullptr: persistent launch of min(persistent_grid, tiles) workgroups fetching
-// tiles from *ctr (base = its value before this launch; the launch adds tiles + grid).
 FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, const int32_t* ptr0, int T, int R,
                              int64_t rows0, float* I1, const int32_t* ptr1, int64_t rows1, int nblk, int D, float lr,
                              float lambda, float* delta0, int delta_init, int64_t users_bytes, int user_sc1,
-                             unsigned long long* ctr, unsigned long long ctr_base, int persistent_grid,
                              void* stream) {
   if (T <= 0) return 0;
   if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
@@ -829,9 +808,6 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
   if (nblk == 1) { I1 = I0; ptr1 = ptr0; rows1 = rows0; }
   const int grid = nblk * T;
-  // ctr != nullptr: persistent_grid workgroups take the grid's tiles from the counter
-  if (ctr != nullptr && persistent_grid <= 0) return (int)hipErrorInvalidValue;
-  const int lgrid = ctr != nullptr ? (persistent_grid < grid ? persistent_grid : grid) : grid;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = 8;
   // user-row cache policy (user_sc1: write-through sc1, see USC1); 8-B records address
@@ -840,15 +816,14 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
   const bool usc1 = user_sc1 != 0;
   const uint32_t ubytes = (uint32_t)(usc1 ? users_bytes : 0);
 #define FPS_TILED_(TPR_, V_, DL_)                                                                               \
-  if (rec8 && usc1) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, true>), dim3(lgrid),      \
+  if (rec8 && usc1) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, true>), dim3(grid),      \
                                        dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, \
-                                       delta0, delta_init, ubytes, ctr, ctr_base, grid);                         \
-  else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, false>), dim3(lgrid),         \
+                                       delta0, delta_init, ubytes);                         \
+  else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, false>), dim3(grid),         \
                                     dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1,    \
-                                    delta0, delta_init, ubytes, ctr, ctr_base, grid);                            \
-  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_, false>), dim3(lgrid), dim3(512), 0, s,\
-                          U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init, ubytes,  \
-                          ctr, ctr_base, grid)
+                                    delta0, delta_init, ubytes);                            \
+  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_, false>), dim3(grid), dim3(512), 0, s,\
+                          U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init, ubytes)
 #define FPS_TILED(TPR_, V_)                      \
   if (delta0 != nullptr) { FPS_TILED_(TPR_, V_, true); } \
   else { FPS_TILED_(TPR_, V_, false); }

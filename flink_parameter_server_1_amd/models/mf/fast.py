@@ -80,8 +80,6 @@ class MFConfig:
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
     rotation: str = "bidir"           # rotate: "bidir" (two counter-rotating rings) | "ring" (one ring)
     emulate_world: int = 0            # W = 1, rotate: rank 0's share of an N-rank job (users / schedule)
-    persistent_sgd: bool = False      # tiled: persistent SGD launches taking tiles from a device counter
-                                      # (no tail round of workgroups per launch; not with graph_capture)
 
 
     def user_seed(self) -> int:
@@ -186,9 +184,6 @@ class DistributedMF:
                 if ps_spec else None
             self._tiler_i = 0
             self._graphs = {} if (cfg.graph_capture and dev.type == "cuda" and exchange == "local") else None
-            # a captured graph would replay one launch's counter base: persistent launches stay eager
-            self._ctr = ops.TileCounter(dev) if (cfg.persistent_sgd and dev.type == "cuda"
-                                                 and self._graphs is None) else None
             self._prefetch = (cfg.prefetch_partition and dev.type == "cuda" and self._graphs is None
                               and exchange != "ps")
             self._ps_spec = ps_spec
@@ -393,7 +388,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):  # both item blocks of a phase in one launch
                     ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
-                                          c.learning_rate, c.lam, user_sc1=self.user_sc1, counter=self._ctr)
+                                          c.learning_rate, c.lam, user_sc1=self.user_sc1)
             return
         nb = 2 * self.rot_w  # item blocks per user phase in the partition layout
         for _ in range(self.rot.K):
@@ -405,11 +400,11 @@ class DistributedMF:
                     if len(act) == 2:  # one block of each ring: disjoint items, one launch
                         (g0, b0), (g1, b1) = act
                         ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                              c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1, counter=self._ctr)
+                                              c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1)
                     else:
                         (g0, b0), = act
                         ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                         c.learning_rate, c.lam, user_sc1=self.user_sc1, counter=self._ctr)
+                                         c.learning_rate, c.lam, user_sc1=self.user_sc1)
             with stage("mf.rotate.end", self.timer):
                 self.rot.end()
 
@@ -434,7 +429,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):
                     ops.mf_sgd_tiled(self.U, rows, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
-                                     c.lam, delta=delta, delta_init=p == 0, user_sc1=self.user_sc1, counter=self._ctr)
+                                     c.lam, delta=delta, delta_init=p == 0, user_sc1=self.user_sc1)
             return delta
         with stage("mf.sgd", self.timer):
             if self.sgd_mode == "grouped":

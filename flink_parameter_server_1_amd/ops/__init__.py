@@ -522,36 +522,8 @@ class TilePartitioner:
         return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
-class TileCounter:
-    """Work counter of the persistent tiled SGD launch (``mf_sgd_tiled(counter=...)``):
-    ``grid`` workgroups take tiles from a device counter instead of one workgroup per
-    tile, so the launch has no tail round of partly filled workgroups.  One counter per
-    sequence of launches on one stream (the host keeps each launch's base)."""
-
-    GRID = 1024  # ~ the resident tile-SGD workgroups of 256 CUs (38 KiB of LDS each)
-
-    def __init__(self, device, grid: Optional[int] = None):
-        self.t = torch.zeros(1, dtype=torch.int64, device=device)
-        self.base = 0
-        self.grid = int(grid or self.GRID)
-
-    def take(self, ntiles: int):
-        """``(counter pointer, base, grid)`` of the next launch over ``ntiles`` tiles."""
-        g = min(self.grid, ntiles)
-        base = self.base
-        self.base += ntiles + g  # every workgroup makes one fetch past the end
-        return self.t.data_ptr(), base, g
-
-
-def _ctr_args(counter, ntiles):
-    if counter is None:
-        return None, 0, 0
-    return counter.take(ntiles)
-
-
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
-                 delta: Optional[torch.Tensor] = None, delta_init: bool = True, user_sc1: bool = False,
-                 counter: Optional[TileCounter] = None):
+                 delta: Optional[torch.Tensor] = None, delta_init: bool = True, user_sc1: bool = False):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
     records from ``TilePartitioner``): one workgroup per tile, every item row owned
     by one lane group (registers), item deltas summed per row -- no item atomics.
@@ -560,8 +532,7 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
     ``delta_init=False`` adds to the deltas of an earlier launch over the same rows
     (the rows then continue from ``I_block + delta``).  ``user_sc1``: user rows loaded /
     stored write-through (``sc1``; 8-B records, user table < 4 GiB) -- about half the
-    Hogwild lost user updates of plain accesses (``profiles/r4_hogwild.md``).
-    ``counter`` (a ``TileCounter``): persistent launch taking tiles from it."""
+    Hogwild lost user updates of plain accesses (``profiles/r4_hogwild.md``)."""
     if delta is not None and (delta.shape != I_block.shape or delta.dtype != torch.float32):
         raise ValueError("mf_sgd_tiled: delta must be an fp32 tensor shaped like the item block")
     if _on_gpu(U):
@@ -570,8 +541,8 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), p0, T, tile_rows, I_block.shape[0], None, None, 0, 1,
                                      U.shape[1], lr, lam, None if delta is None else _c(delta).data_ptr(),
-                                     int(delta_init), U.numel() * 4, int(user_sc1), *_ctr_args(counter, T),
-                                     N.stream_ptr(U.device)), "mf_sgd_tiled")
+                                     int(delta_init), U.numel() * 4, int(user_sc1), N.stream_ptr(U.device)),
+                "mf_sgd_tiled")
         return
     uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
@@ -584,7 +555,7 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
 
 
 def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
-                      block1: Optional[int] = None, user_sc1: bool = False, counter: Optional[TileCounter] = None):
+                      block1: Optional[int] = None, user_sc1: bool = False):
     """``mf_sgd_tiled`` of item blocks ``block`` (rows ``I0``) and ``block1`` (default
     ``block + 1``; rows ``I1``) in one launch of 2T workgroups: the blocks share no
     item row, so they need no ordering, and one launch instead of two halves the
@@ -596,8 +567,8 @@ def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, l
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), base + 4 * block * T, T, tile_rows, I0.shape[0],
                                      _c(I1).data_ptr(), base + 4 * block1 * T, I1.shape[0], 2, U.shape[1], lr, lam,
-                                     None, 1, U.numel() * 4, int(user_sc1), *_ctr_args(counter, 2 * T),
-                                     N.stream_ptr(U.device)), "mf_sgd_tiled_pair")
+                                     None, 1, U.numel() * 4, int(user_sc1), N.stream_ptr(U.device)),
+                "mf_sgd_tiled_pair")
         return
     mf_sgd_tiled(U, I0, rec, ptr, block, T, tile_rows, lr, lam, user_sc1=user_sc1)
     mf_sgd_tiled(U, I1, rec, ptr, block1, T, tile_rows, lr, lam, user_sc1=user_sc1)

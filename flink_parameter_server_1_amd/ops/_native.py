@@ -47,7 +47,7 @@ _SIGNATURES = {
     "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                            c_int, c_vp, c_vp],
     "fps_mf_sgd_tiled": [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_f32,
-                         c_f32, c_vp, c_int, c_i64, c_int, c_vp, c_u64, c_int, c_vp],
+                         c_f32, c_vp, c_int, c_i64, c_int, c_vp],
     "fps_score_filter": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_topk_merge_cand": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp],
     "fps_score_filter_lemp": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,

@@ -402,32 +402,3 @@ def test_mf_sgd_tiled_delta_mode_equals_in_place(phases, rec8):
     assert torch.equal(delta[ni - 600:], torch.zeros_like(delta[ni - 600:]))
     torch.testing.assert_close(U2, U1, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(I0 + delta, I1, rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize("delta", [False, True])
-def test_mf_sgd_tiled_persistent_equals_one_workgroup_per_tile(delta):
-    """Persistent launch (workgroups take tiles from a device counter, ``TileCounter``)
-    == one workgroup per tile, over several launches on one counter (the host keeps
-    each launch's base); unique users (no Hogwild race)."""
-    D, nu, ni, B = 64, 300_000, 40_000, 120_000
-    U0 = torch.rand(nu, D, device=DEV) * 0.1
-    I0 = torch.rand(ni, D, device=DEV) * 0.1
-    uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
-    iid = torch.randint(0, ni, (B,), device=DEV, dtype=torch.int32)
-    r = torch.rand(B, device=DEV)
-    Rt = ops.tile_rows_for(D, ni, 1)
-    T = -(-ni // Rt)
-    ptr, rec = ops.TilePartitioner(1, [ni], Rt, T, DEV, phases=2, users_per_phase=nu // 2).run(uid, iid, r)
-    ctr = ops.TileCounter(DEV, grid=64)  # fewer workgroups than tiles: every workgroup takes many
-    out = []
-    for c in (None, ctr):
-        U, I = U0.clone(), I0.clone()
-        d = torch.full_like(I, float("nan")) if delta else None
-        for p in range(2):
-            ops.mf_sgd_tiled(U, I, rec, ptr, 2 * p, T, Rt, 0.01, 0.0, delta=d, delta_init=p == 0, counter=c)
-        out.append((U, I if d is None else d))
-    torch.cuda.synchronize()
-    assert int(ctr.t.item()) == ctr.base  # every launch advanced the counter by tiles + grid
-    # (a row's ratings are summed in LDS-slot order, which varies run to run: fp32 rounding)
-    torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-5, atol=1e-6)
