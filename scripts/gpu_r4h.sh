@@ -6,6 +6,8 @@ export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc4
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_hogwild_gpu.py -m gpu -x -v --timeout 250 --timeout-method thread > $O/hogwild_tests.log 2>&1 || { tail -30 $O/hogwild_tests.log; exit 1; }
+grep -E "PASS|FAIL" $O/hogwild_tests.log
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
 P2="FETCH_SIZE"
 P3="WRITE_SIZE"
@@ -26,4 +28,5 @@ for pass in 1 2 3; do
 done
 python scripts/pmc_summary.py $O w2v,hash,route,coord,mfps,emu8 > $O/summary.md 2>&1 || { cat $O/summary.md; exit 1; }
 cat $O/summary.md
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mftopk -- python bench/bench_mf_topk.py --steps 6 --warmup 2 > $O/prof_mftopk.log 2>&1 || { tail -20 $O/prof_mftopk.log; exit 1; }
 echo ALLDONE
