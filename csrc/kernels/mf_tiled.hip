@@ -272,7 +272,10 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
       }
       if constexpr (H16) {
         __syncthreads();
-        if (s_ovf) {  // uniform: flush the histogram into the global row and restart it at zero
+        const bool ovf = s_ovf;
+        // every thread has read the flag before any can start the next sub-batch and set it again
+        __syncthreads();
+        if (ovf) {  // uniform: flush the histogram into the global row and restart it at zero
           const int32_t tot = coarse_now();
           if (ck < NC && cl == 0) { hc_acc[ck] += tot - hc_prev[ck]; hc_prev[ck] = 0; }
           const bool first = !s_flushed;

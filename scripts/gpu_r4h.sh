@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc4
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_hogwild_gpu.py -m gpu -x -v --timeout 250 --timeout-method thread > $O/hogwild_tests.log 2>&1 || { tail -30 $O/hogwild_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_hogwild_gpu.py tests/test_kernels_gpu.py -k "hogwild or Hogwild or lost or partition or count or 16" -m gpu -x -v --timeout 250 --timeout-method thread > $O/hogwild_tests.log 2>&1 || { tail -30 $O/hogwild_tests.log; exit 1; }
 grep -E "PASS|FAIL" $O/hogwild_tests.log
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
 P2="FETCH_SIZE"
