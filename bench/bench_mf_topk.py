@@ -40,6 +40,8 @@ def main(argv=None):
     ap.add_argument("--negatives", type=int, default=2)
     ap.add_argument("--memory", type=int, default=16)
     ap.add_argument("--bucket", type=int, default=65536)
+    ap.add_argument("--seed-items", type=int, default=None, help="LempTopK.seed_items (unfused first segment)")
+    ap.add_argument("--max-segment", type=int, default=None, help="LempTopK.max_segment (largest fused segment)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args(argv)
@@ -51,6 +53,12 @@ def main(argv=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
     from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogic
 
+    from flink_parameter_server_1_amd.models.mf.topk_fast import LempTopK
+
+    if a.seed_items:
+        LempTopK.seed_items = a.seed_items
+    if a.max_segment:
+        LempTopK.max_segment = a.max_segment
     comm = Comm.init_from_env()
     dev = comm.device
     worker = OnlineMFTopKWorker(a.items, a.dim, 0.01, K=a.k, worker_k=a.worker_k, memory=a.memory,
@@ -94,7 +102,8 @@ def main(argv=None):
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "dtype": "fp32", "scorer": _scorer(), "data": "synthetic ratings, random-init factors (warm item catalogue)",
             "config": {"users": a.users, "items": a.items, "dim": a.dim, "k": a.k, "worker_k": a.worker_k,
-                       "batch": a.batch, "negatives": a.negatives, "memory": a.memory, "bucket": a.bucket},
+                       "batch": a.batch, "negatives": a.negatives, "memory": a.memory, "bucket": a.bucket,
+                       "seed_items": LempTopK.seed_items, "max_segment": LempTopK.max_segment},
         }), flush=True)
 
 

@@ -16,7 +16,7 @@
 // wait: a lane never waits on another lane's write inside one kernel):
 //   1. find/insert: CAS the key into tab; the CAS winner is the key's unique
 //      inserter ("fresh") -- also across the source segments of one call;
-//   2. assign: fresh lanes take rows (one wave-aggregated atomicAdd per wave)
+//   2. assign: fresh lanes take rows (one atomicAdd per block tile, block scan)
 //      and publish rowmap[slot] / rowkey[row];
 //   3. resolve: every request reads rowmap[slot];
 //   4. (optional) init of the fresh rows: zeros / const / hash-uniform by id.
@@ -62,26 +62,49 @@ __global__ void __launch_bounds__(256) ht_find_insert_kernel(const int32_t* __re
   }
 }
 
-// fresh requests take compact rows; one atomicAdd per wave on the row counter
+// fresh requests take compact rows: one atomicAdd on the row counter per block
+// and tile of 256 x HT_AU requests (a block scan hands out the rows inside the
+// tile).  One atomic per wave serialised ~65k same-address atomics per 4M-key
+// call at the L2 (471 us, 3 % of HBM rate: profiles/r4_counters.md).
+constexpr int HT_AU = 8;
+
 __global__ void __launch_bounds__(256) ht_assign_kernel(const int32_t* __restrict__ keys, int64_t n,
                                                         const int32_t* __restrict__ slot,
                                                         const uint8_t* __restrict__ fresh,
                                                         int32_t* __restrict__ rowmap, int32_t* __restrict__ rowkey,
                                                         int32_t* __restrict__ count, int64_t rcap,
                                                         int32_t* __restrict__ overflow) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); w0 < n; w0 += stride) {
-    const int64_t b = w0 + lane;
-    const bool want = b < n && fresh[b];
-    const unsigned long long m = __ballot(want);
-    if (m == 0ull) continue;  // wave-uniform
-    const int leader = __ffsll((long long)m) - 1;
-    int32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (int32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (want) {
-      const int32_t row = base + (int32_t)__popcll(m & ((1ull << lane) - 1ull));
+  __shared__ int32_t s_wave[4];
+  __shared__ int32_t s_base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int TILE = 256 * HT_AU;
+  for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < n; t0 += (int64_t)gridDim.x * TILE) {  // block-uniform
+    uint32_t fm = 0;  // which of this thread's HT_AU requests are fresh (coalesced: stride 256)
+#pragma unroll
+    for (int j = 0; j < HT_AU; ++j) {
+      const int64_t b = t0 + j * 256 + threadIdx.x;
+      if (b < n && fresh[b]) fm |= 1u << j;
+    }
+    const int c = __popc(fm);
+    int x = c;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+      s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int32_t row = s_base + x - c;
+    for (int w = 0; w < wv; ++w) row += s_wave[w];
+#pragma unroll
+    for (int j = 0; j < HT_AU; ++j) {
+      if (!((fm >> j) & 1u)) continue;
+      const int64_t b = t0 + j * 256 + threadIdx.x;
       if (row < rcap) {
         rowmap[slot[b]] = row;
         rowkey[row] = keys[b];
@@ -89,7 +112,9 @@ __global__ void __launch_bounds__(256) ht_assign_kernel(const int32_t* __restric
         overflow[0] = 2;
         rowmap[slot[b]] = -1;
       }
+      ++row;
     }
+    __syncthreads();  // s_wave / s_base are rewritten by the next tile
   }
 }
 
@@ -164,7 +189,7 @@ FPS_API int fps_ht_lookup(const int32_t* keys, int64_t n, unsigned long long* ta
   hipLaunchKernelGGL(ht_find_insert_kernel, dim3(g), dim3(256), 0, s, keys, n, tab, (uint32_t)(cap - 1), insert,
                      slot_ws, fresh, overflow);
   if (insert)
-    hipLaunchKernelGGL(ht_assign_kernel, dim3(g), dim3(256), 0, s, keys, n, (const int32_t*)slot_ws,
+    hipLaunchKernelGGL(ht_assign_kernel, dim3(grid_for(n, 256 * HT_AU)), dim3(256), 0, s, keys, n, (const int32_t*)slot_ws,
                        (const uint8_t*)fresh, rowmap, rowkey, count, rcap, overflow);
   hipLaunchKernelGGL(ht_resolve_kernel, dim3(g), dim3(256), 0, s, (const int32_t*)slot_ws, n,
                      (const int32_t*)rowmap, row);

@@ -118,6 +118,86 @@ __global__ void __launch_bounds__(256) apply_rows_kernel(float* __restrict__ tab
   }
 }
 
+// 16-byte variants for fp32 rows with D % 4 == 0 (every table the apps build:
+// MF 64, SGNS 300, top-K 64+1 is excluded by the divisibility test).  A lane owns
+// NV float4 of its row (TPR lanes per row, D/4 <= TPR * NV) and issues all of its
+// loads before any store, so a wave has NV x 16 B in flight per lane instead of one
+// dependent 4-B load per loop trip (the scalar kernels above reached ~1.6 TB/s on
+// SGNS's 1200-B rows, profiles/r4_w2v_ps_path_kernel_stats.csv).
+typedef float to_f4 __attribute__((ext_vector_type(4)));
+
+template <int TPR, int NV, typename IDX>
+__global__ void __launch_bounds__(256) gather_rows_v4_kernel(const to_f4* __restrict__ table,
+                                                             const IDX* __restrict__ idx, int64_t n, int D4,
+                                                             to_f4* __restrict__ out, uint8_t* __restrict__ touched,
+                                                             float* __restrict__ flip) {
+  int64_t r, step; int j0;
+  row_coords<TPR>(r, step, j0);
+  for (; r < n; r += step) {
+    const int64_t row = (int64_t)idx[r];
+    const to_f4* src = table + row * D4;
+    to_f4 v[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int j = j0 + q * TPR;
+      if (j < D4) v[q] = src[j];  // hot rows (Zipf ids) are re-read: keep them cacheable
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int j = j0 + q * TPR;
+      if (j < D4) {
+        out[r * D4 + j] = v[q];
+        if (flip != nullptr) {
+          float* f = flip + (row * D4 + j) * 4;
+          if (__float_as_uint(v[q].x) == NEG0_BITS) f[0] = 0.f;
+          if (__float_as_uint(v[q].y) == NEG0_BITS) f[1] = 0.f;
+          if (__float_as_uint(v[q].z) == NEG0_BITS) f[2] = 0.f;
+          if (__float_as_uint(v[q].w) == NEG0_BITS) f[3] = 0.f;
+        }
+      }
+    }
+    if (touched != nullptr && j0 == 0) touched[row] = 1;
+  }
+}
+
+// op 1 (set) and op 4 (add, keys unique in the launch: plain read-modify-write)
+template <int TPR, int NV, int OP>
+__global__ void __launch_bounds__(256) apply_rows_v4_kernel(to_f4* __restrict__ table, const int32_t* __restrict__ idx,
+                                                            int64_t n, int D4, const to_f4* __restrict__ delta,
+                                                            uint8_t* __restrict__ touched) {
+  int64_t r, step; int j0;
+  row_coords<TPR>(r, step, j0);
+  for (; r < n; r += step) {
+    const int64_t row = (int64_t)idx[r];
+    if (row < 0) continue;  // padding slot
+    to_f4* dst = table + row * D4;
+    to_f4 g[NV], w[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int j = j0 + q * TPR;
+      if (j < D4) {
+        g[q] = __builtin_nontemporal_load(delta + r * D4 + j);
+        if (OP == 4) w[q] = dst[j];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int j = j0 + q * TPR;
+      if (j < D4) {
+        to_f4 o;
+        if (OP == 4) {
+          o.x = w[q].x + pos0(g[q].x); o.y = w[q].y + pos0(g[q].y);
+          o.z = w[q].z + pos0(g[q].z); o.w = w[q].w + pos0(g[q].w);
+        } else {
+          o.x = pos0(g[q].x); o.y = pos0(g[q].y); o.z = pos0(g[q].z); o.w = pos0(g[q].w);
+        }
+        dst[j] = o;
+      }
+    }
+    if (touched != nullptr && j0 == 0) touched[row] = 1;
+  }
+}
+
 // ---- de-duplication of request keys (one step, epoch-tagged map, no spins)
 // map[key] = epoch << 32 | (0xffffffff - owner_request_index); atomicMax makes
 // the newest epoch win and, inside it, the smallest request index.
@@ -572,11 +652,54 @@ FPS_API int fps_init_rows(float* table, int64_t n_rows, int D, int64_t id_base, 
   return 0;
 }
 
+// (TPR, NV) of the 16-byte kernels for D4 = D / 4 float4 per row; false: use the scalar kernels
+static inline bool v4_shape(int D, const void* a, const void* b, int& tpr, int& nv) {
+  if (D % 4 != 0 || ((uintptr_t)a & 15) || ((uintptr_t)b & 15)) return false;
+  const int D4 = D / 4;
+  if (D4 > 256) return false;
+  nv = D4 <= 64 ? 1 : D4 <= 128 ? 2 : 4;
+  tpr = 1;
+  while (tpr * nv < D4) tpr <<= 1;
+  return true;
+}
+
+#define V4_SWITCH(tpr, nv, ...)                                                                      \
+  do {                                                                                               \
+    if (nv == 1) {                                                                                   \
+      constexpr int NV = 1;                                                                          \
+      switch (tpr) {                                                                                 \
+        case 1: { constexpr int TPR = 1; __VA_ARGS__; } break;                                      \
+        case 2: { constexpr int TPR = 2; __VA_ARGS__; } break;                                      \
+        case 4: { constexpr int TPR = 4; __VA_ARGS__; } break;                                      \
+        case 8: { constexpr int TPR = 8; __VA_ARGS__; } break;                                      \
+        case 16: { constexpr int TPR = 16; __VA_ARGS__; } break;                                    \
+        case 32: { constexpr int TPR = 32; __VA_ARGS__; } break;                                    \
+        default: { constexpr int TPR = 64; __VA_ARGS__; }                                           \
+      }                                                                                              \
+    } else if (nv == 2) { constexpr int NV = 2, TPR = 64; __VA_ARGS__; }                             \
+    else { constexpr int NV = 4, TPR = 64; __VA_ARGS__; }                                            \
+  } while (0)
+
 FPS_API int fps_gather_rows(const float* table, const void* idx, int idx_is_64, int64_t n, int D, void* out,
                             int out_bf16, uint8_t* touched, int flip_sentinel, void* stream) {
   float* flip = flip_sentinel ? const_cast<float*>(table) : nullptr;
   if (n <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  int tpr, nv;
+  if (!out_bf16 && v4_shape(D, table, out, tpr, nv)) {
+    const int D4 = D / 4;
+    V4_SWITCH(tpr, nv, {
+      const int g = rows_grid(n, TPR);
+      if (idx_is_64)
+        hipLaunchKernelGGL((gather_rows_v4_kernel<TPR, NV, int64_t>), dim3(g), dim3(256), 0, s, (const to_f4*)table,
+                           (const int64_t*)idx, n, D4, (to_f4*)out, touched, flip);
+      else
+        hipLaunchKernelGGL((gather_rows_v4_kernel<TPR, NV, int32_t>), dim3(g), dim3(256), 0, s, (const to_f4*)table,
+                           (const int32_t*)idx, n, D4, (to_f4*)out, touched, flip);
+    });
+    FPS_CHECK_LAUNCH();
+    return 0;
+  }
   TPR_SWITCH(D, {
     const int g = rows_grid(n, TPR);
     if (idx_is_64) {
@@ -620,6 +743,22 @@ FPS_API int fps_apply_rows(float* table, float* state, const int32_t* idx, int64
                            int delta_bf16, int op, float lr, float eps, uint8_t* touched, void* stream) {
   if (n <= 0) return 0;
   if ((op == 3 || op == 5) && state == nullptr) return (int)hipErrorInvalidValue;
+  int tpr, nv;
+  if (!delta_bf16 && (op == 1 || op == 4) && v4_shape(D, table, delta, tpr, nv)) {
+    const int D4 = D / 4;
+    hipStream_t s = (hipStream_t)stream;
+    V4_SWITCH(tpr, nv, {
+      const int g = rows_grid(n, TPR);
+      if (op == 4)
+        hipLaunchKernelGGL((apply_rows_v4_kernel<TPR, NV, 4>), dim3(g), dim3(256), 0, s, (to_f4*)table, idx, n, D4,
+                           (const to_f4*)delta, touched);
+      else
+        hipLaunchKernelGGL((apply_rows_v4_kernel<TPR, NV, 1>), dim3(g), dim3(256), 0, s, (to_f4*)table, idx, n, D4,
+                           (const to_f4*)delta, touched);
+    });
+    FPS_CHECK_LAUNCH();
+    return 0;
+  }
   TPR_SWITCH(D, launch_apply<TPR>(table, state, idx, n, D, delta, delta_bf16, op, lr, eps, touched, (hipStream_t)stream));
   FPS_CHECK_LAUNCH();
   return 0;

@@ -34,6 +34,11 @@ from ... import ops
 
 
 class LempTopK:
+    #: items scored unfused first (their merge sets every query's k-th best)
+    seed_items = 4096
+    #: largest fused segment (segments double from ``seed_items``)
+    max_segment = 1 << 19
+
     def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536, strategy=None):
         """``strategy`` (a ``pruning`` LEMP strategy; None = LENGTH): the bounds the
         device scan applies per block of 32 items before scoring.  LENGTH (and LI /
@@ -57,11 +62,10 @@ class LempTopK:
         #: overflow flagged on the device, instead of two host syncs per segment
         self.fused = True
         self.sync_free = os.environ.get("FPS_TOPK_SYNC_SCAN", "0") != "1"
-        self.seed_items = 4096
         #: fused path: test "every query settled" on the host (one sync) only every
         #: ``break_check`` segments; the device tile bound skips settled work anyway
         self.break_check = int(os.environ.get("FPS_TOPK_BREAK_CHECK", "8"))
-        #: fused path: segments double from ``seed_items`` up to the bucket size
+        #: fused path: segments double from ``seed_items`` up to ``max_segment`` items
         self.geometric = True
         self.overflows = 0
         self._suffix = None  # False once rows were updated out of order
@@ -216,14 +220,22 @@ class LempTopK:
             self.buckets_scanned += 1
         if seed >= N:
             return best_s, best_i
-        # segments grow geometrically up to the bucket size: a segment of n items after
-        # s scanned ones passes ~k ln(1 + n / s) scores per query, so doubling keeps
-        # every merge on the small rank path (one 4096 -> 65536 step passed ~1100)
-        cuts = {seed, *(b for b in range(self.bucket, N, self.bucket) if b > seed)}
+        # segments grow geometrically: a segment of n items after s scanned ones passes
+        # ~k ln(1 + n / s) scores per query, so doubling keeps every merge on the small
+        # rank path (one 4096 -> 65536 step passed ~1100) at log2(N / seed) segments
+        # (8 for 1M items, against 19 when capped at 65536: 4 launches each).  LC keeps
+        # the bucket as the largest segment: it picks its bound per segment from the
+        # segment's length spread, the reference's per-bucket choice.
+        from .pruning import LC
+
+        cap_seg = self.bucket if isinstance(self.strategy, LC) else max(self.bucket, self.max_segment)
+        cuts = {seed}
         c = max(seed, self.seed_items) if self.geometric else N
-        while c < min(N, self.bucket):
+        if not self.geometric:
+            cuts |= {b for b in range(self.bucket, N, self.bucket) if b > seed}
+        while c < N:
             cuts.add(c)
-            c *= 2
+            c += min(c, cap_seg)
         bounds = sorted(cuts) + [N]
         cap = ops.TOPK_CAND_CAP
         ck = torch.empty((B, cap), dtype=torch.int32, device=dev)
@@ -240,8 +252,7 @@ class LempTopK:
             if self.break_check and j and j % self.break_check == 0 and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
-            if s % self.bucket == 0:
-                self.buckets_scanned += 1
+            self.buckets_scanned += len(range(-(-s // self.bucket) * self.bucket, e, self.bucket))
             cnt.zero_()
             if self.bf16:
                 seg_coord = None

@@ -18,8 +18,9 @@ def load(d):
 
 
 def main(root="gpurun_out/pmc", names="mftopk,w2v,mf"):
-    print("| run | kernel | time (s, pass 1) | MFMA busy | waves waiting | HBM read | HBM write | read+write rate |")
-    print("|---|---|---|---|---|---|---|---|")
+    print("| run | kernel | time (s, pass 1) | MFMA busy | waves waiting | LDS bank conflict / LDS active | HBM read | HBM write "
+          "| read+write rate | of 8 TB/s |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for name in names.split(","):
         a1, t1 = load(f"{root}/{name}_1")
         a2, t2 = load(f"{root}/{name}_2")
@@ -32,8 +33,10 @@ def main(root="gpurun_out/pmc", names="mftopk,w2v,mf"):
             rd = a2.get(k, {}).get("FETCH_SIZE", 0) * 1024
             wr = a3.get(k, {}).get("WRITE_SIZE", 0) * 1024
             rate = (rd / t2[k] if t2.get(k) else 0) + (wr / t3[k] if t3.get(k) else 0)
-            print(f"| {name} | `{k}` | {t1.get(k, 0):.4f} | {busy:.0%} | {wait:.0%} | {rd / 1e9:.2f} GB | {wr / 1e9:.2f} GB "
-                  f"| {rate / 1e12:.2f} TB/s |")
+            lds = c.get("SQ_LDS_IDX_ACTIVE", 0)
+            conf = f"{c.get('SQ_LDS_BANK_CONFLICT', 0) / lds:.1%}" if lds else "no LDS"
+            print(f"| {name} | `{k}` | {t1.get(k, 0):.4f} | {busy:.0%} | {wait:.0%} | {conf} | {rd / 1e9:.2f} GB "
+                  f"| {wr / 1e9:.2f} GB | {rate / 1e12:.2f} TB/s | {rate / 8e12:.0%} |")
 
 
 if __name__ == "__main__":

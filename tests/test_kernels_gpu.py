@@ -46,6 +46,37 @@ def test_apply_rows(op, D):
     torch.testing.assert_close(tab.cpu(), ref, rtol=1e-5, atol=1e-5)
 
 
+# 16-byte kernels (D % 4 == 0, aligned): NV = 1 at D <= 256, 2 at 300, 4 at 520;
+# D = 1028 and the misaligned view take the scalar kernels
+@pytest.mark.parametrize("D", [4, 64, 300, 520, 1028])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_gather_apply_v4_paths(D, misaligned):
+    g = torch.Generator(device=DEV).manual_seed(D)
+    base = torch.randn(3001 * D + 1, device=DEV, generator=g)
+    tab = (base[1:] if misaligned else base[:-1]).view(3001, D)
+    tab[::7] = -0.0  # sentinel rows: the gather flips served ones to +0.0
+    idx = torch.randint(0, 3001, (1111,), device=DEV, dtype=torch.int32, generator=g)
+    ref_tab = tab.clone()
+    touched = torch.zeros(3001, dtype=torch.uint8, device=DEV)
+    out = ops.gather_rows(tab, idx, touched=touched, flip=True)
+    assert torch.equal(out, ref_tab[idx.long()])
+    served = torch.zeros(3001, dtype=torch.bool, device=DEV)
+    served[idx.long()] = True
+    flipped = ref_tab.clone()
+    flipped[served] = flipped[served] + 0.0  # -0.0 + 0.0 = +0.0
+    assert torch.equal(tab.view(torch.int32), flipped.view(torch.int32))
+    assert torch.equal(touched.bool(), served)
+    uniq = torch.unique(idx)
+    for op in ("add_unique", "set"):
+        delta = torch.randn(uniq.numel(), D, device=DEV, generator=g)
+        delta[::5] = -0.0
+        ref = tab.cpu().clone()
+        R.apply_rows(ref, uniq.cpu(), delta.cpu(), "add" if op == "add_unique" else "set")
+        ops.apply_rows(tab, uniq, delta, op)
+        assert torch.equal(tab.cpu(), ref)
+        assert not torch.signbit(tab[uniq.long()][tab[uniq.long()] == 0]).any()  # -0.0 deltas leave +0.0
+
+
 def test_apply_adagrad_bf16_delta():
     D = 64
     tab = torch.randn(200, D, device=DEV)
