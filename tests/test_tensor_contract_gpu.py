@@ -57,6 +57,8 @@ def test_hash_table_kernel_matches_cpu_semantics():
         assert bool((r >= 0).all())
         assert torch.equal(t.rowkey.cpu()[r].long(), keys)  # every request maps to its own key's row
         assert int(f.sum()) == torch.unique(keys).numel()   # exactly one inserter per key
+        assert int(t.count) == torch.unique(keys).numel()   # rows are compact: [0, count) all used
+        assert torch.unique(r).numel() == int(t.count)
         assert t.stats()["overflow"] == 0 and t.stats()["load_factor"] <= 0.5
         assert t.grow_events > 0
     # the same id gets the same init values on both devices (hash RNG by id)
