@@ -192,8 +192,25 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
         for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)((i0 + 32) / 32) * D + fq[b]];
       }
     }
-    // the filter of one (32-query block, item block) pair on its accumulator
-    auto filter = [&](const int b, const floatx16& acc) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
+        const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
+        const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
+        if (!__any(pass)) {  // wave-uniform
+          // counted only when the length bound alone would have scored the pair: the
+          // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
+          // adds over LENGTH, not what the length bound skips anyway
+          if (__any(lpass)) ++skipped;
+          continue;
+        }
+        ++scored;
+      }
+      floatx16 acc = {0};
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
+                                                      __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
       const float thr = theta[b] - margin * ql[b] * bm;
       float m = acc[0];
 #pragma unroll
@@ -233,58 +250,6 @@ __global__ void __launch_bounds__(256) score_filter_bf16_kernel(
           }
         }
       }
-    };
-    if constexpr (COORD) {
-      // one pair at a time: bounds, MFMA chain, filter (the coordinate bound's
-      // registers leave no room for QB live accumulators at 2 waves / SIMD)
-#pragma unroll
-      for (int b = 0; b < QB; ++b) {
-        const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
-        if (use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
-          const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
-          if (!__any(pass)) {  // wave-uniform
-            // counted only when the length bound alone would have scored the pair: the
-            // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
-            // adds over LENGTH, not what the length bound skips anyway
-            if (__any(lpass)) ++skipped;
-            continue;
-          }
-          ++scored;
-        } else if (!__any(lpass)) {
-          continue;
-        }
-        floatx16 acc = {0};
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
-                                                        __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
-        filter(b, acc);
-      }
-    } else {
-      // LEMP length bound per pair (the workgroup test above covers 1024 items x 512
-      // queries), then the MFMA chains of the QB blocks interleaved (independent
-      // accumulators: the matrix core takes the next chain's MFMA while the previous
-      // result drains), then the filters
-      bool run[QB];
-      bool any_run = false;
-#pragma unroll
-      for (int b = 0; b < QB; ++b) {
-        run[b] = __any(qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]));
-        any_run |= run[b];
-      }
-      if (!any_run) continue;  // wave-uniform
-      floatx16 acc[QB];
-#pragma unroll
-      for (int b = 0; b < QB; ++b) acc[b] = floatx16{0};
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-#pragma unroll
-        for (int b = 0; b < QB; ++b)
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
-                                                           __builtin_bit_cast(bf16x8, qv[b][s]), acc[b], 0, 0, 0);
-#pragma unroll
-      for (int b = 0; b < QB; ++b)
-        if (run[b]) filter(b, acc[b]);
     }
   }
   if (COORD && use_coord && stats != nullptr && lane == 0) {

@@ -94,6 +94,11 @@ class LempTopK:
         #: bound inside a scan; the grouping and the per-segment launches stayed.)
         self.coord_off_batches = 0
         self.coord_batches = {"on": 0, "off": 0}
+        #: GPU: fresh LENGTH scans replay one hipGraph per (batch size, k) (``_query_graph``);
+        #: FPS_TOPK_GRAPH=0 keeps every scan eager
+        self.graphs = vecs.is_cuda and os.environ.get("FPS_TOPK_GRAPH", "1") != "0"
+        self._graph: dict = {}
+        self._graph_seen: dict = {}
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -145,6 +150,8 @@ class LempTopK:
                     inv = torch.empty_like(perm)
                     inv[perm] = torch.arange(perm.numel(), device=perm.device)
                     res = (res[0][inv], res[1][inv])
+            elif st is None and start == 0 and self.graphs and not self._coord_active() and not ops.DEBUG:
+                res = self._query_graph(Q, qlen, k)
             else:
                 res = self._query_fused(Q, qlen, k, start, st)
             if res is not None:
@@ -196,7 +203,80 @@ class LempTopK:
                 best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
         return best_s, best_i
 
+    def _query_graph(self, Q: torch.Tensor, qlen: torch.Tensor, k: int):
+        """The fused scan of a fresh query batch as one hipGraph replay: the seed
+        segment, every segment's zero / filter / re-score / merge chain and the norms
+        (~35 launches at 1M items) from one host call -- the scan's launches had been
+        issued at ~10 us of host time each (MF + top-K at 4096 queries per batch was
+        host-bound, ``profiles/r4_mf_topk_kernel_stats.csv``).  One graph per (batch
+        size, k), captured on the second batch of that shape (the first runs eagerly);
+        the graph reads the index tensors in place, so ``update_rows`` stays visible
+        and a rebuilt index (a new object) captures its own.  The COORD scans (query
+        grouping, gate, per-batch switch) and continued scans run eagerly."""
+        key = (Q.shape[0], int(k))
+        g = self._graph.get(key)
+        if g is None:
+            seen = self._graph_seen.get(key, 0)
+            self._graph_seen[key] = seen + 1
+            if seen == 0:  # warm-up: eager (lazy allocations, first launches)
+                return self._query_fused(Q, qlen, k)
+            g = self._capture(Q, k)
+            if g is None:
+                return self._query_fused(Q, qlen, k)
+        graph, q_in, best_s, best_i, ovf, scanned = g
+        q_in.copy_(Q)
+        graph.replay()
+        self.buckets_scanned += scanned
+        if int(ovf.item()):  # the scan's one sync, as the eager path's
+            return None
+        # the graph's buffers are rewritten by the next replay: hand out copies
+        return best_s.clone(), best_i.clone()
+
+    def _capture(self, Q: torch.Tensor, k: int):
+        import gc
+
+        q_in = torch.empty_like(Q)
+        q_in.copy_(Q)
+        graph = torch.cuda.CUDAGraph()
+        b0 = self.buckets_scanned
+        enabled = gc.isenabled()
+        gc.disable()  # a collection on this thread inside the capture could free a pinned buffer / event
+        try:
+            with torch.cuda.graph(graph):
+                best_s, best_i, ovf = self._scan(q_in, torch.linalg.vector_norm(q_in, dim=1), k, capturing=True)[:3]
+        except RuntimeError as e:  # a launch that cannot be captured: stay eager for this index
+            import warnings
+
+            warnings.warn(f"LempTopK: scan capture failed ({e}); eager scans")
+            self.graphs = False
+            return None
+        finally:
+            if enabled:
+                gc.enable()
+        scanned = self.buckets_scanned - b0
+        self.buckets_scanned = b0
+        g = (graph, q_in, best_s, best_i, ovf, scanned)
+        self._graph[(Q.shape[0], int(k))] = g
+        return g
+
     def _query_fused(self, Q, qlen, k, start: int = 0, state=None):
+        """The fused scan (``_scan``) and its one host sync: the overflow flag (-> None:
+        the caller rescans) and, with COORD, this batch's skip rate for the per-batch
+        switch."""
+        best_s, best_i, ovf, stats0 = self._scan(Q, qlen, k, start, state)
+        if stats0 is not None:  # one sync: overflow flag + this batch's COORD block pairs
+            o, scored, skipped = torch.cat([ovf, self.coord_stats - stats0]).tolist()
+            if scored + skipped and skipped < self.COORD_MIN_SKIP * (scored + skipped):
+                self.coord_off_batches = self.COORD_REPROBE
+        elif ovf is not None:
+            o = int(ovf.item())
+        else:
+            o = 0
+        if o:
+            return None
+        return best_s, best_i
+
+    def _scan(self, Q, qlen, k, start: int = 0, state=None, capturing: bool = False):
         """GPU scan without a host sync per segment: seed segment scored + merged,
         then per segment the fused 128 x 128 scorer (tiles that cannot beat any of
         their queries' k-th best skip themselves) and the candidate merge, which
@@ -219,7 +299,7 @@ class LempTopK:
             del S
             self.buckets_scanned += 1
         if seed >= N:
-            return best_s, best_i
+            return best_s, best_i, None, None
         # segments grow geometrically: a segment of n items after s scanned ones passes
         # ~k ln(1 + n / s) scores per query, so doubling keeps every merge on the small
         # rank path (one 4096 -> 65536 step passed ~1100) at log2(N / seed) segments
@@ -249,7 +329,7 @@ class LempTopK:
             self._coord_prev.copy_(self.coord_stats)
             stats0 = self.coord_stats.clone()
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
-            if self.break_check and j and j % self.break_check == 0 and \
+            if self.break_check and j and j % self.break_check == 0 and not capturing and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
             self.buckets_scanned += len(range(-(-s // self.bucket) * self.bucket, e, self.bucket))
@@ -271,15 +351,7 @@ class LempTopK:
                 ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen,
                                       self.lengths[s:e])
             ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf)
-        if coord is not None:  # one sync: overflow flag + this batch's COORD block pairs
-            o, scored, skipped = torch.cat([ovf, self.coord_stats - stats0]).tolist()
-            if scored + skipped and skipped < self.COORD_MIN_SKIP * (scored + skipped):
-                self.coord_off_batches = self.COORD_REPROBE
-        else:
-            o = int(ovf.item())
-        if o:
-            return None
-        return best_s, best_i
+        return best_s, best_i, ovf, (stats0 if coord is not None else None)
 
     #: COORD self-disable (see ``coord_off_batches``)
     COORD_MIN_SKIP = 0.25

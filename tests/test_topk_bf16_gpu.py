@@ -142,6 +142,39 @@ def test_lemp_topk_bf16_incremental_update():
 
 
 
+def test_lemp_topk_graph_replay_equals_eager_scan():
+    """The hipGraph scan (``LempTopK._query_graph``: eager first batch, capture on
+    the second, replays after) returns the eager scan's results bit for bit, sees
+    ``update_rows`` between replays, and hands out copies (a result survives the
+    next replay)."""
+    g = torch.Generator().manual_seed(12)
+    n, D, B, k = 200000, 64, 300, 75
+    X = (torch.randn(n, D, generator=g) * torch.rand(n, 1, generator=g)).cuda()
+    ids = torch.arange(n, device="cuda") * 3 + 1
+    gr = LempTopK(ids, X.clone(), bucket_size=65536)
+    ea = LempTopK(ids, X.clone(), bucket_size=65536)
+    ea.graphs = False
+    assert gr.graphs
+    kept = []
+    for step in range(5):
+        Q = torch.randn(B, D, generator=g).cuda()
+        s1, i1 = gr.query(Q, k)
+        s0, i0 = ea.query(Q, k)
+        assert torch.equal(s1, s0) and torch.equal(i1, i0), step
+        kept.append((s1, s0))
+        if step == 2:  # in-place index update between replays
+            pos = torch.randperm(n, generator=g)[:20000].cuda()
+            new = torch.randn(20000, D, generator=g).cuda() * 2.0
+            gr.update_rows(pos, new)
+            ea.update_rows(pos, new)
+    assert (B, k) in gr._graph  # captured and replayed
+    for s1, s0 in kept:  # earlier results were not overwritten by later replays
+        assert torch.equal(s1, s0)
+    assert gr.buckets_scanned == ea.buckets_scanned
+    bs, _ = torch.topk(Q @ ea.vecs.T, k, dim=1)
+    torch.testing.assert_close(s1, bs, rtol=1e-5, atol=1e-4)
+
+
 def test_bf16_filter_tight_margin_worst_case():
     """Parallel rows of elements just below a bf16 rounding midpoint: bf16 rounds every
     element down by ~2^-8, so S_bf16 sits ~2^-7 |q||x| under the exact score -- the margin's
