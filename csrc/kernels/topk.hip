@@ -304,6 +304,99 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* 
   sort_keep_k(skey, sid, nc, best_s + (int64_t)row * k, best_i + (int64_t)row * k, k);
 }
 
+
+// ---- seen-aware merge of gathered partial top-K lists (CollectTopKFromEachWorker,
+// M/matrix/factorization/utils/CollectTopKFromEachWorker.scala:30-59) for the dense
+// ring seen store (models/mf/topk_tensor.py SeenStore): one workgroup per batch
+// entry.  Entry e of user u is the r-th occurrence of u in the batch; it must not
+// recommend the items of u's window as it stands after u's r earlier entries of
+// this batch added their rated items (the reference's per-record order).  The
+// window is rebuilt in LDS -- the ring row as of the batch start with the r earlier
+// items written over its slots (c + j) % M -- so all rounds merge in ONE launch
+// (the torch loop over rounds was ~55 small launches per round).  Kept candidates
+// (id >= 0, finite score, not in the window) are sorted key desc / id asc (the
+// merge kernels' order) and the first K written; rows with fewer than K end in
+// -inf / -1.  ring_cur[u] as of the batch start goes to cpre[e] for the update.
+__global__ void __launch_bounds__(TK_NT) seen_merge_kernel(
+    const float* __restrict__ ss, const int64_t* __restrict__ ii, int m, int K, const int64_t* __restrict__ users,
+    const int64_t* __restrict__ items, const int32_t* __restrict__ rnd, const int32_t* __restrict__ first,
+    const int64_t* __restrict__ by_user, const int32_t* __restrict__ ring, const int64_t* __restrict__ ring_cur,
+    int M, int64_t* __restrict__ cpre, float* __restrict__ best_s, int64_t* __restrict__ best_i) {
+  __shared__ int32_t win[TK_MAXK];
+  __shared__ uint32_t skey[TK_SORT];
+  __shared__ int64_t sid[TK_SORT];
+  __shared__ uint32_t cnt;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  const int64_t u = users[e];
+  const int64_t c = ring_cur[u];
+  const int r = rnd[e], p0 = first[e];
+  if (tid == 0) {
+    cnt = 0u;
+    cpre[e] = c;
+  }
+  for (int q = tid; q < M; q += TK_NT) win[q] = ring[u * M + q];
+  __syncthreads();
+  // the earlier entries' items; only the last M of them survive in the window (distinct slots)
+  for (int j = tid; j < r; j += TK_NT)
+    if (j >= r - M) win[(int)((c + j) % M)] = (int32_t)items[by_user[p0 + j]];
+  __syncthreads();
+  for (int t = tid; t < m; t += TK_NT) {
+    const int64_t id = ii[(int64_t)e * m + t];
+    const float sc = ss[(int64_t)e * m + t];
+    bool keep = id >= 0 && isfinite(sc);
+    if (keep)
+      for (int q = 0; q < M; ++q)
+        if (win[q] == (int32_t)id) { keep = false; break; }
+    if (keep) {
+      const uint32_t slot = atomicAdd(&cnt, 1u);
+      skey[slot] = fkey(sc);
+      sid[slot] = id;
+    }
+  }
+  __syncthreads();
+  const int nc = (int)cnt;
+  int P = 1;
+  while (P < nc || P < K) P <<= 1;
+  for (int i = nc + tid; i < P; i += TK_NT) { skey[i] = 0u; sid[i] = INT64_MAX; }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P; i += TK_NT) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const uint32_t ki = skey[i], kj = skey[j];
+          const int64_t xi = sid[i], xj = sid[j];
+          const bool i_first = ki > kj || (ki == kj && xi < xj);
+          if (desc != i_first) { skey[i] = kj; skey[j] = ki; sid[i] = xj; sid[j] = xi; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < K; i += TK_NT) {
+    const uint32_t kk = skey[i];
+    best_s[(int64_t)e * K + i] = kk ? kfloat(kk) : -INFINITY;
+    best_i[(int64_t)e * K + i] = kk ? sid[i] : -1;
+  }
+}
+
+// the batch's rated items into the ring, after every merge read it: entry e (round r
+// of nu[e] entries of its user) writes slot (c + r) % M if it is among the user's
+// last M entries; the user's last entry advances the cursor
+__global__ void seen_ring_update_kernel(int B, const int64_t* __restrict__ users, const int64_t* __restrict__ items,
+                                        const int32_t* __restrict__ rnd, const int32_t* __restrict__ nu,
+                                        const int64_t* __restrict__ cpre, int32_t* __restrict__ ring,
+                                        int64_t* __restrict__ ring_cur, int M) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B) return;
+  const int64_t u = users[e];
+  const int r = rnd[e], n = nu[e];
+  const int64_t c = cpre[e];
+  if (r >= n - M) ring[u * M + (int)((c + r) % M)] = (int32_t)items[e];
+  if (r == n - 1) ring_cur[u] = c + n;
+}
+
 }  // namespace
 
 // best_s / best_i: [B, k] sorted descending (start: -inf / -1); S: [B, n] with row stride ldS
@@ -328,6 +421,26 @@ FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id
   FPS_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
                      best_s, best_i, k);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ss / ii [B, m] gathered partials (m <= TK_CAP), users / items [B] (int64), rnd / first /
+// nu [B] int32 (occurrence round, position of the user's first entry in by_user, the
+// user's entry count), by_user [B] (entries stably sorted by user), ring [U, M] int32
+// (M <= TK_MAXK), ring_cur [U] int64; cpre [B] int64 scratch.  best_s / best_i [B, K].
+FPS_API int fps_topk_seen_merge(const float* ss, const int64_t* ii, int B, int m, int K, const int64_t* users,
+                                const int64_t* items, const int32_t* rnd, const int32_t* first, const int32_t* nu,
+                                const int64_t* by_user, int32_t* ring, int64_t* ring_cur, int M, int64_t* cpre,
+                                float* best_s, int64_t* best_i, void* stream) {
+  if (B <= 0) return 0;
+  if (K <= 0 || K > TK_MAXK || m < 0 || m > TK_CAP || M <= 0 || M > TK_MAXK) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(seen_merge_kernel, dim3(B), dim3(TK_NT), 0, s, ss, ii, m, K, users, items, rnd, first, by_user,
+                     (const int32_t*)ring, (const int64_t*)ring_cur, M, cpre, best_s, best_i);
+  FPS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(seen_ring_update_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, users, items, rnd, nu,
+                     (const int64_t*)cpre, ring, ring_cur, M);
   FPS_CHECK_LAUNCH();
   return 0;
 }

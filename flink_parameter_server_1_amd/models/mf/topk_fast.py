@@ -98,7 +98,6 @@ class LempTopK:
         #: FPS_TOPK_GRAPH=0 keeps every scan eager
         self.graphs = vecs.is_cuda and os.environ.get("FPS_TOPK_GRAPH", "1") != "0"
         self._graph: dict = {}
-        self._graph_seen: dict = {}
 
     def update_rows(self, pos: torch.Tensor, vecs: torch.Tensor) -> None:
         """Rewrite the items at index positions ``pos`` (distinct, or repeated with equal
@@ -111,6 +110,19 @@ class LempTopK:
         self.lengths[pos] = torch.linalg.vector_norm(v, dim=1)
         self._suffix = False  # the order is stale: bounds take the max of the tail
         self._cb = self._len_host = None
+
+    def refresh_from(self, rows: torch.Tensor, pos: torch.Tensor, table: torch.Tensor) -> None:
+        """``update_rows`` from a table: the current ``table[rows]`` go to index positions
+        ``pos[row]`` (rows with ``pos < 0`` are not indexed and skipped).  One kernel on the
+        GPU (``ops.index_refresh``) instead of the gather / mask / scatter chain."""
+        if self.vecs.is_cuda:
+            ops.index_refresh(rows, pos, table, self.vecs, self.vecs_bf, self.lengths)
+            self._suffix = False
+            self._cb = self._len_host = None
+            return
+        p = pos[rows]
+        ok = p >= 0
+        self.update_rows(p[ok], table[rows[ok]])
 
     def _bound(self, s: int) -> torch.Tensor:
         """max |x| over index positions >= s (a 0-dim tensor)."""
@@ -209,20 +221,18 @@ class LempTopK:
         (~35 launches at 1M items) from one host call -- the scan's launches had been
         issued at ~10 us of host time each (MF + top-K at 4096 queries per batch was
         host-bound, ``profiles/r4_mf_topk_kernel_stats.csv``).  One graph per (batch
-        size, k), captured on the second batch of that shape (the first runs eagerly);
+        size, k), captured after the first batch of that shape (which runs eagerly);
         the graph reads the index tensors in place, so ``update_rows`` stays visible
         and a rebuilt index (a new object) captures its own.  The COORD scans (query
         grouping, gate, per-batch switch) and continued scans run eagerly."""
         key = (Q.shape[0], int(k))
         g = self._graph.get(key)
         if g is None:
-            seen = self._graph_seen.get(key, 0)
-            self._graph_seen[key] = seen + 1
-            if seen == 0:  # warm-up: eager (lazy allocations, first launches)
-                return self._query_fused(Q, qlen, k)
-            g = self._capture(Q, k)
-            if g is None:
-                return self._query_fused(Q, qlen, k)
+            # this batch runs eagerly (it also warms the launches up); the capture that
+            # follows executes nothing, so the next batch of this shape replays
+            res = self._query_fused(Q, qlen, k)
+            self._capture(Q, k)
+            return res
         graph, q_in, best_s, best_i, ovf, scanned = g
         q_in.copy_(Q)
         graph.replay()

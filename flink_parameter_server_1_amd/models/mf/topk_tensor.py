@@ -175,9 +175,32 @@ class RoundPlan:
     device->host sync -- the same trick as the PS count exchange
     (``parallel.tensor_ps``)."""
 
-    def __init__(self, users: torch.Tensor):
-        rnd = occurrence_rounds(users)
+    def __init__(self, users: torch.Tensor, fused: bool = False):
+        """``fused``: plan for the one-launch merge (``ops.topk_seen_merge``): per entry
+        its round, its user's entry count and the position of the user's first entry in
+        the user-sorted order -- no rounds, no host copy."""
         B = users.numel()
+        self.fused = fused
+        if fused:
+            by_user = torch.argsort(users, stable=True)
+            su = users[by_user]
+            start = torch.ones(B, dtype=torch.bool, device=users.device)
+            if B > 1:
+                start[1:] = su[1:] != su[:-1]
+            idx = torch.arange(B, device=users.device)
+            run_start = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
+            run_id = torch.cumsum(start, 0) - 1
+            run_len = torch.zeros(B, dtype=torch.int32, device=users.device)
+            run_len.index_add_(0, run_id, torch.ones(B, dtype=torch.int32, device=users.device))
+            self.by_user = by_user
+            self.rnd = torch.empty(B, dtype=torch.int32, device=users.device)
+            self.rnd[by_user] = (idx - run_start).to(torch.int32)
+            self.first = torch.empty(B, dtype=torch.int32, device=users.device)
+            self.first[by_user] = run_start.to(torch.int32)
+            self.nu = torch.empty(B, dtype=torch.int32, device=users.device)
+            self.nu[by_user] = run_len[run_id]
+            return
+        rnd = occurrence_rounds(users)
         self.order = torch.argsort(rnd, stable=True)
         cnt = torch.zeros(B + 1, dtype=torch.int32, device=users.device)
         cnt.index_add_(0, rnd, torch.ones_like(rnd, dtype=torch.int32))
@@ -396,6 +419,15 @@ def as_reference_records(outputs) -> List[tuple]:
 class _TopKServing:
     """Shared query path: partial LEMP top-K on the local items, gather, seen-aware merge."""
 
+    def _fused_merge(self, ss: Optional[torch.Tensor] = None) -> bool:
+        """The one-launch merge applies: dense ring seen store on the GPU, lists and K
+        within the kernel's LDS capacity."""
+        seen = getattr(self, "seen", None)
+        if not getattr(self, "fused", True) or seen is None or seen.ring is None or not seen.ring.is_cuda or self.K > ops.TOPK_MAX_K \
+                or seen.memory > ops.TOPK_MAX_K:
+            return False
+        return ss is None or ss.shape[1] <= ops.TOPK_CAND_CAP
+
     def _serve(self, Q, valid, users, items, ts, ps, plan: Optional[RoundPlan] = None):
         with stage("topk.score", None):
             if self.index is not None and self.index.vecs.shape[0] > 0:
@@ -407,7 +439,15 @@ class _TopKServing:
             i = torch.where(valid.view(-1, 1), i, torch.full_like(i, -1))
         with stage("topk.merge", None):
             ss, ii = _gather_partials(self.comm, s, i)
-            plan = plan if plan is not None else RoundPlan(users)
+            if plan is not None and plan.fused and self._fused_merge(ss):
+                # every round in one launch + the ring update (topk.hip seen_merge_kernel)
+                best_s, best_i = ops.topk_seen_merge(ss.contiguous(), ii.long().contiguous(), self.K, users.long(),
+                                                     items.long(), plan.rnd, plan.first, plan.nu, plan.by_user,
+                                                     self.seen.ring, self.seen.ring_cur)
+                if self.rank == 0:
+                    ps.output(((users, items, ts), best_s, best_i))
+                return
+            plan = plan if plan is not None and not plan.fused else RoundPlan(users)
             best_s = torch.empty((users.numel(), self.K), device=Q.device)
             best_i = torch.empty((users.numel(), self.K), dtype=torch.long, device=Q.device)
             for a, n in plan.rounds():  # a user's later entries see its earlier ones as seen
@@ -454,7 +494,7 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
 
     def on_recv_batch(self, batch, ps):
         users, items, ts = (t.to(self.device) for t in batch)
-        ps.pull(users, (users, items, ts, RoundPlan(users)))
+        ps.pull(users, (users, items, ts, RoundPlan(users, fused=self._fused_merge())))
 
     def on_pull_recv_batch(self, pulled, ps):
         users, items, ts, plan = pulled.payload
@@ -511,6 +551,9 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self.range, self.seed, self.neg_memory = (range_min, range_max), seed, int(neg_memory)
         self.prefill_items, self.num_users, self.resort_every = prefill_items, num_users, int(resort_every)
         self.served = 0
+        #: GPU: one-launch seen-aware merge and one launch per SGD phase (``mf_online.hip``);
+        #: False keeps the torch chains (the A/B and parity reference)
+        self.fused = True
         self._trained = None  # device counter of SGD updates on this rank (ratings + drawn negatives)
         self.rebuilds = 0
 
@@ -543,7 +586,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
 
     def on_recv_batch(self, batch, ps):
         users, items, ts, rating = (t.to(self.device) for t in batch)
-        ps.pull(users, (users, items, ts, rating.float(), RoundPlan(users)))
+        ps.pull(users, (users, items, ts, rating.float(), RoundPlan(users, fused=self._fused_merge())))
 
     @property
     def trained(self) -> int:
@@ -572,6 +615,9 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         if self.pruning is not None or self._since_sort >= self.resort_every:
             self._stale = True  # LEMP strategies read the sorted order: rebuild instead
             return
+        if rows.is_cuda:
+            self.index.refresh_from(rows.long(), self._pos, self.items.weight)
+            return
         p = self._pos[rows]
         ok = p >= 0
         rows = torch.where(ok, rows, self._index_rows[0])
@@ -599,6 +645,10 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         lr = self.lr
         W_ = self.items.weight
         touched = [loc]
+        if self.fused and U.is_cuda and W_.dtype == torch.float32 and self.dim <= 256:
+            self._learn_fused(U, users, items, rating, own, loc, du)
+            ps.push(du, mask=own)
+            return
         if self.neg_rate > 0:
             rows_own = torch.arange(users.numel(), device=U.device) if self.W == 1 else torch.nonzero(own).flatten()
             ou, oi = users[rows_own].to(torch.int32), items[rows_own].to(torch.int32)
@@ -629,6 +679,36 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self._refresh_index(torch.cat(touched))
         self._trained += own.sum()
         ps.push(du, mask=own)
+
+
+    def _learn_fused(self, U, users, items, rating, own, loc, du):
+        """The learning side on the GPU: one ``mf_online_phase`` launch per negative
+        and one for the ratings (the torch chain's batch semantics: a phase reads the
+        item rows as the previous phases left them), then one index refresh."""
+        W_ = self.items.weight
+        U = U.float().contiguous()
+        touched = [loc]
+        if self.neg_rate > 0:
+            rows_own = None if self.W == 1 else torch.nonzero(own).flatten()
+            ou = users if rows_own is None else users[rows_own]
+            oi = items if rows_own is None else items[rows_own]
+            ou, oi = ou.to(torch.int32), oi.to(torch.int32)
+            uring = (ou.long() % self._ring_users).to(torch.int32)
+            ops.ring_push(self._ring, self._ring_cur, uring, oi, self.neg_memory)
+            ops.known_append(self._known_flag, self._known, self._known_cnt, oi)
+            negs = ops.sample_uniform_reject(ou.numel(), self.neg_rate, self.num_items, oi, uring, self._ring,
+                                             self.neg_memory, seed=self.seed + 7 * self.rank,
+                                             counter=self._neg_counter, device=self.device, known=self._known,
+                                             known_count=self._known_cnt).view(-1, self.neg_rate).long()
+            self._neg_counter += 1
+            nl = torch.where(negs >= 0, negs // self.W, torch.full_like(negs, -1))  # [n_own, neg_rate]
+            nlt = nl.t().contiguous()  # phase-major
+            for j in range(self.neg_rate):  # reference order: negatives first, then the rating
+                ops.mf_online_phase(U, rows_own, nlt[j], None, self.lr, W_, du, self._trained)
+            touched.append(nlt.view(-1))
+        irow = torch.where(own, loc, torch.full_like(loc, -1))
+        ops.mf_online_phase(U, None, irow, rating, self.lr, W_, du, self._trained)
+        self._refresh_index(torch.cat(touched))
 
 
 def ps_online_learner_and_generator_tensor(batches: Iterable, num_users: int, num_items: int, num_factors: int = 10,

@@ -982,6 +982,79 @@ def topk_merge_cand(cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Te
                                             N.stream_ptr(best_s.device)), "topk_merge_cand")
 
 
+def mf_online_phase(U: torch.Tensor, urow: Optional[torch.Tensor], irow: torch.Tensor,
+                    target: Optional[torch.Tensor], lr: float, W: torch.Tensor, du: torch.Tensor,
+                    trained: Optional[torch.Tensor] = None) -> None:
+    """One SGD phase of the online MF + top-K worker (``mf_online.hip``, GPU only): for
+    every entry t with ``irow[t] >= 0``: ``e = target[t] - <U[urow[t]], W[irow[t]]>``
+    (target 0 when None: a negative), ``du[urow[t]] += lr e W[irow[t]]`` (distinct rows),
+    ``W[irow[t]] += lr e U[urow[t]]`` (atomics); ``urow`` None = identity.  ``trained``
+    (int64 scalar, optional) counts the applied entries."""
+    n, D = irow.numel(), U.shape[1]
+    if not (U.is_cuda and U.dtype == W.dtype == du.dtype == torch.float32 and W.shape[1] == D == du.shape[1]):
+        raise ValueError("mf_online_phase: cuda fp32 U / W / du with one D")
+    if irow.dtype != torch.int64 or (urow is not None and (urow.dtype != torch.int64 or urow.numel() != n)) \
+            or (target is not None and target.numel() != n) or D > 256:
+        raise ValueError("mf_online_phase: int64 irow / urow [n], target [n], D <= 256")
+    if DEBUG:
+        check_index(irow, W.shape[0], "mf_online_phase irow", allow_negative=True)
+    N.check(N.require().fps_mf_online_phase(_c(U).data_ptr(), N.ptr(None if urow is None else _c(urow)),
+                                            _c(irow).data_ptr(),
+                                            N.ptr(None if target is None else _c(target.float())), n, D, float(lr),
+                                            W.data_ptr(), du.data_ptr(), N.ptr(trained), N.stream_ptr(U.device)),
+            "mf_online_phase")
+
+
+def index_refresh(rows: torch.Tensor, pos: torch.Tensor, W: torch.Tensor, vecs: torch.Tensor,
+                  vecs_bf: Optional[torch.Tensor], lengths: torch.Tensor) -> None:
+    """Copy the local item rows ``W[rows]`` into a LEMP index at positions ``pos[row]``
+    (``< 0``: not indexed): fp32 vectors, the bf16 shadow (RNE, as ``.bfloat16()``) and
+    the lengths (``mf_online.hip``, GPU only)."""
+    D = W.shape[1]
+    if not (W.is_cuda and rows.dtype == pos.dtype == torch.int64 and vecs.shape[1] == D and D <= 256):
+        raise ValueError("index_refresh: cuda, int64 rows / pos, D <= 256")
+    if vecs_bf is not None and (vecs_bf.dtype != torch.bfloat16 or vecs_bf.shape != vecs.shape):
+        raise ValueError("index_refresh: bf16 shadow of vecs' shape")
+    N.check(N.require().fps_index_refresh(_c(rows).data_ptr(), rows.numel(), _c(pos).data_ptr(), _c(W).data_ptr(), D,
+                                          vecs.data_ptr(), N.ptr(vecs_bf), lengths.data_ptr(),
+                                          N.stream_ptr(W.device)), "index_refresh")
+
+
+def topk_seen_merge(ss: torch.Tensor, ii: torch.Tensor, K: int, users: torch.Tensor, items: torch.Tensor,
+                    rnd: torch.Tensor, first: torch.Tensor, nu: torch.Tensor, by_user: torch.Tensor,
+                    ring: torch.Tensor, ring_cur: torch.Tensor):
+    """Seen-aware merge of gathered partial top-K lists for a whole micro-batch, all
+    occurrence rounds at once (GPU only, K13; ``topk.hip`` ``seen_merge_kernel``), then
+    the batch's rated items into the ring store.  ``ss`` / ``ii`` ``[B, m]`` partial
+    scores / item ids; entry ``e`` of user ``users[e]`` is its user's ``rnd[e]``-th in the
+    batch, the user's entries are ``by_user[first[e] : first[e] + nu[e]]`` (stable);
+    ``ring`` ``[U, M]`` int32 / ``ring_cur`` ``[U]`` int64 the dense seen store (updated).
+    Returns ``best_s`` / ``best_i`` ``[B, K]`` (key desc, ties by smaller id; -inf / -1 past
+    the kept candidates)."""
+    B, m = ss.shape
+    M = ring.shape[1]
+    if not (ss.is_cuda and ss.dtype == torch.float32 and ii.dtype == torch.int64 and ii.shape == ss.shape):
+        raise ValueError("topk_seen_merge: cuda fp32 ss / int64 ii [B, m]")
+    if m > TOPK_CAND_CAP or K > TOPK_MAX_K or M > TOPK_MAX_K or ring.dtype != torch.int32 \
+            or ring_cur.dtype != torch.int64:
+        raise ValueError("topk_seen_merge: m <= TOPK_CAND_CAP, K / M <= TOPK_MAX_K, int32 ring, int64 cursors")
+    for t, dt in ((users, torch.int64), (items, torch.int64), (rnd, torch.int32), (first, torch.int32),
+                  (nu, torch.int32), (by_user, torch.int64)):
+        if t.dtype != dt or t.numel() != B:
+            raise ValueError("topk_seen_merge: users / items / by_user int64 [B], rnd / first / nu int32 [B]")
+    if DEBUG:
+        check_index(users, ring.shape[0], "topk_seen_merge users")
+    best_s = torch.empty((B, K), dtype=torch.float32, device=ss.device)
+    best_i = torch.empty((B, K), dtype=torch.int64, device=ss.device)
+    cpre = torch.empty(B, dtype=torch.int64, device=ss.device)
+    N.check(N.require().fps_topk_seen_merge(
+        _c(ss).data_ptr(), _c(ii).data_ptr(), B, m, int(K), _c(users).data_ptr(), _c(items).data_ptr(),
+        _c(rnd).data_ptr(), _c(first).data_ptr(), _c(nu).data_ptr(), _c(by_user).data_ptr(), ring.data_ptr(),
+        ring_cur.data_ptr(), M, cpre.data_ptr(), best_s.data_ptr(), best_i.data_ptr(), N.stream_ptr(ss.device)),
+        "topk_seen_merge")
+    return best_s, best_i
+
+
 def score_gemm(Q: torch.Tensor, X: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """``out[b, i] = <Q[b], X[i]>`` on MFMA (fp32 in/accumulate, K8 scoring).  ``out`` may be
     a column slice of a wider buffer (row stride taken from it)."""

@@ -143,8 +143,8 @@ def test_lemp_topk_bf16_incremental_update():
 
 
 def test_lemp_topk_graph_replay_equals_eager_scan():
-    """The hipGraph scan (``LempTopK._query_graph``: eager first batch, capture on
-    the second, replays after) returns the eager scan's results bit for bit, sees
+    """The hipGraph scan (``LempTopK._query_graph``: eager first batch, captured
+    after it, replays from the second) returns the eager scan's results bit for bit, sees
     ``update_rows`` between replays, and hands out copies (a result survives the
     next replay)."""
     g = torch.Generator().manual_seed(12)
