@@ -6,15 +6,17 @@
 // the refresh (gather, dot, two index_adds, masks, counters); at 4096 ratings per
 // micro-batch those launches, not the bytes, set the batch time.
 //
-//   mf_online_phase_kernel  -- one SGD phase (a negative j of every rating, or the
-//       ratings themselves): one wave per entry t, lanes over the factors; the entry
-//       reads its user vector U[urow[t]] (the pulled row, fixed over the phases) and
-//       its local item row W[irow[t]] as the phase starts, e = target - <u, w>,
-//       du[urow] += lr e w (entries are distinct rows of du: plain add),
-//       W[irow] += lr e u (float atomics: entries share items).  irow < 0 skips the
-//       entry (a failed negative draw, a rating owned by another rank).  Phases run
-//       as separate launches, so a phase sees the previous phases' item updates --
-//       the batch semantics of the torch form.
+//   mf_online_grad_kernel + mf_online_apply_kernel -- one SGD phase (a negative j of
+//       every rating, or the ratings themselves) in two passes, one wave per entry t,
+//       lanes over the factors.  Pass 1 reads the entry's user vector U[urow[t]] (the
+//       pulled row, fixed over the phases) and its local item row W[irow[t]],
+//       g = lr (target - <u, w>), du[urow] += g w (entries are distinct rows of du)
+//       and keeps g; pass 2 adds g u to W[irow] (float atomics: entries share items).
+//       The split keeps the torch form's batch semantics: every entry of a phase reads
+//       the item rows as the phase starts (one fused pass let an entry read a row
+//       another entry of the same phase was updating: 46 % of the item values off
+//       after 6 batches in tests/test_topk_seen_merge_gpu.py).  irow < 0 skips the
+//       entry (a failed negative draw, a rating owned by another rank).
 //   index_refresh_kernel    -- the touched item rows into the LEMP index copies
 //       (fp32 vectors, bf16 shadow, lengths) at their index positions (pos[row] < 0:
 //       not in the index).  Repeated rows write the same value.
@@ -24,13 +26,15 @@ using namespace fps;
 
 namespace {
 
+// pass 1 of a phase: reads only (every entry sees the item rows as the phase starts)
 template <int NPL>
-__global__ void __launch_bounds__(256) mf_online_phase_kernel(const float* __restrict__ U,
-                                                              const int64_t* __restrict__ urow,
-                                                              const int64_t* __restrict__ irow,
-                                                              const float* __restrict__ target, int64_t n, int D,
-                                                              float lr, float* __restrict__ W, float* __restrict__ du,
-                                                              unsigned long long* __restrict__ trained) {
+__global__ void __launch_bounds__(256) mf_online_grad_kernel(const float* __restrict__ U,
+                                                             const int64_t* __restrict__ urow,
+                                                             const int64_t* __restrict__ irow,
+                                                             const float* __restrict__ target, int64_t n, int D,
+                                                             float lr, const float* __restrict__ W,
+                                                             float* __restrict__ du, float* __restrict__ gbuf,
+                                                             unsigned long long* __restrict__ trained) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -39,28 +43,48 @@ __global__ void __launch_bounds__(256) mf_online_phase_kernel(const float* __res
     const int64_t il = irow[t];
     if (il < 0) continue;  // wave-uniform
     const int64_t r = urow != nullptr ? urow[t] : t;
-    float u[NPL], w[NPL];
+    float w[NPL];
     float dot = 0.f;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
-      u[m] = j < D ? U[r * D + j] : 0.f;
+      const float u = j < D ? U[r * D + j] : 0.f;
       w[m] = j < D ? W[il * D + j] : 0.f;
-      dot += u[m] * w[m];
+      dot += u * w[m];
     }
     dot = group_sum<64>(dot);
     const float g = lr * ((target != nullptr ? target[t] : 0.f) - dot);
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
-      if (j < D) {
-        du[r * D + j] += g * w[m];
-        atomic_add_noret(W + il * D + j, g * u[m]);
-      }
+      if (j < D) du[r * D + j] += g * w[m];
     }
+    if (lane == 0) gbuf[t] = g;
     ++done;
   }
   if (trained != nullptr && lane == 0 && done) atomicAdd(trained, done);
+}
+
+// pass 2: the item updates (float atomics: entries share items)
+template <int NPL>
+__global__ void __launch_bounds__(256) mf_online_apply_kernel(const float* __restrict__ U,
+                                                              const int64_t* __restrict__ urow,
+                                                              const int64_t* __restrict__ irow, int64_t n, int D,
+                                                              const float* __restrict__ gbuf, float* __restrict__ W) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t = wave; t < n; t += nwaves) {
+    const int64_t il = irow[t];
+    if (il < 0) continue;
+    const int64_t r = urow != nullptr ? urow[t] : t;
+    const float g = gbuf[t];
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+      const int j = lane + 64 * m;
+      if (j < D) atomic_add_noret(W + il * D + j, g * U[r * D + j]);
+    }
+  }
 }
 
 template <int NPL>
@@ -107,13 +131,18 @@ __global__ void __launch_bounds__(256) index_refresh_kernel(const int64_t* __res
 // [*, D] user deltas (rows distinct across the n entries); trained (nullable) counts
 // the entries applied.  D <= 256.
 FPS_API int fps_mf_online_phase(const float* U, const int64_t* urow, const int64_t* irow, const float* target,
-                                int64_t n, int D, float lr, float* W, float* du, unsigned long long* trained,
-                                void* stream) {
+                                int64_t n, int D, float lr, float* W, float* du, float* gbuf,
+                                unsigned long long* trained, void* stream) {
   if (n <= 0) return 0;
   if (D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   const int g = grid_for(n, 4, 256 * 16);
-  FPS_NPL_SWITCH(D, hipLaunchKernelGGL(mf_online_phase_kernel<NPL>, dim3(g), dim3(256), 0, (hipStream_t)stream, U,
-                                       urow, irow, target, n, D, lr, W, du, trained));
+  hipStream_t s = (hipStream_t)stream;
+  FPS_NPL_SWITCH(D, {
+    hipLaunchKernelGGL(mf_online_grad_kernel<NPL>, dim3(g), dim3(256), 0, s, U, urow, irow, target, n, D, lr,
+                       (const float*)W, du, gbuf, trained);
+    hipLaunchKernelGGL(mf_online_apply_kernel<NPL>, dim3(g), dim3(256), 0, s, U, urow, irow, n, D,
+                       (const float*)gbuf, W);
+  });
   FPS_CHECK_LAUNCH();
   return 0;
 }

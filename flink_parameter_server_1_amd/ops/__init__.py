@@ -988,8 +988,9 @@ def mf_online_phase(U: torch.Tensor, urow: Optional[torch.Tensor], irow: torch.T
     """One SGD phase of the online MF + top-K worker (``mf_online.hip``, GPU only): for
     every entry t with ``irow[t] >= 0``: ``e = target[t] - <U[urow[t]], W[irow[t]]>``
     (target 0 when None: a negative), ``du[urow[t]] += lr e W[irow[t]]`` (distinct rows),
-    ``W[irow[t]] += lr e U[urow[t]]`` (atomics); ``urow`` None = identity.  ``trained``
-    (int64 scalar, optional) counts the applied entries."""
+    ``W[irow[t]] += lr e U[urow[t]]`` (atomics), every entry reading the item rows as the
+    phase starts; ``urow`` None = identity.  ``trained`` (int64 scalar, optional) counts
+    the applied entries."""
     n, D = irow.numel(), U.shape[1]
     if not (U.is_cuda and U.dtype == W.dtype == du.dtype == torch.float32 and W.shape[1] == D == du.shape[1]):
         raise ValueError("mf_online_phase: cuda fp32 U / W / du with one D")
@@ -998,10 +999,12 @@ def mf_online_phase(U: torch.Tensor, urow: Optional[torch.Tensor], irow: torch.T
         raise ValueError("mf_online_phase: int64 irow / urow [n], target [n], D <= 256")
     if DEBUG:
         check_index(irow, W.shape[0], "mf_online_phase irow", allow_negative=True)
+    gbuf = torch.empty(n, dtype=torch.float32, device=U.device)
     N.check(N.require().fps_mf_online_phase(_c(U).data_ptr(), N.ptr(None if urow is None else _c(urow)),
                                             _c(irow).data_ptr(),
                                             N.ptr(None if target is None else _c(target.float())), n, D, float(lr),
-                                            W.data_ptr(), du.data_ptr(), N.ptr(trained), N.stream_ptr(U.device)),
+                                            W.data_ptr(), du.data_ptr(), gbuf.data_ptr(), N.ptr(trained),
+                                            N.stream_ptr(U.device)),
             "mf_online_phase")
 
 

@@ -55,14 +55,14 @@ def test_seen_merge_equals_round_loop(m, K, memory):
         assert torch.equal(new_store.ring, ref_store.ring) and torch.equal(new_store.ring_cur, ref_store.ring_cur)
 
 
-def _run_online(fused, batches, users, items, D):
+def _run_online(fused, batches, users, items, D, neg=0):
     from flink_parameter_server_1_amd.core.messages import Left
     from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime
     from flink_parameter_server_1_amd.models.mf.topk_tensor import OnlineMFTopKWorker
     from flink_parameter_server_1_amd.parallel.comm import Comm
     from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogic
 
-    w = OnlineMFTopKWorker(items, D, 0.05, K=20, worker_k=20, memory=8, negative_sample_rate=2,
+    w = OnlineMFTopKWorker(items, D, 0.05, K=20, worker_k=20, memory=8, negative_sample_rate=neg,
                            prefill_items=True, num_users=users, resort_every=1000, range_min=-0.3, range_max=0.3)
     w.fused = fused
     logic = DeviceSimplePSLogic(users, D, op="add_renorm", init=("uniform", -0.3, 0.3))
@@ -76,9 +76,11 @@ def _run_online(fused, batches, users, items, D):
 
 def test_online_mf_topk_fused_equals_torch_chains():
     """OnlineMFTopKWorker with the fused merge + SGD phases + index refresh against its
-    torch chains: the first batch's top-K lists are identical (same index, same
-    merge order), and after 6 batches of learning (negatives included) the item
-    shard and the trained counts agree to fp32 atomic-order rounding."""
+    torch chains: the first batch's top-K lists are identical (same index, same merge
+    order), and after 6 batches of learning the item shard and the trained counts
+    agree to fp32 atomic-order rounding.  (Without negatives: the known-item list the
+    negatives are drawn from is appended by atomics, so two runs draw different
+    negatives whichever path runs; with negatives the counts must still agree.)"""
     g = torch.Generator(device=DEV).manual_seed(3)
     users, items, B, D = 800, 4000, 512, 16
     batches = []
@@ -92,11 +94,15 @@ def test_online_mf_topk_fused_equals_torch_chains():
     assert len(tf) == len(tt) == 6
     (_, s_f, i_f), (_, s_t, i_t) = tf[0], tt[0]
     assert torch.equal(i_f, i_t) and torch.equal(s_f, s_t)
-    assert wf.trained == wt.trained > 0
+    assert wf.trained == wt.trained == 6 * B
     torch.testing.assert_close(wf.items.weight, wt.items.weight, rtol=1e-4, atol=1e-5)
     # later batches: same lists up to near-ties moved by the rounding differences
     agree = sum(int((a[2] == b[2]).all(1).sum()) for a, b in zip(tf[1:], tt[1:]))
     assert agree >= 0.98 * 5 * B
+    wf2, _ = _run_online(True, batches, users, items, D, neg=2)
+    wt2, _ = _run_online(False, batches, users, items, D, neg=2)
+    assert wf2.trained == wt2.trained > 6 * B
+    assert bool(torch.isfinite(wf2.items.weight).all())
 
 
 def test_online_learner_and_generator_gpu_matches_per_record():
