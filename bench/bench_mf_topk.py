@@ -42,6 +42,8 @@ def main(argv=None):
     ap.add_argument("--bucket", type=int, default=65536)
     ap.add_argument("--seed-items", type=int, default=None, help="LempTopK.seed_items (unfused first segment)")
     ap.add_argument("--max-segment", type=int, default=None, help="LempTopK.max_segment (largest fused segment)")
+    ap.add_argument("--unfused", action="store_true",
+                    help="torch chains for the merge / SGD and eager scans (the A/B reference)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args(argv)
@@ -64,6 +66,9 @@ def main(argv=None):
     worker = OnlineMFTopKWorker(a.items, a.dim, 0.01, K=a.k, worker_k=a.worker_k, memory=a.memory,
                                 negative_sample_rate=a.negatives, bucket_size=a.bucket, range_min=-0.1,
                                 range_max=0.1, prefill_items=True, num_users=a.users)
+    if a.unfused:
+        worker.fused = False
+        os.environ["FPS_TOPK_GRAPH"] = "0"
     logic = DeviceSimplePSLogic(a.users, a.dim, op="add_renorm", init=("uniform", -0.1, 0.1))
     logic.emit = "none"  # the benchmark keeps no output stream of the user updates
     rt = TensorRuntime(comm, staleness=0, output_sink=lambda e: None).start(worker, logic)
@@ -103,7 +108,8 @@ def main(argv=None):
             "dtype": "fp32", "scorer": _scorer(), "data": "synthetic ratings, random-init factors (warm item catalogue)",
             "config": {"users": a.users, "items": a.items, "dim": a.dim, "k": a.k, "worker_k": a.worker_k,
                        "batch": a.batch, "negatives": a.negatives, "memory": a.memory, "bucket": a.bucket,
-                       "seed_items": LempTopK.seed_items, "max_segment": LempTopK.max_segment},
+                       "seed_items": LempTopK.seed_items, "max_segment": LempTopK.max_segment,
+                       "fused": not a.unfused},
         }), flush=True)
 
 

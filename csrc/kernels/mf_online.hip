@@ -35,6 +35,9 @@ __global__ void __launch_bounds__(256) mf_online_grad_kernel(const float* __rest
                                                              float lr, const float* __restrict__ W,
                                                              float* __restrict__ du, float* __restrict__ gbuf,
                                                              unsigned long long* __restrict__ trained) {
+  __shared__ unsigned long long s_done;
+  if (threadIdx.x == 0) s_done = 0;
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -62,7 +65,11 @@ __global__ void __launch_bounds__(256) mf_online_grad_kernel(const float* __rest
     if (lane == 0) gbuf[t] = g;
     ++done;
   }
-  if (trained != nullptr && lane == 0 && done) atomicAdd(trained, done);
+  // one global atomic per workgroup (one per wave on a single counter serialised
+  // ~4k same-address atomics: 52 us per phase at 4096 entries)
+  if (lane == 0 && done) atomicAdd(&s_done, done);
+  __syncthreads();
+  if (trained != nullptr && threadIdx.x == 0 && s_done) atomicAdd(trained, s_done);
 }
 
 // pass 2: the item updates (float atomics: entries share items)
@@ -135,7 +142,7 @@ FPS_API int fps_mf_online_phase(const float* U, const int64_t* urow, const int64
                                 unsigned long long* trained, void* stream) {
   if (n <= 0) return 0;
   if (D <= 0 || D > 256) return (int)hipErrorInvalidValue;
-  const int g = grid_for(n, 4, 256 * 16);
+  const int g = grid_for(n, 4, 512);
   hipStream_t s = (hipStream_t)stream;
   FPS_NPL_SWITCH(D, {
     hipLaunchKernelGGL(mf_online_grad_kernel<NPL>, dim3(g), dim3(256), 0, s, U, urow, irow, target, n, D, lr,

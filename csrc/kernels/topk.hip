@@ -287,15 +287,21 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* 
 }
 
 // bitonic merge of the rows with more than TK_NT candidates (<= TK_CAP kept)
+// reset (the second of the two kernels, so both read the count first): cnt[row] = 0
+// for the next segment's filter -- no fill launch per segment
 __global__ void __launch_bounds__(TK_NT) topk_merge_cand_kernel(const uint32_t* __restrict__ cand_key,
                                                                 const int64_t* __restrict__ cand_id,
-                                                                const int32_t* __restrict__ cnt, int cap,
+                                                                int32_t* __restrict__ cnt, int cap,
                                                                 float* __restrict__ best_s,
-                                                                int64_t* __restrict__ best_i, int k) {
+                                                                int64_t* __restrict__ best_i, int k, int reset) {
   __shared__ uint32_t skey[TK_SORT];
   __shared__ int64_t sid[TK_SORT];
   const int row = blockIdx.x;
   const int nc = min(min(cnt[row], cap), TK_CAP);
+  if (reset) {
+    __syncthreads();  // every thread has read cnt[row]
+    if (threadIdx.x == 0) cnt[row] = 0;
+  }
   if (nc <= TK_NT) return;  // the rank kernel's row
   for (int i = threadIdx.x; i < nc; i += TK_NT) {
     skey[i] = cand_key[(int64_t)row * cap + i];
@@ -411,16 +417,17 @@ FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int6
 }
 
 // candidate lists [B, cap] from fps_score_filter; every cnt[q] must be <= cap (TK_CAP at most)
-// ovf (nullable): set to 1 when some cnt[q] > cap (that row's merge is incomplete)
-FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id, const int32_t* cnt, int cap, int B,
-                                float* best_s, int64_t* best_i, int k, int32_t* ovf, void* stream) {
+// ovf (nullable): set to 1 when some cnt[q] > cap (that row's merge is incomplete);
+// reset_cnt: cnt[] is zeroed once both kernels read it
+FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id, int32_t* cnt, int cap, int B,
+                                float* best_s, int64_t* best_i, int k, int32_t* ovf, int reset_cnt, void* stream) {
   if (B <= 0) return 0;
   if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(topk_merge_rank_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
                      best_s, best_i, k, ovf);
   FPS_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
-                     best_s, best_i, k);
+                     best_s, best_i, k, reset_cnt);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -139,9 +139,19 @@ class LempTopK:
         Q = Q.float().contiguous()
         B = Q.shape[0]
         dev = Q.device
-        qlen = torch.linalg.vector_norm(Q, dim=1)
         N = self.vecs.shape[0]
         fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
+        if fused and self.sync_free and N > max(self.seed_items, start) and state is None and start == 0 \
+                and (Q.shape[0], int(k)) in self._graph and not self._coord_active() and not ops.DEBUG:
+            if self._uses_coord():  # COORD switched off for this batch (the per-batch switch)
+                self.coord_off_batches -= 1
+                self.coord_batches["off"] += 1
+            res = self._query_graph(Q, None, k)  # the captured scan computes the norms itself
+            if res is not None:
+                return res
+            self.overflows += 1
+            fused = False
+        qlen = torch.linalg.vector_norm(Q, dim=1)
         if fused and self.sync_free and N > max(self.seed_items, start):
             st = None if state is None else (state[0].clone(), state[1].clone())
             if self._uses_coord():
@@ -314,11 +324,13 @@ class LempTopK:
         # ~k ln(1 + n / s) scores per query, so doubling keeps every merge on the small
         # rank path (one 4096 -> 65536 step passed ~1100) at log2(N / seed) segments
         # (8 for 1M items, against 19 when capped at 65536: 4 launches each).  LC keeps
-        # the bucket as the largest segment: it picks its bound per segment from the
-        # segment's length spread, the reference's per-bucket choice.
+        # the bucket as the largest segment while its COORD bound is on: it picks its
+        # bound per segment from the segment's length spread, the reference's
+        # per-bucket choice (switched off, it is the LENGTH scan).
         from .pruning import LC
 
-        cap_seg = self.bucket if isinstance(self.strategy, LC) else max(self.bucket, self.max_segment)
+        lc_buckets = isinstance(self.strategy, LC) and self._coord_active()
+        cap_seg = self.bucket if lc_buckets else max(self.bucket, self.max_segment)
         cuts = {seed}
         c = max(seed, self.seed_items) if self.geometric else N
         if not self.geometric:
@@ -338,12 +350,12 @@ class LempTopK:
             self._coord_gate.fill_(1)
             self._coord_prev.copy_(self.coord_stats)
             stats0 = self.coord_stats.clone()
+        cnt.zero_()  # then zeroed by each segment's merge (reset_cnt)
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and not capturing and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
             self.buckets_scanned += len(range(-(-s // self.bucket) * self.bucket, e, self.bucket))
-            cnt.zero_()
             if self.bf16:
                 seg_coord = None
                 if coord is not None and self._coord_segment(s, e):
@@ -360,7 +372,7 @@ class LempTopK:
             else:
                 ops.score_filter_lemp(Q, self.vecs[s:e], self.ids[s:e], best_s, ck, ci, cnt, qlen,
                                       self.lengths[s:e])
-            ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf)
+            ops.topk_merge_cand(ck, ci, cnt, best_s, best_i, overflow=ovf, reset_cnt=True)
         return best_s, best_i, ovf, (stats0 if coord is not None else None)
 
     #: COORD self-disable (see ``coord_off_batches``)

@@ -971,14 +971,18 @@ def cand_rescore(Q: torch.Tensor, X: torch.Tensor, ids: torch.Tensor, best_s: to
 
 
 def topk_merge_cand(cand_key: torch.Tensor, cand_id: torch.Tensor, cnt: torch.Tensor, best_s: torch.Tensor,
-                    best_i: torch.Tensor, overflow: Optional[torch.Tensor] = None) -> None:
+                    best_i: torch.Tensor, overflow: Optional[torch.Tensor] = None, reset_cnt: bool = False) -> None:
     """Merge ``score_filter`` candidate lists into the running top-k in place (K13).
     ``overflow`` (int32 [1]): set to 1 on the device when a row had more than ``cap``
-    candidates (its merge is incomplete; the caller rescans)."""
+    candidates (its merge is incomplete; the caller rescans).  ``reset_cnt``: ``cnt``
+    (contiguous int32) is zeroed on the device once merged -- ready for the next
+    segment's filter without a fill launch."""
     B, cap = cand_key.shape
+    if reset_cnt and not (cnt.is_contiguous() and cnt.dtype == torch.int32):
+        raise ValueError("topk_merge_cand: reset_cnt needs a contiguous int32 cnt")
     N.check(N.require().fps_topk_merge_cand(_c(cand_key).data_ptr(), _c(cand_id).data_ptr(), _c(cnt).data_ptr(), cap,
                                             B, _c(best_s).data_ptr(), _c(best_i).data_ptr(), best_s.shape[1],
-                                            None if overflow is None else overflow.data_ptr(),
+                                            None if overflow is None else overflow.data_ptr(), int(reset_cnt),
                                             N.stream_ptr(best_s.device)), "topk_merge_cand")
 
 

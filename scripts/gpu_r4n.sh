@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4: merge resets the candidate counts, block-aggregated trained counter, no host norm on graph replays,
+# LC scans without COORD use the LENGTH segments; full GPU suite.
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4n
+mkdir -p $O
+step() { name=$1; shift; timeout -k 10 ${T:-300} "$@" > $O/$name.log 2>&1 || { echo "FAIL $name"; tail -30 $O/$name.log; exit 1; }; echo "$name: $(grep -v amdgpu.ids $O/$name.log | tail -1 | cut -c1-${W:-300})"; }
+T=600 step tests python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+for st in length coord lc:1.3; do step topk_$st python bench/bench_topk.py --strategy $st; done
+step mf_topk python bench/bench_mf_topk.py
+step mf_topk2 python bench/bench_mf_topk.py
+step mf_topk_unfused python bench/bench_mf_topk.py --unfused
+step prof_mftopk rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mftopk -- python bench/bench_mf_topk.py --steps 6 --warmup 2
+echo ALLDONE
