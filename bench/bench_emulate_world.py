@@ -8,7 +8,10 @@ blocks by default).  ``MFConfig(emulate_world=N)`` runs rank 0's exact schedule
 with every block resident (``EmulatedRotation``): the same partition and the
 same launches per sub-step as one GPU of the real job, without the transfers.
 Comparing the emulated step with the N = 1 step separates "compute slower at
-N" from "transfer exposed" before an N-GPU node runs the real thing.
+N" from "transfer exposed" before an N-GPU node runs the real thing.  With
+``--link-gbps`` the transfers are modelled too (``rotation._SymmetricLinks``:
+rank-symmetric timing, a host-timed link delay and a real device copy per block)
+and ``comm_wait_ms_per_step`` is the time the compute stream waited for them.
 
     python bench/bench_emulate_world.py [--ws 1,2,4,8] [--steps 20 --warmup 5]
 
@@ -37,6 +40,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
+                         "timing, host-timed delay + a real device copy); 0 = no transfers")
+    ap.add_argument("--latency-us", type=float, default=5.0)
     a = ap.parse_args()
 
     import torch
@@ -49,7 +56,8 @@ def main():
     base = None
     for W in [int(x) for x in a.ws.split(",")]:
         cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
-                       exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0)
+                       exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0,
+                       emulate_link_gbps=a.link_gbps, emulate_latency_us=a.latency_us)
         m = DistributedMF(cfg, comm)
         data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
         s = 0
@@ -58,6 +66,8 @@ def main():
             s += 1
         m.flush()
         torch.cuda.synchronize()
+        if W > 1:
+            m.rot.wait_ms()  # drop the warm-up's waits
         t0 = time.perf_counter()
         for _ in range(a.steps):
             m.step(*data.batch(s, a.batch))
@@ -65,12 +75,19 @@ def main():
         m.flush()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / a.steps * 1e3
+        wait = m.rot.wait_ms() / a.steps if W > 1 else 0.0
         base = base or ms
         print(json.dumps({"emulated_world": W, "rotation": a.rotation if W > 1 else "local", "ms_per_step": ms,
                           "updates_per_s_per_gpu": a.batch / ms * 1e3, "ratio_to_n1": ms / base,
                           "users_per_gpu": m.users.n_local, "sub_steps": m.rot.K if W > 1 else 1,
                           "tile_rows": getattr(m, "tile_R", None), "tiles_per_block": getattr(m, "tile_T", None),
-                          "user_phases": getattr(m, "user_phases", None)}), flush=True)
+                          "user_phases": getattr(m, "user_phases", None),
+                          "link_gbps": a.link_gbps if W > 1 else None, "latency_us": a.latency_us if W > 1 else None,
+                          "comm_wait_ms_per_step": wait, "exposed_fraction": wait / ms,
+                          "link_bytes_per_step": (m.rot.bytes_sent / (a.steps + a.warmup)) if W > 1 else 0}),
+              flush=True)
+        if W > 1:
+            m.rot.close()
         del m, data
         torch.cuda.empty_cache()
 

@@ -80,6 +80,8 @@ class MFConfig:
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
     rotation: str = "bidir"           # rotate: "bidir" (two counter-rotating rings) | "ring" (one ring)
     emulate_world: int = 0            # W = 1, rotate: rank 0's share of an N-rank job (users / schedule)
+    emulate_link_gbps: float = 0.0    # emulate_world: model the transfers on links of this rate (0: none)
+    emulate_latency_us: float = 5.0   # emulate_world: per-message link latency
 
 
     def user_seed(self) -> int:
@@ -200,7 +202,9 @@ class DistributedMF:
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
         if self.exchange == "rotate":
             if self.emulated:
-                self.rot = EmulatedRotation(self.items.weight, cfg.num_items, Wn, cfg.rotation)
+                self.rot = EmulatedRotation(self.items.weight, cfg.num_items, Wn, cfg.rotation,
+                                            link_gbps=cfg.emulate_link_gbps or None,
+                                            latency_us=cfg.emulate_latency_us)
             else:
                 self.rot = RingRotation(self.comm, self.items.weight, cfg.num_items, cfg.rotation)
             self.rot_w = tile_w  # hash shards of the block layout the ratings are bucketed by

@@ -267,12 +267,102 @@ class RingRotation:
         self.s = 0
 
 
+class _SymmetricLinks:
+    """Host-timed xGMI links of the emulated rank (``EmulatedRotation(link_gbps=...)``).
+
+    In a rotation every rank runs the same schedule on equal work, so the block a
+    rank receives in sub-step ``s`` is posted by its neighbour when the neighbour's
+    sub-step ``s - 1`` ends -- the moment this rank's own ``s - 1`` ends.  A posted
+    transfer starts once that compute-stream event has completed, takes
+    ``latency + bytes / link_gbps`` on its link (the two rings' blocks travel on two
+    different links, in parallel), and is then issued as a real device copy (the send's
+    HBM read + the receive's HBM write of this GPU) on a high-priority link stream;
+    the compute stream waits for it before the sub-step that needs the block.  The
+    delay itself occupies no CU (a host timer).  Unlike the virtual world
+    (``parallel/vworld.py``), only the emulated rank computes, at the full speed of
+    its GPU, so the measured wait is the exposure of the real schedule under rank
+    symmetry rather than the skew of N ranks sharing one GPU."""
+
+    def __init__(self, device, link_gbps: float, latency_us: float):
+        import threading
+
+        self.us_per_byte = 1e-3 / float(link_gbps)  # GB/s -> us per byte
+        self.latency_us = float(latency_us)
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self.device = device
+        self.cv = threading.Condition()
+        self.pending: list = []
+        self.closed = False
+        self.error = None
+        self.thread = threading.Thread(target=self._loop, name="emulated-links", daemon=True)
+        self.thread.start()
+
+    def post(self, after: "torch.cuda.Event", copies, link_bytes: int) -> dict:
+        import threading
+
+        item = {"after": after, "copies": copies, "us": self.latency_us + link_bytes * self.us_per_byte,
+                "t0": None, "done": threading.Event(), "event": None}
+        with self.cv:
+            self.pending.append(item)
+            self.cv.notify_all()
+        return item
+
+    def wait(self, item: dict) -> None:
+        """Host-wait until the transfer was issued, then make the compute stream wait for it."""
+        if not item["done"].wait(timeout=120.0):
+            raise RuntimeError("emulated link: transfer not issued within 120 s")
+        if self.error is not None:
+            raise RuntimeError(f"emulated link failed: {self.error}")
+        torch.cuda.current_stream().wait_event(item["event"])
+
+    def _loop(self) -> None:
+        import time
+
+        try:
+            torch.cuda.set_device(self.device)
+            while True:
+                with self.cv:
+                    if self.closed:
+                        return
+                    now = time.perf_counter()
+                    for item in list(self.pending):
+                        if item["t0"] is None:
+                            if item["after"].query():
+                                item["t0"] = now
+                            continue
+                        if now >= item["t0"] + item["us"] * 1e-6:
+                            self.pending.remove(item)
+                            with torch.cuda.stream(self.stream):
+                                for dst, src in item["copies"]:
+                                    dst.copy_(src, non_blocking=True)
+                                ev = torch.cuda.Event()
+                                ev.record(self.stream)
+                            item["event"] = ev
+                            item["done"].set()
+                    self.cv.wait(timeout=2e-5 if self.pending else 1e-3)
+        except Exception as e:  # surfaced by wait()
+            self.error = repr(e)
+            with self.cv:
+                for item in self.pending:
+                    item["done"].set()
+
+    def close(self) -> None:
+        with self.cv:
+            self.closed = True
+            self.cv.notify_all()
+        self.thread.join(5.0)
+
+
 class EmulatedRotation:
     """Rank 0's rotation schedule of a ``world``-rank job on one device with every
-    block resident: the same launches per sub-step as one GPU of the real job,
-    without transfers (``item`` = the whole ``[num_ids, D]`` table)."""
+    block resident: the same launches per sub-step as one GPU of the real job
+    (``item`` = the whole ``[num_ids, D]`` table).  Without ``link_gbps`` nothing
+    moves; with it every sub-step's transfers are modelled by ``_SymmetricLinks``
+    (the real schedule's timing under rank symmetry) and ``wait_ms`` reports how long
+    the compute stream waited for them."""
 
-    def __init__(self, items: torch.Tensor, num_ids: int, world: int, schedule: str = "bidir"):
+    def __init__(self, items: torch.Tensor, num_ids: int, world: int, schedule: str = "bidir",
+                 link_gbps: Optional[float] = None, latency_us: float = 5.0):
         self.items, self.W, self.schedule = items, world, schedule
         self.Wv = layout_world(world, schedule)
         self.K = 2 * world
@@ -288,26 +378,60 @@ class EmulatedRotation:
         self.at_rest = True
         self.s = 0
         self.bytes_sent = 0
+        self.links = _SymmetricLinks(items.device, link_gbps, latency_us) \
+            if link_gbps and items.is_cuda and world > 1 else None
+        self._scratch = None
+        self._inflight = None
+        self._events: List[tuple] = []
+
+    def _ring_blocks(self, s: int) -> List[int]:
+        W = self.W
+        if self.schedule == "ring":
+            return [s % (2 * W)]
+        return [s % (2 * W), 2 * W + (1 - s) % (2 * W)]
 
     def active_blocks(self):
-        s, W = self.s, self.W
-        if self.schedule == "ring":
-            g = [s % (2 * W)]
-        else:
-            g = [s % (2 * W), 2 * W + (1 - s) % (2 * W)]
-        return [(b, self.blocks[b]) for b in g]
+        return [(b, self.blocks[b]) for b in self._ring_blocks(self.s)]
 
     def begin(self):
         if self.at_rest:
             self.blocks = [self.items[ids].contiguous() for ids in self.ids]
             self.at_rest = False
             self.s = 0
+        if self.links is not None and self.s >= 1:
+            # sub-step s: each ring sends the block it finished in s - 1 and receives the
+            # block it needs in s + 1 (posted when s - 1 ended, as the neighbour's is)
+            if self._scratch is None:
+                cap = max(b.shape[0] for b in self.blocks)
+                self._scratch = [torch.empty((cap, self.items.shape[1]), dtype=self.items.dtype,
+                                             device=self.items.device) for _ in self._ring_blocks(0)]
+            after = torch.cuda.Event()
+            after.record()
+            copies, link_bytes = [], 0
+            for out_b, in_b, buf in zip(self._ring_blocks(self.s - 1), self._ring_blocks(self.s + 1), self._scratch):
+                n = min(self.blocks[out_b].shape[0], self.blocks[in_b].shape[0])
+                copies.append((buf[:n], self.blocks[out_b][:n]))
+                nbytes = self.blocks[in_b].numel() * self.blocks[in_b].element_size()
+                link_bytes = max(link_bytes, nbytes)  # the rings use different links: in parallel
+                self.bytes_sent += self.blocks[out_b].numel() * self.blocks[out_b].element_size()
+            self._inflight = self.links.post(after, copies, link_bytes)
 
     def end(self):
+        if self._inflight is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.links.wait(self._inflight)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._events.append((e0, e1))
+            self._inflight = None
         self.s += 1
 
     def wait_ms(self, reset: bool = True) -> float:
-        return 0.0
+        ms = sum(a.elapsed_time(b) for a, b in self._events)
+        if reset:
+            self._events = []
+        return ms
 
     def home(self):
         if self.at_rest:
@@ -317,3 +441,7 @@ class EmulatedRotation:
         self.blocks = None
         self.at_rest = True
         self.s = 0
+
+    def close(self) -> None:
+        if self.links is not None:
+            self.links.close()

@@ -230,3 +230,32 @@ def test_sgns_pipeline_async_equals_sync():
     for a, b in zip(res, sync):
         assert torch.equal(a[0], b[0])
         torch.testing.assert_close(a[1], b[1], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("schedule", ["bidir", "ring"])
+def test_emulated_links_model_transfers_without_changing_results(schedule):
+    """``EmulatedRotation(link_gbps=...)`` (rank 0's schedule with rank-symmetric
+    host-timed links): the modelled transfers never touch the blocks (results equal
+    the link-free emulation bit for bit); a fast link hides behind the sub-steps,
+    a 0.2 GB/s one (~0.48 ms per 96 KB quarter-shard block, far longer than a
+    sub-step of 375 ratings) makes the compute stream wait, and the wait is reported."""
+    from flink_parameter_server_1_amd.models.mf import fast
+
+    out = {}
+    for gbps in (0.0, 50.0, 0.2):
+        cfg = fast.MFConfig(num_users=NU, num_items=NI, dim=D, learning_rate=0.05, range_min=0.0, range_max=0.2,
+                            exchange="rotate", rotation=schedule, emulate_world=4, emulate_link_gbps=gbps)
+        m = fast.DistributedMF(cfg)
+        for u, i, r in _unique_batches(0, 4, 3, m.users.n_local, NI, B):
+            m.step(u, i, r)
+        m.flush()
+        torch.cuda.synchronize()
+        out[gbps] = (m.I.cpu().clone(), m.U.cpu().clone(), m.rot.wait_ms(), m.rot.bytes_sent)
+        m.rot.close()
+    assert torch.equal(out[0.0][0], out[50.0][0]) and torch.equal(out[0.0][1], out[50.0][1])
+    assert torch.equal(out[0.0][0], out[0.2][0]) and torch.equal(out[0.0][1], out[0.2][1])
+    assert out[0.0][2] == 0.0 and out[0.0][3] == 0
+    assert out[50.0][3] > 0
+    subs = 3 * (8 - 1)  # transfers per step: every sub-step but the first
+    assert out[0.2][2] > 0.25 * subs  # ms: most of the ~0.48 ms per transfer is exposed
+    assert out[50.0][2] < out[0.2][2] / 10
