@@ -1,6 +1,5 @@
 #!/bin/bash
-# Round 4: merge resets the candidate counts, block-aggregated trained counter, no host norm on graph replays,
-# LC scans without COORD use the LENGTH segments; full GPU suite.
+# Round 4: full GPU suite; top-K / MF+top-K after the launch cuts; emulated N = 2/4/8 with rank-symmetric links.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4n
@@ -11,5 +10,7 @@ for st in length coord lc:1.3; do step topk_$st python bench/bench_topk.py --str
 step mf_topk python bench/bench_mf_topk.py
 step mf_topk2 python bench/bench_mf_topk.py
 step mf_topk_unfused python bench/bench_mf_topk.py --unfused
+W=2000 T=500 step emu_links50 python -u bench/bench_emulate_world.py --ws 1,2,4,8 --steps 10 --warmup 3 --link-gbps 50
+W=2000 T=500 step emu_links25 python -u bench/bench_emulate_world.py --ws 8 --steps 10 --warmup 3 --link-gbps 25
 step prof_mftopk rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mftopk -- python bench/bench_mf_topk.py --steps 6 --warmup 2
 echo ALLDONE
