@@ -197,7 +197,7 @@ def main(argv=None):
         torch.cuda.empty_cache()
         n_loc = model.users.n_local
         hog = lost_updates(n_loc, a.items, a.batch / n_loc, getattr(model, "user_phases", 1),
-                           user_update=a.user_update)
+                           user_update=a.user_update, world=n if model.exchange == "rotate" else 1)
         torch.cuda.empty_cache()
     comm.barrier()
 

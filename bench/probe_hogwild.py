@@ -65,16 +65,25 @@ def lost_update_count(U, uid, v, users: int, nmax: int = 24, chunk: int = 200_00
 
 
 def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int = 0, lr: float = 1e-4,
-                 count_updates: bool = True, user_update: str = "store") -> dict:
+                 count_updates: bool = True, user_update: str = "store", world: int = 1) -> dict:
+    """``users`` rows of ONE worker; ``world > 1``: that worker is rank 0 of a
+    ``world``-GPU rotation job (``MFConfig(emulate_world=world)``: the same blocks,
+    sub-steps and partition as one GPU of the real job, so the race is measured on
+    the geometry the N-GPU bench runs)."""
     import torch
 
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     dev = torch.device("cuda", 0)
-    cfg = MFConfig(num_users=users, num_items=items, dim=64, learning_rate=lr, user_phases=phases,
-                   prefetch_partition=False, user_update=user_update)
+    if world > 1:
+        cfg = MFConfig(num_users=users * world, num_items=items, dim=64, learning_rate=lr, user_phases=phases,
+                       prefetch_partition=False, user_update=user_update, exchange="rotate", emulate_world=world)
+    else:
+        cfg = MFConfig(num_users=users, num_items=items, dim=64, learning_rate=lr, user_phases=phases,
+                       prefetch_partition=False, user_update=user_update)
     m = DistributedMF(cfg, Comm(device=dev, local=True))
+    assert m.users.n_local == users
     assert m.sgd_mode == ("flat" if user_update == "atomic" else "tiled")
     g = torch.Generator(device=dev).manual_seed(seed)
     with torch.no_grad():
@@ -95,12 +104,16 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
     share = want.norm(dim=1) / cnt.clamp_min(1)  # ~ one rating's contribution
     lost = (err > 0.2 * share) & (cnt > 1)
     rated = cnt > 0
-    out = {"users": users, "items": items, "ratings": n, "ratings_per_user": per_user,
+    if world > 1 and hasattr(m.rot, "close"):
+        m.rot.close()
+    out = {"users": users, "items": items, "ratings": n, "ratings_per_user": per_user, "world": world,
            "phases": getattr(m, "user_phases", None), "tile_rows": getattr(m, "tile_R", None), "user_update": cfg.user_update, "users_with_lost_update": int(lost.sum()),
            "rated_users": int(rated.sum()), "lost_user_fraction": float(lost.sum()) / max(int(rated.sum()), 1),
            "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())}
     if count_updates:
-        nl, nc = lost_update_count(m.U, uid, v, users)
+        # users with more ratings than the solver's width are not counted (reported in updates_checked)
+        nmax = max(24, min(64, int(cnt.max())))
+        nl, nc = lost_update_count(m.U, uid, v, users, nmax=nmax, chunk=max(20_000, 200_000 * 24 // nmax))
         out.update({"lost_updates": nl, "updates_checked": nc, "lost_update_fraction": nl / max(nc, 1)})
     return out
 
@@ -113,10 +126,11 @@ def main(argv=None):
     ap.add_argument("--phases", default="1,4")
     ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"])
     ap.add_argument("--no-count", action="store_true", help="skip the per-update least-squares count")
+    ap.add_argument("--world", type=int, default=1, help="rank 0 of an N-GPU rotation job (emulated schedule)")
     a = ap.parse_args(argv)
     for p in [int(x) for x in a.phases.split(",")]:
         print(json.dumps(lost_updates(a.users, a.items, a.per_user, p, count_updates=not a.no_count,
-                                      user_update=a.user_update)), flush=True)
+                                      user_update=a.user_update, world=a.world)), flush=True)
 
 
 if __name__ == "__main__":
