@@ -11,13 +11,16 @@ pass() {  # name counters...
   echo "$name ok"
 }
 pass p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
-pass p2 SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD
 pass p3 FETCH_SIZE
 pass p4 TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr TD_BUSY_avr
+pass p2 SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD
 python - <<'PY' > $O/summary.txt
 import csv, glob, collections
 for p in ("p1", "p2", "p3", "p4"):
-    f = glob.glob(f"gpurun_out/pmc_topk4/{p}/*/*counter_collection.csv")[0]
+    fs = glob.glob(f"gpurun_out/pmc_topk4/{p}/*/*counter_collection.csv")
+    if not fs:
+        continue
+    f = fs[0]
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):
