@@ -12,6 +12,8 @@ step mf_topk2 python bench/bench_mf_topk.py
 step mf_topk_unfused python bench/bench_mf_topk.py --unfused
 W=2000 T=500 step emu_links50 python -u bench/bench_emulate_world.py --ws 1,2,4,8 --steps 10 --warmup 3 --link-gbps 50
 W=2000 T=500 step emu_links25 python -u bench/bench_emulate_world.py --ws 8 --steps 10 --warmup 3 --link-gbps 25
+step w2v_ps python bench/bench_w2v.py --mode standard --ps-path
+step prof_w2vps rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_w2vps -- python bench/bench_w2v.py --mode standard --ps-path --steps 5 --warmup 2
 W=600 step hog_emu8 python bench/probe_hogwild.py --users 1250000 --items 1000000 --per-user 51.2 --phases 1 --world 8
 step prof_mftopk rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mftopk -- python bench/bench_mf_topk.py --steps 6 --warmup 2
 echo ALLDONE
