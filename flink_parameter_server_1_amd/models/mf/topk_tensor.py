@@ -435,8 +435,9 @@ class _TopKServing:
             else:
                 s = torch.full((Q.shape[0], self.worker_k), float("-inf"), device=Q.device)
                 i = torch.full((Q.shape[0], self.worker_k), -1, dtype=torch.long, device=Q.device)
-            s = torch.where(valid.view(-1, 1), s, torch.full_like(s, float("-inf")))
-            i = torch.where(valid.view(-1, 1), i, torch.full_like(i, -1))
+            if valid is not None:  # None: every query row is valid
+                s = torch.where(valid.view(-1, 1), s, torch.full_like(s, float("-inf")))
+                i = torch.where(valid.view(-1, 1), i, torch.full_like(i, -1))
         with stage("topk.merge", None):
             ss, ii = _gather_partials(self.comm, s, i)
             if plan is not None and plan.fused and self._fused_merge(ss):
@@ -631,11 +632,15 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         if self._stale or self.index is None:
             self._rebuild_index()
         self._since_sort += 1
-        self._serve(U, torch.ones(users.numel(), dtype=torch.bool, device=U.device), users, items, ts, ps, plan)
+        self._serve(U, None, users, items, ts, ps, plan)
         # learning: the owner of each rated item (non-owned rows masked, not compacted)
         n = self.items.n_local
-        own = (items.long() % self.W) == self.rank
-        loc = torch.where(own, items.long() // self.W, torch.zeros_like(items, dtype=torch.long))
+        if self.W == 1:  # every item is local, row = id
+            own = torch.ones(items.shape, dtype=torch.bool, device=items.device)
+            loc = items.long()
+        else:
+            own = (items.long() % self.W) == self.rank
+            loc = torch.where(own, items.long() // self.W, torch.zeros_like(items, dtype=torch.long))
         if not self.prefill_items:
             # a first rating initialises the item: the index must take it in (one sync)
             if bool((own & ~self.valid[loc]).any()):
@@ -701,13 +706,14 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
                                              counter=self._neg_counter, device=self.device, known=self._known,
                                              known_count=self._known_cnt).view(-1, self.neg_rate).long()
             self._neg_counter += 1
-            nl = torch.where(negs >= 0, negs // self.W, torch.full_like(negs, -1))  # [n_own, neg_rate]
+            # [n_own, neg_rate] local rows, -1 = no negative drawn
+            nl = negs if self.W == 1 else torch.where(negs >= 0, negs // self.W, torch.full_like(negs, -1))
             nlt = nl.t().contiguous()  # phase-major
             for j in range(self.neg_rate):  # reference order: negatives first, then the rating
                 ops.mf_online_phase(U, rows_own, nlt[j], None, self.lr, W_, du, self._trained)
             touched.append(nlt.view(-1))
-        irow = torch.where(own, loc, torch.full_like(loc, -1))
-        ops.mf_online_phase(U, None, irow, rating, self.lr, W_, du, self._trained)
+        irow = loc if self.W == 1 else torch.where(own, loc, torch.full_like(loc, -1))
+        ops.mf_online_phase(U, None, irow.contiguous(), rating, self.lr, W_, du, self._trained)
         self._refresh_index(torch.cat(touched))
 
 
