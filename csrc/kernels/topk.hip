@@ -403,6 +403,55 @@ __global__ void seen_ring_update_kernel(int B, const int64_t* __restrict__ users
   if (r == n - 1) ring_cur[u] = c + n;
 }
 
+
+// Occurrence plan of a batch for the one-launch merge: su = users sorted (stable),
+// by_user = their entries.  Per entry: its round (0 for a user's first entry in the
+// batch ...), the position of its user's first entry in by_user and its user's
+// entry count.  One workgroup: each thread takes a contiguous chunk of sorted
+// positions; the run start carried into a chunk is an inclusive max-scan of the
+// chunks' last run starts, the run end a min-scan from the right.
+constexpr int RP_NT = 1024;
+
+__global__ void __launch_bounds__(RP_NT) round_plan_kernel(const int64_t* __restrict__ su,
+                                                           const int64_t* __restrict__ by_user, int B,
+                                                           int32_t* __restrict__ rnd, int32_t* __restrict__ first,
+                                                           int32_t* __restrict__ nu) {
+  __shared__ int32_t s_lo[RP_NT], s_hi[RP_NT];
+  const int t = threadIdx.x;
+  const int C = (B + RP_NT - 1) / RP_NT;
+  const int a = min(B, t * C), b = min(B, a + C);
+  int32_t last_start = -1, first_end = INT32_MAX;  // in this chunk
+  for (int i = a; i < b; ++i)
+    if (i == 0 || su[i] != su[i - 1]) last_start = i;
+  for (int i = b - 1; i >= a; --i)
+    if (i + 1 == B || su[i + 1] != su[i]) first_end = i + 1;  // a run ends after i
+  s_lo[t] = last_start;
+  s_hi[t] = first_end;
+  __syncthreads();
+  for (int o = 1; o < RP_NT; o <<= 1) {  // inclusive max-scan (left) and min-scan (right)
+    const int32_t lo = t >= o ? s_lo[t - o] : -1;
+    const int32_t hi = t + o < RP_NT ? s_hi[t + o] : INT32_MAX;
+    __syncthreads();
+    s_lo[t] = max(s_lo[t], lo);
+    s_hi[t] = min(s_hi[t], hi);
+    __syncthreads();
+  }
+  int32_t start = t > 0 ? s_lo[t - 1] : -1;  // the run start carried into this chunk
+  for (int i = a; i < b; ++i) {
+    if (i == 0 || su[i] != su[i - 1]) start = i;
+    const int64_t e = by_user[i];
+    rnd[e] = i - start;
+    first[e] = start;
+  }
+  int32_t end = t + 1 < RP_NT ? s_hi[t + 1] : B;  // the run end carried in from the right
+  if (end == INT32_MAX) end = B;
+  for (int i = b - 1; i >= a; --i) {
+    if (i + 1 == B || su[i + 1] != su[i]) end = i + 1;
+    const int64_t e = by_user[i];
+    nu[e] = end - first[e];  // first[e] was written by this thread above
+  }
+}
+
 }  // namespace
 
 // best_s / best_i: [B, k] sorted descending (start: -inf / -1); S: [B, n] with row stride ldS
@@ -448,6 +497,17 @@ FPS_API int fps_topk_seen_merge(const float* ss, const int64_t* ii, int B, int m
   FPS_CHECK_LAUNCH();
   hipLaunchKernelGGL(seen_ring_update_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, users, items, rnd, nu,
                      (const int64_t*)cpre, ring, ring_cur, M);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// su / by_user [B]: users sorted (stable) and their entries -> rnd / first / nu [B] int32
+// (round_plan_kernel); B <= 1M (one workgroup)
+FPS_API int fps_round_plan(const int64_t* su, const int64_t* by_user, int B, int32_t* rnd, int32_t* first,
+                           int32_t* nu, void* stream) {
+  if (B <= 0) return 0;
+  if (B > (1 << 20)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(round_plan_kernel, dim3(1), dim3(RP_NT), 0, (hipStream_t)stream, su, by_user, B, rnd, first, nu);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -181,6 +181,9 @@ class RoundPlan:
         the user-sorted order -- no rounds, no host copy."""
         B = users.numel()
         self.fused = fused
+        if fused and users.is_cuda and B <= (1 << 20):  # one kernel after the sort
+            self.by_user, self.rnd, self.first, self.nu = ops.round_plan(users)
+            return
         if fused:
             by_user = torch.argsort(users, stable=True)
             su = users[by_user]

@@ -1054,6 +1054,23 @@ def index_refresh(rows: torch.Tensor, pos: torch.Tensor, W: torch.Tensor, vecs: 
                                           N.stream_ptr(W.device)), "index_refresh")
 
 
+def round_plan(users: torch.Tensor):
+    """``(by_user, rnd, first, nu)`` of a batch of users (GPU, one launch after the sort,
+    ``topk.hip`` ``round_plan_kernel``): ``by_user`` = entries stably sorted by user,
+    ``rnd[e]`` = e's occurrence round, ``first[e]`` = position in ``by_user`` of the
+    first entry of e's user, ``nu[e]`` = that user's entry count (int32)."""
+    B = users.numel()
+    if not users.is_cuda or B > (1 << 20):
+        raise ValueError("round_plan: a cuda tensor of at most 2^20 users")
+    su, by_user = torch.sort(users.long(), stable=True)
+    rnd = torch.empty(B, dtype=torch.int32, device=users.device)
+    first = torch.empty_like(rnd)
+    nu = torch.empty_like(rnd)
+    N.check(N.require().fps_round_plan(su.data_ptr(), by_user.data_ptr(), B, rnd.data_ptr(), first.data_ptr(),
+                                       nu.data_ptr(), N.stream_ptr(users.device)), "round_plan")
+    return by_user, rnd, first, nu
+
+
 def topk_seen_merge(ss: torch.Tensor, ii: torch.Tensor, K: int, users: torch.Tensor, items: torch.Tensor,
                     rnd: torch.Tensor, first: torch.Tensor, nu: torch.Tensor, by_user: torch.Tensor,
                     ring: torch.Tensor, ring_cur: torch.Tensor):

@@ -141,3 +141,17 @@ def test_online_learner_and_generator_gpu_matches_per_record():
         assert (u, it, ts) == (ru, rit, rts)
         assert [x[1] for x in lst] == [x[1] for x in rlst], ts
         np.testing.assert_allclose([x[0] for x in lst], [x[0] for x in rlst], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("B", [1, 5, 1000, 4096, 70_000])
+def test_round_plan_kernel_equals_torch_plan(B):
+    """``ops.round_plan`` (one workgroup after the sort) == the torch form of the fused
+    RoundPlan, including long runs across thread chunks."""
+    g = torch.Generator(device=DEV).manual_seed(B)
+    users = torch.randint(0, max(2, B // 3), (B,), device=DEV, generator=g)
+    if B > 100:
+        users[: B // 2] = 17  # one run covering many chunks
+    by_user, rnd, first, nu = ops.round_plan(users)
+    ref = RoundPlan(users.cpu(), fused=True)  # the torch path (CPU)
+    assert torch.equal(by_user.cpu(), ref.by_user)
+    assert torch.equal(rnd.cpu(), ref.rnd) and torch.equal(first.cpu(), ref.first) and torch.equal(nu.cpu(), ref.nu)
