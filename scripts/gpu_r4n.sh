@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4n
 mkdir -p $O
 step() { name=$1; shift; timeout -k 10 ${T:-300} "$@" > $O/$name.log 2>&1 || { echo "FAIL $name"; tail -30 $O/$name.log; exit 1; }; echo "$name: $(grep -v amdgpu.ids $O/$name.log | tail -1 | cut -c1-${W:-300})"; }
-T=600 step tests python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+T=600 step tests python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread
 for st in length coord lc:1.3; do step topk_$st python bench/bench_topk.py --strategy $st; done
 step mf_topk python bench/bench_mf_topk.py
 step mf_topk2 python bench/bench_mf_topk.py
