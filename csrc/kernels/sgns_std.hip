@@ -57,9 +57,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
                                                        const int32_t* __restrict__ pos_neg, int64_t P, int D, int k,
                                                        float lr, float* __restrict__ d_in, float* __restrict__ d_out,
                                                        float* __restrict__ loss, int chunk,
-                                                       float* __restrict__ gbuf, const int32_t* __restrict__ rpc,
-                                                       const int32_t* __restrict__ rpo,
-                                                       const int32_t* __restrict__ rpn) {
+                                                       float* __restrict__ gbuf) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t p0 = wave * chunk;
@@ -82,7 +80,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
     if (c != cur) {  // a new center run: push the previous run's change, load this center
       flush();
       cur = c;
-      const float* src = rows_in + (int64_t)(rpc != nullptr ? rpc[p] : c) * D;
+      const float* src = rows_in + (int64_t)c * D;
 #pragma unroll
       for (int m = 0; m < NPL; ++m) {
         const int j = lane + 64 * m;
@@ -95,20 +93,17 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
 #pragma unroll
     for (int m = 0; m < NPL; ++m) dh[m] = 0.f;
     for (int x0 = 0; x0 <= k; x0 += SG) {  // x = 0: the context, x >= 1: negative x-1
-      int32_t row[SG], rrow[SG];
+      int32_t row[SG];
       float xv[SG][NPL], part[SG];
 #pragma unroll
       for (int q = 0; q < SG; ++q) {
         const int x = x0 + q;
         row[q] = x == 0 ? o : (x <= k ? pos_neg[p * k + x - 1] : -1);
         if (x > 0 && row[q] == o) row[q] = -1;  // word2vec skips a negative equal to the target
-        // the row read: the delta row itself, or its table row (rpo / rpn: zero-copy serve)
-        rrow[q] = row[q] < 0 ? 0 : (x == 0 ? (rpo != nullptr ? rpo[p] : o)
-                                            : (rpn != nullptr ? rpn[p * k + x - 1] : row[q]));
       }
 #pragma unroll
       for (int q = 0; q < SG; ++q) {  // all loads of the group in flight
-        const float* src = rows_out + (int64_t)rrow[q] * D;
+        const float* src = rows_out + (int64_t)(row[q] < 0 ? 0 : row[q]) * D;
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
           const int j = lane + 64 * m;
@@ -252,13 +247,9 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 // Sorted form, pass 1: centers as in fps_sgns_standard (d_in), output-row
 // coefficients into gbuf[P * (k + 1)] (zeroed by the caller; skipped negatives
 // stay 0).
-// rpc / rpo / rpn (nullable, all or none): the rows to READ for the centers, contexts and
-// negatives when they differ from the delta rows pos_* (the PS path's zero-copy serve:
-// the pulled rows are the shard itself, the deltas per unique key).
 FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, const int32_t* pos_c,
                                    const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
-                                   float* d_in, float* loss, float* gbuf, const int32_t* rpc, const int32_t* rpo,
-                                   const int32_t* rpn, void* stream) {
+                                   float* d_in, float* loss, float* gbuf, void* stream) {
   if (P <= 0) return 0;
   if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
   const int chunk = 16;
@@ -268,7 +259,7 @@ FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, 
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGC(NPL_)                                                                                            \
   hipLaunchKernelGGL((sgns_std_kernel<NPL_, true>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, loss, chunk, gbuf, rpc, rpo, rpn)
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, loss, chunk, gbuf)
   if (D <= 64) FPS_SGC(1);
   else if (D <= 128) FPS_SGC(2);
   else if (D <= 256) FPS_SGC(4);
@@ -318,8 +309,7 @@ FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGS(NPL_)                                                                                            \
   hipLaunchKernelGGL((sgns_std_kernel<NPL_, false>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, loss, chunk, (float*)nullptr,             \
-                     (const int32_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr)
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, loss, chunk, (float*)nullptr)
   if (D <= 64) FPS_SGS(1);
   else if (D <= 128) FPS_SGS(2);
   else if (D <= 256) FPS_SGS(4);

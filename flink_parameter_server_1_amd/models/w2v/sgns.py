@@ -81,9 +81,6 @@ class DistributedSGNS:
         # both, so the SGNS tables always de-duplicate
         self.ps_in.dedup_mode = True
         self.ps_out.dedup_mode = True
-        # world 1: the kernels read the shards in place (no gather of the unique rows;
-        # the deltas stay per unique key and are pushed as before)
-        self.ps_in.zero_copy_rows = self.ps_out.zero_copy_rows = cfg.mode == "standard"
         # PS path: both tables planned together (one count exchange per micro-batch),
         # one micro-batch ahead (lookahead): the host reads counts enqueued a step
         # earlier and never idles the device; staleness 1 when pipelined
@@ -188,19 +185,12 @@ class DistributedSGNS:
         dev = rows_in.device
         d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
         d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
-        pos_c = plan_in.pos.contiguous()
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
-        read_pos = None
-        if plan_in.row_map is not None and plan_out.row_map is not None:  # zero-copy serve: read the shards
-            read_pos = (plan_in.row_map[pos_c.long()], plan_out.row_map[pos_o.long()],
-                        plan_out.row_map[pos_neg.long()])
-        elif plan_in.row_map is not None or plan_out.row_map is not None:
-            raise RuntimeError("SGNS: both tables zero-copy or neither")
         with stage("sgns.step", self.timer):
             if self.standard:
-                loss = ops.sgns_standard(rows_in.float(), rows_out.float(), pos_c, pos_o, pos_neg,
-                                         c.negatives, lr, d_in, d_out, with_loss=with_loss, read_pos=read_pos)
+                loss = ops.sgns_standard(rows_in.float(), rows_out.float(), plan_in.pos.contiguous(), pos_o, pos_neg,
+                                         c.negatives, lr, d_in, d_out, with_loss=with_loss)
             else:
                 loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
                                      c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,

@@ -758,7 +758,7 @@ SGNS_METHODS = ("sorted", "atomic")
 
 
 def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d_in, d_out,
-                  with_loss: bool = False, method: Optional[str] = None, read_pos=None):
+                  with_loss: bool = False, method: Optional[str] = None):
     """Standard skip-gram negative sampling (K6, ``kernels/sgns_std.hip``): ``k``
     independent negatives per pair (``pos_neg[P * k]``), word2vec's objective.
     ``d_in`` / ``d_out`` receive the deltas (the tables themselves on the local
@@ -775,32 +775,11 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
       (``rows_in``; on the PS path the pulled rows).
     * ``method="atomic"``: Hogwild float atomics per pair and row, inside the pass.
 
-    ``read_pos = (rpc, rpo, rpn)`` (optional, same shapes as ``pos_c`` / ``pos_o`` /
-    ``pos_neg``): the rows of ``rows_in`` / ``rows_out`` to READ when they differ from
-    the delta rows ``pos_*`` -- the PS path's zero-copy serve, where the pulled rows
-    are the shard itself and the deltas are per unique key (sorted method only).
-
     CPU: the mini-batch form."""
     P = pos_c.numel()
     D = rows_in.shape[1]
     if pos_neg.numel() != P * k:
         raise ValueError("sgns_standard: pos_neg needs k rows per pair")
-    if read_pos is not None:
-        rpc, rpo, rpn = read_pos
-        if rpc.numel() != P or rpo.numel() != P or rpn.numel() != P * k or \
-                any(t.dtype != torch.int32 for t in read_pos):
-            raise ValueError("sgns_standard: read_pos = int32 (rpc [P], rpo [P], rpn [P * k])")
-        if not rows_in.is_cuda:  # the torch twin: the gathered serve (one row per delta position)
-            g_in = torch.zeros_like(d_in)
-            g_in[pos_c.long()] = rows_in[rpc.long()]
-            g_out = torch.zeros_like(d_out)
-            g_out[pos_o.long()] = rows_out[rpo.long()]
-            g_out[pos_neg.long()] = rows_out[rpn.long()]
-            rows_in, rows_out, read_pos = g_in, g_out, None
-        if DEBUG:
-            check_index(rpc, rows_in.shape[0], "sgns_standard rpc")
-            check_index(rpo, rows_out.shape[0], "sgns_standard rpo")
-            check_index(rpn, rows_out.shape[0], "sgns_standard rpn")
     if rows_in.is_cuda:
         for t in (rows_in, rows_out, d_in, d_out):
             if t.dtype != torch.float32:
@@ -811,24 +790,18 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
         method = method or os.environ.get("FPS_SGNS_METHOD", "sorted")
         if method not in SGNS_METHODS:
             raise ValueError(f"sgns_standard: method must be one of {SGNS_METHODS}")
-        if read_pos is not None and method != "sorted":
-            raise ValueError("sgns_standard: read_pos needs the sorted method")
         if method == "sorted":
             lib = N.require()
             s = N.stream_ptr(rows_in.device)
             k1 = int(k) + 1
             gbuf = torch.zeros(P * k1, dtype=torch.float32, device=rows_in.device)
-            rp = [None, None, None] if read_pos is None else [_c(t) for t in read_pos]
             N.check(lib.fps_sgns_standard_coef(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                                _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
-                                               _c(d_in).data_ptr(), N.ptr(loss), gbuf.data_ptr(), N.ptr(rp[0]),
-                                               N.ptr(rp[1]), N.ptr(rp[2]), s), "sgns_coef")
+                                               _c(d_in).data_ptr(), N.ptr(loss), gbuf.data_ptr(), s), "sgns_coef")
             keys = torch.cat([pos_o.reshape(P, 1), pos_neg.reshape(P, int(k))], dim=1).reshape(-1)
             srow, perm = torch.sort(keys.to(torch.int32))
-            centers = pos_c if rp[0] is None else rp[0]  # pass 2 reads the center rows
-            N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(),
-                                      _c(centers).data_ptr(), k1, P * k1, _c(rows_in).data_ptr(), D,
-                                      _c(d_out).data_ptr(), s), "sgns_rows")
+            N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
+                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), s), "sgns_rows")
             return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,

@@ -65,9 +65,6 @@ class PullPlan:
     #: with atomics instead of the unique-key read-modify-write
     unique: bool = True
     ready: Optional[object] = None  # event to wait for before the plan's device data is read
-    #: zero-copy serve (``TensorPS.zero_copy_rows``): the pulled "rows" are the shard
-    #: itself and unique key j lives at its row ``row_map[j]`` (int32)
-    row_map: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -135,12 +132,6 @@ class TensorPS:
         #: rows are the table): for owners whose workers only READ the pulled rows and
         #: accept reading them fresher than served (never staler: the bound still holds)
         self.zero_copy_identity = False
-        #: world 1, dense shard, de-duplicating plans: serve the shard itself instead of
-        #: gathering the unique rows, with ``plan.row_map`` telling the consumer where
-        #: unique key j lives (the consumer reads the rows in place; its deltas stay per
-        #: unique key).  For consumers that take a row map (SGNS); the read happens when
-        #: the consumer computes -- never staler than the gathered copy would be
-        self.zero_copy_rows = False
 
     @property
     def stats(self) -> dict:
@@ -370,23 +361,12 @@ class TensorPS:
         return self.plan_end(self.plan_begin(keys, flag, dedup))
 
     # --------------------------------------------------------------------- pull
-    def _zero_copy_rows(self, plan: PullPlan) -> bool:
-        return (self.zero_copy_rows and self.comm.world == 1 and not plan.identity and plan.valid is None
-                and plan.unique and isinstance(self.table, ShardedTable) and not self.table.sentinel
-                and self.table.optimizer != "fn" and self.wire_dtype == self.table.weight.dtype)
-
     def serve(self, plan: PullPlan) -> torch.Tensor:
         with stage("ps.serve", self.timer):
             if plan.recv_rows is None:  # dense shards: the local key is the row; sparse: lookup-or-insert
                 plan.recv_rows = self.table.rows_for(plan.recv_keys)[0]
             touched = getattr(self.table, "touched", None)
             sentinel = getattr(self.table, "sentinel", False)
-            if self._zero_copy_rows(plan):
-                rows = plan.recv_rows[: plan.n_unique]
-                plan.row_map = rows if rows.dtype == torch.int32 else rows.to(torch.int32)
-                if touched is not None:
-                    ops.mark_rows(touched, plan.row_map)
-                return self.table.weight
             if not plan.identity or (touched is None and not sentinel):
                 return self.table.serve_rows(plan.recv_rows, self.wire_dtype)
             # identity plan: every row is served, only the keys present count as pulled
@@ -404,8 +384,6 @@ class TensorPS:
     def pull_planned(self, plan: PullPlan, async_op: bool = False):
         """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``."""
         served = self.serve(plan)
-        if plan.row_map is not None:  # zero-copy (world 1): the shard itself, nothing to move
-            return (served, None) if async_op else served
         with stage("ps.answer-a2a", self.timer):
             if async_op:
                 return self.comm.all_to_all_async(served, plan.recv_splits, plan.send_splits)

@@ -369,41 +369,3 @@ def test_sgns_ps_path_steady_state_never_idles_the_device_on_counts(pipeline):
         assert stalls == [0, 0], stalls
     else:  # both tables' counts share one event: the first plan_end waits, the second finds it done
         assert stalls[0] >= 10 and stalls[1] == 0, stalls
-
-
-@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
-def test_sgns_ps_zero_copy_serve_equals_gathered_serve(device):
-    """World 1, PS path: the kernels read the shards in place (``TensorPS.zero_copy_rows``,
-    ``plan.row_map`` -> ``sgns_standard(read_pos=...)``) instead of the gathered unique
-    rows.  Synchronous (no pipeline) the two serve the same values: embeddings agree to
-    float-atomic summation order, the dumps cover the same rows, and the zero-copy
-    plans really took the in-place path."""
-    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
-        synthetic_corpus
-    from flink_parameter_server_1_amd.parallel.comm import Comm
-
-    out = {}
-    c, o = skipgram_pairs(synthetic_corpus(30000, 3000, seed=1, device=device), 4)  # the same pairs for both
-    for zc in (True, False):
-        m = DistributedSGNS(SGNSConfig(vocab_size=3000, dim=64, learning_rate=0.01, local_direct=False,
-                                       pipeline=False), comm=Comm(device=torch.device(device)))
-        m.ps_in.zero_copy_rows = m.ps_out.zero_copy_rows = zc
-        seen_map = []
-        orig = m._compute
-
-        def spy(rows, plans, payload, _orig=orig, _seen=seen_map):
-            _seen.append(all(p.row_map is not None for p in plans))
-            return _orig(rows, plans, payload)
-
-        m.pipe.compute = spy
-        for i in range(6):
-            s = (i * 2048) % (c.numel() - 2048)
-            m.step(c[s:s + 2048], o[s:s + 2048])
-        m.flush()
-        ids, w = m.embeddings()
-        o_ = torch.argsort(ids)
-        out[zc] = (ids[o_].cpu(), w[o_].cpu(), m.w_out.weight.cpu().clone(), seen_map)
-    assert torch.equal(out[True][0], out[False][0])
-    torch.testing.assert_close(out[True][1], out[False][1], rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(out[True][2], out[False][2], rtol=1e-4, atol=1e-6)
-    assert out[True][3] and all(out[True][3]) and not any(out[False][3])
