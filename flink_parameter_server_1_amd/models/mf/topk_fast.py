@@ -33,6 +33,13 @@ import torch
 from ... import ops
 
 
+def _row_norms(Q: torch.Tensor) -> torch.Tensor:
+    """|q| per row.  ``torch.linalg.vector_norm`` over the rows of a [4096, 64] batch ran
+    as a 60 us reduction kernel (``profiles/r4_mf_topk_fused_kernel_stats.csv``); the
+    bounds that use it carry a relative slack, so the summation order is free."""
+    return Q.square().sum(1).sqrt_()
+
+
 class LempTopK:
     #: items scored unfused first (their merge sets every query's k-th best)
     seed_items = 4096
@@ -151,7 +158,7 @@ class LempTopK:
                 return res
             self.overflows += 1
             fused = False
-        qlen = torch.linalg.vector_norm(Q, dim=1)
+        qlen = _row_norms(Q)
         if fused and self.sync_free and N > max(self.seed_items, start):
             st = None if state is None else (state[0].clone(), state[1].clone())
             if self._uses_coord():
@@ -263,7 +270,7 @@ class LempTopK:
         gc.disable()  # a collection on this thread inside the capture could free a pinned buffer / event
         try:
             with torch.cuda.graph(graph):
-                best_s, best_i, ovf = self._scan(q_in, torch.linalg.vector_norm(q_in, dim=1), k, capturing=True)[:3]
+                best_s, best_i, ovf = self._scan(q_in, _row_norms(q_in), k, capturing=True)[:3]
         except RuntimeError as e:  # a launch that cannot be captured: stay eager for this index
             import warnings
 
