@@ -55,17 +55,46 @@ def _write_stamp(target: str, digest: str):
         f.write(digest + "\n")
 
 
+#: per-source code-generation flags.  score_bf16.hip: MFMA accumulators in VGPRs (the
+#: default form kept them in AGPRs, and every 32 x 32 block's filter first copied its 16
+#: scores out with v_accvgpr_read: 16 of the ~30 vector instructions per 4 MFMAs)
+PER_FILE_FLAGS = {"score_bf16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build_kernels(force: bool = False, verbose: bool = True) -> str:
+    """One object per source (compiled in parallel, each with its own digest stamp:
+    a change rebuilds only its file), linked into one shared object."""
+    from concurrent.futures import ThreadPoolExecutor
+
     os.makedirs(OUT, exist_ok=True)
+    objdir = os.path.join(OUT, "obj")
+    os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
     target = os.path.join(OUT, "libfps_kernels.so")
-    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-munsafe-fp-atomics",
-             "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels")]
-    digest = _digest(srcs + hdrs, " ".join(flags))
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-Wno-unused-result",
+             "-I", os.path.join(CSRC, "kernels")]
+
+    def obj(src):
+        extra = PER_FILE_FLAGS.get(os.path.basename(src), [])
+        o = os.path.join(objdir, os.path.basename(src) + ".o")
+        d = _digest([src] + hdrs, " ".join(flags + extra))
+        if force or not _up_to_date(o, d):
+            cmd = [_hipcc()] + flags + extra + ["-c", src, "-o", o + ".tmp"]
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(o + ".tmp", o)
+            _write_stamp(o, d)
+        return o
+
+    workers = int(os.environ.get("MAX_JOBS", "8"))
+    with ThreadPoolExecutor(max_workers=max(1, min(workers, 16))) as ex:
+        objs = list(ex.map(obj, srcs))
+    digest = _digest(objs, "link")
     if not force and _up_to_date(target, digest):
         return target
-    cmd = [_hipcc()] + flags + srcs + ["-o", target + ".tmp"]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", target + ".tmp"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
