@@ -77,7 +77,7 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 // block, item block) pairs scored / skipped by the coordinate bound (pairs the length
 // bound skips by itself are in neither).
 template <int D, int QB, bool MASK = false, bool COORD = false>
-__global__ void __launch_bounds__(256) score_filter_bf16_kernel(
+__global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
     float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
