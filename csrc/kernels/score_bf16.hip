@@ -79,7 +79,7 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 template <int D, int QB, bool MASK = false, bool COORD = false>
 __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
-    const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xlen,
+    const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xbm,
     float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
     const int32_t* __restrict__ qf, const float* __restrict__ qbf, const float2* __restrict__ cb,
     int32_t* __restrict__ stats, const int32_t* __restrict__ gate) {
@@ -102,9 +102,11 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   const int r = lane & 31, h = lane >> 5;
 
   // LEMP bound per workgroup: no query of the tile can be beaten by the range's
-  // longest item -> the whole workgroup leaves before any load of X
+  // longest item -> the whole workgroup leaves before any load of X.  xbm[b] = the
+  // longest item of 32-item block b (one value per MFMA block: a scalar load in the
+  // loop below instead of a per-lane length load and a 64-lane max per block)
   float xm = 0.f;
-  for (int i = i_begin + tid; i < i_end; i += 256) xm = fmaxf(xm, xlen[i]);
+  for (int b = (i_begin >> 5) + tid; b < ((i_end + 31) >> 5); b += 256) xm = fmaxf(xm, xbm[b]);
   xm = group_max<64>(xm);
   if (lane == 0) red[wave] = xm;
   __syncthreads();
@@ -156,7 +158,7 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   int scored = 0, skipped = 0;
   // software pipeline: block i0 + 32 is requested before block i0's MFMAs
   uint4 xv[S];
-  float xl;
+  float xl;        // the next block's longest item (wave-uniform)
   float2 cbv[QB];  // COORD: this block's range of each query's focus coordinate (prefetched with xv)
   {
     const int i = i_begin + r;
@@ -164,7 +166,7 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
 #pragma unroll
     for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
-    xl = ok ? xlen[i] : 0.f;
+    xl = xbm[i_begin >> 5];
     if (COORD && use_coord) {
 #pragma unroll
       for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)(i_begin / 32) * D + fq[b]];
@@ -179,14 +181,14 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
 #pragma unroll
       for (int b = 0; b < QB; ++b) cbc[b] = cbv[b];
     }
-    const float bm = group_max<64>(xl);  // longest item of this block
+    const float bm = xl;  // longest item of this block
     if (i0 + 32 < i_end) {
       const int i = i0 + 32 + r;
       const bool ok = i < i_end;
       const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
 #pragma unroll
       for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
-      xl = ok ? xlen[i] : 0.f;
+      xl = xbm[(i0 + 32) >> 5];
       if (COORD && use_coord) {  // the next block's coordinate ranges: no dependent load before the bound
 #pragma unroll
         for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)((i0 + 32) / 32) * D + fq[b]];
@@ -349,18 +351,18 @@ FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, i
   return 0;
 }
 
-// Qb [B, D], Xb [N, D] bf16 (uint16 storage, RNE from the fp32 vectors); qlen [B],
-// xlen [N] the fp32 norms; cand_pos [B, cap] int64 receives item positions (0..N-1),
+// Qb [B, D], Xb [N, D] bf16 (uint16 storage, RNE from the fp32 vectors); qlen [B] the
+// fp32 query norms, xbm [ceil(N / 32)] the longest fp32 item norm of every 32-item block; cand_pos [B, cap] int64 receives item positions (0..N-1),
 // cnt [B] (zeroed by the caller) counts every candidate.  D in {32, 64, 128}.
 // COORD bound (optional, all or none): qf [B] focus coordinates, qbf [B] = q_f / |q|,
 // cb [N / 32][D] float2 coordinate ranges of the 32-item blocks (N a multiple of 32
 // or the last block's range over its items); stats (optional) = 2 counters.
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
-                                  int k, const float* qlen, const float* xlen, float margin, float slack,
+                                  int k, const float* qlen, const float* xbm, float margin, float slack,
                                   int64_t* cand_pos, int32_t* cnt, int cap, const int32_t* qf, const float* qbf,
                                   const float2* cb, int32_t* stats, const int32_t* gate, void* stream) {
   if (B <= 0 || N <= 0) return 0;
-  if (k <= 0 || cap <= 0 || qlen == nullptr || xlen == nullptr) return (int)hipErrorInvalidValue;
+  if (k <= 0 || cap <= 0 || qlen == nullptr || xbm == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nit = (N + SB_ITEMS - 1) / SB_ITEMS;
   const bool coord = qf != nullptr && qbf != nullptr && cb != nullptr;
@@ -370,11 +372,11 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
     if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
     if (coord)                                                                                              \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true>), dim3((unsigned)(nqt * nit)),    \
-                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
+                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
                          cap, qf, qbf, cb, stats, gate);                                                    \
     else                                                                                                    \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false>), dim3((unsigned)(nqt * nit)),   \
-                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xlen, margin, slack, cand_pos, cnt, \
+                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
                          cap, qf, qbf, cb, stats, gate);                                                    \
   }
   // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4

@@ -352,6 +352,9 @@ class LempTopK:
         cnt = torch.empty(B, dtype=torch.int32, device=dev)
         ovf = torch.zeros(1, dtype=torch.int32, device=dev)
         Qb = Q.bfloat16() if self.bf16 else None
+        # the longest item of every 32-item block (the scorer's per-block length bound),
+        # recomputed per scan: update_rows / refresh_from change the lengths in place
+        xbm = ops.block_max32(self.lengths) if self.bf16 else None
         coord = self._coord_inputs(Q, qlen, bounds) if self.bf16 else None
         if coord is not None:
             self._coord_gate.fill_(1)
@@ -362,15 +365,17 @@ class LempTopK:
             if self.break_check and j and j % self.break_check == 0 and not capturing and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
+            assert s % 32 == 0, "fused segments start on 32-item blocks"
             self.buckets_scanned += len(range(-(-s // self.bucket) * self.bucket, e, self.bucket))
             if self.bf16:
                 seg_coord = None
                 if coord is not None and self._coord_segment(s, e):
                     qf, qbf = coord
                     seg_coord = (qf, qbf, self._cb[s // 32: -(-e // 32)])
-                ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, self.lengths[s:e],
+                ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, None,
                                       coord=seg_coord, stats=self.coord_stats if seg_coord is not None else None,
-                                      gate=self._coord_gate if seg_coord is not None else None)
+                                      gate=self._coord_gate if seg_coord is not None else None,
+                                      xbm=xbm[s // 32: -(-e // 32)])
                 if seg_coord is not None:
                     ops.coord_gate(self.coord_stats, self._coord_prev, self._coord_gate)
                 # (re-score fused into the rank merge, one query per workgroup: 59 us against

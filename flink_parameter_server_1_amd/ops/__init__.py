@@ -906,9 +906,20 @@ def coord_block_bounds(X: torch.Tensor, xlen: torch.Tensor) -> torch.Tensor:
     return torch.stack([xn.amin(1), xn.amax(1)], 2).contiguous()
 
 
+def block_max32(xlen: torch.Tensor) -> torch.Tensor:
+    """``[ceil(n / 32)]`` max of every 32 consecutive entries (the last block over its own)."""
+    n = xlen.numel()
+    nb = -(-n // 32)
+    x = xlen.float()
+    if nb * 32 != n:
+        x = torch.cat([x, x.new_zeros(nb * 32 - n)])
+    return x.view(nb, 32).amax(1)
+
+
 def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, cand_pos: torch.Tensor,
-                      cnt: torch.Tensor, qlen: torch.Tensor, xlen: torch.Tensor, coord=None,
-                      stats: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None) -> None:
+                      cnt: torch.Tensor, qlen: torch.Tensor, xlen: Optional[torch.Tensor], coord=None,
+                      stats: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
+                      xbm: Optional[torch.Tensor] = None) -> None:
     """Candidate filter on bf16 MFMA (GPU only, K8 fast path): every item ``i`` whose bf16
     score can exceed ``best_s[b, -1]`` (margin ``bf16_score_margin(D) |q_b| max|x|``) gets
     its position appended to row ``b`` of ``cand_pos`` ``[B, cap]`` (int64); ``cnt[b]``
@@ -923,8 +934,12 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     cap = cand_pos.shape[1]
     if Qb.dtype != torch.bfloat16 or Xb.dtype != torch.bfloat16 or Xb.shape[1] != D or D not in BF16_SCORE_DIMS:
         raise ValueError(f"score_filter_bf16: bf16 [B, D] / [n, D] with D in {BF16_SCORE_DIMS}")
+    if xbm is None:  # the kernel reads the longest item of every 32-item block
+        if xlen is None or xlen.numel() != n:
+            raise ValueError("score_filter_bf16: xlen [n] or xbm [ceil(n / 32)]")
+        xbm = block_max32(xlen)
     if best_s.shape[0] != B or cnt.numel() != B or cand_pos.dtype != torch.int64 or qlen.numel() != B \
-            or xlen.numel() != n:
+            or xbm.numel() != -(-n // 32):
         raise ValueError("score_filter_bf16: shape mismatch")
     qf = qbf = cb = None
     if coord is not None:
@@ -937,7 +952,7 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     slack = 1.0 + 1e-4 + D * 2.4e-7
     N.check(N.require().fps_score_filter_bf16(
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
-        _c(qlen.float()).data_ptr(), _c(xlen.float()).data_ptr(), bf16_score_margin(D), slack,
+        _c(qlen.float()).data_ptr(), _c(xbm.float()).data_ptr(), bf16_score_margin(D), slack,
         _c(cand_pos).data_ptr(), _c(cnt).data_ptr(), cap, N.ptr(qf), N.ptr(qbf), N.ptr(cb), N.ptr(stats),
         N.ptr(gate), N.stream_ptr(Qb.device)), "score_filter_bf16")
 
