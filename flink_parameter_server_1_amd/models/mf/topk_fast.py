@@ -365,7 +365,6 @@ class LempTopK:
             if self.break_check and j and j % self.break_check == 0 and not capturing and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):
                 break
-            assert s % 32 == 0, "fused segments start on 32-item blocks"
             self.buckets_scanned += len(range(-(-s // self.bucket) * self.bucket, e, self.bucket))
             if self.bf16:
                 seg_coord = None
@@ -375,7 +374,8 @@ class LempTopK:
                 ops.score_filter_bf16(Qb, self.vecs_bf[s:e], best_s, ci, cnt, qlen, None,
                                       coord=seg_coord, stats=self.coord_stats if seg_coord is not None else None,
                                       gate=self._coord_gate if seg_coord is not None else None,
-                                      xbm=xbm[s // 32: -(-e // 32)])
+                                      xbm=xbm[s // 32: -(-e // 32)] if s % 32 == 0
+                                      else ops.block_max32(self.lengths[s:e]))
                 if seg_coord is not None:
                     ops.coord_gate(self.coord_stats, self._coord_prev, self._coord_gate)
                 # (re-score fused into the rank merge, one query per workgroup: 59 us against
