@@ -44,6 +44,7 @@ def main():
                     help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
                          "timing, host-timed delay + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
+    ap.add_argument("--no-overlap", action="store_true", help="sub-steps on one stream (MFConfig.overlap_substeps)")
     a = ap.parse_args()
 
     import torch
@@ -57,7 +58,8 @@ def main():
     for W in [int(x) for x in a.ws.split(",")]:
         cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
                        exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0,
-                       emulate_link_gbps=a.link_gbps, emulate_latency_us=a.latency_us)
+                       emulate_link_gbps=a.link_gbps, emulate_latency_us=a.latency_us,
+                       overlap_substeps=not a.no_overlap)
         m = DistributedMF(cfg, comm)
         data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
         s = 0
@@ -84,6 +86,7 @@ def main():
                           "user_phases": getattr(m, "user_phases", None),
                           "link_gbps": a.link_gbps if W > 1 else None, "latency_us": a.latency_us if W > 1 else None,
                           "comm_wait_ms_per_step": wait, "exposed_fraction": wait / ms,
+                          "overlap_substeps": not a.no_overlap,
                           "link_bytes_per_step": (m.rot.bytes_sent / (a.steps + a.warmup)) if W > 1 else 0}),
               flush=True)
         if W > 1:

@@ -79,6 +79,8 @@ class MFConfig:
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
     rotation: str = "bidir"           # rotate: "bidir" (two counter-rotating rings) | "ring" (one ring)
+    overlap_substeps: bool = True     # rotate, tiled: sub-steps alternate two compute streams, so sub-step
+                                      # s + 1 (other item blocks) fills the tail of s (same users: Hogwild)
     emulate_world: int = 0            # W = 1, rotate: rank 0's share of an N-rank job (users / schedule)
     emulate_link_gbps: float = 0.0    # emulate_world: model the transfers on links of this rate (0: none)
     emulate_latency_us: float = 5.0   # emulate_world: per-message link latency
@@ -197,6 +199,9 @@ class DistributedMF:
             # (a priority stream for the SGD and CU-masked streams splitting the CUs
             # between them were measured slower and removed, profiles/r2_partition.md)
             self._side = torch.cuda.Stream(dev) if (self._prefetch or ps_spec) else None
+            # rotation sub-steps on alternating streams (``MFConfig.overlap_substeps``)
+            self._overlap = cfg.overlap_substeps and self.exchange == "rotate" and dev.type == "cuda"
+            self._aux = torch.cuda.Stream(dev) if self._overlap else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
             self._local_blocks = [self.items.weight[:h0], self.items.weight[h0:]]
@@ -395,22 +400,58 @@ class DistributedMF:
                                           c.learning_rate, c.lam, user_sc1=self.user_sc1)
             return
         nb = 2 * self.rot_w  # item blocks per user phase in the partition layout
-        for _ in range(self.rot.K):
-            with stage("mf.rotate.begin", self.timer):
-                self.rot.begin()  # transfer of the next blocks overlaps this sub-step
-            with stage("mf.sgd", self.timer):
-                act = self.rot.active_blocks()
-                for p in range(self.user_phases):
-                    if len(act) == 2:  # one block of each ring: disjoint items, one launch
-                        (g0, b0), (g1, b1) = act
-                        ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                              c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1)
-                    else:
-                        (g0, b0), = act
-                        ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                         c.learning_rate, c.lam, user_sc1=self.user_sc1)
-            with stage("mf.rotate.end", self.timer):
-                self.rot.end()
+
+        def sub_step():
+            act = self.rot.active_blocks()
+            for p in range(self.user_phases):
+                if len(act) == 2:  # one block of each ring: disjoint items, one launch
+                    (g0, b0), (g1, b1) = act
+                    ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
+                                          c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1)
+                else:
+                    (g0, b0), = act
+                    ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
+                                     c.learning_rate, c.lam, user_sc1=self.user_sc1)
+
+        if not self._overlap:
+            for _ in range(self.rot.K):
+                with stage("mf.rotate.begin", self.timer):
+                    self.rot.begin()  # transfer of the next blocks overlaps this sub-step
+                with stage("mf.sgd", self.timer):
+                    sub_step()
+                with stage("mf.rotate.end", self.timer):
+                    self.rot.end()
+            return
+        # Sub-steps alternate two compute streams: sub-step s + 1 updates other item
+        # blocks, so it may start in the tail of s (a launch of ~2k workgroups leaves the
+        # CUs half idle for its last round).  Stream roles per sub-step s on `cur`:
+        #   begin(s) is posted from the stream of s - 1: its sends carry the blocks s - 1
+        #     finished, so they must follow s - 1 and only s - 1;
+        #   end(s) waits for the transfers from the stream of s + 1, the one that reads
+        #     the arriving blocks.
+        # The first sub-step's blocks leave their rest state on `main`; `main` joins the
+        # other stream after the last sub-step.
+        main = torch.cuda.current_stream(self.U.device)
+        aux = self._aux
+        aux.wait_stream(main)  # the partition (staged event) and the previous step
+        streams = (main, aux)
+        for s in range(self.rot.K):
+            cur, prev, nxt = streams[s % 2], streams[(s - 1) % 2], streams[(s + 1) % 2]
+            with torch.cuda.stream(cur if s == 0 else prev):
+                with stage("mf.rotate.begin", self.timer):
+                    self.rot.begin()
+            if s == 0:
+                aux.wait_stream(main)  # sub-step 1 on aux reads blocks that left rest on main
+            with torch.cuda.stream(cur):
+                with stage("mf.sgd", self.timer):
+                    sub_step()
+            with torch.cuda.stream(nxt):
+                with stage("mf.rotate.end", self.timer):
+                    # the next sub-step's stream waits for the arriving blocks; this one
+                    # too: it posts the next transfers, whose receives reuse the buffers
+                    # these transfers' sends read
+                    self.rot.end(also=(cur,))
+        main.wait_stream(aux)
 
     def _item_deltas(self, rows, pos, n_unique, uid_local, rating, staged=None):
         """SGD of one micro-batch on its pulled item rows ``rows[pos[b]]``; returns

@@ -211,8 +211,12 @@ class RingRotation:
             self._works = self.comm.p2p(sends, recvs)
             self.bytes_sent += sum(x.numel() * x.element_size() for x, _ in sends)
 
-    def end(self):
-        """Finish a sub-step (after its compute was enqueued) and rotate roles."""
+    def end(self, also=()):
+        """Finish a sub-step (after its compute was enqueued) and rotate roles: the
+        current stream -- the one that reads the arriving blocks -- waits for this
+        sub-step's transfers, and so does every stream in ``also`` (with sub-steps on
+        alternating streams, the stream that posts the next transfers: its receives
+        reuse the buffers these sends read)."""
         if self._works:
             cuda = self.home_t.is_cuda
             if cuda:
@@ -228,6 +232,10 @@ class RingRotation:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
                 self._events.append((e0, e1))
+                for st in also:
+                    with torch.cuda.stream(st):
+                        for w in self._works:
+                            w.wait()
             else:
                 self._host_wait_s += time.perf_counter() - t0
         self._works = None
@@ -416,7 +424,7 @@ class EmulatedRotation:
                 self.bytes_sent += self.blocks[out_b].numel() * self.blocks[out_b].element_size()
             self._inflight = self.links.post(after, copies, link_bytes)
 
-    def end(self):
+    def end(self, also=()):
         if self._inflight is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -424,6 +432,8 @@ class EmulatedRotation:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             self._events.append((e0, e1))
+            for st in also:
+                st.wait_event(self._inflight["event"])
             self._inflight = None
         self.s += 1
 
