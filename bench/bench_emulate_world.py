@@ -10,7 +10,7 @@ same launches per sub-step as one GPU of the real job, without the transfers.
 Comparing the emulated step with the N = 1 step separates "compute slower at
 N" from "transfer exposed" before an N-GPU node runs the real thing.  With
 ``--link-gbps`` the transfers are modelled too (``rotation._SymmetricLinks``:
-rank-symmetric timing, a host-timed link delay and a real device copy per block)
+rank-symmetric timing, a device-timed link delay and a real device copy per block)
 and ``comm_wait_ms_per_step`` is the time the compute stream waited for them.
 
     python bench/bench_emulate_world.py [--ws 1,2,4,8] [--steps 20 --warmup 5]
@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--rotation", default="bidir", choices=["bidir", "ring"])
     ap.add_argument("--link-gbps", type=float, default=0.0,
                     help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
-                         "timing, host-timed delay + a real device copy); 0 = no transfers")
+                         "timing, a one-wave device sleep for the link time + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
     ap.add_argument("--no-overlap", action="store_true", help="sub-steps on one stream (MFConfig.overlap_substeps)")
     a = ap.parse_args()

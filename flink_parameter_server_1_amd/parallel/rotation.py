@@ -75,6 +75,28 @@ def layout_world(world: int, schedule: str) -> int:
     return 2 * world if schedule == "bidir" else world
 
 
+def _mark(stream=None) -> "torch.cuda.Event":
+    """A timing event recorded on ``stream`` (default: the current stream)."""
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(stream)
+    return e
+
+
+def _exposed_ms(events) -> float:
+    """Exposed transfer time of ``(e0, e1, ec)`` records: ``e0`` / ``e1`` bracket the
+    wait on the stream of the next sub-step, ``ec`` (or None) marks where the other
+    compute stream stood (the previous sub-step, still running).  With one compute
+    stream the exposure is the wait itself; with two, only the part of it after the
+    other stream's sub-step ended left the GPU without a sub-step to run."""
+    ms = 0.0
+    for e0, e1, ec in events:
+        d = e0.elapsed_time(e1)
+        if ec is not None:
+            d = min(d, ec.elapsed_time(e1))
+        ms += max(0.0, d)
+    return ms
+
+
 class _Ring:
     """One ring of ``2W`` blocks (see the module docstring)."""
 
@@ -220,8 +242,8 @@ class RingRotation:
         if self._works:
             cuda = self.home_t.is_cuda
             if cuda:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record()
+                ec = _mark(also[0]) if also else None  # where the other compute stream is now
+                e0 = _mark()
             else:
                 import time
 
@@ -229,9 +251,7 @@ class RingRotation:
             for w in self._works:
                 w.wait()
             if cuda:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record()
-                self._events.append((e0, e1))
+                self._events.append((e0, _mark(), ec))
                 for st in also:
                     with torch.cuda.stream(st):
                         for w in self._works:
@@ -244,9 +264,9 @@ class RingRotation:
         self.s += 1
 
     def wait_ms(self, reset: bool = True) -> float:
-        """Milliseconds the compute stream waited for transfers since the last call
-        (synchronises on the recorded events)."""
-        ms = self._host_wait_s * 1e3 + sum(a.elapsed_time(b) for a, b in self._events)
+        """Milliseconds the compute streams waited for transfers with nothing else to
+        run, since the last call (synchronises on the recorded events)."""
+        ms = self._host_wait_s * 1e3 + _exposed_ms(self._events)
         if reset:
             self._events, self._host_wait_s = [], 0.0
         return ms
@@ -276,89 +296,45 @@ class RingRotation:
 
 
 class _SymmetricLinks:
-    """Host-timed xGMI links of the emulated rank (``EmulatedRotation(link_gbps=...)``).
+    """Device-timed xGMI links of the emulated rank (``EmulatedRotation(link_gbps=...)``).
 
     In a rotation every rank runs the same schedule on equal work, so the block a
     rank receives in sub-step ``s`` is posted by its neighbour when the neighbour's
     sub-step ``s - 1`` ends -- the moment this rank's own ``s - 1`` ends.  A posted
-    transfer starts once that compute-stream event has completed, takes
-    ``latency + bytes / link_gbps`` on its link (the two rings' blocks travel on two
-    different links, in parallel), and is then issued as a real device copy (the send's
-    HBM read + the receive's HBM write of this GPU) on a high-priority link stream;
-    the compute stream waits for it before the sub-step that needs the block.  The
-    delay itself occupies no CU (a host timer).  Unlike the virtual world
-    (``parallel/vworld.py``), only the emulated rank computes, at the full speed of
-    its GPU, so the measured wait is the exposure of the real schedule under rank
-    symmetry rather than the skew of N ranks sharing one GPU."""
+    transfer runs on a high-priority link stream: it waits for that compute-stream
+    event, spends ``latency + bytes / link_gbps`` in a one-wave device sleep (the two
+    rings' blocks travel on two different links, in parallel), then a real device copy
+    of the block (the send's HBM read and the receive's HBM write of this GPU) -- all
+    enqueued at post time, so waiting on a transfer is a pure stream wait, as on RCCL
+    (no host thread, no host block).  Only the emulated rank computes, at the full
+    speed of its GPU: the measured wait is the exposure of the real schedule under
+    rank symmetry, not the skew of N ranks sharing one GPU (``parallel/vworld.py``)."""
 
     def __init__(self, device, link_gbps: float, latency_us: float):
-        import threading
+        from .vworld import _Sleep
 
+        self._sleep = _Sleep
         self.us_per_byte = 1e-3 / float(link_gbps)  # GB/s -> us per byte
         self.latency_us = float(latency_us)
-        self.stream = torch.cuda.Stream(device=device, priority=-1)
         self.device = device
-        self.cv = threading.Condition()
-        self.pending: list = []
-        self.closed = False
-        self.error = None
-        self.thread = threading.Thread(target=self._loop, name="emulated-links", daemon=True)
-        self.thread.start()
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
 
-    def post(self, after: "torch.cuda.Event", copies, link_bytes: int) -> dict:
-        import threading
+    def post(self, after: "torch.cuda.Event", copies, link_bytes: int) -> "torch.cuda.Event":
+        us = self.latency_us + link_bytes * self.us_per_byte
+        self.stream.wait_event(after)
+        with torch.cuda.stream(self.stream):
+            self._sleep.us(self.device, us)
+            for dst, src in copies:
+                dst.copy_(src, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        return done
 
-        item = {"after": after, "copies": copies, "us": self.latency_us + link_bytes * self.us_per_byte,
-                "t0": None, "done": threading.Event(), "event": None}
-        with self.cv:
-            self.pending.append(item)
-            self.cv.notify_all()
-        return item
-
-    def wait(self, item: dict) -> None:
-        """Host-wait until the transfer was issued, then make the compute stream wait for it."""
-        if not item["done"].wait(timeout=120.0):
-            raise RuntimeError("emulated link: transfer not issued within 120 s")
-        if self.error is not None:
-            raise RuntimeError(f"emulated link failed: {self.error}")
-        torch.cuda.current_stream().wait_event(item["event"])
-
-    def _loop(self) -> None:
-        import time
-
-        try:
-            torch.cuda.set_device(self.device)
-            while True:
-                with self.cv:
-                    if self.closed:
-                        return
-                    now = time.perf_counter()
-                    for item in list(self.pending):
-                        if item["t0"] is None:
-                            if item["after"].query():
-                                item["t0"] = now
-                            continue
-                        if now >= item["t0"] + item["us"] * 1e-6:
-                            self.pending.remove(item)
-                            with torch.cuda.stream(self.stream):
-                                for dst, src in item["copies"]:
-                                    dst.copy_(src, non_blocking=True)
-                                ev = torch.cuda.Event()
-                                ev.record(self.stream)
-                            item["event"] = ev
-                            item["done"].set()
-                    self.cv.wait(timeout=2e-5 if self.pending else 1e-3)
-        except Exception as e:  # surfaced by wait()
-            self.error = repr(e)
-            with self.cv:
-                for item in self.pending:
-                    item["done"].set()
+    def wait(self, done: "torch.cuda.Event") -> None:
+        torch.cuda.current_stream().wait_event(done)
 
     def close(self) -> None:
-        with self.cv:
-            self.closed = True
-            self.cv.notify_all()
-        self.thread.join(5.0)
+        pass
 
 
 class EmulatedRotation:
@@ -426,19 +402,17 @@ class EmulatedRotation:
 
     def end(self, also=()):
         if self._inflight is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
+            ec = _mark(also[0]) if also else None
+            e0 = _mark()
             self.links.wait(self._inflight)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            self._events.append((e0, e1))
+            self._events.append((e0, _mark(), ec))
             for st in also:
-                st.wait_event(self._inflight["event"])
+                st.wait_event(self._inflight)
             self._inflight = None
         self.s += 1
 
     def wait_ms(self, reset: bool = True) -> float:
-        ms = sum(a.elapsed_time(b) for a, b in self._events)
+        ms = _exposed_ms(self._events)
         if reset:
             self._events = []
         return ms
