@@ -236,6 +236,7 @@ def main(argv=None):
                 "unique_items_per_step_per_gpu": (model.ps.stats["unique"] / max(model.ps.stats["steps"], 1))
                 if model.exchange == "ps" else None,
                 "rotation": model.cfg.rotation if model.exchange == "rotate" else None,
+                "overlap_substeps": bool(getattr(model, "_overlap", False)),
                 "rotation_bytes_sent_rank0": model.rot.bytes_sent if model.exchange == "rotate" else None,
                 "comm_wait_ms_per_step": max(waits),
                 "comm_wait_ms_per_step_per_rank": waits,

@@ -44,7 +44,8 @@ def main():
                     help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
                          "timing, a one-wave device sleep for the link time + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
-    ap.add_argument("--no-overlap", action="store_true", help="sub-steps on one stream (MFConfig.overlap_substeps)")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="sub-steps on alternating compute streams (MFConfig.overlap_substeps; auto: from 4 ranks)")
     a = ap.parse_args()
 
     import torch
@@ -59,7 +60,7 @@ def main():
         cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
                        exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0,
                        emulate_link_gbps=a.link_gbps, emulate_latency_us=a.latency_us,
-                       overlap_substeps=not a.no_overlap)
+                       overlap_substeps={"auto": "auto", "on": True, "off": False}[a.overlap])
         m = DistributedMF(cfg, comm)
         data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
         s = 0
@@ -86,7 +87,7 @@ def main():
                           "user_phases": getattr(m, "user_phases", None),
                           "link_gbps": a.link_gbps if W > 1 else None, "latency_us": a.latency_us if W > 1 else None,
                           "comm_wait_ms_per_step": wait, "exposed_fraction": wait / ms,
-                          "overlap_substeps": not a.no_overlap,
+                          "overlap_substeps": bool(getattr(m, "_overlap", False)),
                           "link_bytes_per_step": (m.rot.bytes_sent / (a.steps + a.warmup)) if W > 1 else 0}),
               flush=True)
         if W > 1:

@@ -66,7 +66,7 @@ def lost_update_count(U, uid, v, users: int, nmax: int = 24, chunk: int = 200_00
 
 def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int = 0, lr: float = 1e-4,
                  count_updates: bool = True, user_update: str = "store", world: int = 1,
-                 overlap_substeps: bool = True) -> dict:
+                 overlap_substeps="auto") -> dict:
     """``users`` rows of ONE worker; ``world > 1``: that worker is rank 0 of a
     ``world``-GPU rotation job (``MFConfig(emulate_world=world)``: the same blocks,
     sub-steps and partition as one GPU of the real job, so the race is measured on
@@ -109,7 +109,7 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
     if world > 1 and hasattr(m.rot, "close"):
         m.rot.close()
     out = {"users": users, "items": items, "ratings": n, "ratings_per_user": per_user, "world": world,
-           "overlap_substeps": overlap_substeps if world > 1 else None,
+           "overlap_substeps": bool(getattr(m, "_overlap", False)) if world > 1 else None,
            "phases": getattr(m, "user_phases", None), "tile_rows": getattr(m, "tile_R", None), "user_update": cfg.user_update, "users_with_lost_update": int(lost.sum()),
            "rated_users": int(rated.sum()), "lost_user_fraction": float(lost.sum()) / max(int(rated.sum()), 1),
            "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())}
@@ -130,12 +130,14 @@ def main(argv=None):
     ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"])
     ap.add_argument("--no-count", action="store_true", help="skip the per-update least-squares count")
     ap.add_argument("--world", type=int, default=1, help="rank 0 of an N-GPU rotation job (emulated schedule)")
-    ap.add_argument("--no-overlap", action="store_true", help="world > 1: sub-steps on one stream")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="world > 1: sub-steps on alternating streams (auto: from 4 ranks)")
     a = ap.parse_args(argv)
     for p in [int(x) for x in a.phases.split(",")]:
         print(json.dumps(lost_updates(a.users, a.items, a.per_user, p, count_updates=not a.no_count,
                                       user_update=a.user_update, world=a.world,
-                                      overlap_substeps=not a.no_overlap)), flush=True)
+                                      overlap_substeps={"auto": "auto", "on": True,
+                                                        "off": False}[a.overlap])), flush=True)
 
 
 if __name__ == "__main__":

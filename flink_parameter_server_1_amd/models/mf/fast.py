@@ -79,8 +79,11 @@ class MFConfig:
     exchange: str = "auto"            # W > 1: "rotate" (item-block ring, default) | "ps" (pull/push);
                                       # W = 1: "local" (default); "rotate"/"ps" run those paths without peers
     rotation: str = "bidir"           # rotate: "bidir" (two counter-rotating rings) | "ring" (one ring)
-    overlap_substeps: bool = True     # rotate, tiled: sub-steps alternate two compute streams, so sub-step
-                                      # s + 1 (other item blocks) fills the tail of s (same users: Hogwild)
+    overlap_substeps: object = "auto"  # rotate, tiled: sub-steps alternate two compute streams, so sub-step
+                                      # s + 1 (other item blocks) fills the tail of s (same users: Hogwild).
+                                      # "auto": from 4 ranks on -- with 2 ranks a block takes ~40 % of a
+                                      # sub-step on the link and the overlap eats that slack
+                                      # (profiles/r4_emulate_overlap.jsonl)
     emulate_world: int = 0            # W = 1, rotate: rank 0's share of an N-rank job (users / schedule)
     emulate_link_gbps: float = 0.0    # emulate_world: model the transfers on links of this rate (0: none)
     emulate_latency_us: float = 5.0   # emulate_world: per-message link latency
@@ -200,7 +203,12 @@ class DistributedMF:
             # between them were measured slower and removed, profiles/r2_partition.md)
             self._side = torch.cuda.Stream(dev) if (self._prefetch or ps_spec) else None
             # rotation sub-steps on alternating streams (``MFConfig.overlap_substeps``)
-            self._overlap = cfg.overlap_substeps and self.exchange == "rotate" and dev.type == "cuda"
+            ov = cfg.overlap_substeps
+            if ov == "auto":
+                ov = Wn >= 4
+            elif not isinstance(ov, bool):
+                raise ValueError(f"overlap_substeps must be True, False or 'auto', not {ov!r}")
+            self._overlap = ov and self.exchange == "rotate" and dev.type == "cuda"
             self._aux = torch.cuda.Stream(dev) if self._overlap else None
             self._staged = None
             h0 = shard_halves(cfg.num_items, 1)[0]
