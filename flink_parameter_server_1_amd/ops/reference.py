@@ -62,6 +62,9 @@ def apply_rows(table, idx, delta, op="add", lr=0.0, eps=1e-10, state=None, touch
     delta = torch.where(delta == 0, torch.zeros_like(delta), delta)
     if touched is not None:
         touched[idx] = 1
+    if op == "add_unique" and idx.numel() and torch.unique(idx).numel() != idx.numel():
+        # the GPU kernel is a plain read-modify-write per row: repeated rows lose updates
+        raise ValueError("add_unique with repeated rows")
     if op in ("add", "add_unique"):
         table.index_add_(0, idx, delta)
     elif op == "set":

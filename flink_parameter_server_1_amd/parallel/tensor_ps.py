@@ -65,6 +65,10 @@ class PullPlan:
     #: with atomics instead of the unique-key read-modify-write
     unique: bool = True
     ready: Optional[object] = None  # event to wait for before the plan's device data is read
+    #: every peer's segment of ``recv_keys`` holds distinct keys (each peer chose a
+    #: de-duplicating plan; ranks choose per batch size, so a small batch on one rank
+    #: may arrive as a request plan at owners whose own plan de-duplicates)
+    recv_unique: bool = True
 
 
 @dataclass
@@ -242,6 +246,12 @@ class TensorPS:
                                static=True)
         return n, counts, uniq, pos, True
 
+    @staticmethod
+    def _wire_counts(counts: torch.Tensor, W: int, unique: bool) -> torch.Tensor:
+        """Per-peer counts as sent in the count exchange: ``2 * count + 1`` for a
+        request plan, so an owner knows which segments may repeat keys."""
+        return counts.view(W, 1).to(torch.int32) * 2 + (0 if unique else 1)
+
     def _pending(self, n, counts, uniq, pos, unique: bool = True, flag: int = 0) -> PendingPlan:
         """Stage A's count exchange of a computed (de-duplicated or request) plan."""
         W = self.comm.world
@@ -260,7 +270,7 @@ class TensorPS:
             self._plan_seq += 1
             return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
-        send = torch.cat([counts.view(W, 1).to(torch.int32), flags], dim=1).contiguous()  # [W, 2]
+        send = torch.cat([self._wire_counts(counts, W, unique), flags], dim=1).contiguous()  # [W, 2]
         with stage("ps.count-a2a", self.timer):
             recv = self.comm.exchange_counts(send)
         both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 4]
@@ -294,13 +304,15 @@ class TensorPS:
                     self._stats["host_stalls"] += 1
             pp.event.synchronize()
         sc, _, rc, rf = pp.cols
+        recv_unique = pp.unique
         if pp.host.dim() == 1:  # world 1
             c = int(pp.host[sc])
             send_splits, recv_splits, peer_flags = [c], [c], [pp.flag]
-        else:
+        else:  # counts travel as 2 * count + (request plan)
             h = pp.host.tolist()
-            send_splits = [int(r[sc]) for r in h]
-            recv_splits = [int(r[rc]) for r in h]
+            send_splits = [int(r[sc]) >> 1 for r in h]
+            recv_splits = [int(r[rc]) >> 1 for r in h]
+            recv_unique = not any(int(r[rc]) & 1 for r in h)
             peer_flags = [int(r[rf]) for r in h]
         n_unique = int(sum(send_splits))
         with stage("ps.key-a2a", self.timer):
@@ -308,7 +320,8 @@ class TensorPS:
         self._stats["pulls"] += pp.n
         self._stats["unique"] += n_unique
         self._stats["steps"] += 1
-        return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n, unique=pp.unique)
+        return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n, unique=pp.unique,
+                        recv_unique=recv_unique)
 
     @staticmethod
     def plan_begin_multi(pss: Sequence["TensorPS"], keys_list: Sequence[torch.Tensor], flag: int = 0,
@@ -333,7 +346,7 @@ class TensorPS:
             send = torch.cat([c[:1].to(torch.int32) for c in counts])  # [T]
             both = send
         else:
-            cols = [c.view(W, 1).to(torch.int32) for c in counts]
+            cols = [TensorPS._wire_counts(c, W, staged[j][4]) for c, j in zip(counts, dyn)]
             cols.append(torch.full((W, 1), int(flag), dtype=torch.int32, device=dev))
             send = torch.cat(cols, dim=1).contiguous()  # [W, T + 1]
             with stage("ps.count-a2a", pss[0].timer):
@@ -443,7 +456,7 @@ class TensorPS:
             self._stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
             # (a request plan repeats keys inside a segment: atomic add)
-            seg_add = opt == "add" and len(plan.recv_splits) <= 16 and plan.unique
+            seg_add = opt == "add" and len(plan.recv_splits) <= 16 and plan.unique and plan.recv_unique
             if opt == "fn":  # user rule: sequential over the source segments (keys repeat across them)
                 if fresh is not None:  # the id is absent only for its first push, in segment order
                     fresh = self._first_fresh(recv_keys, fresh)
