@@ -10,6 +10,12 @@ numbers measure the engine itself -- dedup, count exchange, key / row / delta
 all-to-alls, gather, apply, the host control loop -- as micro-batches/s and
 pulled+pushed keys/s per micro-batch size (the config #1 plumbing question on
 the device path).  Synthetic uniform keys.
+
+``--capacity`` switches to fixed-shape plans (``TensorPS.capacity`` = the batch
+size): at world > 1 no split size reaches the host and ``--graph`` captures the
+steps with their RCCL all-to-alls.  ``--loopback`` (world 1) runs those
+all-to-alls through a one-rank RCCL group, so a one-GPU box measures the captured
+world > 1 step shape with real RCCL kernels in it.
 """
 from __future__ import annotations
 
@@ -29,7 +35,10 @@ def main(argv=None):
     ap.add_argument("--batches", default="1,64,4096,262144")
     ap.add_argument("--seconds", type=float, default=2.0, help="timed seconds per micro-batch size")
     ap.add_argument("--staleness", type=int, default=0)
-    ap.add_argument("--graph", action="store_true", help="replay captured hipGraph steps (world 1, core.step_graph)")
+    ap.add_argument("--graph", action="store_true", help="replay captured hipGraph steps (core.step_graph)")
+    ap.add_argument("--capacity", action="store_true", help="fixed-shape plans, capacity = the batch size")
+    ap.add_argument("--loopback", action="store_true",
+                    help="world 1: all-to-alls through a one-rank RCCL group (implies --capacity)")
     a = ap.parse_args(argv)
 
     import torch
@@ -41,6 +50,21 @@ def main(argv=None):
 
     comm = Comm.init_from_env()
     dev = comm.device
+    if a.loopback:
+        import socket
+
+        import torch.distributed as dist
+
+        if comm.world != 1 or dev.type != "cuda":
+            raise SystemExit("--loopback is a one-GPU, world-1 mode")
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        comm = Comm(device=dev)
+        comm.loopback = True
+        a.capacity = True
 
     def sync():
         if dev.type == "cuda":
@@ -55,7 +79,7 @@ def main(argv=None):
         logic = DeviceSimplePSLogic(a.keys, a.dim, op="add", init=("zeros",))
         logic.emit = "none"
         rt = TensorRuntime(comm, staleness=a.staleness, output_sink=lambda e: None,
-                           graph=a.graph).start(worker, logic)
+                           graph=a.graph, capacity=B if a.capacity else None).start(worker, logic)
         g = torch.Generator(device=dev)
         g.manual_seed(11 + comm.rank)
         pool = [torch.randint(0, a.keys, (B,), generator=g, device=dev) for _ in range(8)]
@@ -83,10 +107,22 @@ def main(argv=None):
         dt = comm.max_over_ranks(time.perf_counter() - t0)
         results.append({"batch": B, "steps": steps, "graph_replays": rt.graphs.replays if rt.graphs else 0, "micro_batches_per_s": steps / dt,
                         "keys_per_s": comm.world * steps * B / dt, "us_per_step": dt / steps * 1e6})
+        if rt.graphs is not None:
+            rt.graphs.release()
+        del rt
+    if a.loopback:  # the graphs that reference the communicator are gone: tear it down
+        import gc
+
+        import torch.distributed as dist
+
+        gc.collect()
+        sync()
+        dist.destroy_process_group()
     if comm.rank == 0:
         print(json.dumps({"metric": "tensor-engine plumbing: micro-batches/s and keys/s (whole node)",
                           "n_gpus": comm.world, "dtype": "fp32", "data": "synthetic uniform keys",
-                          "config": {"keys": a.keys, "dim": a.dim, "staleness": a.staleness, "graph": a.graph}, "results": results}),
+                          "config": {"keys": a.keys, "dim": a.dim, "staleness": a.staleness, "graph": a.graph,
+                                     "fixed_plans": bool(a.capacity), "rccl_loopback": a.loopback}, "results": results}),
               flush=True)
 
 

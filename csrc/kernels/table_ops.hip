@@ -57,6 +57,13 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
   row_coords<TPR>(r, step, j0);
   for (; r < n; r += step) {
     const int64_t row = (int64_t)idx[r];
+    if (row < 0) {  // padding slot of a fixed-shape plan: a zero row, nothing marked
+      for (int j = j0; j < D; j += TPR) {
+        if (OUT_BF16) ((uint16_t*)out)[r * D + j] = 0;
+        else ((float*)out)[r * D + j] = 0.f;
+      }
+      continue;
+    }
     const float* src = table + row * D;
     for (int j = j0; j < D; j += TPR) {
       const float v = src[j];
@@ -135,6 +142,14 @@ __global__ void __launch_bounds__(256) gather_rows_v4_kernel(const to_f4* __rest
   row_coords<TPR>(r, step, j0);
   for (; r < n; r += step) {
     const int64_t row = (int64_t)idx[r];
+    if (row < 0) {  // padding slot of a fixed-shape plan
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const int j = j0 + q * TPR;
+        if (j < D4) out[r * D4 + j] = to_f4{0.f, 0.f, 0.f, 0.f};
+      }
+      continue;
+    }
     const to_f4* src = table + row * D4;
     to_f4 v[NV];
 #pragma unroll
@@ -463,7 +478,7 @@ namespace {
 // touched[rows[i]] = 1 (close-time dump bookkeeping of the in-place update paths)
 __global__ void mark_rows_kernel(uint8_t* __restrict__ touched, const int32_t* __restrict__ rows, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    touched[rows[i]] = 1;
+    if (rows[i] >= 0) touched[rows[i]] = 1;  // < 0: a padding slot
 }
 }  // namespace
 

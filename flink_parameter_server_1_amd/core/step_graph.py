@@ -1,4 +1,4 @@
-"""hipGraph replay of the tensor engine's fixed-shape micro-batch step (world 1).
+"""hipGraph replay of the tensor engine's fixed-shape micro-batch step.
 
 At small micro-batches the tensor engine is bound by its host control loop:
 every ``submit`` runs the worker's Python callbacks, the dedup / gather /
@@ -9,7 +9,11 @@ amortise -- it processes one record per message (``M/FlinkParameterServer.scala:
 queries) needs it gone.  With static world-1 plans (``TensorPS.static``) the
 whole step -- plan, pull, the worker's ``on_pull_recv_batch``, push, apply --
 has shapes fixed by the batch's shapes and issues no host sync, so it can be
-captured once into a hipGraph and replayed:
+captured once into a hipGraph and replayed.  At world > 1 the fixed-shape plans
+of ``TensorPS.capacity`` do the same (every exchange has host-known, constant
+splits), and the step's three RCCL all-to-alls are captured with it; the peers'
+end-of-input flags are read from the replayed step's buffer one micro-batch
+later (``BoundedStalenessPipeline.poll_flags``):
 
 * the first ``warmup`` micro-batches of a new shape signature run eagerly
   (they size the workspaces); the next is captured on the capture stream
@@ -27,7 +31,8 @@ callbacks must be a pure device function of the batch and of device state --
 no host syncs, no Python-side state that changes per micro-batch (the
 replayed step does not run Python).  Workers declare it with
 ``graph_safe = True``.  Anything that would make a captured step wrong makes
-the runtime run eagerly instead: world > 1, a non-static plan, staleness or
+the runtime run eagerly instead: world > 1 without fixed-shape plans or over a
+host-staged (gloo) transport, a non-static plan, staleness or
 lookahead (the pipeline carries state across ``submit`` calls), locking or
 sequential-combine PS logics, sparse (growing) shards, arbitrary pushes, a
 stage timer or ``FPS_DEBUG``.  A capture that fails (a callback synced)
@@ -112,11 +117,12 @@ def _tensor_attrs(obj) -> Dict[str, torch.Tensor]:
 
 
 class _Entry:
-    __slots__ = ("graph", "inputs", "emits", "counters", "stats", "held")
+    __slots__ = ("graph", "inputs", "emits", "counters", "stats", "held", "flags")
 
-    def __init__(self, graph, inputs, emits, counters, stats, held):
+    def __init__(self, graph, inputs, emits, counters, stats, held, flags=None):
         self.graph, self.inputs, self.emits = graph, inputs, emits
         self.counters, self.stats, self.held = counters, stats, held
+        self.flags = flags  # fixed-shape plans: the peers' flags in the graph's receive buffer
 
 
 class StepGraphs:
@@ -131,6 +137,7 @@ class StepGraphs:
         self.disabled_trace: Optional[str] = None
         self.replays = 0
         self.captures = 0
+        self.released = False  # after ``release``: every later step runs eagerly
 
     # ----------------------------------------------------------- eligibility
     def why_not(self) -> Optional[str]:
@@ -139,15 +146,18 @@ class StepGraphs:
         ps_logic, ps = rt.ps_logic, rt.ps_logic.ps if rt.ps_logic is not None else None
         if rt.device.type != "cuda":
             return "not on a GPU"
-        if rt.comm.world != 1:
-            return "world > 1 (plans need host-known split sizes)"
+        collective = rt.comm.world != 1 or getattr(rt.comm, "loopback", False)
+        if collective and not (ps is not None and ps.fixed()):
+            return "world > 1 without fixed-shape plans (TensorRuntime(capacity=...)): split sizes are host-read"
+        if collective and rt.comm.backend != "nccl":
+            return "only RCCL collectives can be captured (gloo stages through host memory)"
         if ops.DEBUG:
             return "FPS_DEBUG range checks sync"
         if rt.pipe is None or ps_logic.locking:
             return "locking PS logic (per-round host decisions)"
         if rt.pipe.staleness != 0 or rt.pipe.lookahead:
             return "staleness / lookahead pipelines carry state across submits"
-        if not getattr(ps, "static", False):
+        if not (getattr(ps, "static", False) or ps.fixed()):
             return "plan is not static"
         if getattr(ps_logic.table, "sparse", False):
             return "sparse shards grow (reallocate) under a captured step"
@@ -160,6 +170,13 @@ class StepGraphs:
         if not getattr(rt.worker_logic, "graph_safe", False):
             return "the worker logic does not declare graph_safe = True"
         return None
+
+    def release(self) -> None:
+        """Destroy the captured graphs (their memory pools, and the RCCL work baked into
+        them: a communicator is only torn down once no graph references it)."""
+        self.entries.clear()
+        self.seen.clear()
+        self.released = True
 
     # --------------------------------------------------------------- running
     def _held(self) -> List[Tuple[Any, str, torch.Tensor]]:
@@ -174,7 +191,7 @@ class StepGraphs:
 
     def submit(self, batch: Any, flag: int) -> bool:
         """Run ``batch`` through a captured step if possible; False = run it eagerly."""
-        if self.disabled is not None or batch is None or flag:
+        if self.disabled is not None or self.released or batch is None or flag:
             return False
         leaves: List[torch.Tensor] = []
         sig = _flatten(batch, leaves)
@@ -227,6 +244,7 @@ class StepGraphs:
             rt.ps_logic.ps.stats.clear()
             rt.ps_logic.ps.stats.update(s0)
             rt.pipe.submitted = sub0
+            rt.pipe._flags_dev = None
             return None
         finally:
             rt._capture_emits = None
@@ -240,7 +258,8 @@ class StepGraphs:
         for k, v in ds.items():
             rt.ps_logic.ps.stats[k] -= v
         rt.pipe.submitted = sub0
-        e = _Entry(g, inputs, emits, dc, ds, self._held())
+        flags, rt.pipe._flags_dev = rt.pipe._flags_dev, None  # the capture executed nothing
+        e = _Entry(g, inputs, emits, dc, ds, self._held(), flags)
         self.entries[sig] = e
         self.captures += 1
         return e
@@ -250,6 +269,9 @@ class StepGraphs:
         for dst, src in zip(e.inputs, leaves):
             dst.copy_(src, non_blocking=True)
         e.graph.replay()
+        if e.flags is not None:
+            rt.pipe._flags_dev = e.flags
+            rt.pipe.poll_flags()
         for k, v in e.counters.items():
             rt.counters.c[k] += v
         st = rt.ps_logic.ps.stats

@@ -200,9 +200,12 @@ class TensorRuntime:
 
     def __init__(self, comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
                  output_sink: Optional[Callable[[Any], None]] = None, lookahead: Optional[bool] = None,
-                 graph: bool = False):
+                 graph: bool = False, capacity: Optional[int] = None):
         """``graph``: replay fixed-shape micro-batch steps from captured hipGraphs
-        (``core.step_graph``; world 1, static plans, a ``graph_safe`` worker)."""
+        (``core.step_graph``: static plans at world 1, fixed-shape plans over RCCL at
+        world > 1, a ``graph_safe`` worker).  ``capacity``: the most keys this rank
+        pulls per micro-batch -- fixed-shape plans (``TensorPS.capacity``: no host
+        copy of split sizes; required by ``graph`` at world > 1)."""
         self.comm = comm or Comm()
         self.device = self.comm.device
         self.staleness = int(staleness)
@@ -216,6 +219,7 @@ class TensorRuntime:
         self.ps_logic: Optional[DevicePSLogic] = None
         self._started = False
         self.graph = bool(graph)
+        self.capacity = capacity
         self.graphs: Optional[StepGraphs] = None
         self._capture_emits: Optional[List[Any]] = None
 
@@ -231,8 +235,11 @@ class TensorRuntime:
         if ps_logic.locking:
             self.pipe = None
         else:
-            # world 1 on the GPU: static plans, so no micro-batch waits on the device
-            ps_logic.ps.static = c.world == 1 and self.device.type == "cuda"
+            # world 1 on the GPU: static plans, so no micro-batch waits on the device;
+            # fixed-shape plans wherever a capacity is given and static plans are not used
+            ps_logic.ps.capacity = self.capacity
+            ps_logic.ps.static = c.world == 1 and self.device.type == "cuda" and \
+                (self.capacity is None or not getattr(c, "loopback", False))
             self.pipe = BoundedStalenessPipeline(ps_logic.ps, self._compute, self.staleness,
                                                  lookahead=self.lookahead)
         self._started = True
@@ -474,6 +481,8 @@ class TensorRuntime:
         outputs collected on this rank (empty with an ``output_sink``)."""
         if self.pipe is not None:
             self.pipe.drain()
+        if self.graphs is not None:  # no replays after the end: free the graphs now
+            self.graphs.release()
         with stage("engine.close", self.timer):
             self.worker_logic.close(self.client)
             for out in self.ps_logic.close():
@@ -485,7 +494,7 @@ class TensorRuntime:
 
     def _run_phase(self, source: Iterable) -> None:
         it = iter(source)
-        self.pipe.all_flagged = False
+        self.pipe.reset_flags()
         done = False
         while True:
             if not done:

@@ -39,6 +39,9 @@ class PAConfig:
     partition: str = "range"      # range | hash
     wire_dtype: str = "fp32"
     local_direct: bool = True     # W = 1: the PA kernel reads / atomically updates the table in place
+    #: the most feature requests (nnz) a rank submits per micro-batch: fixed-shape PS
+    #: plans (``TensorPS.capacity``: no split sizes on the host, capturable steps)
+    capacity: Optional[int] = None
 
 
 class DistributedPA:
@@ -68,7 +71,7 @@ class DistributedPA:
         logic = Logic(cfg.feature_count, self.L, **kw) if cfg.partition == "range" else \
             Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
         self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
-        self.runtime = TensorRuntime(self.comm, staleness=0).start(self.worker, logic)
+        self.runtime = TensorRuntime(self.comm, staleness=0, capacity=cfg.capacity).start(self.worker, logic)
         self.timer = None  # utils.metrics.StageTimer (optional)
 
     @property

@@ -77,19 +77,21 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
         N.check(N.require().fps_mark_rows(touched.data_ptr(), _c(rows.to(torch.int32)).data_ptr(), rows.numel(),
                                           N.stream_ptr(touched.device)), "mark_rows")
         return
-    touched[rows.long()] = 1
+    r = rows.long()
+    touched[r[r >= 0]] = 1
 
 
 def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
                 touched: torch.Tensor = None, flip: bool = False) -> torch.Tensor:
-    """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2).
+    """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2);
+    ``idx[r] < 0`` (a padding slot of a fixed-shape plan) serves a zero row.
     The HIP kernel serves fp32 tables; fp64 tables (the bit-parity configuration
     against the per-record engine's doubles) take the torch twin on any device.
     ``flip``: served entries holding the untouched sentinel -0.0 become +0.0 in the
     table (``ShardedTable(touch_sentinel=True)``)."""
     n = idx.numel()
     if DEBUG:
-        check_index(idx, table.shape[0], "gather_rows")
+        check_index(idx, table.shape[0], "gather_rows", allow_negative=True)
     d = table.shape[1]
     if out is None:
         out = torch.empty((n, d), dtype=out_dtype, device=table.device)
@@ -1121,6 +1123,7 @@ def flip_sentinel(table: torch.Tensor, rows: torch.Tensor) -> None:
     """Torch twin of the kernels' untouched-row sentinel flip: entries of ``table[rows]``
     holding -0.0 become +0.0 (``ShardedTable(touch_sentinel=True)``)."""
     r = rows.long()
+    r = r[r >= 0]  # padding slots
     x = table[r]
     table[r] = torch.where((x == 0) & torch.signbit(x), torch.zeros_like(x), x)
 

@@ -45,10 +45,13 @@ def init_values(ids: torch.Tensor, dim: int, lo: float, hi: float, seed: int) ->
 
 
 def gather_rows(table, idx, out_dtype=torch.float32, touched=None):
+    """``table[idx]``; idx < 0 (a padding slot) serves a zero row and marks nothing."""
     idx = idx.long()
+    keep = idx >= 0
     if touched is not None:
-        touched[idx] = 1
-    return table[idx].to(out_dtype)
+        touched[idx[keep]] = 1
+    out = table[idx.clamp_min(0)].to(out_dtype)
+    return torch.where(keep.view(-1, *([1] * (out.dim() - 1))), out, torch.zeros_like(out))
 
 
 OPS = {"add": 0, "set": 1, "sgd": 2, "adagrad": 3}

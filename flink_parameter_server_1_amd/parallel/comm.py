@@ -46,6 +46,9 @@ class Comm:
                 device = torch.device("cpu")
         self.device = torch.device(device)
         self.bytes_sent = 0
+        #: run the all-to-alls through the process group even at world 1 (a one-rank
+        #: RCCL group on a one-GPU box: exercises captured RCCL collectives in tests)
+        self.loopback = False
         #: bytes this rank put on the wire to each peer (all-to-alls + point-to-point)
         self.peer_bytes = [0] * self.world
 
@@ -107,7 +110,7 @@ class Comm:
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Variable-split all-to-all along dim 0 (rows of any trailing shape)."""
         n_out = int(sum(recv_splits))
-        if self.world == 1:
+        if self.world == 1 and not self.loopback:
             if out is None:  # nothing leaves the rank: hand the buffer through
                 return send[:n_out]
             out[:n_out].copy_(send[:n_out])
@@ -129,7 +132,7 @@ class Comm:
         """Non-blocking all-to-all: returns ``(out, work)``; ``work.wait()`` orders the
         caller's stream after the transfer (no host block).  ``work`` is None at world 1."""
         n_out = int(sum(recv_splits))
-        if self.world == 1:
+        if self.world == 1 and not self.loopback:
             return send[:n_out], None
         if self._staged(send):  # host-staged transport is synchronous
             return self.all_to_all(send, send_splits, recv_splits), None

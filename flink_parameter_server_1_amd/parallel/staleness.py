@@ -32,7 +32,8 @@ receives / returns lists (rows, plans, deltas) in table order.
 End of input: every ``submit`` carries a ``flag`` that reaches all peers with
 the counts; ``all_flagged`` turns True on every rank at the same micro-batch once
 every rank flagged it (the ``FlinkEOF`` barrier, ``M/utils/FlinkEOF.scala:97-107``,
-without an extra collective).
+without an extra collective).  Fixed-shape plans keep the flags on the device; they
+reach the host one ``submit`` later (``poll_flags``), the same micro-batch on every rank.
 """
 from __future__ import annotations
 
@@ -65,6 +66,8 @@ class BoundedStalenessPipeline:
         self.max_observed = 0  # pushes of earlier batches still pending when a pull was served
         self.all_flagged = False
         self.submitted = 0
+        self._flags_dev: Optional[torch.Tensor] = None  # newest fixed plan's peer flags (device)
+        self._flags_host = None  # (pinned copy, event) of the previous one
 
     def submit(self, keys: torch.Tensor, payload: Any = None, flag: int = 0, presence=None) -> List[Any]:
         """Begin the pull of a new micro-batch; finish (compute + push) every
@@ -81,7 +84,38 @@ class BoundedStalenessPipeline:
             self._pull_next()
         while len(self._pulled) > self.staleness:
             out.append(self._finish(self._pulled.popleft()))
+        self.poll_flags()
         return out
+
+    def poll_flags(self) -> None:
+        """Fixed-shape plans: read the previous pulled plan's peer flags (copied to
+        pinned memory one ``submit`` ago: by now the device is past them) and start
+        the copy of the newest.  Every rank reads the same plan's flags at the same
+        ``submit``, so ``all_flagged`` turns on everywhere at once, one micro-batch
+        after the flags were sent.  A replayed hipGraph step calls this itself."""
+        dev = self._flags_dev
+        if dev is None or (dev.is_cuda and torch.cuda.is_current_stream_capturing()):
+            return
+        if self._flags_host is not None:
+            host, ev = self._flags_host
+            if ev is not None:
+                ev.synchronize()
+            if all(int(f) != 0 for f in host.tolist()):
+                self.all_flagged = True
+        self._flags_dev = None
+        if dev.is_cuda:
+            host = torch.empty(tuple(dev.shape), dtype=dev.dtype, pin_memory=True)
+            host.copy_(dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = dev.clone(), None
+        self._flags_host = (host, ev)
+
+    def reset_flags(self) -> None:
+        """A new input phase: forget every flag seen so far."""
+        self.all_flagged = False
+        self._flags_dev, self._flags_host = None, None
 
     def drain(self) -> List[Any]:
         out = []
@@ -108,7 +142,9 @@ class BoundedStalenessPipeline:
         if not self.multi:
             pps = [pps]
         plans = [ps.plan_end(pp) for ps, pp in zip(self.pss, pps)]
-        if plans[0].peer_flags and all(f != 0 for f in plans[0].peer_flags):
+        if plans[0].flags_dev is not None:
+            self._flags_dev = plans[0].flags_dev
+        elif plans[0].peer_flags and all(f != 0 for f in plans[0].peer_flags):
             self.all_flagged = True
         pulled = [ps.pull_planned(plan, async_op=True) for ps, plan in zip(self.pss, plans)]
         self.max_observed = max(self.max_observed, len(self._pulled))

@@ -26,6 +26,15 @@ Replaces the reference's per-record Flink iteration
     9. owners apply them (K3: add / set / sgd / adagrad / add_renorm).
 
 ``world == 1`` keeps the same code path with local copies instead of RCCL.
+
+Fixed-shape plans (``TensorPS.capacity``): every rank sends every peer exactly
+``C`` key slots per micro-batch with its (count, flag) in a two-int header --
+one all-to-all of ``[W, C + 2]`` int32 replaces the count exchange, its host copy
+and the key all-to-all; padding slots carry key -1 (served as zero rows, skipped
+by the apply).  No split size is ever needed on the host, so a micro-batch step
+has fixed shapes and can be captured with its RCCL collectives into a hipGraph
+(``core.step_graph``); peers' end-of-input flags reach the host one micro-batch
+later (``BoundedStalenessPipeline.poll_flags``).
 Staleness: every request in a micro-batch reads the table as of step 6;
 ``parallel.staleness.BoundedStalenessPipeline`` orders the stages of several
 micro-batches so pull ``k`` is served before the pushes of ``k-s .. k-1``
@@ -69,6 +78,9 @@ class PullPlan:
     #: de-duplicating plan; ranks choose per batch size, so a small batch on one rank
     #: may arrive as a request plan at owners whose own plan de-duplicates)
     recv_unique: bool = True
+    #: fixed-shape plan: the peers' flags stay on the device (``[W]`` int32)
+    flags_dev: Optional[torch.Tensor] = None
+    fixed: bool = False
 
 
 @dataclass
@@ -93,6 +105,8 @@ class PendingPlan:
     #: columns of ``host`` holding (sent count, sent flag, recv count, recv flag): several
     #: tables planned together (``plan_begin_multi``) share one exchange and one host copy
     cols: tuple = (0, 1, 2, 3)
+    #: fixed-shape plan: the received ``[W, C + 2]`` header + key slots
+    fixed: Optional[torch.Tensor] = None
 
 
 class TensorPS:
@@ -136,6 +150,14 @@ class TensorPS:
         #: rows are the table): for owners whose workers only READ the pulled rows and
         #: accept reading them fresher than served (never staler: the bound still holds)
         self.zero_copy_identity = False
+        #: fixed-shape plans (module docstring): the most keys a rank plans per
+        #: micro-batch.  ``C`` = this capacity for request plans, capped at the largest
+        #: shard for de-duplicating ones; the plan kind is chosen from the capacity, so
+        #: every rank picks the same.  Each exchange then moves ``W * C`` rows instead of
+        #: the unique keys: for the small, host-bound micro-batches.  Used by
+        #: ``plan_begin`` (the pipelined path); ``plan()`` keeps dynamic plans.
+        self.capacity: Optional[int] = None
+        self._slots: Optional[torch.Tensor] = None
 
     @property
     def stats(self) -> dict:
@@ -152,11 +174,11 @@ class TensorPS:
             self._lazy = {}
         return self._stats
 
-    def _count_lazy(self, key: str, valid: torch.Tensor) -> None:
+    def _count_lazy(self, key: str, valid: torch.Tensor, bound: Optional[int] = None) -> None:
         if valid.is_cuda and torch.cuda.is_current_stream_capturing():
             # a captured step (core.step_graph) replays its host-side increments: count the
             # bound there (a device counter inside the graph would not be read per replay)
-            self._stats[key] += valid.numel()
+            self._stats[key] += valid.numel() if bound is None else bound
             return
         n = valid.sum()
         self._lazy[key] = n if key not in self._lazy else self._lazy[key] + n
@@ -184,26 +206,78 @@ class TensorPS:
         return (self.static and self.comm.world == 1 and not getattr(self.table, "sparse", False)
                 and getattr(self.table, "partition", "") != "lookup" and n >= int(self.table.key_space))
 
+    def fixed(self) -> bool:
+        """Does ``plan_begin`` make fixed-shape plans?"""
+        return self.capacity is not None and not self.static and not getattr(self.table, "sparse", False)
+
+    def fixed_slots(self, unique: bool) -> int:
+        """``C``: key slots per peer of a fixed-shape plan (the same on every rank)."""
+        C = int(self.capacity)
+        if unique:  # de-duplicated keys to one owner: at most its shard's rows
+            t = self.table
+            C = min(C, max(t.part.shard_size(t.num_ids, r) for r in range(self.comm.world)))
+        return max(C, 1)
+
+    def _fixed_plan(self, keys: torch.Tensor, flag: int, dedup: Optional[bool]) -> PendingPlan:
+        """Stage A of a fixed-shape plan: dedup (or route), slot layout, and the one
+        ``[W, C + 2]`` all-to-all of (count, flag, keys) -- no host copy."""
+        n = keys.numel()
+        if n > self.capacity:
+            raise ValueError(f"fixed-shape plans: {n} keys in a micro-batch, capacity {self.capacity}")
+        W = self.comm.world
+        unique = bool(dedup) or self.dedups(int(self.capacity))  # from the capacity: every rank alike
+        C = self.fixed_slots(unique)
+        with stage("ps.dedup" if unique else "ps.route", self.timer):
+            counts, prefix, uniq, pos = self.dedup.run(keys) if unique else self.dedup.route(keys)
+        dev = keys.device
+        if self._slots is None or self._slots.numel() != C or self._slots.device != dev:
+            self._slots = torch.arange(C, dtype=torch.int64, device=dev)
+        j = self._slots.view(1, C)
+        start = prefix[:W].to(torch.int64).view(W, 1)
+        valid = j < counts[:W].to(torch.int64).view(W, 1)
+        if uniq.numel() == 0:
+            uniq = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        idx = (start + j).clamp_max(uniq.numel() - 1)
+        send = torch.empty((W, C + 2), dtype=torch.int32, device=dev)
+        send[:, 0] = counts[:W]
+        send[:, 1] = int(flag)
+        send[:, 2:] = torch.where(valid, uniq[idx], torch.full_like(idx, -1, dtype=torch.int32))
+        # request b -> slot of its key: owner segment * C + rank inside the owner's group
+        u = pos.to(torch.int64)
+        owner = torch.searchsorted(prefix[1:W + 1].to(torch.int64).contiguous(), u, right=True)
+        slot = (owner * C + (u - start.view(W)[owner])).to(torch.int32)
+        if self.dedup.clear_after:
+            self.dedup.reset_claims(keys)
+        with stage("ps.key-a2a", self.timer):
+            recv = self.comm.all_to_all(send.view(-1), [C + 2] * W, [C + 2] * W).view(W, C + 2)
+        self._count_lazy("unique", counts[:W], bound=n)
+        return PendingPlan(n, counts, None, slot, None, None, int(flag), n_bound=W * C, unique=unique, static=True,
+                           fixed=recv)
+
     # ----------------------------------------------------------------- planning
     def plan_begin(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None,
-                   presence=None) -> PendingPlan:
+                   presence=None, fixed: bool = True) -> PendingPlan:
         """Stage A: dedup + count exchange, counts copied to pinned host memory
         asynchronously.  Collective: every rank calls it once per micro-batch
         (with empty ``keys`` when it has nothing to pull).  ``flag`` (an int) is
         delivered to every peer with the counts (``PullPlan.peer_flags``).  ``dedup``:
         force (True) the de-duplicating plan instead of ``dedups(n)``'s choice.
         ``presence``: ``(uint8 flags [key space], event)`` of the keys, computed by the
-        caller (an identity plan then skips its marking pass; other plans ignore it)."""
-        a = self._stage_a(keys, flag, dedup, presence)
+        caller (an identity plan then skips its marking pass; other plans ignore it).
+        ``fixed = False``: a dynamic plan even with a ``capacity`` set."""
+        a = self._stage_a(keys, flag, dedup, presence, fixed)
         if isinstance(a, PendingPlan):
             return a
         return self._pending(*a, flag=flag)
 
-    def _stage_a(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None, presence=None):
+    def _stage_a(self, keys: torch.Tensor, flag: int = 0, dedup: Optional[bool] = None, presence=None,
+                 fixed: bool = True):
         """The device part of stage A: a finished (static) ``PendingPlan``, or
         ``(n, counts, uniq, pos, unique)`` still needing the count exchange."""
         keys = self.table.route_keys(keys.to(device=self.table.device)).to(torch.int32).contiguous()
         n = keys.numel()
+        if fixed and self.fixed():
+            return self._fixed_plan(keys, flag, dedup)
         if self.identity_for(n):
             ks = int(self.table.key_space)
             if self._iota is None or self._iota.numel() != ks:
@@ -286,6 +360,12 @@ class TensorPS:
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
+        if pp.fixed is not None:  # fixed-shape plan: the keys arrived in stage A
+            W, C = pp.fixed.shape[0], pp.fixed.shape[1] - 2
+            self._stats["pulls"] += pp.n
+            self._stats["steps"] += 1
+            return PullPlan([C] * W, [C] * W, pp.fixed[:, 2:].reshape(-1), pp.pos, W * C, [], pp.n,
+                            unique=pp.unique, recv_unique=pp.unique, flags_dev=pp.fixed[:, 1], fixed=True)
         if pp.static:  # static world-1 plan: sizes known on the host, nothing to wait for
             if pp.ready is not None and self.table.device.type == "cuda":
                 torch.cuda.current_stream(self.table.device).wait_event(pp.ready)
@@ -371,7 +451,7 @@ class TensorPS:
              dedup: Optional[bool] = None) -> PullPlan:
         """Stages A + B back to back (the host waits on this micro-batch's counts).
         Plans never alias the dedup workspace, so ``persistent`` is implied."""
-        return self.plan_end(self.plan_begin(keys, flag, dedup))
+        return self.plan_end(self.plan_begin(keys, flag, dedup, fixed=False))
 
     # --------------------------------------------------------------------- pull
     def serve(self, plan: PullPlan) -> torch.Tensor:
@@ -452,6 +532,8 @@ class TensorPS:
         opt = op or self.table.optimizer
         if plan.valid is not None:
             self._count_lazy("pushes", plan.valid)
+        elif plan.fixed:
+            self._count_lazy("pushes", recv_keys >= 0)
         else:
             self._stats["pushes"] += plan.n_unique
         with stage("ps.apply", self.timer):
@@ -484,7 +566,7 @@ class TensorPS:
         if return_updated:
             if not sum(plan.recv_splits):  # nothing arrived at this shard (host-known sizes)
                 return None
-            if self.masked_push:  # rows the push skipped drop out when the consumer reads (no sync here)
+            if self.masked_push or plan.fixed:  # skipped / padding rows drop out when the consumer reads
                 k = recv_keys.long().clamp_min(0)
                 return MaskedPair(self.table.global_ids(k), self.table.weight[k], recv_keys >= 0)
             return self.table.global_ids(recv_keys), self.table.weight[recv_keys.long()]

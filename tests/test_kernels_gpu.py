@@ -77,6 +77,30 @@ def test_gather_apply_v4_paths(D, misaligned):
         assert not torch.signbit(tab[uniq.long()][tab[uniq.long()] == 0]).any()  # -0.0 deltas leave +0.0
 
 
+@pytest.mark.parametrize("D,out_dtype", [(64, torch.float32), (300, torch.float32), (7, torch.float32),
+                                         (64, torch.bfloat16)])
+def test_gather_padding_slots_serve_zero_rows(D, out_dtype):
+    """Fixed-shape plans pad with row -1: a zero row, no touched mark, no sentinel flip
+    (16-byte, scalar and bf16-wire gathers) -- same as the torch twin."""
+    tab = torch.randn(500, D, device=DEV)
+    tab[::3] = -0.0
+    idx = torch.randint(0, 500, (777,), device=DEV, dtype=torch.int32)
+    idx[::4] = -1
+    ref_tab, ref_touched = tab.cpu().clone(), torch.zeros(500, dtype=torch.uint8)
+    touched = torch.zeros(500, dtype=torch.uint8, device=DEV)
+    out = ops.gather_rows(tab, idx, out_dtype=out_dtype, touched=touched, flip=True)
+    ref = R.gather_rows(ref_tab, idx.cpu(), out_dtype, ref_touched)
+    ops.flip_sentinel(ref_tab, idx.cpu())
+    # (as floats: a repeated sentinel row may be served before or after its flip, -0.0 or +0.0)
+    assert torch.equal(out.cpu().float(), ref.float())
+    assert torch.equal(out[::4].float(), torch.zeros_like(out[::4].float()))
+    assert torch.equal(touched.cpu(), ref_touched)
+    assert torch.equal(tab.cpu().view(torch.int32), ref_tab.view(torch.int32))
+    marks = torch.zeros(500, dtype=torch.uint8, device=DEV)
+    ops.mark_rows(marks, idx)
+    assert torch.equal(marks.cpu(), ref_touched)
+
+
 def test_apply_adagrad_bf16_delta():
     D = 64
     tab = torch.randn(200, D, device=DEV)

@@ -41,7 +41,7 @@ def _batches(sizes, seed=0):
     return out
 
 
-def _run(batches, graph, logic_cls=DeviceSimplePSLogic):
+def _run(batches, graph, logic_cls=DeviceSimplePSLogic, capacity=None, loopback=False):
     sink = FoldSink(KEYS, DIM, device=DEV)
     lefts = []
 
@@ -51,7 +51,9 @@ def _run(batches, graph, logic_cls=DeviceSimplePSLogic):
             lefts.append(tuple(t.clone() for t in e.value))
 
     logic = logic_cls(KEYS, DIM, op="add", init=("uniform", -0.1, 0.1), seed=3)
-    rt = TensorRuntime(Comm(device=DEV), staleness=0, output_sink=on, graph=graph).start(_Worker(), logic)
+    comm = Comm(device=DEV)
+    comm.loopback = loopback
+    rt = TensorRuntime(comm, staleness=0, output_sink=on, graph=graph, capacity=capacity).start(_Worker(), logic)
     for b in batches:
         rt.submit(b)
     rt.finish()
@@ -120,3 +122,63 @@ def test_syncing_worker_falls_back_to_eager():
             assert any("capture disabled" in str(r.message) for r in rec)
         tables.append(logic.table.weight.clone())
     torch.testing.assert_close(tables[1], tables[0], rtol=1e-5, atol=1e-5)
+
+
+@pytest.fixture
+def rccl_loopback():
+    """A one-rank RCCL process group: the all-to-alls of fixed-shape plans then run
+    through RCCL kernels (``Comm.loopback``) on a one-GPU box."""
+    import torch.distributed as dist
+    from dist_utils import free_port
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
+                            device_id=DEV)
+    try:
+        yield
+    finally:
+        import gc
+
+        gc.collect()  # captured graphs that reference the communicator go first
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+
+
+def test_graph_replay_captures_rccl_collectives(rccl_loopback):
+    """The world > 1 step shape: fixed-shape plans whose key / row / delta all-to-alls
+    go through RCCL, captured into the hipGraph with the kernels around them.  Eager
+    and replayed steps equal the world-1 static plans' results."""
+    batches = _batches([256] * 12, seed=4)
+    w0, s0, l0, _ = _run(batches, graph=False)
+    w1, s1, l1, rt1 = _run(batches, graph=False, capacity=256, loopback=True)
+    w2, s2, l2, rt2 = _run(batches, graph=True, capacity=256, loopback=True)
+    assert rt1.ps_logic.ps.fixed() and rt2.ps_logic.ps.fixed()
+    assert rt2.graphs.disabled is None, rt2.graphs.disabled_trace
+    assert rt2.graphs.captures == 1 and rt2.graphs.replays == 12 - 2
+    for w, s, lefts in ((w1, s1, l1), (w2, s2, l2)):
+        torch.testing.assert_close(w, w0, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(s.tables["right"], s0.tables["right"], rtol=1e-5, atol=1e-5)
+        assert torch.equal(s.seen["right"], s0.seen["right"])
+        assert len(lefts) == 12
+        for a, b in zip(l0, lefts):
+            assert torch.equal(a[0], b[0])
+            torch.testing.assert_close(a[1], b[1], rtol=1e-5, atol=1e-5)
+
+
+def test_graph_execute_ends_on_lagged_flags(rccl_loopback):
+    """``execute()`` with captured RCCL steps: the end-of-input flags are read from the
+    replayed steps' buffers one micro-batch late, and the job still ends with the
+    eager model."""
+    batches = _batches([128] * 8, seed=5)
+    models = []
+    for graph in (False, True):
+        logic = DeviceSimplePSLogicWithClose(KEYS, DIM, op="add", init=("uniform", -0.1, 0.1), seed=3)
+        comm = Comm(device=DEV)
+        comm.loopback = True
+        rt = TensorRuntime(comm, output_sink=lambda e: None, graph=graph, capacity=128)
+        rt.execute(batches, _Worker(), logic)
+        if graph:
+            assert rt.graphs.replays >= 5 and rt.graphs.disabled is None
+        models.append(logic.table.weight.clone())
+    torch.testing.assert_close(models[1], models[0], rtol=1e-5, atol=1e-5)

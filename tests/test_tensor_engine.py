@@ -85,7 +85,7 @@ class _CountWorker(BatchedWorkerLogic):
         ps.output((pulled.keys, pulled.values()))
 
 
-def _model_load(rank, world, n_params, staleness, dedup=None):
+def _model_load(rank, world, n_params, staleness, dedup=None, capacity=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     comm = Comm()
@@ -94,23 +94,27 @@ def _model_load(rank, world, n_params, staleness, dedup=None):
     keys = [k for _ in range(3) for k in range(n_params)]
     mine = keys[rank::world]
     batches = [torch.tensor(mine[s:s + 7]) for s in range(0, len(mine), 7)]
-    rt = TensorRuntime(comm, staleness=staleness)
+    rt = TensorRuntime(comm, staleness=staleness, capacity=capacity)
     logic = DeviceSimplePSLogicWithClose(n_params, 1, op="add", dedup=dedup)
     out = rt.execute(batches, _CountWorker(), logic, model=model)
+    if capacity is not None and world > 1:  # fixed-shape plans: no count exchange, no host copy
+        assert logic.ps.fixed() and logic.ps.stats["host_waits"] == 0
     if dedup is False:  # request plans: every pull of the run shipped its key as is
         assert logic.ps.stats["unique"] == logic.ps.stats["pulls"]
     return [(e.value[0], e.value[1]) for e in out if isinstance(e, Right)]
 
 
-@pytest.mark.parametrize("world,staleness,dedup", [(1, 0, None), (3, 0, None), (4, 2, None), (1, 0, False),
-                                                   (3, 0, False), (2, 1, False)])
-def test_tensor_model_load_exact(world, staleness, dedup):
+@pytest.mark.parametrize("world,staleness,dedup,capacity", [
+    (1, 0, None, None), (3, 0, None, None), (4, 2, None, None), (1, 0, False, None), (3, 0, False, None),
+    (2, 1, False, None), (3, 0, None, 7), (4, 2, None, 7), (2, 1, False, 7), (3, 0, True, 9)])
+def test_tensor_model_load_exact(world, staleness, dedup, capacity):
     """FlinkSimpleStackTest 'model load': 50 params loaded as 10*i, pulled and
     pushed +1 three times each -> the close-time dump is exactly 10*i + 3.  With
     ``dedup=False`` (request plans) keys repeat inside micro-batches and their +1s
-    are applied one by one (atomic adds)."""
-    res = run_ranks(_model_load, world, 50, staleness, dedup) if world > 1 else \
-        [_model_load(0, 1, 50, staleness, dedup)]
+    are applied one by one (atomic adds).  ``capacity``: fixed-shape plans (every
+    exchange [W, C] slots with padding, flags read one micro-batch later)."""
+    res = run_ranks(_model_load, world, 50, staleness, dedup, capacity) if world > 1 else \
+        [_model_load(0, 1, 50, staleness, dedup, capacity)]
     dump = {}
     for r in res:
         for ids, vals in r:
@@ -157,19 +161,20 @@ def test_set_rule_with_masked_pushes_and_last_writer():
     assert w == [100.0, -1.0, 102.0, -1.0, -1.0, -1.0, -1.0, -1.0]
 
 
-def _uneven(rank, world):
+def _uneven(rank, world, capacity=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     # rank r has r+1 micro-batches (different lengths: the EOF flag protocol)
     batches = [torch.tensor([rank * 10 + j]) for j in range(rank + 1)]
     logic = DeviceRangePSLogicWithClose(world * 10, 1)
-    out = TensorRuntime(Comm(), staleness=1).execute(batches, _CountWorker(), logic)
+    out = TensorRuntime(Comm(), staleness=1, capacity=capacity).execute(batches, _CountWorker(), logic)
     dump = [e.value for e in out if isinstance(e, Right)]
     return {k: v for ids, vals in dump for k, v in zip(ids.tolist(), vals.reshape(-1).tolist())}
 
 
-def test_uneven_inputs_terminate_on_every_rank():
-    res = run_ranks(_uneven, 3)
+@pytest.mark.parametrize("capacity", [None, 1])
+def test_uneven_inputs_terminate_on_every_rank(capacity):
+    res = run_ranks(_uneven, 3, capacity)
     merged = {}
     for d in res:
         merged.update(d)
@@ -284,3 +289,27 @@ def test_lock_logic_unsorted_keys_route_rows_to_their_key(world):
                 assert 1000.0 * k < v <= 1000.0 * k + 4 * world, (k, v)
     assert vals[3] == 3000.0 + 4 * world and vals[1] == 1000.0 + 2 * world and vals[0] == 2 * world
     assert vals[2] == 2000.0 and vals[4] == 4000.0
+
+
+def _per_push_outputs(rank, world, capacity):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    g = torch.Generator().manual_seed(rank)
+    batches = [torch.randint(0, 30, (int(torch.randint(1, 9, (1,), generator=g)),), generator=g)
+               for _ in range(5 + rank)]
+    out = TensorRuntime(Comm(), capacity=capacity).execute(batches, _CountWorker(), DeviceSimplePSLogic(30, 1, op="add"))
+    pushes = [dict(zip(e.value[0].tolist(), e.value[1].reshape(-1).tolist())) for e in out if isinstance(e, Right)]
+    pushes = [p for p in pushes if p]  # fixed plans emit (empty) outputs for the steps after the end
+    lefts = [(e.value[0].tolist(), e.value[1].reshape(-1).tolist()) for e in out if isinstance(e, Left)]
+    return pushes, lefts
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fixed_shape_plans_equal_dynamic_plans(world):
+    """Per-push PS outputs (``SimplePSLogic``) and the pulled values with fixed-shape
+    plans equal the dynamic plans' on every rank (uneven micro-batch counts).  Fixed
+    plans learn the end of input one micro-batch later and cannot tell an empty push
+    output on the host: their extra outputs are empty."""
+    dyn = run_ranks(_per_push_outputs, world, None)
+    fix = run_ranks(_per_push_outputs, world, 8)
+    assert dyn == fix

@@ -177,11 +177,12 @@ def test_mf_ps_path_async_equals_sync_bitwise(world):
     _assert_same(res, sync)
 
 
-def _pa_run(comm, dedup):
+def _pa_run(comm, dedup, capacity=None):
     from flink_parameter_server_1_amd.models.pa.fast import DistributedPA, PAConfig, synthetic_sparse_batch
 
     F = 1 << 22
-    m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=False), comm)
+    m = DistributedPA(PAConfig(feature_count=F, kind="binary", local_direct=False, capacity=capacity), comm)
+    assert m.ps.fixed() == (capacity is not None)
     m.ps.dedup_mode = dedup
     for s in range(6):
         m.train_step(*synthetic_sparse_batch(2048, 32, F, seed=comm.rank + 3, step=s % 3, device="cuda"))
@@ -197,6 +198,21 @@ def test_pa_ps_path_async_equals_sync(dedup):
     for (ia, wa), (ib, wb) in zip(res, sync):
         assert torch.equal(ia, ib)
         torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-6)  # float atomics: summation order only
+
+
+@pytest.mark.parametrize("dedup", [True, False])
+def test_pa_fixed_shape_plans_async_equals_sync_and_dynamic(dedup):
+    """Fixed-shape plans (``TensorPS.capacity``: one [W, C + 2] key all-to-all, padded
+    row / delta all-to-alls, nothing read on the host) under RCCL semantics: async ==
+    sync, and both == the dynamic plans' model (float atomics: summation order)."""
+    cap = 2048 * 32
+    sync = run_virtual(_pa_run, 4, dedup, cap, mode="sync")
+    res = run_virtual(_pa_run, 4, dedup, cap, mode="async", latency_us=300.0)
+    dyn = run_virtual(_pa_run, 4, dedup, mode="sync")
+    for (ia, wa), (ib, wb), (ic, wc) in zip(res, sync, dyn):
+        assert torch.equal(ia, ib) and torch.equal(ia, ic)
+        torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(wa, wc, rtol=1e-4, atol=1e-6)
 
 
 def test_virtual_world_reports_collective_desync():
