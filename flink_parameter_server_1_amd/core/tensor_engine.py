@@ -608,10 +608,12 @@ def fold_outputs(outputs: Iterable) -> tuple:
 
 def transform_tensor(source: Iterable, worker_logic: BatchedWorkerLogic, ps_logic: DevicePSLogic, *,
                      comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
-                     output_sink: Optional[Callable] = None, model=None, worker_model=None) -> List[Any]:
+                     output_sink: Optional[Callable] = None, model=None, worker_model=None, graph: bool = False,
+                     capacity: Optional[int] = None) -> List[Any]:
     """Tensor-engine ``transform`` on this rank (SPMD under torchrun): ``source``
-    is this rank's iterable of micro-batches."""
-    rt = TensorRuntime(comm, staleness, iteration_wait_time, output_sink)
+    is this rank's iterable of micro-batches.  ``graph`` / ``capacity``: captured
+    steps / fixed-shape plans (``TensorRuntime``)."""
+    rt = TensorRuntime(comm, staleness, iteration_wait_time, output_sink, graph=graph, capacity=capacity)
     return rt.execute(source, worker_logic, ps_logic, model=model, worker_model=worker_model)
 
 

@@ -511,17 +511,20 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
 
 def ps_top_k_generator_tensor(queries: Iterable, ps_model, worker_model, num_users: int, num_factors: int = 10,
                               user_memory: int = 0, K: int = 100, worker_k: int = 75, bucket_size: int = 4096,
-                              pruning_algorithm=None, comm: Optional[Comm] = None, reference_quirks: bool = False):
+                              pruning_algorithm=None, comm: Optional[Comm] = None, reference_quirks: bool = False,
+                              capacity: Optional[int] = None):
     """``psTopKGenerator`` on the tensor engine (this rank's part of the job).
 
     ``queries``: the broadcast ``(user, item, ts)`` micro-batches (the same on every
     rank); ``ps_model``: this rank's ``(user, [vec..., len])`` records (``Left``);
     ``worker_model``: this rank's ``(item, [vec..., len])`` records (``Right``).
-    Returns rank 0's ``Left(((user, item, ts), scores [B, K], items [B, K]))``."""
+    Returns rank 0's ``Left(((user, item, ts), scores [B, K], items [B, K]))``.
+    ``capacity`` (the largest micro-batch): fixed-shape PS plans -- at W > 1 no
+    micro-batch waits for a count exchange on the host."""
     worker = TopKQueryWorker(K, worker_k, user_memory, bucket_size, pruning_algorithm, reference_quirks, num_users)
     logic = DeviceSimplePSLogic(num_users, num_factors + 1, op="set", init=("const", -1.0), track_touched=False)
     logic.emit = "none"
-    rt = TensorRuntime(comm, staleness=0)
+    rt = TensorRuntime(comm, staleness=0, capacity=capacity)
     return rt.execute(queries, worker, logic, model=ps_model, worker_model=worker_model)
 
 
@@ -725,15 +728,18 @@ def ps_online_learner_and_generator_tensor(batches: Iterable, num_users: int, nu
                                            learning_rate: float = 0.01, negative_sample_rate: int = 0,
                                            user_memory: int = 65535, K: int = 100, worker_k: int = 75,
                                            bucket_size: int = 4096, pruning_algorithm=None, seed: int = 0,
-                                           comm: Optional[Comm] = None, output_sink=None):
+                                           comm: Optional[Comm] = None, output_sink=None,
+                                           capacity: Optional[int] = None):
     """``psOnlineLearnerAndGenerator`` on the tensor engine (this rank's part):
     ``batches`` = the broadcast ``(user, item, ts, rating)`` micro-batches (same on
     every rank).  Outputs: rank 0's top-K records (``Left``) and every rank's PS
-    user updates ``Right((users, vectors))`` (``SimplePSLogic`` emits on push)."""
+    user updates ``Right((users, vectors))`` (``SimplePSLogic`` emits on push).
+    ``capacity`` (the largest micro-batch): fixed-shape PS plans (no per-batch count
+    exchange read on the host at W > 1)."""
     worker = OnlineMFTopKWorker(num_items, num_factors, learning_rate, K, worker_k, user_memory,
                                 negative_sample_rate, bucket_size, pruning_algorithm, range_min, range_max, seed,
                                 num_users=num_users)
     logic = DeviceSimplePSLogic(num_users, num_factors, op="add_renorm", init=("uniform", range_min, range_max),
                                 seed=seed)
-    rt = TensorRuntime(comm, staleness=0, output_sink=output_sink)
+    rt = TensorRuntime(comm, staleness=0, output_sink=output_sink, capacity=capacity)
     return rt.execute(batches, worker, logic)

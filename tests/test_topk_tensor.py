@@ -105,7 +105,7 @@ def _topk_data(W, seed=0, users=30, items=200, D=6, n=60):
     return model, ratings
 
 
-def _tensor_topk(rank, world, model, ratings, K, wk, mem, strategy, mb):
+def _tensor_topk(rank, world, model, ratings, K, wk, mem, strategy, mb, capacity=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     ps_model = [(e.value[0], list(e.value[1][1]) + [e.value[1][0]]) for e in model if isinstance(e, Left)]
@@ -115,19 +115,22 @@ def _tensor_topk(rank, world, model, ratings, K, wk, mem, strategy, mb):
     q = [(torch.tensor([r.user for r in ratings[s:s + mb]]), torch.tensor([r.item for r in ratings[s:s + mb]]),
           torch.tensor([r.timestamp for r in ratings[s:s + mb]])) for s in range(0, len(ratings), mb)]
     out = ps_top_k_generator_tensor(q, ps_mine, w_model, num_users=30, num_factors=6, user_memory=mem, K=K,
-                                    worker_k=wk, bucket_size=32, pruning_algorithm=strategy, comm=Comm())
+                                    worker_k=wk, bucket_size=32, pruning_algorithm=strategy, comm=Comm(),
+                                    capacity=capacity)
     return as_reference_records(out)
 
 
-@pytest.mark.parametrize("world,mem,strategy,mb", [(1, 0, None, 7), (1, 5, COORD(), 1), (2, 5, LI(2, 1.5), 4),
-                                                   (3, -1, INCR(2), 5)])
-def test_tensor_topk_generator_matches_per_record(world, mem, strategy, mb):
+@pytest.mark.parametrize("world,mem,strategy,mb,capacity", [
+    (1, 0, None, 7, None), (1, 5, COORD(), 1, None), (2, 5, LI(2, 1.5), 4, None), (3, -1, INCR(2), 5, None),
+    (2, 5, LI(2, 1.5), 4, 4), (3, -1, INCR(2), 5, 5)])
+def test_tensor_topk_generator_matches_per_record(world, mem, strategy, mb, capacity):
+    """``capacity``: fixed-shape PS plans (W > 1: no count exchange read on the host)."""
     K, wk = 10, 8
     model, ratings = _topk_data(world)
     ref = ps_top_k_generator(ratings, model, num_factors=6, user_memory=mem, K=K, worker_k=wk, bucket_size=16,
                              pruning_algorithm=strategy or COORD(), worker_parallelism=world, ps_parallelism=world)
-    res = run_ranks(_tensor_topk, world, model, ratings, K, wk, mem, strategy, mb) if world > 1 else \
-        [_tensor_topk(0, 1, model, ratings, K, wk, mem, strategy, mb)]
+    res = run_ranks(_tensor_topk, world, model, ratings, K, wk, mem, strategy, mb, capacity) if world > 1 else \
+        [_tensor_topk(0, 1, model, ratings, K, wk, mem, strategy, mb, capacity)]
     got = res[0]
     assert all(r == [] for r in res[1:])  # only rank 0 emits (the merge runs at parallelism 1)
     assert len(got) == len(ref) == len(ratings)
@@ -207,3 +210,40 @@ def test_seen_store_sorted_mode_long_stream_with_pruning():
             if len(dq) > 3:
                 dq.popleft()
     assert st.keys.numel() < 3000 * 4  # pruned
+
+
+def _online_w(rank, world, batches, users, items, capacity):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    out = ps_online_learner_and_generator_tensor(batches, users, items, num_factors=5, range_min=-0.3, range_max=0.3,
+                                                 learning_rate=0.2, user_memory=4, K=6, worker_k=6, bucket_size=8,
+                                                 seed=9, comm=Comm(), capacity=capacity)
+    recs = as_reference_records(out)
+    ps_users = {}
+    for e in out:
+        if isinstance(e, Right):
+            ids, vals = e.value
+            for k, v in zip(ids.tolist(), vals.tolist()):
+                ps_users[k] = v
+    return recs, ps_users
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_online_learner_fixed_shape_plans_equal_dynamic(world):
+    """MF + top-K at W > 1 with fixed-shape PS plans: the same top-K lists and PS user
+    vectors as the dynamic plans."""
+    rng = np.random.default_rng(11)
+    users, items = 20, 60
+    batches = [(torch.tensor(rng.integers(0, users, 4)), torch.tensor(rng.integers(0, items, 4)),
+                torch.arange(4 * t, 4 * t + 4), torch.tensor(rng.random(4), dtype=torch.float32))
+               for t in range(12)]
+    dyn = run_ranks(_online_w, world, batches, users, items, None)
+    fix = run_ranks(_online_w, world, batches, users, items, 4)
+    for (rd, ud), (rf, uf) in zip(dyn, fix):
+        assert [r[:3] for r in rd] == [r[:3] for r in rf]
+        for a, b in zip(rd, rf):
+            assert [x[1] for x in a[3]] == [x[1] for x in b[3]]
+            np.testing.assert_allclose([x[0] for x in a[3]], [x[0] for x in b[3]], rtol=1e-6, atol=1e-7)
+        assert ud.keys() == uf.keys()
+        for k in ud:
+            np.testing.assert_allclose(ud[k], uf[k], rtol=1e-6, atol=1e-7)
