@@ -40,6 +40,9 @@ def main(argv=None):
                     help="standard: 5 independent negatives per pair (word2vec's objective, the reported number); "
                          "shared: block-shared negatives (Ji et al.), a different estimator")
     ap.add_argument("--negatives", type=int, default=5)
+    ap.add_argument("--no-fuse-local-push", action="store_true",
+                    help="PS path at one rank: push delta buffers and apply them (default: the kernel adds its "
+                         "pushes into the owner's tables)")
     a = ap.parse_args(argv)
 
     import torch
@@ -53,6 +56,7 @@ def main(argv=None):
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
                                    wire_dtype=a.wire, shared_negatives=a.shared_negatives,
                                    local_direct=not a.ps_path, mode=a.mode, negatives=a.negatives,
+                                   fuse_local_push=not a.no_fuse_local_push,
                                    **({} if a.neg_group is None else {"neg_group": a.neg_group})), comm=comm)
     toks = synthetic_corpus(max(a.pairs // a.window, 1 << 16) * 2, a.vocab, seed=comm.rank, device=dev)
     c, o = skipgram_pairs(toks, a.window)
@@ -93,6 +97,7 @@ def main(argv=None):
                                      f"{a.shared_negatives} shared per {32 * m.cfg.neg_group} pairs, weight "
                                      f"{a.negatives}/{a.shared_negatives}"),
                        "exchange": "local-direct" if m._direct else "ps",
+                       "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1),
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)
 

@@ -26,6 +26,9 @@
 // rows_in / rows_out are the rows read (the tables themselves on the local path,
 // the pulled rows on the PS path); d_in / d_out receive the deltas (the tables
 // themselves -> Hogwild in place; or per-unique-row delta buffers to push).
+// wmap_in / wmap_out (nullable) redirect the delta of row r to row wmap[r]: the
+// PS path at world 1 adds its pushes straight into the owner's tables (pulled
+// row r = table row wmap[r]) while reading the pulled snapshot.
 #include "common.h"
 
 using namespace fps;
@@ -56,6 +59,8 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
                                                        const int32_t* __restrict__ pos_o,
                                                        const int32_t* __restrict__ pos_neg, int64_t P, int D, int k,
                                                        float lr, float* __restrict__ d_in, float* __restrict__ d_out,
+                                                       const int32_t* __restrict__ wmap_in,
+                                                       const int32_t* __restrict__ wmap_out,
                                                        float* __restrict__ loss, int chunk,
                                                        float* __restrict__ gbuf) {
   const int lane = threadIdx.x & 63;
@@ -68,7 +73,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
   float lsum = 0.f;
   auto flush = [&]() {
     if (cur < 0) return;
-    float* dst = d_in + (int64_t)cur * D;
+    float* dst = d_in + (int64_t)(wmap_in != nullptr ? wmap_in[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
@@ -134,7 +139,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
 #pragma unroll
           for (int m = 0; m < NPL; ++m) dh[m] += g * xv[q][m];
         } else {
-          float* dst = d_out + (int64_t)row[q] * D;
+          float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[row[q]] : row[q]) * D;
 #pragma unroll
           for (int m = 0; m < NPL; ++m) {
             const int j = lane + 64 * m;
@@ -170,7 +175,8 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
                                                         const float* __restrict__ gbuf,
                                                         const int32_t* __restrict__ pos_c, int k1, int64_t n,
                                                         const float* __restrict__ rows_h, int D,
-                                                        float* __restrict__ d_out) {
+                                                        float* __restrict__ d_out,
+                                                        const int32_t* __restrict__ wmap_out) {
   __shared__ int32_t s_row[4][SR_C], s_cen[4][SR_C];
   __shared__ float s_g[4][SR_C];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -191,7 +197,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
   int32_t cur = s_row[wv][0];
   bool whole = t0 == 0 || srow[t0 - 1] != cur;  // the current run starts inside this range
   auto start = [&]() {
-    const float* dst = d_out + (int64_t)cur * D;
+    const float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
@@ -200,7 +206,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
     }
   };
   auto flush = [&](bool complete) {
-    float* dst = d_out + (int64_t)cur * D;
+    float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = lane + 64 * m;
@@ -249,7 +255,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 // stay 0).
 FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, const int32_t* pos_c,
                                    const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
-                                   float* d_in, float* loss, float* gbuf, void* stream) {
+                                   float* d_in, const int32_t* wmap_in, float* loss, float* gbuf, void* stream) {
   if (P <= 0) return 0;
   if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
   const int chunk = 16;
@@ -259,7 +265,8 @@ FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, 
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGC(NPL_)                                                                                            \
   hipLaunchKernelGGL((sgns_std_kernel<NPL_, true>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, loss, chunk, gbuf)
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, wmap_in, (const int32_t*)nullptr,  \
+                     loss, chunk, gbuf)
   if (D <= 64) FPS_SGC(1);
   else if (D <= 128) FPS_SGC(2);
   else if (D <= 256) FPS_SGC(4);
@@ -273,7 +280,8 @@ FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, 
 // Sorted form, pass 2: d_out[srow[t]] += gbuf[perm[t]] * rows_h[pos_c[perm[t] / k1]]
 // over the n = P * k1 entries sorted by output row.
 FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float* gbuf, const int32_t* pos_c, int k1,
-                          int64_t n, const float* rows_h, int D, float* d_out, void* stream) {
+                          int64_t n, const float* rows_h, int D, float* d_out, const int32_t* wmap_out,
+                          void* stream) {
   if (n <= 0) return 0;
   if (D <= 0 || D > 512 || k1 <= 0) return (int)hipErrorInvalidValue;
   const int64_t blocks = (n + 4 * SR_C - 1) / (4 * SR_C);
@@ -281,7 +289,7 @@ FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float*
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGR(NPL_)                                                                                            \
   hipLaunchKernelGGL(sgns_rows_kernel<NPL_>, dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf, pos_c, k1, \
-                     n, rows_h, D, d_out)
+                     n, rows_h, D, d_out, wmap_out)
   if (D <= 64) FPS_SGR(1);
   else if (D <= 128) FPS_SGR(2);
   else if (D <= 256) FPS_SGR(4);
@@ -297,7 +305,8 @@ FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float*
 // D <= 512.  loss (optional, zeroed by the caller) receives the summed loss.
 FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const int32_t* pos_c,
                               const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
-                              float* d_in, float* d_out, float* loss, void* stream) {
+                              float* d_in, float* d_out, const int32_t* wmap_in, const int32_t* wmap_out, float* loss,
+                              void* stream) {
   if (P <= 0) return 0;
   if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
   // ~16 pairs per wave: long enough to reuse a center across its window, short
@@ -309,7 +318,7 @@ FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGS(NPL_)                                                                                            \
   hipLaunchKernelGGL((sgns_std_kernel<NPL_, false>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, loss, chunk, (float*)nullptr)
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, wmap_in, wmap_out, loss, chunk, (float*)nullptr)
   if (D <= 64) FPS_SGS(1);
   else if (D <= 128) FPS_SGS(2);
   else if (D <= 256) FPS_SGS(4);

@@ -21,7 +21,10 @@ micro-batch of (center, context) pairs:
    for split sizes in steady state;
 3. ``ops.sgns_standard`` (K6, ``sgns_std.hip``) / ``ops.sgns_step`` (MFMA,
    ``sgns.hip``) computes per-row deltas;
-4. push both delta sets; the PS adds them.
+4. push both delta sets; the PS adds them.  At one rank the owner is the worker:
+   ``fuse_local_push`` (default) has the kernel add the deltas straight into the
+   tables (the pulled snapshot is still what it reads; the PS's add is the same
+   sum), so the delta buffers, their zeroing and the apply pass go away.
 
 With one rank (``local_direct``, default) steps 2 and 4 collapse: the kernel
 reads the rows straight from the local tables and adds its deltas into them
@@ -60,6 +63,7 @@ class SGNSConfig:
     neg_group: int = 4            # v4: consecutive 32-pair blocks sharing one negative set (1, 2, 4):
                                   # 4 measured +6 % pairs/s at the same loss curve (profiles/r2_sgns.md)
     local_direct: bool = True     # W = 1: kernel reads / atomically updates the local tables in place
+    fuse_local_push: bool = True  # W = 1 PS path: the kernel adds its pushes into the tables (no delta buffers)
     mode: str = "standard"        # "standard": `negatives` independent negatives per pair | "shared"
 
 
@@ -183,20 +187,38 @@ class DistributedSGNS:
         rows_in, rows_out = rows
         plan_in, plan_out = plans
         dev = rows_in.device
-        d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
-        d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
+        fused = self._fused_push(plans)
+        if fused:  # pulled row j of a table is its row recv_keys[j]: deltas go there, in place
+            d_in, d_out = self.w_in.weight, self.w_out.weight
+            wm_in, wm_out = plan_in.recv_keys, plan_out.recv_keys
+        else:
+            d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
+            d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
+            wm_in = wm_out = None
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
         with stage("sgns.step", self.timer):
             if self.standard:
                 loss = ops.sgns_standard(rows_in.float(), rows_out.float(), plan_in.pos.contiguous(), pos_o, pos_neg,
-                                         c.negatives, lr, d_in, d_out, with_loss=with_loss)
+                                         c.negatives, lr, d_in, d_out, with_loss=with_loss, wmap_in=wm_in,
+                                         wmap_out=wm_out)
             else:
                 loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
                                      c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
                                      neg_k=c.shared_negatives, neg_group=c.neg_group)
         self.pairs_seen += P
+        if fused:
+            for ps, plan in zip((self.ps_in, self.ps_out), plans):
+                ps.note_local_push(plan)
+            return None, (float(loss.item()) / max(P, 1) if with_loss else None)
         return [d_in, d_out], (float(loss.item()) / max(P, 1) if with_loss else None)
+
+    def _fused_push(self, plans) -> bool:
+        """World 1, additive tables, de-duplicating plans: the owner is this rank and each
+        pulled row maps to one table row, so the kernel can apply the push itself."""
+        return (self.cfg.fuse_local_push and self.standard and self.comm.world == 1
+                and self.w_in.optimizer == "add" and self.w_out.optimizer == "add"
+                and all(p.unique and p.valid is None and not p.fixed for p in plans))
 
     def embeddings(self, only_touched: bool = True):
         self.flush()

@@ -760,11 +760,14 @@ SGNS_METHODS = ("sorted", "atomic")
 
 
 def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d_in, d_out,
-                  with_loss: bool = False, method: Optional[str] = None):
+                  with_loss: bool = False, method: Optional[str] = None, wmap_in=None, wmap_out=None):
     """Standard skip-gram negative sampling (K6, ``kernels/sgns_std.hip``): ``k``
     independent negatives per pair (``pos_neg[P * k]``), word2vec's objective.
     ``d_in`` / ``d_out`` receive the deltas (the tables themselves on the local
-    path).  Returns the summed loss (a device / host 1-element tensor) or None.
+    path).  ``wmap_in`` / ``wmap_out`` (int32, optional): the delta of row ``r`` goes
+    to row ``wmap[r]`` of ``d_in`` / ``d_out`` (world-1 PS path: pushes added straight
+    into the owner's tables).  Returns the summed loss (a device / host 1-element
+    tensor) or None.
 
     GPU: one wave per 16 pairs, sequential inside a wave's center runs (the
     center's change is added once per run).  Output rows (context + negatives):
@@ -789,6 +792,8 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
         if D > 512:
             raise ValueError("sgns_standard: D <= 512")
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
+        wmap_in = None if wmap_in is None else _c(wmap_in.to(torch.int32))
+        wmap_out = None if wmap_out is None else _c(wmap_out.to(torch.int32))
         method = method or os.environ.get("FPS_SGNS_METHOD", "sorted")
         if method not in SGNS_METHODS:
             raise ValueError(f"sgns_standard: method must be one of {SGNS_METHODS}")
@@ -799,19 +804,32 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
             gbuf = torch.zeros(P * k1, dtype=torch.float32, device=rows_in.device)
             N.check(lib.fps_sgns_standard_coef(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                                _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
-                                               _c(d_in).data_ptr(), N.ptr(loss), gbuf.data_ptr(), s), "sgns_coef")
+                                               _c(d_in).data_ptr(), N.ptr(wmap_in), N.ptr(loss), gbuf.data_ptr(), s),
+                    "sgns_coef")
             keys = torch.cat([pos_o.reshape(P, 1), pos_neg.reshape(P, int(k))], dim=1).reshape(-1)
             srow, perm = torch.sort(keys.to(torch.int32))
             N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
-                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), s), "sgns_rows")
+                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out), s),
+                    "sgns_rows")
             return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
-                                              _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(loss),
-                                              N.stream_ptr(rows_in.device)), "sgns_standard")
+                                              _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(wmap_in),
+                                              N.ptr(wmap_out), N.ptr(loss), N.stream_ptr(rows_in.device)),
+                "sgns_standard")
         return loss
     # CPU: the mini-batch form (every pair reads the rows as of the call); the
     # kernel's exact per-wave order is ``reference.sgns_standard`` (numerics tests)
+    if wmap_in is not None or wmap_out is not None:
+        tmp_in = torch.zeros((rows_in.shape[0], D), dtype=d_in.dtype)
+        tmp_out = torch.zeros((rows_out.shape[0], D), dtype=d_out.dtype)
+        total = R.sgns_standard_batched(rows_in, rows_out, pos_c, pos_o, pos_neg, int(k), lr, tmp_in, tmp_out)
+        for d, tmp, wm in ((d_in, tmp_in, wmap_in), (d_out, tmp_out, wmap_out)):
+            if wm is None:
+                d += tmp
+            else:
+                d.index_add_(0, wm.long(), tmp)
+        return torch.tensor([total]) if with_loss else None
     total = R.sgns_standard_batched(rows_in, rows_out, pos_c, pos_o, pos_neg, int(k), lr, d_in, d_out)
     return torch.tensor([total]) if with_loss else None
 

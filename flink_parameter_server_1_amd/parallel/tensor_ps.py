@@ -590,6 +590,13 @@ class TensorPS:
         out[order] = first & (gf[grp] > 0) & (sr >= 0)
         return out
 
+    def note_local_push(self, plan: PullPlan) -> None:
+        """Book a push the worker applied to this (local, additive) shard itself
+        (world 1: its compute kernel added the deltas to ``recv_keys``' rows)."""
+        if self.comm.world != 1 or getattr(self.table, "optimizer", "") != "add":
+            raise ValueError("local pushes need world 1 and an additive table")
+        self._stats["pushes"] += plan.n_unique
+
     def reduce_requests(self, plan: PullPlan, deltas: torch.Tensor, op: str = "add",
                         mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Per-request ``[B, D]`` deltas -> per-unique-key ``[U, D]``: summed for
