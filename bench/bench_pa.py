@@ -33,6 +33,9 @@ def main(argv=None):
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--ps-path", action="store_true",
                     help="N = 1: run the pull / push protocol through the tensor engine instead of updating in place")
+    ap.add_argument("--no-fuse-local-push", action="store_true",
+                    help="PS path at one rank: push a delta buffer and apply it (default: the kernel adds its push "
+                         "into the owner's table)")
     a = ap.parse_args(argv)
 
     import torch
@@ -43,7 +46,7 @@ def main(argv=None):
     comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire,
-                               local_direct=not a.ps_path),
+                               local_direct=not a.ps_path, fuse_local_push=not a.no_fuse_local_push),
                       comm)
     batches = [synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=comm.rank + 1, step=s, label_count=a.labels,
                                       device=dev, zipf=a.zipf) for s in range(4)]
@@ -74,7 +77,8 @@ def main(argv=None):
             "data": "synthetic sparse CSR (hidden linear model labels)", "train_batch_accuracy": acc,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire,
-                       "exchange": "local-direct" if m._direct else "ps"},
+                       "exchange": "local-direct" if m._direct else "ps",
+                       "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1)},
         }), flush=True)
 
 

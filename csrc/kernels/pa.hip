@@ -17,6 +17,9 @@
 //     (each example's deltas independent: the reference's shared builder
 //      accumulates across examples).
 // Unlabelled examples (label < 0 for multiclass, 0 for binary) only predict.
+// wmap (nullable): the delta of pulled row r goes to row wmap[r] of ``delta`` -- at one
+// rank the PS push is added straight into the owner's table (the pulled snapshot is
+// still what the margins read).
 #include "common.h"
 
 using namespace fps;
@@ -36,7 +39,7 @@ __global__ void __launch_bounds__(256) pa_binary_kernel(const int64_t* __restric
                                                         const float* __restrict__ w, const int8_t* __restrict__ y,
                                                         int64_t B, int variant, float C, float* __restrict__ delta,
                                                         int8_t* __restrict__ pred, float* __restrict__ loss_out,
-                                                        float* __restrict__ flip) {
+                                                        float* __restrict__ flip, const int32_t* __restrict__ wmap) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -61,7 +64,8 @@ __global__ void __launch_bounds__(256) pa_binary_kernel(const int64_t* __restric
     if (lane == 0 && loss_out) atomicAdd(loss_out, loss);
     const float mult = pa_tau(variant, loss, n2, C) * (float)label;
     if (mult == 0.f) continue;
-    for (int64_t j = s + lane; j < e; j += 64) atomic_add_noret(delta + pos[j], mult * xval[j]);
+    for (int64_t j = s + lane; j < e; j += 64)
+      atomic_add_noret(delta + (wmap != nullptr ? wmap[pos[j]] : pos[j]), mult * xval[j]);
   }
 }
 
@@ -73,7 +77,8 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
                                                        int L, const int32_t* __restrict__ y, int64_t B, int mode,
                                                        int variant, float C, const float* __restrict__ cost,
                                                        float* __restrict__ delta, int32_t* __restrict__ pred,
-                                                       float* __restrict__ loss_out, float* __restrict__ flip) {
+                                                       float* __restrict__ loss_out, float* __restrict__ flip,
+                                                       const int32_t* __restrict__ wmap) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -109,7 +114,9 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
       if (loss_out) { const float ls = group_sum<64>(loss); if (lane == 0) atomicAdd(loss_out, ls); }
       const float mult = cl ? pa_tau(variant, loss, n2, C) * yc : 0.f;
       if (__ballot(mult != 0.f) == 0ull) continue;
-      if (cl) for (int64_t j = s; j < e; ++j) atomic_add_noret(delta + (int64_t)pos[j] * L + lane, xval[j] * mult);
+      if (cl)
+        for (int64_t j = s; j < e; ++j)
+          atomic_add_noret(delta + (int64_t)(wmap != nullptr ? wmap[pos[j]] : pos[j]) * L + lane, xval[j] * mult);
     } else {
       const float dy = __shfl(d, label, 64);
       float score = -INFINITY;
@@ -129,8 +136,9 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
       const float tau = n2 > 0.f ? loss / (2.f * n2) : 0.f;
       for (int64_t j = s + lane; j < e; j += 64) {
         const float v = tau * xval[j];
-        atomic_add_noret(delta + (int64_t)pos[j] * L + label, v);
-        atomic_add_noret(delta + (int64_t)pos[j] * L + q, -v);
+        const int64_t o = (int64_t)(wmap != nullptr ? wmap[pos[j]] : pos[j]) * L;
+        atomic_add_noret(delta + o + label, v);
+        atomic_add_noret(delta + o + q, -v);
       }
     }
   }
@@ -142,21 +150,22 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
 // table's untouched sentinel -0.0 into +0.0 (ShardedTable touch_sentinel).
 FPS_API int fps_pa_binary(const int64_t* indptr, const float* xval, const int32_t* pos, const float* w,
                           const int8_t* y, int64_t B, int variant, float C, float* delta, int8_t* pred,
-                          float* loss_out, float* flip, void* stream) {
+                          float* loss_out, float* flip, const int32_t* wmap, void* stream) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(pa_binary_kernel, dim3(grid_for(B, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, indptr,
-                     xval, pos, w, y, B, variant, C, delta, pred, loss_out, flip);
+                     xval, pos, w, y, B, variant, C, delta, pred, loss_out, flip, wmap);
   FPS_CHECK_LAUNCH();
   return 0;
 }
 
 FPS_API int fps_pa_multi(const int64_t* indptr, const float* xval, const int32_t* pos, const float* W, int L,
                          const int32_t* y, int64_t B, int mode, int variant, float C, const float* cost,
-                         float* delta, int32_t* pred, float* loss_out, float* flip, void* stream) {
+                         float* delta, int32_t* pred, float* loss_out, float* flip, const int32_t* wmap,
+                         void* stream) {
   if (B <= 0) return 0;
   if (L < 1 || L > 64) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pa_multi_kernel, dim3(grid_for(B, 4, 256 * 16)), dim3(256), 0, (hipStream_t)stream, indptr,
-                     xval, pos, W, L, y, B, mode, variant, C, cost, delta, pred, loss_out, flip);
+                     xval, pos, W, L, y, B, mode, variant, C, cost, delta, pred, loss_out, flip, wmap);
   FPS_CHECK_LAUNCH();
   return 0;
 }

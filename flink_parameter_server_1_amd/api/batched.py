@@ -112,6 +112,18 @@ class BatchedPSClient:
     def push(self, deltas: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         raise NotImplementedError
 
+    def local_push_target(self):
+        """``(table, row_map)`` when the answered pull's push may be applied by the
+        worker itself -- the owner is this rank (world 1), the PS rule is a plain
+        additive one and the pulled rows are a snapshot, not the table -- else None.
+        Adding the delta of pulled row ``r`` to ``table[row_map[r]]`` (float atomics)
+        is then the push; call ``push_applied()`` afterwards instead of ``push*``."""
+        return None
+
+    def push_applied(self) -> None:
+        """The answered pull's push was added to ``local_push_target()``'s table."""
+        raise NotImplementedError
+
     def push_unique(self, deltas: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         raise NotImplementedError
 

@@ -75,6 +75,7 @@ class _Client(BatchedPSClient):
         self._acc: Optional[torch.Tensor] = None
         self._mask: Optional[torch.Tensor] = None
         self._direct: Optional[torch.Tensor] = None
+        self._applied = False  # the worker added this answer's push to the table itself
         self._seq: List[tuple] = []  # (pos, deltas, mask) per push, combine="sequential"
         self._arb_keys: List[torch.Tensor] = []
         self._arb_vals: List[torch.Tensor] = []
@@ -183,6 +184,31 @@ class _Client(BatchedPSClient):
         else:
             self._acc += d.to(self._acc.dtype) * mask.view(-1, 1).to(self._acc.dtype)
         self._mask |= mask
+
+    def local_push_target(self):
+        plan = self._plan
+        if plan is None:
+            raise RuntimeError("local_push_target() is only valid inside on_pull_recv_batch")
+        rt, logic = self.rt, self.rt.ps_logic
+        ps = logic.ps if logic is not None else None
+        if ps is None or rt.comm.world != 1 or getattr(rt.comm, "loopback", False) or logic.locking:
+            return None
+        t = ps.table
+        if (logic.op != "add" or logic.combine != "sum" or logic.emit == "push" or ps.masked_push
+                or getattr(t, "optimizer", "") != "add" or getattr(t, "sparse", False) or plan.fixed
+                or t.weight.dtype != torch.float32 or plan.recv_rows is None or self._served_is_table(plan)):
+            return None
+        return t.weight, plan.recv_rows
+
+    def _served_is_table(self, plan) -> bool:
+        """A zero-copy serve hands the table itself out: a push into it would be read
+        back by the same micro-batch."""
+        return bool(getattr(plan, "zero_copy", False))
+
+    def push_applied(self) -> None:
+        if self._plan is None:
+            raise RuntimeError("push_applied() is only valid inside on_pull_recv_batch")
+        self._applied = True
 
     def push_keys(self, keys, deltas):
         if not self.rt.worker_logic.arbitrary_pushes:
@@ -334,6 +360,7 @@ class TensorRuntime:
     def _compute(self, rows, plan, reqs):
         c = self.client
         c._plan, c._acc, c._mask, c._direct = plan, None, None, None
+        c._applied = False
         c._arb_keys, c._arb_vals, c._seq = [], [], []
         with stage("engine.on_pull_recv", self.timer):
             for r in reqs:
@@ -350,7 +377,12 @@ class TensorRuntime:
         if not self.worker_logic.pushes:  # a query-only worker: no push round at all
             return
         ps = self.ps_logic.ps
-        if self.ps_logic.combine == "sequential":
+        if c._applied:  # the worker's kernel added the push to the (local) table already
+            if c._direct is not None or c._acc is not None or c._seq:
+                raise RuntimeError("push_applied() and push() on the same answer")
+            ps.note_local_push(plan)
+            self.counters.add("pushes", plan.n_unique)
+        elif self.ps_logic.combine == "sequential":
             self._push_rounds(plan, c)
         elif c._direct is not None:
             deltas, mask = c._direct, None
@@ -360,7 +392,7 @@ class TensorRuntime:
             deltas = torch.zeros((plan.n_unique, self.ps_logic.dim), dtype=self.ps_logic.dtype, device=self.device)
             mask = torch.zeros(plan.n_unique, dtype=torch.bool, device=self.device)
         emit = self.ps_logic.emit == "push"
-        if self.ps_logic.combine != "sequential":
+        if self.ps_logic.combine != "sequential" and not c._applied:
             updated = ps.push(plan, deltas, lr=self.ps_logic.lr, return_updated=emit, mask=mask)
             self.counters.add("pushes", plan.n_unique)
             for out in self.ps_logic.after_push(updated):

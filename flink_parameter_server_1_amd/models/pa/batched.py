@@ -41,6 +41,8 @@ class PAWorker(BatchedWorkerLogic):
         self.last = None          # (predictions [B], loss) of the latest micro-batch
         self.examples = 0
         self._seen = 0
+        #: apply the push in the kernel when the PS offers a local target (world 1)
+        self.fuse_local_push = True
 
     def open(self, ctx):
         self.device = torch.device(ctx.device)
@@ -57,14 +59,24 @@ class PAWorker(BatchedWorkerLogic):
     def on_pull_recv_batch(self, pulled, ps):
         indptr, values, labels, ids = pulled.payload
         rows = pulled.rows.float().contiguous()
-        delta = torch.zeros((pulled.n_unique, self.L), dtype=torch.float32, device=rows.device)
+        # one rank owns every feature: the kernel adds the push to the table itself
+        # (reading the pulled snapshot), no delta buffer, zeroing or apply pass
+        target = ps.local_push_target() if self.fuse_local_push else None
+        if target is not None:
+            delta, wmap = target
+        else:
+            delta = torch.zeros((pulled.n_unique, self.L), dtype=torch.float32, device=rows.device)
+            wmap = None
         if self.kind == "binary":
             pred, loss = ops.pa_binary(indptr, values, pulled.pos, rows.view(-1), labels, self.variant, self.C,
-                                       delta.view(-1), self.with_loss)
+                                       delta.view(-1), self.with_loss, wmap=wmap)
         else:
             pred, loss = ops.pa_multi(indptr, values, pulled.pos, rows, labels, self.kind, self.variant, self.C,
-                                      self.cost, delta, self.with_loss)
-        ps.push_unique(delta)
+                                      self.cost, delta, self.with_loss, wmap=wmap)
+        if target is not None:
+            ps.push_applied()
+        else:
+            ps.push_unique(delta)
         B = indptr.numel() - 1
         if ids is None:
             ids = torch.arange(self._seen, self._seen + B, device=labels.device)

@@ -42,6 +42,7 @@ class PAConfig:
     #: the most feature requests (nnz) a rank submits per micro-batch: fixed-shape PS
     #: plans (``TensorPS.capacity``: no split sizes on the host, capturable steps)
     capacity: Optional[int] = None
+    fuse_local_push: bool = True  # W = 1 PS path: the kernel adds its pushes into the table (no delta buffer)
 
 
 class DistributedPA:
@@ -71,6 +72,7 @@ class DistributedPA:
         logic = Logic(cfg.feature_count, self.L, **kw) if cfg.partition == "range" else \
             Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
         self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
+        self.worker.fuse_local_push = cfg.fuse_local_push
         self.runtime = TensorRuntime(self.comm, staleness=0, capacity=cfg.capacity).start(self.worker, logic)
         self.timer = None  # utils.metrics.StageTimer (optional)
 

@@ -1146,11 +1146,19 @@ def flip_sentinel(table: torch.Tensor, rows: torch.Tensor) -> None:
     table[r] = torch.where((x == 0) & torch.signbit(x), torch.zeros_like(x), x)
 
 
+def _wmap_cpu(delta, rows: int):
+    """CPU twin of the kernels' write map: a zero buffer over the pulled rows, added
+    into ``delta`` at the map afterwards."""
+    return torch.zeros((rows,) + tuple(delta.shape[1:]), dtype=delta.dtype)
+
+
 def pa_binary(indptr, xval, pos, w, y, variant: str, C: float, delta, with_loss: bool = False,
-              flip: Optional[torch.Tensor] = None):
+              flip: Optional[torch.Tensor] = None, wmap: Optional[torch.Tensor] = None):
     """Binary PA on a CSR micro-batch (K10); returns ``(pred int8[B], loss or None)``.
     ``flip`` (the in-place path: the table itself): the first pull of a feature turns
-    its untouched sentinel -0.0 into +0.0."""
+    its untouched sentinel -0.0 into +0.0.  ``wmap`` (int32, optional): the delta of
+    pulled row ``r`` is added to ``delta[wmap[r]]`` (a push the worker applies to the
+    owner's table itself)."""
     B = indptr.numel() - 1
     if flip is not None and not xval.is_cuda:
         flip_sentinel(flip.view(-1, 1), pos)
@@ -1158,18 +1166,25 @@ def pa_binary(indptr, xval, pos, w, y, variant: str, C: float, delta, with_loss:
         pred = torch.empty(B, dtype=torch.int8, device=xval.device)
         loss = torch.zeros(1, device=xval.device) if with_loss else None
         lib = N.require()
+        wm = None if wmap is None else _c(wmap.to(torch.int32))
         N.check(lib.fps_pa_binary(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(w).data_ptr(),
                                   _c(y).data_ptr(), B, PA_VARIANTS[variant], C, _c(delta).data_ptr(),
-                                  pred.data_ptr(), N.ptr(loss), N.ptr(flip), N.stream_ptr(xval.device)), "pa_binary")
+                                  pred.data_ptr(), N.ptr(loss), N.ptr(flip), N.ptr(wm), N.stream_ptr(xval.device)),
+                "pa_binary")
         return pred, loss
+    if wmap is not None:
+        tmp = _wmap_cpu(delta.view(-1, 1), w.numel())
+        pred, loss = R.pa_binary(indptr, xval, pos, w, y, PA_VARIANTS[variant], C, tmp.view(-1))
+        delta.view(-1).index_add_(0, wmap.long(), tmp.view(-1))
+        return pred, torch.tensor([loss])
     pred, loss = R.pa_binary(indptr, xval, pos, w, y, PA_VARIANTS[variant], C, delta)
     return pred, torch.tensor([loss])
 
 
 def pa_multi(indptr, xval, pos, W, y, mode: str, variant: str, C: float, cost, delta, with_loss: bool = False,
-             flip: Optional[torch.Tensor] = None):
+             flip: Optional[torch.Tensor] = None, wmap: Optional[torch.Tensor] = None):
     """Multiclass PA (OVA / cost PB / cost ML) on a CSR micro-batch (K11/K12); L <= 64.
-    ``flip``: as ``pa_binary``."""
+    ``flip`` / ``wmap``: as ``pa_binary``."""
     B = indptr.numel() - 1
     L = W.shape[1]
     if flip is not None and not xval.is_cuda:
@@ -1178,11 +1193,17 @@ def pa_multi(indptr, xval, pos, W, y, mode: str, variant: str, C: float, cost, d
         pred = torch.empty(B, dtype=torch.int32, device=xval.device)
         loss = torch.zeros(1, device=xval.device) if with_loss else None
         lib = N.require()
+        wm = None if wmap is None else _c(wmap.to(torch.int32))
         N.check(lib.fps_pa_multi(_c(indptr).data_ptr(), _c(xval).data_ptr(), _c(pos).data_ptr(), _c(W).data_ptr(), L,
                                  _c(y).data_ptr(), B, PA_MODES[mode], PA_VARIANTS[variant], C, N.ptr(cost),
-                                 _c(delta).data_ptr(), pred.data_ptr(), N.ptr(loss), N.ptr(flip),
+                                 _c(delta).data_ptr(), pred.data_ptr(), N.ptr(loss), N.ptr(flip), N.ptr(wm),
                                  N.stream_ptr(xval.device)), "pa_multi")
         return pred, loss
+    if wmap is not None:
+        tmp = _wmap_cpu(delta, W.shape[0])
+        pred, loss = R.pa_multi(indptr, xval, pos, W, y, PA_MODES[mode], PA_VARIANTS[variant], C, cost, tmp)
+        delta.index_add_(0, wmap.long(), tmp)
+        return pred, torch.tensor([loss])
     pred, loss = R.pa_multi(indptr, xval, pos, W, y, PA_MODES[mode], PA_VARIANTS[variant], C, cost, delta)
     return pred, torch.tensor([loss])
 

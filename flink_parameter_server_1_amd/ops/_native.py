@@ -79,9 +79,9 @@ _SIGNATURES = {
     "fps_sgns_step": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4g": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp],
-    "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_score_gemm": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp],
-    "fps_pa_multi": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "fps_pa_multi": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_ht_lookup": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                       c_int, c_f32, c_f32, c_u32, c_vp],
     "fps_ht_rehash": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],

@@ -81,6 +81,8 @@ class PullPlan:
     #: fixed-shape plan: the peers' flags stay on the device (``[W]`` int32)
     flags_dev: Optional[torch.Tensor] = None
     fixed: bool = False
+    #: the serve handed out the shard itself (``zero_copy_identity``), not a snapshot
+    zero_copy: bool = False
 
 
 @dataclass
@@ -465,6 +467,7 @@ class TensorPS:
             # identity plan: every row is served, only the keys present count as pulled
             if self.zero_copy_identity and self.wire_dtype == self.table.weight.dtype:
                 out = self.table.weight  # the pulled rows ARE the shard (read-only consumer)
+                plan.zero_copy = True
             else:
                 out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
             if sentinel:  # flip the untouched sentinel of the present rows only
@@ -595,7 +598,10 @@ class TensorPS:
         (world 1: its compute kernel added the deltas to ``recv_keys``' rows)."""
         if self.comm.world != 1 or getattr(self.table, "optimizer", "") != "add":
             raise ValueError("local pushes need world 1 and an additive table")
-        self._stats["pushes"] += plan.n_unique
+        if plan.valid is not None:  # static plan: its padding rows are never pushed
+            self._count_lazy("pushes", plan.valid)
+        else:
+            self._stats["pushes"] += plan.n_unique
 
     def reduce_requests(self, plan: PullPlan, deltas: torch.Tensor, op: str = "add",
                         mask: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -195,3 +195,60 @@ def test_pa_request_plan_matches_dedup_plan_gpu():
             assert m.ps.stats["unique"] == m.ps.stats["pulls"]
     assert torch.equal(dumps[0][0], dumps[1][0])
     torch.testing.assert_close(dumps[0][1], dumps[1][1], rtol=1e-4, atol=1e-6)
+
+
+def _pa_ps(dev, kind, L, dedup, fuse, F=1 << 20):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    m = DistributedPA(PAConfig(feature_count=F, kind=kind, label_count=L, local_direct=False, fuse_local_push=fuse),
+                      Comm(device=torch.device(dev)))
+    m.ps.dedup_mode = dedup
+    for s in range(6):
+        m.train_step(*synthetic_sparse_batch(512, 16, F, seed=5, step=s % 3, label_count=L, device=dev, zipf=1.0))
+    ids, w = m.dump()
+    o = torch.argsort(ids)
+    return ids[o].cpu(), w[o].reshape(ids.numel(), -1).cpu(), m.ps.stats["pushes"], m.runtime.counters.c["pushes"]
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("kind,L,dedup", [("binary", 1, True), ("binary", 1, False), ("ova", 4, None),
+                                          ("ml", 4, True)])
+def test_pa_ps_path_fused_local_push_equals_pushed_deltas(dev, kind, L, dedup):
+    """World 1: the PA kernel adding its push straight into the table through the write
+    map (``local_push_target``) == a pushed delta buffer applied by the PS: the same
+    touched features and weights (GPU: float atomics, summation order), the same push
+    counts."""
+    a = _pa_ps(dev, kind, L, dedup, True)
+    b = _pa_ps(dev, kind, L, dedup, False)
+    assert torch.equal(a[0], b[0])
+    tol = dict(rtol=1e-6, atol=1e-7) if dev == "cpu" else dict(rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(a[1], b[1], **tol)
+    assert a[2] == b[2] > 0 and a[3] == b[3]
+
+
+def test_local_push_target_refused_where_the_push_is_not_a_plain_local_add():
+    """No target when the pulled rows are the table (zero-copy serve), the rule is not a
+    plain add, or per-push outputs are emitted; pushes then travel as deltas."""
+    from flink_parameter_server_1_amd.api.batched import BatchedWorkerLogic
+    from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogic, DeviceSimplePSLogicWithClose
+
+    seen = []
+
+    class W(BatchedWorkerLogic):
+        def on_recv_batch(self, batch, ps):
+            ps.pull(batch)
+
+        def on_pull_recv_batch(self, pulled, ps):
+            seen.append(ps.local_push_target() is not None)
+            ps.push(torch.ones(len(pulled), 1))
+
+    for logic, expect in ((DeviceSimplePSLogicWithClose(50, 1, op="add"), True),
+                          (DeviceSimplePSLogic(50, 1, op="add"), False),  # emits every push
+                          (DeviceSimplePSLogicWithClose(50, 1, op="set"), False)):
+        seen.clear()
+        rt = TensorRuntime(Comm(), output_sink=lambda e: None).start(W(), logic)
+        rt.submit(torch.tensor([1, 2, 2, 7]))
+        rt.finish()
+        assert seen == [expect], (logic, seen)
