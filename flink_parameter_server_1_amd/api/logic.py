@@ -44,6 +44,9 @@ class RuntimeContext:
     device: Any = "cpu"
     task_name: str = ""
     config: Dict[str, Any] = field(default_factory=dict)
+    #: the rank's communicator (``parallel.comm.Comm`` or a virtual world's), for workers
+    #: that exchange data of their own (the top-K workers' candidate gather)
+    comm: Any = None
 
     # Flink-style accessors
     def getIndexOfThisSubtask(self) -> int:  # noqa: N802

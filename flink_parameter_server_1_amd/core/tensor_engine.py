@@ -256,7 +256,7 @@ class TensorRuntime:
         c = self.comm
         ps_logic.open(c)
         ps_logic.ps.timer = self.timer
-        worker_logic.open(RuntimeContext(c.rank, c.world, c.rank, c.world, self.device, "worker"))
+        worker_logic.open(RuntimeContext(c.rank, c.world, c.rank, c.world, self.device, "worker", comm=c))
         self.client = _Client(self)
         if ps_logic.locking:
             self.pipe = None

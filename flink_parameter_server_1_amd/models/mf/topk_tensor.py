@@ -480,7 +480,7 @@ class TopKQueryWorker(BatchedWorkerLogic, _TopKServing):
 
     def open(self, ctx):
         self.rank, self.device = ctx.rank, torch.device(ctx.device)
-        self.comm = Comm(device=self.device)
+        self.comm = getattr(ctx, "comm", None) or Comm(device=self.device)
         self.seen = SeenStore(self.memory, self.device, self.num_users)
 
     def update_model_batch(self, ids, values):
@@ -568,7 +568,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         from ...parallel.table import ShardedTable
 
         self.W, self.rank, self.device = ctx.world_size, ctx.rank, torch.device(ctx.device)
-        self.comm = Comm(device=self.device)
+        self.comm = getattr(ctx, "comm", None) or Comm(device=self.device)
         self._trained = torch.zeros((), dtype=torch.int64, device=self.device)
         self.seen = SeenStore(self.memory, self.device, self.num_users)
         self.items = ShardedTable(self.num_items, self.dim, self.rank, self.W, "hash",
