@@ -17,7 +17,7 @@ def load(d):
     return agg, {k: sum(v.values()) for k, v in dur.items()}
 
 
-def main(root="gpurun_out/pmc", names="mftopk,w2v,mf"):
+def main(root="gpurun_out/pmc", names="mftopk,w2v,mf", top="4"):
     print("| run | kernel | time (s, pass 1) | MFMA busy | waves waiting | LDS bank conflict / LDS active | HBM read | HBM write "
           "| read+write rate | of 8 TB/s |")
     print("|---|---|---|---|---|---|---|---|---|---|")
@@ -25,7 +25,7 @@ def main(root="gpurun_out/pmc", names="mftopk,w2v,mf"):
         a1, t1 = load(f"{root}/{name}_1")
         a2, t2 = load(f"{root}/{name}_2")
         a3, t3 = load(f"{root}/{name}_3")
-        for k in sorted(a1, key=lambda k: -t1.get(k, 0))[:4]:
+        for k in sorted(a1, key=lambda k: -t1.get(k, 0))[:int(top)]:
             c = a1[k]
             gui = c.get("GRBM_GUI_ACTIVE", 0) / 8  # summed over the 8 XCDs
             busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / 1024 / gui if gui else 0  # per SIMD
