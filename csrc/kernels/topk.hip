@@ -9,14 +9,14 @@
 //   1. tau = current k-th best.  Count the row's scores > tau (after the first
 //      bucket nearly none pass: the reference's own pruning argument,
 //      M/matrix/factorization/workers/PSTopKGeneratorWorker.scala:35-114).
-//   2. If more than CAP pass (first bucket), raise the threshold with a 2-level
-//      radix histogram (11 + 11 bits of the order-preserving float key) to the
-//      largest value that still keeps >= k candidates.
+//   2. If more than max(2k, 128) pass (first bucket), raise the threshold with a
+//      radix histogram digit by digit (11 + 11 + 10 bits of the order-preserving
+//      float key) to the largest value that still keeps >= k candidates.
 //   3. Collect the candidates into LDS, append the running top-k, bitonic-sort
 //      (key desc, then item id asc for ties) and keep the first k.
 //
-// Exact whenever fewer than CAP scores share the 22-bit key prefix of the k-th
-// best (ties beyond that are cut at CAP).
+// Exact whenever fewer than CAP scores tie with the k-th best (ties beyond that
+// are cut at CAP).
 #include "common.h"
 
 using namespace fps;
@@ -140,34 +140,33 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
     __syncthreads();
   }
   uint32_t thr = ktau + 1;  // keys >= thr are candidates
-  if (cnt > TK_CAP) {
-    // 2a. histogram of the top 11 key bits over the candidates
-    for (int i = tid; i < TK_BINS; i += TK_NT) hist[i] = 0;
-    __syncthreads();
-    for (int j = tid; j < n; j += TK_NT) {
-      const uint32_t kk = fkey(s[j]);
-      if (kk >= thr) atomicAdd(&hist[kk >> 21], 1u);
-    }
-    __syncthreads();
-    const int b1 = select_bin(hist, (uint32_t)k, &above, &bin_sel);
-    uint32_t total = above + hist[b1];
-    uint32_t t1 = (uint32_t)b1 << 21;
-    thr = t1 > thr ? t1 : thr;
-    __syncthreads();
-    if (total > TK_CAP) {
-      // 2b. refine inside bin b1 with the next 11 bits
-      const uint32_t need2 = (uint32_t)k > above ? (uint32_t)k - above : 1u;
+  // 2. more candidates than the sort should take (the first bucket / the seed segment:
+  //    all n): raise the threshold digit by digit (11 + 11 + 10 bits of the key) until
+  //    at most `target` keys pass -- the last digit makes it the exact k-th key, so the
+  //    bitonic sort below runs over ~k + k entries instead of up to TK_CAP + k (a
+  //    4096-entry sort per row was most of the seed segment's 184 us per 4096 rows)
+  const uint32_t target = (uint32_t)max(2 * k, 128);
+  if (cnt > target) {
+    uint32_t need = (uint32_t)k, above_sum = 0, prefix = 0;
+    for (int lvl = 0; lvl < 3; ++lvl) {
+      const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);  // digit = key bits [sh, sh + 11 or 10)
+      const int psh = lvl == 1 ? 21 : 10;                   // the digits above it: key >> psh
+      const uint32_t dmask = lvl == 2 ? 1023u : 2047u;
       for (int i = tid; i < TK_BINS; i += TK_NT) hist[i] = 0;
       __syncthreads();
       for (int j = tid; j < n; j += TK_NT) {
         const uint32_t kk = fkey(s[j]);
-        if ((kk >> 21) == (uint32_t)b1 && kk >= thr) atomicAdd(&hist[(kk >> 10) & (TK_BINS - 1)], 1u);
+        if (kk >= thr && (lvl == 0 || (kk >> psh) == (prefix >> psh))) atomicAdd(&hist[(kk >> sh) & dmask], 1u);
       }
       __syncthreads();
-      const int b2 = select_bin(hist, need2, &above, &bin_sel);
-      const uint32_t t2 = ((uint32_t)b1 << 21) | ((uint32_t)b2 << 10);
-      thr = t2 > thr ? t2 : thr;
+      const int b = select_bin(hist, need, &above, &bin_sel);
+      const uint32_t total = above_sum + above + hist[b];
+      prefix |= (uint32_t)b << sh;
+      thr = prefix > thr ? prefix : thr;
+      above_sum += above;
+      need = need > above ? need - above : 1u;
       __syncthreads();
+      if (total <= target) break;
     }
   }
   // 3. collect candidates (key >= thr), cut at TK_CAP
