@@ -113,6 +113,13 @@ __device__ void sort_keep_k(uint32_t* skey, int64_t* sid, int nc, float* bs, int
   }
 }
 
+// REG: the row (n <= TK_NT * TK_REG) is loaded once into registers, every pass below
+// reads them -- the streaming passes each waited out 16 dependent global-load round
+// trips per thread (the seed segment's 4096 x 4096 merge: 181 us with or without the
+// smaller sort)
+constexpr int TK_REG = 16;
+
+template <bool REG>
 __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restrict__ S, int64_t ldS, int n,
                                                            const int64_t* __restrict__ ids,
                                                            float* __restrict__ best_s, int64_t* __restrict__ best_i,
@@ -126,6 +133,26 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   const float* s = S + (int64_t)row * ldS;
   float* bs = best_s + (int64_t)row * k;
   int64_t* bi = best_i + (int64_t)row * k;
+  uint32_t kr[REG ? TK_REG : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int q = 0; q < TK_REG; ++q) {  // all loads in flight at once
+      const int j = tid + q * TK_NT;
+      kr[q] = j < n ? fkey(s[j]) : 0u;
+    }
+  }
+  // body(j, key) over this thread's entries of the row
+  auto for_keys = [&](auto&& body) {
+    if constexpr (REG) {
+#pragma unroll
+      for (int q = 0; q < TK_REG; ++q) {
+        const int j = tid + q * TK_NT;
+        if (j < n) body(j, kr[q]);
+      }
+    } else {
+      for (int j = tid; j < n; j += TK_NT) body(j, fkey(s[j]));
+    }
+  };
   const float tau = bs[k - 1];
   const uint32_t ktau = fkey(tau);
   // 1. count candidates strictly above tau (an empty running list: all n pass,
@@ -134,7 +161,7 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   __syncthreads();
   if (tau != -INFINITY) {
     uint32_t c = 0;
-    for (int j = tid; j < n; j += TK_NT) c += fkey(s[j]) > ktau;
+    for_keys([&](int, uint32_t kk) { c += kk > ktau; });
     c = (uint32_t)group_sum<64>((float)c);  // exact for counts < 2^24
     if ((tid & 63) == 0) atomicAdd(&cnt, c);
     __syncthreads();
@@ -143,8 +170,7 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   // 2. more candidates than the sort should take (the first bucket / the seed segment:
   //    all n): raise the threshold digit by digit (11 + 11 + 10 bits of the key) until
   //    at most `target` keys pass -- the last digit makes it the exact k-th key, so the
-  //    bitonic sort below runs over ~k + k entries instead of up to TK_CAP + k (a
-  //    4096-entry sort per row was most of the seed segment's 184 us per 4096 rows)
+  //    bitonic sort below runs over ~k + k entries instead of up to TK_CAP + k
   const uint32_t target = (uint32_t)max(2 * k, 128);
   if (cnt > target) {
     uint32_t need = (uint32_t)k, above_sum = 0, prefix = 0;
@@ -154,10 +180,9 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
       const uint32_t dmask = lvl == 2 ? 1023u : 2047u;
       for (int i = tid; i < TK_BINS; i += TK_NT) hist[i] = 0;
       __syncthreads();
-      for (int j = tid; j < n; j += TK_NT) {
-        const uint32_t kk = fkey(s[j]);
+      for_keys([&](int, uint32_t kk) {
         if (kk >= thr && (lvl == 0 || (kk >> psh) == (prefix >> psh))) atomicAdd(&hist[(kk >> sh) & dmask], 1u);
-      }
+      });
       __syncthreads();
       const int b = select_bin(hist, need, &above, &bin_sel);
       const uint32_t total = above_sum + above + hist[b];
@@ -172,13 +197,12 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   // 3. collect candidates (key >= thr), cut at TK_CAP
   if (tid == 0) cnt = 0;
   __syncthreads();
-  for (int j = tid; j < n; j += TK_NT) {
-    const uint32_t kk = fkey(s[j]);
+  for_keys([&](int j, uint32_t kk) {
     if (kk >= thr) {
       const uint32_t slot = atomicAdd(&cnt, 1u);
       if (slot < TK_CAP) { skey[slot] = kk; sid[slot] = ids[j]; }
     }
-  }
+  });
   __syncthreads();
   const int nc = (int)min(cnt, (uint32_t)TK_CAP);
   sort_keep_k(skey, sid, nc, bs, bi, k);
@@ -458,8 +482,12 @@ FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int6
                            int64_t* best_i, int k, void* stream) {
   if (B <= 0 || n <= 0) return 0;
   if (k <= 0 || k > TK_MAXK) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s, best_i,
-                     k);
+  if (n <= TK_NT * TK_REG)
+    hipLaunchKernelGGL(topk_merge_kernel<true>, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s,
+                       best_i, k);
+  else
+    hipLaunchKernelGGL(topk_merge_kernel<false>, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s,
+                       best_i, k);
   FPS_CHECK_LAUNCH();
   return 0;
 }
