@@ -36,3 +36,27 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def rccl_loopback():
+    """A one-rank RCCL process group on cuda:0: the collectives and point-to-point
+    calls of ``parallel.comm.Comm`` then run through RCCL kernels on a one-GPU box
+    (``Comm.loopback`` for the all-to-alls; p2p to the own rank)."""
+    import torch
+    import torch.distributed as dist
+    from dist_utils import free_port
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        yield
+    finally:
+        import gc
+
+        gc.collect()  # captured graphs that reference the communicator go first
+        torch.cuda.synchronize()
+        dist.destroy_process_group()

@@ -124,27 +124,6 @@ def test_syncing_worker_falls_back_to_eager():
     torch.testing.assert_close(tables[1], tables[0], rtol=1e-5, atol=1e-5)
 
 
-@pytest.fixture
-def rccl_loopback():
-    """A one-rank RCCL process group: the all-to-alls of fixed-shape plans then run
-    through RCCL kernels (``Comm.loopback``) on a one-GPU box."""
-    import torch.distributed as dist
-    from dist_utils import free_port
-
-    if dist.is_initialized():
-        pytest.skip("a process group is already initialised")
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
-                            device_id=DEV)
-    try:
-        yield
-    finally:
-        import gc
-
-        gc.collect()  # captured graphs that reference the communicator go first
-        torch.cuda.synchronize()
-        dist.destroy_process_group()
-
-
 def test_graph_replay_captures_rccl_collectives(rccl_loopback):
     """The world > 1 step shape: fixed-shape plans whose key / row / delta all-to-alls
     go through RCCL, captured into the hipGraph with the kernels around them.  Eager
