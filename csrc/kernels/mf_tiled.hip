@@ -740,6 +740,11 @@ FPS_API int64_t fps_tile_partition_ws_ints(int W, int T, int P) {
 // single-level scatter, the atomic two-level scatter and a capacity-slot variant
 // without counting pass were measured slower and removed in round 3
 // (profiles/r1_mf_partition_levels.md, r2_tp4.md).
+// count-kernel counter width: 16-bit packed unless set to 0 (A/B switch, FPS_TP_H16=0;
+// above 16k buckets always 16-bit)
+static int g_tp_h16 = 1;
+FPS_API void fps_tile_partition_set_h16(int v) { g_tp_h16 = v; }
+
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                                const int32_t* half, int R, int T, int P, int upp, int32_t* ws, int4* tmp, int32_t* ptr,
                                void* rec, int rec8, uint8_t* seen, void* stream) {
@@ -764,9 +769,12 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
   const int Gc = (G + sub - 1) / sub;
   int32_t* bhist = H1 + 1024 * (int64_t)NC;  // [1 + Gc][KT]: totals, then one row per count workgroup
-  // more than 16k buckets: 16-bit LDS counters (<= 64 KiB, the default dynamic-LDS
-  // ceiling, and room on the CU for two SGD workgroups beside the count workgroup)
-  const bool h16 = KT > 16384;
+  // 16-bit LDS counters (<= 64 KiB at 31k buckets, the default dynamic-LDS ceiling,
+  // and room on the CU for two SGD workgroups beside the count workgroup).  Also below
+  // 16k buckets, where 32-bit ones would fit: half the LDS per count workgroup, and the
+  // SGD beside it ran +0.4 % (local headline) / +0.8 % (PS path), same box
+  // (profiles/r4_count_width_ab.txt)
+  const bool h16 = g_tp_h16 != 0 || KT > 16384;  // 32-bit counters only fit 16k buckets
   const size_t hb_bytes = sizeof(int32_t) * (size_t)(h16 ? (KT + 1) / 2 : KT);
   if (h16) {
     hipLaunchKernelGGL(tp3_count_kernel<true>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,

@@ -494,6 +494,9 @@ class TilePartitioner:
                                               self.upp)
             return ptr, (u, row, r)
         lib = N.require()
+        h16 = os.environ.get("FPS_TP_H16")  # A/B switch of the count kernel's counter width
+        if h16 is not None:
+            lib.fps_tile_partition_set_h16(int(h16))
         n = uid.numel()
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))

@@ -307,6 +307,24 @@ def test_tile_partition_matches_reference(W, R, rec8, skew, phases):
     assert torch.equal(seen.cpu().bool(), torch.bincount(iid.long(), minlength=NI) > 0)
 
 
+@pytest.mark.parametrize("W,R,skew", [(1, 128, True), (8, 64, False), (1, 16, True)])
+def test_tile_partition_32bit_counters_match_reference(W, R, skew, monkeypatch):
+    """The 32-bit counter path of the count kernel (``FPS_TP_H16=0``; 16-bit packed
+    counters are the default at every bucket count): same partition as the reference."""
+    monkeypatch.setenv("FPS_TP_H16", "0")
+    try:
+        test_tile_partition_matches_reference(W, R, True, skew, 3)
+    finally:
+        monkeypatch.delenv("FPS_TP_H16")
+        N_lib().fps_tile_partition_set_h16(1)
+
+
+def N_lib():
+    from flink_parameter_server_1_amd.ops import _native
+
+    return _native.require()
+
+
 def R_tile(*a):
     return R.tile_partition(*a)
 
