@@ -118,21 +118,27 @@ __device__ void sort_keep_k(uint32_t* skey, int64_t* sid, int nc, float* bs, int
 // trips per thread (the seed segment's 4096 x 4096 merge: 181 us with or without the
 // smaller sort)
 constexpr int TK_REG = 16;
+// the register-row variant sorts at most TK_SORT_R entries (its threshold ends on the
+// exact k-th key, so only ties beyond TK_SORT_R - k are cut): 20 KiB of LDS instead of
+// 56 KiB, 8 workgroups per CU instead of 2
+constexpr int TK_SORT_R = 1024;
 
 template <bool REG>
 __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restrict__ S, int64_t ldS, int n,
                                                            const int64_t* __restrict__ ids,
                                                            float* __restrict__ best_s, int64_t* __restrict__ best_i,
                                                            int k) {
+  constexpr int SORT = REG ? TK_SORT_R : TK_SORT;
   __shared__ uint32_t hist[TK_BINS];
-  __shared__ uint32_t skey[TK_SORT];
-  __shared__ int64_t sid[TK_SORT];
+  __shared__ uint32_t skey[SORT];
+  __shared__ int64_t sid[SORT];
   __shared__ uint32_t cnt, above;
   __shared__ int bin_sel;
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* s = S + (int64_t)row * ldS;
   float* bs = best_s + (int64_t)row * k;
   int64_t* bi = best_i + (int64_t)row * k;
+  const uint32_t cap = REG ? (uint32_t)(TK_SORT_R - k) : (uint32_t)TK_CAP;  // candidates kept
   uint32_t kr[REG ? TK_REG : 1];
   if constexpr (REG) {
 #pragma unroll
@@ -194,17 +200,17 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
       if (total <= target) break;
     }
   }
-  // 3. collect candidates (key >= thr), cut at TK_CAP
+  // 3. collect candidates (key >= thr), cut at `cap`
   if (tid == 0) cnt = 0;
   __syncthreads();
   for_keys([&](int j, uint32_t kk) {
     if (kk >= thr) {
       const uint32_t slot = atomicAdd(&cnt, 1u);
-      if (slot < TK_CAP) { skey[slot] = kk; sid[slot] = ids[j]; }
+      if (slot < cap) { skey[slot] = kk; sid[slot] = ids[j]; }
     }
   });
   __syncthreads();
-  const int nc = (int)min(cnt, (uint32_t)TK_CAP);
+  const int nc = (int)min(cnt, cap);
   sort_keep_k(skey, sid, nc, bs, bi, k);
 }
 
