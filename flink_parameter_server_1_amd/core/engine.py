@@ -363,7 +363,8 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
               worker_receiver=None, worker_sender=None, ps_receiver=None, ps_sender=None,
               iteration_wait_time: Optional[float] = None, data_partitioner: Optional[Callable] = None,
               runtime=None, output_sink: Optional[Callable] = None, backend: str = "record",
-              comm=None, staleness: int = 0, num_ids: Optional[int] = None, combine: str = "sum") -> List[Any]:
+              comm=None, staleness: int = 0, num_ids: Optional[int] = None, combine: str = "sum",
+              graph: bool = False, capacity: Optional[int] = None) -> List[Any]:
     """Run a parameter-server job; returns the ``Left(wout)``/``Right(psout)`` stream.
 
     Covers the three reference overloads (``M/FlinkParameterServer.scala:62-336``):
@@ -394,7 +395,8 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
     being dropped: wire adapters (the wire is SoA tensors; batching =
     ``core.microbatch.MicroBatcher``), ``w_in_partition`` (answers always return
     to the requester), ``data_partitioner`` / ``runtime`` (each rank passes its
-    own source), parallelisms other than the world size.
+    own source), parallelisms other than the world size.  ``graph`` / ``capacity``
+    (tensor backend): hipGraph-replayed steps / fixed-shape plans (``TensorRuntime``).
     """
     if backend == "tensor":
         return _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_update, param_partitioner,
@@ -402,7 +404,9 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
                                  dict(worker_receiver=worker_receiver, worker_sender=worker_sender,
                                       ps_receiver=ps_receiver, ps_sender=ps_sender,
                                       data_partitioner=data_partitioner, runtime=runtime),
-                                 iteration_wait_time, output_sink, comm, staleness, num_ids, combine)
+                                 iteration_wait_time, output_sink, comm, staleness, num_ids, combine, graph, capacity)
+    if graph or capacity is not None:
+        raise ValueError("graph / capacity configure the tensor backend (backend='tensor')")
     if backend != "record":
         raise ValueError(f"backend must be 'record' or 'tensor', not {backend!r}")
     if num_ids is not None or combine != "sum" or comm is not None or staleness:
@@ -436,7 +440,7 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
 
 def _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_update, param_partitioner,
                       w_in_partition, worker_parallelism, ps_parallelism, adapters, iteration_wait_time, output_sink,
-                      comm, staleness, num_ids, combine):
+                      comm, staleness, num_ids, combine, graph=False, capacity=None):
     """``transform(backend="tensor")``: map the overloads onto the tensor engine
     (see ``transform``), refusing what it cannot honour."""
     import torch
@@ -486,7 +490,8 @@ def _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_u
                 raise ValueError("param_partitioner needs a dense shard allocated by the logic")
             ps_logic.partition = param_partitioner
     return transform_tensor(training_data, worker_logic, ps_logic, comm=comm, staleness=staleness,
-                            iteration_wait_time=iteration_wait_time, output_sink=output_sink)
+                            iteration_wait_time=iteration_wait_time, output_sink=output_sink, graph=graph,
+                            capacity=capacity)
 
 
 def _execute_local(rt: LocalRuntime, training_data, worker_logic, ps_logic, param_partitioner, w_in_partition,

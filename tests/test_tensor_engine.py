@@ -313,3 +313,23 @@ def test_fixed_shape_plans_equal_dynamic_plans(world):
     dyn = run_ranks(_per_push_outputs, world, None)
     fix = run_ranks(_per_push_outputs, world, 8)
     assert dyn == fix
+
+
+def _transform_fixed(rank, world, capacity):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    batches = [torch.tensor([rank * 7 + j, 3, 3]) for j in range(3)]
+    out = transform(batches, _CountWorker(), DeviceSimplePSLogicWithClose(40, 1, op="add"), backend="tensor",
+                    comm=Comm(), capacity=capacity)
+    return sorted((int(i), float(v)) for e in out if isinstance(e, Right)
+                  for i, v in zip(e.value[0].tolist(), e.value[1].reshape(-1).tolist()))
+
+
+def test_transform_tensor_passes_capacity_and_refuses_it_elsewhere():
+    """``transform(backend="tensor", capacity=...)`` runs fixed-shape plans (same dump as
+    dynamic plans at W = 2); the record backend refuses the tensor-only options."""
+    dyn = run_ranks(_transform_fixed, 2, None)
+    fix = run_ranks(_transform_fixed, 2, 3)
+    assert dyn == fix and dyn[0]
+    with pytest.raises(ValueError, match="tensor backend"):
+        transform([], _CountWorker(), None, capacity=4)
