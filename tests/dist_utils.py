@@ -40,7 +40,13 @@ def run_ranks(fn, world, *args):
     import pickle
 
     out_dir = tempfile.mkdtemp(prefix="fps_dist_")
-    mp.spawn(_entry, args=(world, free_port(), fn, args, out_dir), nprocs=world, join=True)
+    for attempt in range(2):
+        try:
+            mp.spawn(_entry, args=(world, free_port(), fn, args, out_dir), nprocs=world, join=True)
+            break
+        except Exception as e:  # a rendezvous port taken by a parallel test worker: once more
+            if attempt or not any(m in str(e) for m in ("Address already in use", "EADDRINUSE")):
+                raise
     results = []
     for r in range(world):
         with open(os.path.join(out_dir, f"r{r}.pkl"), "rb") as f:
