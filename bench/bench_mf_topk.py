@@ -44,6 +44,8 @@ def main(argv=None):
     ap.add_argument("--max-segment", type=int, default=None, help="LempTopK.max_segment (largest fused segment)")
     ap.add_argument("--unfused", action="store_true",
                     help="torch chains for the merge / SGD and eager scans (the A/B reference)")
+    ap.add_argument("--capacity", action="store_true",
+                    help="fixed-shape PS plans (capacity = the batch): at N > 1 no count exchange read on the host")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args(argv)
@@ -71,7 +73,8 @@ def main(argv=None):
         os.environ["FPS_TOPK_GRAPH"] = "0"
     logic = DeviceSimplePSLogic(a.users, a.dim, op="add_renorm", init=("uniform", -0.1, 0.1))
     logic.emit = "none"  # the benchmark keeps no output stream of the user updates
-    rt = TensorRuntime(comm, staleness=0, output_sink=lambda e: None).start(worker, logic)
+    rt = TensorRuntime(comm, staleness=0, output_sink=lambda e: None,
+                       capacity=a.batch if a.capacity else None).start(worker, logic)
     g = torch.Generator(device=dev)
     g.manual_seed(5)  # the same broadcast batches on every rank
 
@@ -109,7 +112,7 @@ def main(argv=None):
             "config": {"users": a.users, "items": a.items, "dim": a.dim, "k": a.k, "worker_k": a.worker_k,
                        "batch": a.batch, "negatives": a.negatives, "memory": a.memory, "bucket": a.bucket,
                        "seed_items": LempTopK.seed_items, "max_segment": LempTopK.max_segment,
-                       "fused": not a.unfused},
+                       "fused": not a.unfused, "fixed_plans": bool(a.capacity) and comm.world > 1},
         }), flush=True)
 
 
