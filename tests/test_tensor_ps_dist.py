@@ -104,3 +104,59 @@ def test_mixed_plan_kinds_apply_every_request(world):
     ids = torch.cat([r[3] for r in res])
     w = torch.cat([r[4] for r in res])
     torch.testing.assert_close(w, counts[ids][:, None].expand(-1, 4), rtol=0, atol=0)
+
+
+def _fixed_slots_and_targets(rank, world):
+    from flink_parameter_server_1_amd.api.batched import BatchedWorkerLogic
+    from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.parallel.table import ShardedTable
+    from flink_parameter_server_1_amd.parallel.tensor_ps import TensorPS
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogicWithClose
+
+    comm = Comm()
+    tab = ShardedTable(10, 2, comm.rank, comm.world, "hash", ("zeros",))
+    ps = TensorPS(tab, comm)
+    ps.capacity = 50
+    slots = (ps.fixed_slots(True), ps.fixed_slots(False))  # de-duplicating plans: at most the largest shard
+    seen = []
+
+    class W(BatchedWorkerLogic):
+        def on_recv_batch(self, batch, c):
+            c.pull(batch)
+
+        def on_pull_recv_batch(self, pulled, c):
+            seen.append(c.local_push_target())  # world > 1: the owners are other ranks
+            c.push(torch.ones(len(pulled), 1))
+
+    rt = TensorRuntime(comm, output_sink=lambda e: None).start(W(), DeviceSimplePSLogicWithClose(10, 1, op="add"))
+    rt.submit(torch.tensor([rank, 3]))
+    rt.finish()
+    return slots, seen
+
+
+def test_fixed_slots_and_no_local_push_target_across_ranks():
+    res = run_ranks(_fixed_slots_and_targets, 2)
+    for slots, seen in res:
+        assert slots == (5, 50)  # 10 ids over 2 shards: 5 rows per shard
+        assert seen == [None]
+
+
+def test_poll_flags_reads_one_submit_late():
+    """Fixed-shape plans: the flags of plan k reach the host at submit k + 1, and a new
+    input phase forgets them."""
+    from flink_parameter_server_1_amd.parallel.staleness import BoundedStalenessPipeline
+
+    pipe = BoundedStalenessPipeline.__new__(BoundedStalenessPipeline)
+    pipe.all_flagged, pipe._flags_dev, pipe._flags_host = False, None, None
+    pipe._flags_dev = torch.tensor([1, 0], dtype=torch.int32)
+    pipe.poll_flags()  # copies plan 0's flags, nothing read yet
+    assert not pipe.all_flagged
+    pipe._flags_dev = torch.tensor([1, 1], dtype=torch.int32)
+    pipe.poll_flags()  # reads plan 0's (not all set), copies plan 1's
+    assert not pipe.all_flagged
+    pipe._flags_dev = torch.tensor([1, 1], dtype=torch.int32)
+    pipe.poll_flags()  # reads plan 1's: every rank flagged
+    assert pipe.all_flagged
+    pipe.reset_flags()
+    assert not pipe.all_flagged and pipe._flags_host is None and pipe._flags_dev is None
