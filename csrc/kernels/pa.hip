@@ -51,7 +51,10 @@ __global__ void __launch_bounds__(256) pa_binary_kernel(const int64_t* __restric
       const float wv = w[pos[j]];
       // in place (flip = the table): a feature's first pull turns its -0.0 "untouched"
       // sentinel into +0.0 (table_ops.hip gather_rows_kernel), no byte-mark pass
-      if (flip != nullptr && __float_as_uint(wv) == 0x80000000u) flip[pos[j]] = 0.f;
+      // (a CAS, not a store: another wave may already have added into the fresh row,
+      // and a plain +0.0 store would overwrite its update)
+      if (flip != nullptr && __float_as_uint(wv) == 0x80000000u)
+        atomicCAS(reinterpret_cast<unsigned int*>(flip + pos[j]), 0x80000000u, 0u);
       m = fmaf(x, wv, m);
       n2 = fmaf(x, x, n2);
     }
@@ -91,7 +94,8 @@ __global__ void __launch_bounds__(256) pa_multi_kernel(const int64_t* __restrict
       if (cl) {
         const int64_t o = (int64_t)pos[j] * L + lane;
         const float wv = W[o];
-        if (flip != nullptr && __float_as_uint(wv) == 0x80000000u) flip[o] = 0.f;  // first pull (see binary)
+        if (flip != nullptr && __float_as_uint(wv) == 0x80000000u)  // first pull (see binary): CAS, never a store
+          atomicCAS(reinterpret_cast<unsigned int*>(flip + o), 0x80000000u, 0u);
         d = fmaf(x, wv, d);
       }
       n2 = fmaf(x, x, n2);

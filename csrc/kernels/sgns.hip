@@ -568,13 +568,6 @@ FPS_API int fps_sgns_step_v4g(const void* rows_in, const void* rows_out, int row
   return 0;
 }
 
-FPS_API int fps_sgns_step_v4(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
-                             const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,
-                             float neg_weight, float* d_in, float* d_out, float* loss_out, void* stream) {
-  return fps_sgns_step_v4g(rows_in, rows_out, rows_bf16, pos_c, pos_o, pos_neg, n_pairs, D, lr, neg_weight, d_in,
-                           d_out, loss_out, 1, stream);
-}
-
 // pos_neg holds K = 32 negative rows per block of 32 pairs (ceil(n_pairs/32) blocks)
 FPS_API int fps_sgns_step(const void* rows_in, const void* rows_out, int rows_bf16, const int32_t* pos_c,
                           const int32_t* pos_o, const int32_t* pos_neg, int64_t n_pairs, int D, float lr,

@@ -48,6 +48,12 @@ __global__ void __launch_bounds__(256) init_rows_kernel(float* __restrict__ tabl
 // store to the cache line the gather just read, and only on a row's first touch.
 constexpr uint32_t NEG0_BITS = 0x80000000u;
 __device__ __forceinline__ float pos0(float x) { return x == 0.f ? 0.f : x; }  // -0.0 -> +0.0
+// the flip is a CAS, never a plain store: a pipelined kernel may already be adding into
+// the fresh row (the next batch's gather beside this batch's push), and a +0.0 store
+// would overwrite its update; the CAS only replaces a value that is still the sentinel
+__device__ __forceinline__ void flip_neg0(float* p) {
+  atomicCAS(reinterpret_cast<unsigned int*>(p), NEG0_BITS, 0u);
+}
 
 template <int TPR, bool OUT_BF16, typename IDX>
 __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ table, const IDX* __restrict__ idx,
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
       const float v = src[j];
       if (OUT_BF16) ((uint16_t*)out)[r * D + j] = f32_to_bf16(v);
       else ((float*)out)[r * D + j] = v;
-      if (flip != nullptr && __float_as_uint(v) == NEG0_BITS) flip[row * D + j] = 0.f;
+      if (flip != nullptr && __float_as_uint(v) == NEG0_BITS) flip_neg0(flip + row * D + j);
     }
     if (touched != nullptr && j0 == 0) touched[row] = 1;
   }
@@ -164,10 +170,10 @@ __global__ void __launch_bounds__(256) gather_rows_v4_kernel(const to_f4* __rest
         out[r * D4 + j] = v[q];
         if (flip != nullptr) {
           float* f = flip + (row * D4 + j) * 4;
-          if (__float_as_uint(v[q].x) == NEG0_BITS) f[0] = 0.f;
-          if (__float_as_uint(v[q].y) == NEG0_BITS) f[1] = 0.f;
-          if (__float_as_uint(v[q].z) == NEG0_BITS) f[2] = 0.f;
-          if (__float_as_uint(v[q].w) == NEG0_BITS) f[3] = 0.f;
+          if (__float_as_uint(v[q].x) == NEG0_BITS) flip_neg0(f + 0);
+          if (__float_as_uint(v[q].y) == NEG0_BITS) flip_neg0(f + 1);
+          if (__float_as_uint(v[q].z) == NEG0_BITS) flip_neg0(f + 2);
+          if (__float_as_uint(v[q].w) == NEG0_BITS) flip_neg0(f + 3);
         }
       }
     }
@@ -480,6 +486,16 @@ __global__ void mark_rows_kernel(uint8_t* __restrict__ touched, const int32_t* _
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (rows[i] >= 0) touched[rows[i]] = 1;  // < 0: a padding slot
 }
+
+// identity plans over a sentinel table: flip the -0.0 entries of the rows whose mask
+// byte is set (the present keys), one thread per entry; rows without the mask are not
+// read (a whole-table masked_fill read and rewrote every row per micro-batch)
+__global__ void flip_masked_kernel(float* __restrict__ table, const uint8_t* __restrict__ mask, int64_t n_rows,
+                                   int D) {
+  const int64_t total = n_rows * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    if (mask[i / D] && __float_as_uint(table[i]) == NEG0_BITS) flip_neg0(table + i);
+}
 }  // namespace
 
 namespace {
@@ -654,6 +670,14 @@ FPS_API int fps_mark_rows(uint8_t* touched, const int32_t* rows, int64_t n, void
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mark_rows_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, touched,
                      rows, n);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+FPS_API int fps_flip_masked(float* table, const uint8_t* mask, int64_t n_rows, int D, void* stream) {
+  if (n_rows <= 0 || D <= 0) return 0;
+  hipLaunchKernelGGL(flip_masked_kernel, dim3(grid_for(n_rows * D, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream,
+                     table, mask, n_rows, D);
   FPS_CHECK_LAUNCH();
   return 0;
 }

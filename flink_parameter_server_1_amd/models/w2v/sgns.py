@@ -58,7 +58,9 @@ class SGNSConfig:
     unigram_power: float = 0.75
     seed: int = 0
     wire_dtype: str = "fp32"
-    pipeline: bool = True         # W > 1: row all-to-alls of batch k+1 overlap the SGNS step of batch k
+    pipeline: bool = True         # PS path (any W, world 1 included): the pulls of batch k+1 overlap the SGNS step
+                                  # of batch k, so each batch reads rows one batch stale (staleness 1); False =
+                                  # synchronous pulls (staleness 0)
     shared_negatives: int = 16    # negatives shared by each block of 32 pairs (16: kernel v4, 32: v3)
     neg_group: int = 4            # v4: consecutive 32-pair blocks sharing one negative set (1, 2, 4):
                                   # 4 measured +6 % pairs/s at the same loss curve (profiles/r2_sgns.md)

@@ -1149,6 +1149,19 @@ def flip_sentinel(table: torch.Tensor, rows: torch.Tensor) -> None:
     table[r] = torch.where((x == 0) & torch.signbit(x), torch.zeros_like(x), x)
 
 
+def flip_masked(table: torch.Tensor, mask: torch.Tensor) -> None:
+    """Sentinel flip of the rows whose ``mask`` entry is set (bool / uint8 ``[rows]``):
+    their -0.0 entries become +0.0.  Rows outside the mask are not read."""
+    if _on_gpu(table) and table.dtype == torch.float32:
+        m = mask.view(torch.uint8) if mask.dtype == torch.bool else mask
+        N.check(N.require().fps_flip_masked(_c(table).data_ptr(), _c(m).data_ptr(), table.shape[0],
+                                            table[0].numel() if table.shape[0] else 0, N.stream_ptr(table.device)),
+                "flip_masked")
+        return
+    w = table.view(table.shape[0], -1)
+    w.masked_fill_((w == 0) & torch.signbit(w) & mask.bool().view(-1, 1), 0.0)
+
+
 def _wmap_cpu(delta, rows: int):
     """CPU twin of the kernels' write map: a zero buffer over the pulled rows, added
     into ``delta`` at the map afterwards."""

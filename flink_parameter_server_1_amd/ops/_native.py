@@ -31,6 +31,7 @@ _SIGNATURES = {
     "fps_abi_version": [],
     "fps_init_rows": [c_vp, c_i64, c_int, c_i64, c_i64, c_f32, c_f32, c_u32, c_vp],
     "fps_mark_rows": [c_vp, c_vp, c_i64, c_vp],
+    "fps_flip_masked": [c_vp, c_vp, c_i64, c_int, c_vp],
     "fps_dedup_flags": [c_vp, c_i64, c_vp, c_vp, c_u32, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                         c_vp],
     "fps_dedup_flags_ws_ints": [c_i64, c_int],
@@ -78,7 +79,6 @@ _SIGNATURES = {
     "fps_known_append": [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "fps_sample_alias": [c_vp, c_vp, ctypes.c_int32, c_i64, c_u32, ctypes.c_uint64, c_vp, c_vp],
     "fps_sgns_step": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
-    "fps_sgns_step_v4": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp],
     "fps_sgns_step_v4g": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_vp, c_vp, c_vp, c_int, c_vp],
     "fps_pa_binary": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_score_gemm": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_vp],

@@ -246,7 +246,7 @@ class HashShardTable:
         if self.optimizer == "add_renorm":
             self.state[rows.long()] = self._store[rows.long()].norm(dim=1).float()
 
-    def dump(self, only_touched: bool = True):
+    def dump(self, only_touched: bool = True, raw: bool = False):
         """``(ids, rows)`` of every stored id (exactly the inserted ones)."""
         n = self.n_local
         return self.rowkey[:n].long(), self._store[:n]

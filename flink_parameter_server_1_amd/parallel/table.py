@@ -254,15 +254,20 @@ class ShardedTable:
             return
         ops.apply_rows(self.weight, loc, vals, "set", touched=self.touched)
 
-    def dump(self, only_touched: bool = True):
-        """(global ids, values) of this shard -- the close-time model output."""
+    def dump(self, only_touched: bool = True, raw: bool = False):
+        """(global ids, values) of this shard -- the close-time model output.  ``raw``:
+        values exactly as stored (snapshots keep the -0.0 untouched sentinel so a restore
+        keeps the touched set; model outputs print +0.0)."""
         if only_touched and self.sentinel:
             loc = torch.nonzero(self.touched_mask(), as_tuple=False).flatten()
         elif only_touched and self.touched is not None:
             loc = torch.nonzero(self.touched, as_tuple=False).flatten()
         else:
             loc = torch.arange(self.n_local, device=self.device)
-        return self.global_ids(loc), self.weight[loc]
+        vals = self.weight[loc]
+        if self.sentinel and not raw:  # model outputs never carry the sentinel: untouched entries print 0.0, not -0.0
+            vals = vals + 0.0
+        return self.global_ids(loc), vals
 
     def touched_mask(self) -> Optional[torch.Tensor]:
         """bool[n_local]: rows pulled or pushed so far (None: not tracked)."""

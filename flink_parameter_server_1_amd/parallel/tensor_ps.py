@@ -471,8 +471,7 @@ class TensorPS:
             else:
                 out = self.table.serve_rows(plan.recv_rows, self.wire_dtype, mark=False)
             if sentinel:  # flip the untouched sentinel of the present rows only
-                w = self.table.weight
-                w.masked_fill_((w == 0) & torch.signbit(w) & plan.valid.view(-1, 1), 0.0)
+                ops.flip_masked(self.table.weight, plan.valid)
             else:
                 touched |= plan.valid.view(torch.uint8)
             return out

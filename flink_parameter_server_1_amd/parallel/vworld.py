@@ -501,6 +501,7 @@ class VirtualComm(Comm):
         self.device = vw.device
         self.bytes_sent = 0
         self.peer_bytes = [0] * self.world
+        self.loopback = False  # Comm's world-1 all-to-all reads it (run_virtual(fn, 1))
 
     def _staged(self, t: torch.Tensor) -> bool:
         return False

@@ -178,7 +178,7 @@ def save_table(table, path: str, step: int = 0, only_touched: bool = False) -> N
     optimizer state (Adagrad accumulators / add_renorm lengths: ``<path>.state``)
     and the touched flags (``<path>.touched``), so a resumed run applies the same
     update rule to the same state and dumps the same touched rows."""
-    ids, vals = table.dump(only_touched)
+    ids, vals = table.dump(only_touched, raw=True)
     save_snapshot(path, ids, vals, part_kind=table.part_kind, num_ids=table.num_ids, world=table.world,
                   rank=table.rank, step=step)
     loc = table.local_of(ids.to(table.device)) if ids.numel() else ids.long()

@@ -85,3 +85,40 @@ def test_pa_paths_dump_the_pulled_features(device):
         o = torch.argsort(ids)
         out.append((ids[o].cpu(), w[o].reshape(-1).cpu()))
     assert torch.equal(out[0][0], out[1][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["binary", "multi"])
+def test_sentinel_flip_never_clobbers_a_concurrent_add(kind):
+    """the PA kernels flip a first-pulled feature's -0.0 sentinel in the
+    table while other waves already add their updates into it.  Many examples share ONE
+    fresh feature; the pulled snapshot stays -0.0 so every wave sees the sentinel and
+    flips.  The table must hold the exact sum of the updates (a plain +0.0 store would
+    drop every add that landed before it)."""
+    from flink_parameter_server_1_amd import ops
+
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    B, nnz, F, L = 8192, 8, 4096, 4
+    idx = torch.randint(1, F, (B, nnz), generator=g)
+    idx[:, 0] = 0  # the shared fresh feature
+    ip = (torch.arange(B + 1) * nnz).long().to(dev)
+    pos = idx.reshape(-1).to(torch.int32).to(dev)
+    val = (torch.rand(B * nnz, generator=g) + 0.5).to(dev)
+    if kind == "binary":
+        y = (torch.randint(0, 2, (B,), generator=g) * 2 - 1).to(torch.int8).to(dev)
+        snap = torch.full((F,), -0.0, device=dev)
+        table = torch.full((F,), -0.0, device=dev)
+        ref = torch.zeros(F, device=dev)
+        ops.pa_binary(ip, val, pos, snap, y, "PA-I", 1.0, table, flip=table)
+        ops.pa_binary(ip, val, pos, torch.zeros(F, device=dev), y, "PA-I", 1.0, ref)
+    else:
+        y = torch.randint(0, L, (B,), generator=g).to(torch.int32).to(dev)
+        snap = torch.full((F, L), -0.0, device=dev)
+        table = torch.full((F, L), -0.0, device=dev)
+        ref = torch.zeros(F, L, device=dev)
+        ops.pa_multi(ip, val, pos, snap, y, "ova", "PA-I", 1.0, None, table, flip=table)
+        ops.pa_multi(ip, val, pos, torch.zeros(F, L, device=dev), y, "ova", "PA-I", 1.0, None, ref)
+    torch.cuda.synchronize()
+    assert not torch.signbit(table[0]).any()  # the shared feature was flipped (and added to)
+    torch.testing.assert_close(table + 0.0, ref, rtol=1e-4, atol=1e-4)
