@@ -109,6 +109,11 @@ def main(argv=None):
                     help="fail fast: end this rank (exit 17) when a step makes no progress for this long (0 = off)")
     ap.add_argument("--no-hogwild-probe", action="store_true",
                     help="skip the side probe of lost user updates (run after the timed loop, reported in config)")
+    ap.add_argument("--verify", dest="verify", action="store_true", default=None,
+                    help="before timing, run a small instance of this exchange on the real process group and compare "
+                         "it with a sequential CPU replay (parallel/verify.py); a mismatch exits non-zero before any "
+                         "value is printed.  Default: on at N > 1")
+    ap.add_argument("--no-verify", dest="verify", action="store_false")
     ap.add_argument("--metrics-jsonl", default=None,
                     help="append per-step stage timings (HIP events) and counters of rank 0 to this JSON-lines file")
     a = ap.parse_args(argv)
@@ -122,16 +127,46 @@ def main(argv=None):
     comm = Comm.init_from_env()
     if comm.device.type == "cuda" and not ops.native_available():
         raise RuntimeError("gfx950 kernel library not built: run python csrc/build.py")
+    dev = comm.device
     n = comm.world
     if a.gpus != n:  # unreachable after _launch_guard; kept as a hard invariant
         raise SystemExit(f"[bench] --gpus {a.gpus} but the process group has {n} ranks")
+    verify = None
+    if a.verify if a.verify is not None else n > 1:
+        # the exchange of THIS job on THIS process group against a sequential replay,
+        # before anything is timed; every rank learns the verdict and exits on a mismatch
+        import torch.distributed as dist
+        from flink_parameter_server_1_amd.parallel import verify as V
+
+        ex = a.exchange if a.exchange in ("rotate", "ps") else ("rotate" if n > 1 else "local")
+        if ex == "local":
+            ex = "rotate"  # world 1: the rotation path without peers
+        mut = os.environ.get("FPS_VERIFY_MUTANT")  # fault injection: the check's own tests
+        verify = V.rotation_check(comm, schedule=a.rotation, exchange=ex, pipeline=not a.no_pipeline, wire=a.wire,
+                                  rotation_cls=V.mutant_rotation(mut) if mut else None)
+        ids = [V.device_identity(comm)]
+        if n > 1:
+            ids = [None] * n
+            dist.all_gather_object(ids, V.device_identity(comm))
+        verify["devices"] = ids
+        verify["rccl_version"] = V.rccl_version() if comm.device.type == "cuda" else None
+        if comm.backend == "nccl":  # one GPU per rank: a shared device would make the check meaningless
+            uu = [d.get("uuid") or d.get("device") for d in ids]
+            if len(set(uu)) != n:
+                verify["verify_ok"] = False
+                verify["verify_error"] = f"ranks share devices: {uu}"
+        if not verify["verify_ok"]:
+            if comm.rank == 0:
+                print(f"[bench] VERIFY FAILED: {json.dumps(verify)}", file=sys.stderr, flush=True)
+            sys.exit(3)
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
                    user_phases=a.user_phases, rotation=a.rotation)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
-    dev = comm.device
 
     def sync():
         if dev.type == "cuda":
@@ -254,6 +289,9 @@ def main(argv=None):
                 "lost_user_update_fraction": None if hog is None else hog.get("lost_update_fraction"),
             },
         }
+        if verify is not None:
+            out["verify_ok"] = verify["verify_ok"]
+            out["verify"] = verify
         print(json.dumps(out), flush=True)
     if timer is not None:
         timer.step_end()  # the flush's stages

@@ -55,3 +55,46 @@ def run_ranks(fn, world, *args):
             raise AssertionError(f"rank {r} failed:\n{err}")
         results.append(res)
     return results
+
+
+def _nccl_entry(rank, world, port, fn, args, out_dir):
+    """One rank of a real multi-GPU world: GPU ``rank``, RCCL (``nccl``) process group."""
+    import pickle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    try:
+        torch.cuda.set_device(rank)
+        dev = torch.device("cuda", rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        from flink_parameter_server_1_amd.parallel.comm import Comm
+
+        res, err = fn(Comm(device=dev), *args), None
+        torch.cuda.synchronize(dev)
+    except Exception:  # pragma: no cover - reported by the parent
+        res, err = None, traceback.format_exc()
+    with open(os.path.join(out_dir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump((res, err), f)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def run_nccl(fn, world, *args):
+    """Run ``fn(comm, *args)`` on ``world`` processes, one GPU each, over RCCL.  Every
+    child is a fresh interpreter (spawn), so nothing of the parent's GPU state is
+    inherited.  Returns the list of results (CPU objects)."""
+    import pickle
+
+    out_dir = tempfile.mkdtemp(prefix="fps_nccl_")
+    mp.spawn(_nccl_entry, args=(world, free_port(), fn, args, out_dir), nprocs=world, join=True)
+    results = []
+    for r in range(world):
+        with open(os.path.join(out_dir, f"r{r}.pkl"), "rb") as f:
+            res, err = pickle.load(f)
+        if err:
+            raise AssertionError(f"rank {r} failed:\n{err}")
+        results.append(res)
+    return results

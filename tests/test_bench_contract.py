@@ -55,6 +55,9 @@ def test_bench_two_ranks_gloo(exchange):
     d = lines[0]
     assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * 4096
     assert d["config"]["exchange"] == exchange
+    # --verify is on by default at N > 1: the job's exchange on its process group == the sequential replay
+    assert d["verify_ok"] is True and d["verify"]["verify_exchange"] == exchange
+    assert d["verify"]["verify_world"] == 2 and len(d["verify"]["devices"]) == 2
 
 
 def test_bench_gpus_without_torchrun_launches_ranks():
@@ -70,6 +73,18 @@ def test_bench_gpus_without_torchrun_launches_ranks():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
     assert len(d["config"]["bytes_sent_per_rank"]) == 2 and min(d["config"]["bytes_sent_per_rank"]) > 0
+
+
+def test_bench_verify_failure_prints_no_value():
+    """A broken exchange (FPS_VERIFY_MUTANT: the rotation sends the block it is about to
+    update instead of the finished one) must end every rank non-zero with no JSON line."""
+    env = dict(_env(), FPS_VERIFY_MUTANT="wrong_buffer")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", _free_port(), os.path.join(ROOT, "bench.py"), "--gpus", "2"] + TINY
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    assert _json_lines(p.stdout) == []
+    assert "VERIFY FAILED" in p.stderr
 
 
 def test_bench_world_size_mismatch_fails():
