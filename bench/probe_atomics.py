@@ -1,0 +1,48 @@
+"""Probe: per-user integer atomics at the headline geometry (64M ratings, 10M users).
+Design input for exact user rows (docs/ROUND5.md): what a per-rating ordinal
+(returning atomicAdd) or a per-rating lock (CAS + exchange) costs on gfx950."""
+import ctypes
+import json
+import os
+
+import torch
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libprobe_atomics.so")
+
+
+def main():
+    lib = ctypes.CDLL(LIB)
+    lib.probe_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                              ctypes.c_void_p]
+    n, users = 1 << 26, 10_000_000
+    dev = torch.device("cuda")
+    uid = torch.randint(0, users, (n,), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(users, dtype=torch.int32, device=dev)
+    ord_ = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    names = {0: "plain gather (baseline)", 1: "returning atomicAdd", 2: "no-return atomicAdd",
+             3: "lock CAS + exchange", 4: "returning atomicAdd, 1 lane per 16"}
+    for which in (0, 1, 2, 3, 4):
+        ts = []
+        for rep in range(4):
+            cnt.zero_()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = lib.probe_run(which, uid.data_ptr(), cnt.data_ptr(), ord_.data_ptr(), n, st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, rc
+            if rep:
+                ts.append(e0.elapsed_time(e1))
+        ok = None
+        if which in (1, 4):  # ordinals of each user are 0..c-1
+            c = torch.bincount(uid.long(), minlength=users)
+            ok = bool(torch.equal(cnt.long(), c)) and int(ord_.max()) == int(c.max()) - 1
+        if which == 3:
+            ok = int(cnt.abs().sum()) == 0
+        print(json.dumps({"probe": names[which], "ms": min(ts), "per_s": n / (min(ts) / 1e3), "ok": ok}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

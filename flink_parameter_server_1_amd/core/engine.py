@@ -377,8 +377,8 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
     ``backend="tensor"`` runs the job on the tensor engine instead
     (``core.tensor_engine``, one process per GPU under torchrun):
     ``training_data`` is this rank's iterable of micro-batches,
-    ``worker_logic`` a ``BatchedWorkerLogic``; worker / PS parallelism = the
-    world size of ``comm``; ``staleness`` bounds the micro-batches in flight
+    ``worker_logic`` a ``BatchedWorkerLogic``; worker / PS parallelism = at most
+    the world size of ``comm`` (default: equal to it); ``staleness`` bounds the micro-batches in flight
     (the ``pullLimit`` analogue, ``tensor_engine.staleness_for_pull_limit``).
     The three overloads map to:
 
@@ -395,7 +395,8 @@ def transform(training_data, worker_logic: WorkerLogic, ps_logic: Optional[Param
     being dropped: wire adapters (the wire is SoA tensors; batching =
     ``core.microbatch.MicroBatcher``), ``w_in_partition`` (answers always return
     to the requester), ``data_partitioner`` / ``runtime`` (each rank passes its
-    own source), parallelisms other than the world size.  ``graph`` / ``capacity``
+    own source), parallelisms above the world size (``worker_parallelism`` /
+    ``ps_parallelism`` below it leave ranks without a worker / shard).  ``graph`` / ``capacity``
     (tensor backend): hipGraph-replayed steps / fixed-shape plans (``TensorRuntime``).
     """
     if backend == "tensor":
@@ -462,9 +463,9 @@ def _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_u
         raise TypeError("backend='tensor' needs a BatchedWorkerLogic (api.batched)")
     comm = comm or Comm()
     for name, par in (("worker_parallelism", worker_parallelism), ("ps_parallelism", ps_parallelism)):
-        if par is not None and int(par) != comm.world:
-            raise ValueError(f"backend='tensor': {name}={par} but the job has {comm.world} ranks (one worker and "
-                             "one PS shard per rank)")
+        if par is not None and not 1 <= int(par) <= comm.world:
+            raise ValueError(f"backend='tensor': {name}={par} but the job has {comm.world} ranks (at most one "
+                             "worker and one PS shard per rank)")
     if ps_logic is None:
         if param_init is None or param_update is None:
             raise ValueError("give ps_logic or (param_init, param_update)")
@@ -491,7 +492,7 @@ def _transform_tensor(training_data, worker_logic, ps_logic, param_init, param_u
             ps_logic.partition = param_partitioner
     return transform_tensor(training_data, worker_logic, ps_logic, comm=comm, staleness=staleness,
                             iteration_wait_time=iteration_wait_time, output_sink=output_sink, graph=graph,
-                            capacity=capacity)
+                            capacity=capacity, worker_parallelism=worker_parallelism, ps_parallelism=ps_parallelism)
 
 
 def _execute_local(rt: LocalRuntime, training_data, worker_logic, ps_logic, param_partitioner, w_in_partition,

@@ -226,13 +226,26 @@ class TensorRuntime:
 
     def __init__(self, comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
                  output_sink: Optional[Callable[[Any], None]] = None, lookahead: Optional[bool] = None,
-                 graph: bool = False, capacity: Optional[int] = None):
+                 graph: bool = False, capacity: Optional[int] = None, worker_parallelism: Optional[int] = None,
+                 ps_parallelism: Optional[int] = None):
         """``graph``: replay fixed-shape micro-batch steps from captured hipGraphs
         (``core.step_graph``: static plans at world 1, fixed-shape plans over RCCL at
         world > 1, a ``graph_safe`` worker).  ``capacity``: the most keys this rank
         pulls per micro-batch -- fixed-shape plans (``TensorPS.capacity``: no host
-        copy of split sizes; required by ``graph`` at world > 1)."""
+        copy of split sizes; required by ``graph`` at world > 1).
+
+        ``worker_parallelism`` / ``ps_parallelism`` (each <= the world, default the
+        world): ranks ``>= worker_parallelism`` run no worker input (they still join
+        every collective), ranks ``>= ps_parallelism`` hold no PS shard -- the
+        reference's independent ``workerParallelism`` / ``psParallelism``
+        (``M/FlinkParameterServer.scala:126-138``: shard ``|id| % psParallelism``)."""
         self.comm = comm or Comm()
+        W = self.comm.world
+        self.worker_parallelism = int(worker_parallelism or W)
+        self.ps_parallelism = int(ps_parallelism or W)
+        for name, v in (("worker_parallelism", self.worker_parallelism), ("ps_parallelism", self.ps_parallelism)):
+            if not 1 <= v <= W:
+                raise ValueError(f"{name}={v} on a job of {W} ranks: need 1 <= {name} <= ranks")
         self.device = self.comm.device
         self.staleness = int(staleness)
         self.lookahead = lookahead
@@ -254,9 +267,14 @@ class TensorRuntime:
         """Open both logics on this rank (``open`` of the reference's operators)."""
         self.worker_logic, self.ps_logic = worker_logic, ps_logic
         c = self.comm
+        if self.ps_parallelism != c.world:
+            if ps_logic.locking or ps_logic.sparse:
+                raise ValueError("ps_parallelism < ranks needs a dense, non-locking PS logic")
+            ps_logic.ps_parallelism = self.ps_parallelism
         ps_logic.open(c)
         ps_logic.ps.timer = self.timer
-        worker_logic.open(RuntimeContext(c.rank, c.world, c.rank, c.world, self.device, "worker", comm=c))
+        worker_logic.open(RuntimeContext(min(c.rank, self.worker_parallelism - 1), self.worker_parallelism, c.rank,
+                                         c.world, self.device, "worker", comm=c))
         self.client = _Client(self)
         if ps_logic.locking:
             self.pipe = None
@@ -546,6 +564,8 @@ class TensorRuntime:
         if ps_logic.locking:
             raise NotImplementedError("execute() with a locking PS logic: drive it with submit()/finish()")
         self.start(worker_logic, ps_logic)
+        if self.comm.rank >= self.worker_parallelism:
+            source = ()  # no worker subtask on this rank: it serves its shard and joins the collectives
         if model is not None or worker_model is not None:
             self.load_model(model, worker_model)
         if self.iteration_wait_time is not None:
@@ -641,11 +661,14 @@ def fold_outputs(outputs: Iterable) -> tuple:
 def transform_tensor(source: Iterable, worker_logic: BatchedWorkerLogic, ps_logic: DevicePSLogic, *,
                      comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
                      output_sink: Optional[Callable] = None, model=None, worker_model=None, graph: bool = False,
-                     capacity: Optional[int] = None) -> List[Any]:
+                     capacity: Optional[int] = None, worker_parallelism: Optional[int] = None,
+                     ps_parallelism: Optional[int] = None) -> List[Any]:
     """Tensor-engine ``transform`` on this rank (SPMD under torchrun): ``source``
     is this rank's iterable of micro-batches.  ``graph`` / ``capacity``: captured
-    steps / fixed-shape plans (``TensorRuntime``)."""
-    rt = TensorRuntime(comm, staleness, iteration_wait_time, output_sink, graph=graph, capacity=capacity)
+    steps / fixed-shape plans; ``worker_parallelism`` / ``ps_parallelism``: at most
+    the world each (``TensorRuntime``)."""
+    rt = TensorRuntime(comm, staleness, iteration_wait_time, output_sink, graph=graph, capacity=capacity,
+                       worker_parallelism=worker_parallelism, ps_parallelism=ps_parallelism)
     return rt.execute(source, worker_logic, ps_logic, model=model, worker_model=worker_model)
 
 

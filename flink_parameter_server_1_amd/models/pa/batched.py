@@ -90,13 +90,17 @@ class PAWorker(BatchedWorkerLogic):
 def transform_pa_tensor(batches: Iterable, feature_count: int, kind: str = "binary", label_count: int = 1,
                         variant: str = "PA", C: float = 1.0, range_partitioning: bool = True, model=None,
                         cost: Optional[torch.Tensor] = None, comm: Optional[Comm] = None, staleness: int = 0,
-                        wire: str = "fp32"):
+                        wire: str = "fp32", worker_parallelism: Optional[int] = None,
+                        ps_parallelism: Optional[int] = None):
     """``transformBinary`` / ``transformMulticlass`` on the tensor engine (this rank's
     part; ``batches`` = this rank's CSR micro-batches).  ``model`` = this rank's
-    ``(feature, weight(s))`` warm-start records (``transformWithModelLoad``)."""
+    ``(feature, weight(s))`` warm-start records (``transformWithModelLoad``).
+    ``ps_parallelism`` P <= ranks: the model lives in P shards (``rangePartitionerPS``
+    over P, ``PassiveAggressiveParameterServer.scala:372-384``) on ranks 0..P-1."""
     L = 1 if kind == "binary" else label_count
     Logic = DeviceRangePSLogicWithClose if range_partitioning else DeviceSimplePSLogicWithClose
     logic = Logic(feature_count, L, init=("zeros",), wire_dtype=wire) if range_partitioning else \
         Logic(feature_count, L, init=("zeros",), partition="hash", wire_dtype=wire)
-    rt = TensorRuntime(comm, staleness=staleness)
+    rt = TensorRuntime(comm, staleness=staleness, worker_parallelism=worker_parallelism,
+                       ps_parallelism=ps_parallelism)
     return rt.execute(batches, PAWorker(kind, L, variant, C, cost), logic, model=model)

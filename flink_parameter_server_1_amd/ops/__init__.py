@@ -201,8 +201,15 @@ class DedupWorkspace:
     FLAGS_MAX_RATIO = 8
 
     def __init__(self, num_ids: int, W: int, part_kind: int = 0, block: int = 1, device="cpu",
-                 hashed: Optional[bool] = None, method: Optional[str] = None):
+                 hashed: Optional[bool] = None, method: Optional[str] = None, out_world: Optional[int] = None):
+        """``W`` = number of PS shards the keys route to (hash ``|id| % W``, range by
+        ``block``); ``out_world`` (>= W, default W) = ranks of the all-to-all: the
+        returned ``counts`` / ``prefix`` cover every rank, ranks >= W (no shard) get
+        zero keys -- ``ps_parallelism < world`` without a host owner table."""
         self.num_ids, self.W, self.part_kind, self.block = num_ids, W, part_kind, block
+        self.out_world = int(out_world or W)
+        if self.out_world < W:
+            raise ValueError(f"out_world {out_world} < shards {W}")
         self.method = method or os.environ.get("FPS_DEDUP")  # None = auto | "claim" | "flags"
         if self.method not in (None, "claim", "flags"):
             raise ValueError(f"dedup method must be 'claim' or 'flags', not {self.method!r}")
@@ -239,7 +246,8 @@ class DedupWorkspace:
 
     def run(self, keys: torch.Tensor):
         if self.device.type != "cuda":
-            return R.dedup(keys, self.W, self.part_kind, self.block)
+            c, p, u, q = R.dedup(keys, self.W, self.part_kind, self.block)
+            return self._widen(c, p) + (u, q)
         n = keys.numel()
         self._grow(max(n, 1))
         self.epoch += 1
@@ -272,14 +280,25 @@ class DedupWorkspace:
             N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch, self.W,
                                   self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
                                   self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup")
-        return self.counts, self.prefix, self.uniq, self.pos[:n]
+        return self._widen(self.counts, self.prefix) + (self.uniq, self.pos[:n])
+
+    def _widen(self, counts, prefix):
+        """``(counts[out_world], prefix[out_world + 1])``: the shards' counts, then zeros
+        for the ranks without a shard (their prefix entries repeat the total)."""
+        if self.out_world == self.W:
+            return counts, prefix
+        E = self.out_world - self.W
+        counts = torch.cat([counts[:self.W], counts.new_zeros(E)])
+        prefix = torch.cat([prefix[:self.W + 1], prefix[self.W:self.W + 1].expand(E)])
+        return counts, prefix
 
     def route(self, keys: torch.Tensor):
         """Like ``run`` but WITHOUT de-duplication: every request is its own entry of
         ``uniq`` (grouped by owning shard), ``pos`` a permutation of the requests.
         Same return layout as ``run``."""
         if self.device.type != "cuda":
-            return R.route(keys, self.W, self.part_kind, self.block)
+            c, p, u, q = R.route(keys, self.W, self.part_kind, self.block)
+            return self._widen(c, p) + (u, q)
         n = keys.numel()
         self._grow(max(n, 1))
         self.counts.zero_()
@@ -287,7 +306,7 @@ class DedupWorkspace:
                                                self.counts.data_ptr(), self.prefix.data_ptr(),
                                                self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(),
                                                N.stream_ptr(self.device)), "route_requests")
-        return self.counts, self.prefix, self.uniq, self.pos[:n]
+        return self._widen(self.counts, self.prefix) + (self.uniq, self.pos[:n])
 
     def reset_claims(self, keys: torch.Tensor) -> None:
         """Empty the claim entries of ``keys`` (the step's unique keys).  In

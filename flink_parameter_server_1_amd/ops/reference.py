@@ -50,6 +50,8 @@ def gather_rows(table, idx, out_dtype=torch.float32, touched=None):
     keep = idx >= 0
     if touched is not None:
         touched[idx[keep]] = 1
+    if table.shape[0] == 0:  # a rank without a shard serves only padding slots
+        return torch.zeros((idx.numel(),) + tuple(table.shape[1:]), dtype=out_dtype, device=table.device)
     out = table[idx.clamp_min(0)].to(out_dtype)
     return torch.where(keep.view(-1, *([1] * (out.dim() - 1))), out, torch.zeros_like(out))
 

@@ -102,7 +102,8 @@ class ShardedTable:
         else:
             self.part = HashPartitioner(world) if partition == "hash" else RangePartitioner(world, num_ids)
         self.block = 1 if partition == "hash" else self.part.block
-        self.n_local = self.part.shard_size(self.num_ids, rank)
+        # rank >= world: a rank of a larger job holding no shard (ps_parallelism < ranks)
+        self.n_local = self.part.shard_size(self.num_ids, rank) if rank < world else 0
         self.optimizer = optimizer
         self.seed = seed
         self.init_spec = init

@@ -117,8 +117,17 @@ class TensorPS:
         self.comm = comm
         self.wire_dtype = wire_dtype
         # sparse-id tables (parallel.hash_table) dedup through the per-batch hashed claim map
-        self.dedup = ops.DedupWorkspace(table.key_space, comm.world, table.part_kind, table.block, table.device,
-                                        hashed=True if getattr(table, "sparse", False) else None)
+        #: PS shards (``ps_parallelism``): shard s lives on rank s; ranks >= shards hold
+        #: none and receive no keys.  The owner of a key is computed on the device from
+        #: the table's partition over ``shards`` (``|id| % P`` or ``|id| // ceil(F/P)``)
+        self.shards = int(getattr(table, "world", comm.world))
+        if self.shards > comm.world or self.shards < 1:
+            raise ValueError(f"{self.shards} PS shards on {comm.world} ranks: need 1 <= shards <= ranks")
+        if self.shards != comm.world and getattr(table, "sparse", False):
+            raise ValueError("sparse (hash-table) shards need one shard per rank")
+        self.dedup = ops.DedupWorkspace(table.key_space, self.shards, table.part_kind, table.block, table.device,
+                                        hashed=True if getattr(table, "sparse", False) else None,
+                                        out_world=comm.world)
         self._stats = {"pulls": 0, "unique": 0, "steps": 0, "host_waits": 0, "host_stalls": 0, "pushes": 0}
         #: plans whose counts went to the host through an event (``PendingPlan.seq``)
         self._plan_seq = 0
@@ -217,7 +226,7 @@ class TensorPS:
         C = int(self.capacity)
         if unique:  # de-duplicated keys to one owner: at most its shard's rows
             t = self.table
-            C = min(C, max(t.part.shard_size(t.num_ids, r) for r in range(self.comm.world)))
+            C = min(C, max(t.part.shard_size(t.num_ids, r) for r in range(self.shards)))
         return max(C, 1)
 
     def _fixed_plan(self, keys: torch.Tensor, flag: int, dedup: Optional[bool]) -> PendingPlan:

@@ -89,14 +89,17 @@ class DevicePSLogic:
                  lr: float = 0.0, dtype=torch.float32, track_touched: bool = True,
                  table: Optional[ShardedTable] = None, ps: Optional[TensorPS] = None, sparse: bool = False,
                  capacity: int = 1 << 14, init_fn: Optional[Callable] = None, update_fn: Optional[Callable] = None,
-                 combine: str = "sum", dedup: Optional[bool] = None):
+                 combine: str = "sum", dedup: Optional[bool] = None, ps_parallelism: Optional[int] = None):
         """``table`` / ``ps``: serve an existing shard (and its PS front) instead of
         allocating one at ``open`` -- how the model classes (``DistributedMF``,
         ``DistributedPA``) run their PS path through this engine.  ``sparse``: a
         device hash-table shard (``num_ids`` may be None, ``capacity`` = initial
         rows per shard; it grows).  ``dedup``: de-duplicate each micro-batch's pulled
         keys (True), ship every request (False), or let the PS decide by batch size
-        (None, ``TensorPS.dedups``); additive rules only ship requests."""
+        (None, ``TensorPS.dedups``); additive rules only ship requests.
+        ``ps_parallelism``: shards P <= ranks (default: one per rank); shard s lives on
+        rank s, the owner of an id is ``|id| % P`` (hash) or ``|id| // ceil(F/P)``
+        (range), computed on the device -- no host owner table."""
         if op not in OPS:
             raise ValueError(f"op must be one of {OPS}, not {op!r}")
         if combine not in COMBINE:
@@ -117,6 +120,7 @@ class DevicePSLogic:
         self.sparse, self.capacity = bool(sparse), int(capacity)
         self.init_fn, self.update_fn, self.combine = init_fn, update_fn, combine
         self.dedup = dedup
+        self.ps_parallelism = ps_parallelism
         self.table: Optional[ShardedTable] = None
         self.ps: Optional[TensorPS] = None
 
@@ -124,6 +128,11 @@ class DevicePSLogic:
     def open(self, comm: Comm) -> None:
         """Allocate this rank's shard (``ParameterServerLogic.open``)."""
         table, ps = self._given
+        P = int(self.ps_parallelism or comm.world)
+        if not 1 <= P <= comm.world:
+            raise ValueError(f"ps_parallelism={P} on {comm.world} ranks: need 1 <= P <= ranks")
+        if P != comm.world and (self.sparse or self.locking or table is not None):
+            raise ValueError("ps_parallelism < ranks needs a dense, non-locking shard allocated by the logic")
         if table is not None:
             self.table = table
         elif self.sparse:
@@ -133,13 +142,13 @@ class DevicePSLogic:
         else:
             partition, owner = self.partition, None
             if not isinstance(partition, str):
-                owner, partition = owner_table(partition, self.num_ids, comm.world), "lookup"
+                owner, partition = owner_table(partition, self.num_ids, P), "lookup"
             track = self.track_touched or self.emit == "close" or self.op == "fn"
             # zero-init additive fp32 shards track touched rows by the -0.0 sentinel
             # (ShardedTable touch_sentinel: no byte-mark pass per micro-batch)
             sentinel = (track and tuple(self.init) == ("zeros",) and self.op in ("add", "sgd")
                         and self.dtype == torch.float32 and partition != "lookup" and self.init_fn is None)
-            self.table = ShardedTable(self.num_ids, self.dim, comm.rank, comm.world, partition, self.init,
+            self.table = ShardedTable(self.num_ids, self.dim, comm.rank, P, partition, self.init,
                                       self.seed, comm.device, optimizer=self.op, track_touched=track,
                                       dtype=self.dtype, owner=owner, init_fn=self.init_fn, update_fn=self.update_fn,
                                       touch_sentinel=sentinel)

@@ -47,13 +47,24 @@ def run_ranks(fn, world, *args):
         except Exception as e:  # a rendezvous port taken by a parallel test worker: once more
             if attempt or not any(m in str(e) for m in ("Address already in use", "EADDRINUSE")):
                 raise
-    results = []
+    return _collect(out_dir, world)
+
+
+def _collect(out_dir, world):
+    """Per-rank results; on failure every failed rank's traceback, the root cause (an
+    error that is not a peer's closed connection) first."""
+    import pickle
+
+    results, errs = [], []
     for r in range(world):
         with open(os.path.join(out_dir, f"r{r}.pkl"), "rb") as f:
             res, err = pickle.load(f)
         if err:
-            raise AssertionError(f"rank {r} failed:\n{err}")
+            errs.append((r, err))
         results.append(res)
+    if errs:
+        errs.sort(key=lambda e: "Connection closed" in e[1] or "Connection reset" in e[1])
+        raise AssertionError("\n".join(f"rank {r} failed:\n{e}" for r, e in errs))
     return results
 
 
@@ -90,11 +101,4 @@ def run_nccl(fn, world, *args):
 
     out_dir = tempfile.mkdtemp(prefix="fps_nccl_")
     mp.spawn(_nccl_entry, args=(world, free_port(), fn, args, out_dir), nprocs=world, join=True)
-    results = []
-    for r in range(world):
-        with open(os.path.join(out_dir, f"r{r}.pkl"), "rb") as f:
-            res, err = pickle.load(f)
-        if err:
-            raise AssertionError(f"rank {r} failed:\n{err}")
-        results.append(res)
-    return results
+    return _collect(out_dir, world)

@@ -127,7 +127,34 @@ def _pa_restore(comm, directory):
     return ids[o].cpu(), w[o].reshape(-1).cpu()
 
 
+def _model_load_wp(comm, wp, pp, capacity):
+    from test_tensor_engine import _model_load
+
+    return _model_load(comm.rank, comm.world, 50, 0, None, capacity, wp, pp, comm=comm)
+
+
 # ------------------------------------------------------------------ tests
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("capacity", [None, 7])
+def test_model_load_worker_4_ps_3_exact(backend, capacity):
+    """FlinkSimpleStackTest's model-load job (workerParallelism 4, psParallelism 3:
+    FlinkSimpleStackTest.scala:135-138) on four ranks: shard ``|id| % 3`` on ranks 0-2,
+    rank 3 has no shard -- the dump is exactly ``10 i + 3``."""
+    W = 4 if backend == "virtual" else min(N_GPUS, 4)
+    if W < 4:
+        pytest.skip("needs 4 GPUs")
+    res = _run(backend, _model_load_wp, W, 4, 3, capacity)
+    dump = {}
+    for r in res:
+        for ids, vals in r:
+            for k, v in zip(ids.tolist(), vals.reshape(-1).tolist()):
+                assert k not in dump
+                dump[k] = v
+    assert dump == {k: 10.0 * k + 3 for k in range(50)}
+
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("exchange,schedule,overlap", [("rotate", "bidir", "auto"), ("rotate", "ring", False),

@@ -85,16 +85,18 @@ class _CountWorker(BatchedWorkerLogic):
         ps.output((pulled.keys, pulled.values()))
 
 
-def _model_load(rank, world, n_params, staleness, dedup=None, capacity=None):
+def _model_load(rank, world, n_params, staleness, dedup=None, capacity=None, wp=None, pp=None, comm=None):
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    comm = Comm()
-    # this rank's slice of the model stream (10*i) and of the data (each key 3 times)
+    comm = comm or Comm()
+    wp_ = wp or world
+    # this rank's slice of the model stream (10*i) and of the data (each key 3 times,
+    # spread over the wp_ worker ranks; ranks >= wp_ run no worker)
     model = [(k, [10.0 * k]) for k in range(n_params) if k % world == rank]
     keys = [k for _ in range(3) for k in range(n_params)]
-    mine = keys[rank::world]
-    batches = [torch.tensor(mine[s:s + 7]) for s in range(0, len(mine), 7)]
-    rt = TensorRuntime(comm, staleness=staleness, capacity=capacity)
+    mine = keys[rank::wp_] if rank < wp_ else []
+    batches = [torch.tensor(mine[s:s + 7], device=comm.device) for s in range(0, len(mine), 7)]
+    rt = TensorRuntime(comm, staleness=staleness, capacity=capacity, worker_parallelism=wp, ps_parallelism=pp)
     logic = DeviceSimplePSLogicWithClose(n_params, 1, op="add", dedup=dedup)
     out = rt.execute(batches, _CountWorker(), logic, model=model)
     if capacity is not None and world > 1:  # fixed-shape plans: no count exchange, no host copy
@@ -121,6 +123,114 @@ def test_tensor_model_load_exact(world, staleness, dedup, capacity):
             for k, v in zip(ids.tolist(), vals.reshape(-1).tolist()):
                 dump[k] = v
     assert dump == {k: 10.0 * k + 3 for k in range(50)}
+
+
+def _dump_of(res):
+    dump = {}
+    for r in res:
+        for ids, vals in r:
+            for k, v in zip(ids.tolist(), vals.reshape(-1).tolist()):
+                assert k not in dump  # every key dumped by exactly one shard
+                dump[k] = v
+    return dump
+
+
+@pytest.mark.parametrize("world,wp,pp,staleness,capacity", [
+    (4, 4, 3, 0, None), (4, 4, 3, 2, None), (4, 3, 2, 1, None), (4, 4, 1, 0, None), (4, 4, 3, 0, 7)])
+def test_tensor_model_load_worker_and_ps_parallelism_differ(world, wp, pp, staleness, capacity):
+    """FlinkSimpleStackTest's model-load configuration itself (workerParallelism 4,
+    psParallelism 3, FlinkSimpleStackTest.scala:135-138) on the tensor engine: shard
+    ``|id| % 3`` on ranks 0-2 computed on the device, rank 3 holds no shard; with
+    wp < world the last ranks run no worker but still serve and join every collective."""
+    res = run_ranks(_model_load, world, 50, staleness, None, capacity, wp, pp)
+    assert _dump_of(res) == {k: 10.0 * k + 3 for k in range(50)}
+    assert all(ids.numel() == 0 for r in res[pp:] for ids, _ in r)  # ranks without a shard dump nothing
+
+
+def _pa_examples(n, F, workers, nnz, seed):
+    """Examples dealt round-robin to ``workers`` (Flink rebalance); example j only uses
+    features f with f % workers == j % workers, so workers share no feature and each
+    one's model updates are sequential in both engines."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for j in range(n):
+        w = j % workers
+        feats = np.unique(rng.integers(0, F // workers, nnz) * workers + w)
+        out.append(({int(f): float(v) for f, v in zip(feats, rng.random(feats.size) + 0.1)},
+                    bool(rng.integers(0, 2))))
+    return out
+
+
+def _pa_tensor_rank(rank, world, examples, F, P, range_part):
+    from flink_parameter_server_1_amd.models.pa.batched import transform_pa_tensor
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+
+    batches = []
+    for x, y in examples[rank::world]:  # one example per micro-batch, staleness 0
+        k = sorted(x)
+        batches.append((torch.tensor([0, len(k)], dtype=torch.int64), torch.tensor(k, dtype=torch.int32),
+                        torch.tensor([x[f] for f in k], dtype=torch.float32),
+                        torch.tensor([1 if y else -1], dtype=torch.int8)))
+    out = transform_pa_tensor(batches, F, "binary", variant="PA", range_partitioning=range_part, comm=Comm(),
+                              ps_parallelism=P)
+    w = {}
+    for e in out:
+        if isinstance(e, Right):
+            for f, v in zip(e.value[0].tolist(), e.value[1].reshape(-1).tolist()):
+                assert f not in w
+                w[f] = v
+    return w
+
+
+@pytest.mark.parametrize("P,range_part", [(2, True), (3, False), (1, True)])
+def test_pa_binary_with_fewer_shards_than_ranks_equals_per_record(P, range_part):
+    """PA binary at psParallelism P of 4 ranks (range partitioning over P, as
+    ``rangePartitionerPS``) equals the per-record engine at workerParallelism 4,
+    psParallelism P, pullLimit 1: the same features in the model dump, the same weights."""
+    from flink_parameter_server_1_amd.models.pa.algorithms import PassiveAggressiveBinaryAlgorithm
+    from flink_parameter_server_1_amd.models.pa.server import transform_binary
+    from flink_parameter_server_1_amd.models.pa.sparse import SparseVector
+
+    F, W = 4000, 4
+    ex = _pa_examples(48, F, W, 12, seed=P)
+    recs = [Left((SparseVector(sorted(x), [x[f] for f in sorted(x)], F), y)) for x, y in ex]
+    out = transform_binary(None, input_source=recs, worker_parallelism=W, ps_parallelism=P,
+                           passive_aggressive_method=PassiveAggressiveBinaryAlgorithm.build_pa(), pull_limit=1,
+                           feature_count=F, range_partitioning=range_part)
+    ref = {int(e.value[0]): float(np.asarray(e.value[1]).reshape(-1)[0]) for e in out if isinstance(e, Right)}
+    res = run_ranks(_pa_tensor_rank, W, ex, F, P, range_part)
+    got = {}
+    for r in res:
+        assert not (set(r) & set(got))
+        got.update(r)
+    assert set(got) == set(ref) and len(ref) > 0
+    for f in ref:
+        assert abs(got[f] - ref[f]) <= 1e-5 * max(1.0, abs(ref[f])), (f, got[f], ref[f])
+
+
+def test_fewer_shards_than_ranks_need_no_host_owner_table():
+    """Range / hash ownership over P < ranks is computed on the device from the key
+    (``DedupWorkspace(shards=P, out_world=ranks)``): a 1B-feature range shard set
+    routes keys without any per-id host table; a rank without a shard allocates none."""
+    import tracemalloc
+
+    from flink_parameter_server_1_amd import ops
+    from flink_parameter_server_1_amd.parallel.table import ShardedTable
+
+    F, P, W = 1_000_000_000, 2, 4
+    tracemalloc.start()
+    empty = ShardedTable(F, 1, 3, P, "range", ("zeros",), touch_sentinel=True)  # rank 3 of 4: no shard
+    ws = ops.DedupWorkspace(F, P, 1, empty.block, "cpu", hashed=True, out_world=W)
+    keys = torch.tensor([0, 7, F // 2 - 1, F // 2, F - 1, 7], dtype=torch.int32)
+    counts, prefix, uniq, pos = ws.run(keys)
+    peak = tracemalloc.get_traced_memory()[1]
+    tracemalloc.stop()
+    assert empty.n_local == 0 and empty.weight.numel() == 0
+    assert counts.tolist() == [3, 2, 0, 0] and prefix.tolist() == [0, 3, 5, 5, 5]
+    assert peak < 64 << 20  # nothing proportional to the 1B-id space
+    # unique LOCAL keys grouped by shard: shard 0 = ids [0, F/2), shard 1 = [F/2, F)
+    assert sorted(uniq[:3].tolist()) == [0, 7, F // 2 - 1] and sorted(uniq[3:5].tolist()) == [0, F // 2 - 1]
+    assert uniq[pos].tolist()[5] == 7 and pos[1] == pos[5]  # the repeated key maps to one slot
 
 
 def test_transform_backend_tensor_and_outputs():
