@@ -115,28 +115,37 @@ __device__ __forceinline__ void f4_st(float4* p, float4 v) {
   else *p = v;
 }
 
-// K3: exclusive scan of KT totals into ptr[KT+1] (one 1024-thread workgroup)
-__global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restrict__ totals_g, int KT,
+// K3: exclusive scan of KT totals into ptr[KT+1] (one 1024-thread workgroup).  No
+// staging of the totals in LDS: a 128 KiB static LDS array made this one-workgroup
+// launch wait for a CU with that much free LDS while the SGD workgroups of the
+// previous step held them (0.45 ms average, 1.2 ms max on the side stream,
+// profiles/r4_final_bench_kernel_stats.csv); it now needs 64 B of LDS and runs
+// beside them.  Each thread sums `per` consecutive totals from global memory, the
+// 1024 partial sums are scanned by wave shuffles + 16 wave totals.
+__global__ void __launch_bounds__(1024) tile_scan_kernel(const int32_t* __restrict__ totals, int KT,
                                                          int32_t* __restrict__ ptr) {
-  __shared__ int32_t part[1024];
-  __shared__ int32_t totals[TP_MAX_BUCKETS];  // KT <= TP_MAX_BUCKETS: staged by coalesced loads
-  for (int k = threadIdx.x; k < KT; k += 1024) totals[k] = totals_g[k];
-  __syncthreads();
+  __shared__ int32_t wsum[16];
   const int per = (KT + 1023) / 1024;
-  const int k0 = threadIdx.x * per;
+  const int k0 = threadIdx.x * per, k1 = min(KT, k0 + per);
   int32_t s = 0;
-  for (int k = k0; k < min(KT, k0 + per); ++k) s += totals[k];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-    const int32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
+  for (int k = k0; k < k1; ++k) s += totals[k];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
-  int32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (int k = k0; k < min(KT, k0 + per); ++k) { ptr[k] = run; run += totals[k]; }
-  if (threadIdx.x == 1023) ptr[KT] = part[1023];
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int32_t run = inc - s;
+  for (int q = 0; q < wv; ++q) run += wsum[q];
+  for (int k = k0; k < k1; ++k) { const int32_t t = totals[k]; ptr[k] = run; run += t; }
+  if (threadIdx.x == 1023) {
+    int32_t tot = 0;
+    for (int q = 0; q < 16; ++q) tot += wsum[q];
+    ptr[KT] = tot;
+  }
 }
 
 // Packed rating records.  REC8 (users < 2^24, R <= 256): 8 B {uid | row_in_tile << 24,
@@ -340,12 +349,33 @@ __global__ void __launch_bounds__(1024) tp3_colscan_kernel(int32_t* __restrict__
   if (w < G) H1[(int64_t)w * NC + k] = before + inc - v;
 }
 
-// work items of level 2: wptr[c] = sum over c' < c of ceil(ccount[c'] / CH)
+// work items of level 2: wptr[c] = sum over c' < c of ceil(ccount[c'] / CH); one wave,
+// 4 coarse keys per lane (NC <= 256) and a shuffle scan (was one thread walking NC
+// dependent loads)
 __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, int32_t* __restrict__ wptr) {
-  if (threadIdx.x != 0) return;
-  int32_t run = 0;
-  for (int c = 0; c < NC; ++c) { wptr[c] = run; run += (ccount[c] + TP3_CH - 1) / TP3_CH; }
-  wptr[NC] = run;
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x;
+  int32_t v[4], s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * l + q;
+    v[q] = c < NC ? (ccount[c] + TP3_CH - 1) / TP3_CH : 0;
+    s += v[q];
+  }
+  int32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (l >= o) inc += y;
+  }
+  int32_t run = inc - s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * l + q;
+    if (c < NC) wptr[c] = run;
+    run += v[q];
+  }
+  if (l == 63) wptr[NC] = inc;
 }
 
 
