@@ -36,6 +36,12 @@ def main(argv=None):
     ap.add_argument("--no-fuse-local-push", action="store_true",
                     help="PS path at one rank: push a delta buffer and apply it (default: the kernel adds its push "
                          "into the owner's table)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="N > 1: run rank 0 of an N-rank PS job on this one GPU under rank symmetry "
+                         "(parallel/emulated.py: every all-to-all answered by this rank's own send buffer, "
+                         "transfers modelled on device-timed links); reports the per-GPU rate at N")
+    ap.add_argument("--link-gbps", type=float, default=50.0, help="--emulate-world: per-peer link rate (GB/s)")
+    ap.add_argument("--latency-us", type=float, default=5.0, help="--emulate-world: per-message link latency")
     a = ap.parse_args(argv)
 
     import torch
@@ -43,7 +49,13 @@ def main(argv=None):
     from flink_parameter_server_1_amd.models.pa.fast import DistributedPA, PAConfig, synthetic_sparse_batch
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    comm = Comm.init_from_env()
+    if a.emulate_world > 1:
+        from flink_parameter_server_1_amd.parallel.emulated import SymmetricComm
+
+        comm = SymmetricComm(a.emulate_world, device=torch.device("cuda", 0) if torch.cuda.is_available() else "cpu",
+                             link_gbps=a.link_gbps, latency_us=a.latency_us)
+    else:
+        comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire,
                                local_direct=not a.ps_path, fuse_local_push=not a.no_fuse_local_push),
@@ -59,12 +71,16 @@ def main(argv=None):
         m.train_step(*batches[s % 4])
     comm.barrier()
     sync()
+    emu = a.emulate_world > 1
+    if emu and dev.type == "cuda":
+        comm.wait_ms()  # drop the warm-up's waits
     t0 = time.perf_counter()
     for s in range(a.steps):
         m.train_step(*batches[s % 4])
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
+    wait_ms = comm.wait_ms() / a.steps if emu and dev.type == "cuda" else 0.0
     ip, idx, val, lab = batches[0]  # accuracy on a trained batch (1B features: held-out rows share few features)
     pred = m.predict(ip, idx, val)
     acc = float(((pred.to(torch.int8) == lab) if a.kind == "binary" else (pred == lab)).float().mean())
@@ -75,6 +91,8 @@ def main(argv=None):
             "feature_updates_per_s": ex * a.nnz / dt, "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
             "data": "synthetic sparse CSR (hidden linear model labels)", "train_batch_accuracy": acc,
+            "emulated_world": a.emulate_world if emu else None, "per_gpu_rate": a.batch * a.steps / dt,
+            "exposed_wait_ms_per_step": wait_ms if emu else None, "link_gbps": a.link_gbps if emu else None,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire,
                        "exchange": "local-direct" if m._direct else "ps",

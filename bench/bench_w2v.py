@@ -43,6 +43,12 @@ def main(argv=None):
     ap.add_argument("--no-fuse-local-push", action="store_true",
                     help="PS path at one rank: push delta buffers and apply them (default: the kernel adds its "
                          "pushes into the owner's tables)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="N > 1: run rank 0 of an N-rank PS job on this one GPU under rank symmetry "
+                         "(parallel/emulated.py: every all-to-all answered by this rank's own send buffer, "
+                         "transfers modelled on device-timed links); reports the per-GPU rate at N")
+    ap.add_argument("--link-gbps", type=float, default=50.0, help="--emulate-world: per-peer link rate (GB/s)")
+    ap.add_argument("--latency-us", type=float, default=5.0, help="--emulate-world: per-message link latency")
     a = ap.parse_args(argv)
 
     import torch
@@ -51,7 +57,13 @@ def main(argv=None):
         synthetic_corpus
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    comm = Comm.init_from_env()
+    if a.emulate_world > 1:
+        from flink_parameter_server_1_amd.parallel.emulated import SymmetricComm
+
+        comm = SymmetricComm(a.emulate_world, device=torch.device("cuda", 0) if torch.cuda.is_available() else "cpu",
+                             link_gbps=a.link_gbps, latency_us=a.latency_us)
+    else:
+        comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
                                    wire_dtype=a.wire, shared_negatives=a.shared_negatives,
@@ -76,6 +88,9 @@ def main(argv=None):
     m.flush()
     comm.barrier()
     sync()
+    emu = a.emulate_world > 1
+    if emu and dev.type == "cuda":
+        comm.wait_ms()  # drop the warm-up's waits
     t0 = time.perf_counter()
     for i in range(a.steps):
         m.step(*batch(i + 1 + a.warmup))
@@ -83,6 +98,7 @@ def main(argv=None):
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
+    wait_ms = comm.wait_ms() / a.steps if emu and dev.type == "cuda" else 0.0
     loss1 = m.step(*batch(0), with_loss=True)
     if comm.rank == 0:
         total = a.pairs * a.steps * comm.world
@@ -90,6 +106,10 @@ def main(argv=None):
             "metric": "word2vec SGNS pair-updates/sec (whole node)", "value": total / dt, "unit": "pairs/s",
             "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "dtype": "fp32",
+            "emulated_world": a.emulate_world if emu else None,
+            "per_gpu_rate": a.pairs * a.steps / dt,
+            "exposed_wait_ms_per_step": wait_ms if emu else None,
+            "link_gbps": a.link_gbps if emu else None,
             "data": "synthetic Zipf topic corpus", "loss_first_last": [loss0, loss1],
             "config": {"model": f"sgns vocab={a.vocab} dim={a.dim} window={a.window} negatives={a.negatives}",
                        "mode": a.mode,

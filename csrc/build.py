@@ -61,19 +61,22 @@ def _write_stamp(target: str, digest: str):
 PER_FILE_FLAGS = {"score_bf16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
-def build_kernels(force: bool = False, verbose: bool = True) -> str:
+def build_kernels(force: bool = False, verbose: bool = True, variant: str = None, defines=()) -> str:
     """One object per source (compiled in parallel, each with its own digest stamp:
-    a change rebuilds only its file), linked into one shared object."""
+    a change rebuilds only its file), linked into one shared object.  ``variant`` +
+    ``defines`` (``NAME=VALUE``): an A/B build of the library with extra macros, into
+    ``_lib/ab/<variant>/libfps_kernels.so`` (select it with ``FPS_KERNELS_SO``)."""
     from concurrent.futures import ThreadPoolExecutor
 
-    os.makedirs(OUT, exist_ok=True)
-    objdir = os.path.join(OUT, "obj")
+    out = OUT if variant is None else os.path.join(OUT, "ab", variant)
+    os.makedirs(out, exist_ok=True)
+    objdir = os.path.join(out, "obj")
     os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    target = os.path.join(OUT, "libfps_kernels.so")
+    target = os.path.join(out, "libfps_kernels.so")
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-Wno-unused-result",
-             "-I", os.path.join(CSRC, "kernels")]
+             "-I", os.path.join(CSRC, "kernels")] + [f"-D{d}" for d in defines]
 
     def obj(src):
         extra = PER_FILE_FLAGS.get(os.path.basename(src), [])
@@ -145,11 +148,16 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["kernels", "host"])
+    ap.add_argument("--variant", default=None, help="A/B build name (with -D NAME=VALUE macros)")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--asan-selftest", action="store_true",
                     help="build + run the host runtime self-test under ASan/UBSan, then exit")
     a = ap.parse_args(argv)
     if a.asan_selftest:
         return asan_selftest()
+    if a.variant:
+        print(build_kernels(a.force, variant=a.variant, defines=a.defines))
+        return 0
     if a.only in (None, "kernels"):
         print(build_kernels(a.force))
     if a.only in (None, "host"):

@@ -717,12 +717,22 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
   }
 }
 
+// Build-time knobs of the tile SGD (A/B variants: csrc/build.py --variant NAME -D ...):
+// user rows in flight per lane group, and the minimum waves per SIMD the register
+// allocation must leave room for (2 = two 512-thread workgroups per CU)
+#ifndef FPS_TG_PF
+#define FPS_TG_PF 8
+#endif
+#ifndef FPS_TG_MINW
+#define FPS_TG_MINW 2
+#endif
+
 // One workgroup per tile.  (A persistent grid taking tiles from a device counter, to
 // drop the tail round of the 16 small launches per step at N = 8, was measured slower:
 // 9.58e9 vs 9.87e9 updates/s at N = 1, 7.64 vs 7.45 ms emulated N = 8 --
 // profiles/r4_persistent_sgd_ab.txt; removed.)
 template <int TPR, int V, int PF, bool REC8, bool DELTA, bool USC1>
-__global__ void __launch_bounds__(512) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
+__global__ void __launch_bounds__(512, FPS_TG_MINW) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
                                                                int64_t block_rows, float lr, float lambda,
@@ -850,7 +860,7 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
   if (nblk == 1) { I1 = I0; ptr1 = ptr0; rows1 = rows0; }
   const int grid = nblk * T;
   hipStream_t s = (hipStream_t)stream;
-  constexpr int PF = 8;
+  constexpr int PF = FPS_TG_PF;
   // user-row cache policy (user_sc1: write-through sc1, see USC1); 8-B records address
   // users with 32-bit offsets, the buffer descriptor needs the table < 4 GiB
   if (user_sc1 && !(rec8 && users_bytes > 0 && users_bytes < (int64_t)0xFFFFFFFF)) return (int)hipErrorInvalidValue;
