@@ -98,7 +98,8 @@ def main(argv=None):
                     help="tiled SGD: partition each batch on the main stream instead of prefetching it")
     ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"],
                     help="store: Hogwild user rows (plain accesses); sc1: write-through user rows (about half the lost "
-                         "user updates); atomic: float-atomic user updates, flat kernel (none lost)")
+                         "user updates); atomic: exact -- the tiled kernel adds every user delta with float atomics "
+                         "(none lost)")
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--user-phases", type=int, default=0,
@@ -289,6 +290,11 @@ def main(argv=None):
                 "lost_user_update_fraction": None if hog is None else hog.get("lost_update_fraction"),
             },
         }
+        lf = out["config"]["lost_user_update_fraction"]
+        # updates that survive the Hogwild user-row race (value counts every rating's update;
+        # user_update="atomic" loses none): value x (1 - lost fraction), None when unmeasured
+        out["effective_updates_per_s"] = value * (1.0 - lf) if lf is not None else \
+            (value if a.user_update == "atomic" else None)
         if verify is not None:
             out["verify_ok"] = verify["verify_ok"]
             out["verify"] = verify

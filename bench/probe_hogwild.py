@@ -86,7 +86,7 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
                        prefetch_partition=False, user_update=user_update)
     m = DistributedMF(cfg, Comm(device=dev, local=True))
     assert m.users.n_local == users
-    assert m.sgd_mode == ("flat" if user_update == "atomic" else "tiled")
+    assert m.sgd_mode == "tiled"  # "atomic": the tiled kernel with float-atomic user deltas (exact)
     g = torch.Generator(device=dev).manual_seed(seed)
     with torch.no_grad():
         m.U.zero_()

@@ -541,10 +541,14 @@ __device__ __forceinline__ void get_rec(const typename RecT<REC8>::type& x, int6
 // tile -- or a later launch without dl_init (the next user phase) -- starts from
 // I + Dl (the row as the earlier work left it) and adds its sum to Dl.  Replaces a working copy of the pulled rows and a subtraction pass
 // (round 3: clone + SGD + sub_, 1.3 GB of extra traffic at 1M x 64 rows).
-// USC1: user rows loaded and stored write-through (`sc1`: loads bypass the CU's L1,
-// stores drop the line from the writing XCD's L2), so a user row updated on another CU
-// or XCD is not re-read from a stale cached copy (the Hogwild race on user rows,
-// profiles/r4_hogwild.md).  Buffer addressing: the table must be < 4 GiB.
+// UM (user-row mode): 0 = plain loads / stores (Hogwild across workgroups);
+// 1 = write-through (`sc1`: loads bypass the CU's L1, stores drop the line from the
+// writing XCD's L2), so a user row updated on another CU or XCD is not re-read from a
+// stale cached copy (about half the lost updates, profiles/r4_hogwild.md);
+// 2 = exact: sc1 loads and the user delta ADDED with float atomics (executed at the
+// memory side, never lost: a concurrent update of the same user is summed, as the
+// item deltas of one tile are; the read it was computed from may be stale, as a
+// Hogwild read).  Buffer addressing (UM >= 1): the table must be < 4 GiB.
 typedef unsigned int tg_u4 __attribute__((ext_vector_type(4)));
 
 template <bool REC8>
@@ -555,7 +559,7 @@ struct TgShared {
 };
 
 // one tile of the tile-grouped SGD (see mf_sgd_tilegroup_kernel)
-template <int TPR, int V, int PF, bool REC8, bool DELTA, bool USC1>
+template <int TPR, int V, int PF, bool REC8, bool DELTA, int UM>
 __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, float* __restrict__ U,
                                                float* __restrict__ I, const void* __restrict__ rec_,
                                                const int32_t* __restrict__ ptr, int R, int64_t block_rows,
@@ -583,7 +587,7 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
   float4* Ug = reinterpret_cast<float4*>(U);
   float4* Dg = DELTA ? reinterpret_cast<float4*>(Dl) + r0 * D4 : nullptr;
   __amdgpu_buffer_rsrc_t urs;
-  if constexpr (USC1) urs = __builtin_amdgcn_make_buffer_rsrc(U, (short)0, (int)ubytes, 0x00020000);
+  if constexpr (UM >= 1) urs = __builtin_amdgcn_make_buffer_rsrc(U, (short)0, (int)ubytes, 0x00020000);
   if (DELTA && dl_init && beg == end) {  // no ratings in this tile: its rows' deltas are zero
     for (int k = threadIdx.x; k < nr * D4; k += blockDim.x) f4_st<true>(Dg + k, make_float4(0.f, 0.f, 0.f, 0.f));
     return;
@@ -665,7 +669,7 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
           ur[q] = (Off)u * D4;
 #pragma unroll
           for (int v = 0; v < V; ++v) {
-            if constexpr (USC1)
+            if constexpr (UM >= 1)
               uv[q][v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                                         urs, (int)((uint32_t)(ur[q] + j + v * TPR) * 16u), 0, 16));
             else
@@ -688,7 +692,13 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
             nu.y = u.y + lr * (e * i.y - lambda * u.y);
             nu.z = u.z + lr * (e * i.z - lambda * u.z);
             nu.w = u.w + lr * (e * i.w - lambda * u.w);
-            if constexpr (USC1)
+            if constexpr (UM == 2) {
+              float* up = reinterpret_cast<float*>(Ug + ur[q] + j + v * TPR);
+              atomic_add_noret(up + 0, nu.x - u.x);
+              atomic_add_noret(up + 1, nu.y - u.y);
+              atomic_add_noret(up + 2, nu.z - u.z);
+              atomic_add_noret(up + 3, nu.w - u.w);
+            } else if constexpr (UM == 1)
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tg_u4, nu), urs,
                                                      (int)((uint32_t)(ur[q] + j + v * TPR) * 16u), 0, 16);
             else
@@ -731,7 +741,7 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
 // drop the tail round of the 16 small launches per step at N = 8, was measured slower:
 // 9.58e9 vs 9.87e9 updates/s at N = 1, 7.64 vs 7.45 ms emulated N = 8 --
 // profiles/r4_persistent_sgd_ab.txt; removed.)
-template <int TPR, int V, int PF, bool REC8, bool DELTA, bool USC1>
+template <int TPR, int V, int PF, bool REC8, bool DELTA, int UM>
 __global__ void __launch_bounds__(512, FPS_TG_MINW) mf_sgd_tilegroup_kernel(float* __restrict__ U, float* __restrict__ I,
                                                                const void* __restrict__ rec_,
                                                                const int32_t* __restrict__ ptr, int R,
@@ -740,7 +750,7 @@ __global__ void __launch_bounds__(512, FPS_TG_MINW) mf_sgd_tilegroup_kernel(floa
                                                                const int32_t* __restrict__ ptr1,
                                                                float* __restrict__ Dl, int dl_init, uint32_t ubytes) {
   __shared__ TgShared<REC8> sh;
-  tilegroup_tile<TPR, V, PF, REC8, DELTA, USC1>(sh, blockIdx.x, U, I, rec_, ptr, R, block_rows, lr, lambda, I1,
+  tilegroup_tile<TPR, V, PF, REC8, DELTA, UM>(sh, blockIdx.x, U, I, rec_, ptr, R, block_rows, lr, lambda, I1,
                                                 block_rows1, T0, ptr1, Dl, dl_init, ubytes);
 }
 
@@ -851,30 +861,30 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
 // to delta0 (delta_init) or added to it (a later user phase over the same rows).
 FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, const int32_t* ptr0, int T, int R,
                              int64_t rows0, float* I1, const int32_t* ptr1, int64_t rows1, int nblk, int D, float lr,
-                             float lambda, float* delta0, int delta_init, int64_t users_bytes, int user_sc1,
+                             float lambda, float* delta0, int delta_init, int64_t users_bytes, int user_mode,
                              void* stream) {
   if (T <= 0) return 0;
   if (nblk != 1 && nblk != 2) return (int)hipErrorInvalidValue;
   if (delta0 != nullptr && nblk != 1) return (int)hipErrorInvalidValue;
   if (R <= 0 || R > TG_MAX_R) return (int)hipErrorInvalidValue;
+  if (user_mode < 0 || user_mode > 2) return (int)hipErrorInvalidValue;
   if (nblk == 1) { I1 = I0; ptr1 = ptr0; rows1 = rows0; }
   const int grid = nblk * T;
   hipStream_t s = (hipStream_t)stream;
   constexpr int PF = FPS_TG_PF;
-  // user-row cache policy (user_sc1: write-through sc1, see USC1); 8-B records address
-  // users with 32-bit offsets, the buffer descriptor needs the table < 4 GiB
-  if (user_sc1 && !(rec8 && users_bytes > 0 && users_bytes < (int64_t)0xFFFFFFFF)) return (int)hipErrorInvalidValue;
-  const bool usc1 = user_sc1 != 0;
-  const uint32_t ubytes = (uint32_t)(usc1 ? users_bytes : 0);
-#define FPS_TILED_(TPR_, V_, DL_)                                                                               \
-  if (rec8 && usc1) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, true>), dim3(grid),      \
-                                       dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, \
-                                       delta0, delta_init, ubytes);                         \
-  else if (rec8) hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, true, DL_, false>), dim3(grid),         \
-                                    dim3(512), 0, s, U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1,    \
-                                    delta0, delta_init, ubytes);                            \
-  else hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, false, DL_, false>), dim3(grid), dim3(512), 0, s,\
-                          U, I0, rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init, ubytes)
+  // user-row mode (UM above: 0 plain, 1 write-through sc1, 2 exact atomic deltas); modes
+  // 1 / 2 address users with 32-bit offsets of 8-B records and a buffer descriptor: the
+  // table must be < 4 GiB
+  if (user_mode && !(rec8 && users_bytes > 0 && users_bytes < (int64_t)0xFFFFFFFF)) return (int)hipErrorInvalidValue;
+  const uint32_t ubytes = (uint32_t)(user_mode ? users_bytes : 0);
+#define FPS_TILED_K(TPR_, V_, R8_, DL_, UM_)                                                                               \
+  hipLaunchKernelGGL((mf_sgd_tilegroup_kernel<TPR_, V_, PF, R8_, DL_, UM_>), dim3(grid), dim3(512), 0, s, U, I0,   \
+                     rec, ptr0, R, rows0, lr, lambda, I1, rows1, T, ptr1, delta0, delta_init, ubytes)
+#define FPS_TILED_(TPR_, V_, DL_)                                 \
+  if (rec8 && user_mode == 2) { FPS_TILED_K(TPR_, V_, true, DL_, 2); }       \
+  else if (rec8 && user_mode == 1) { FPS_TILED_K(TPR_, V_, true, DL_, 1); }  \
+  else if (rec8) { FPS_TILED_K(TPR_, V_, true, DL_, 0); }                    \
+  else { FPS_TILED_K(TPR_, V_, false, DL_, 0); }
 #define FPS_TILED(TPR_, V_)                      \
   if (delta0 != nullptr) { FPS_TILED_(TPR_, V_, true); } \
   else { FPS_TILED_(TPR_, V_, false); }
@@ -888,6 +898,7 @@ FPS_API int fps_mf_sgd_tiled(float* U, float* I0, const void* rec, int rec8, con
   }
 #undef FPS_TILED
 #undef FPS_TILED_
+#undef FPS_TILED_K
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -64,7 +64,8 @@ class MFConfig:
     seed: int = 0
     user_update: str = "store"        # "store" (Hogwild, plain accesses) | "sc1" (Hogwild, write-through user
                                       # rows: ~half the lost user updates, profiles/r4_hogwild.md) | "atomic"
-                                      # (no lost update: float atomics, flat kernel)
+                                      # (exact: no lost update -- the tiled kernel adds every user delta with
+                                      # float atomics; the flat kernel where the tiled one does not apply)
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
@@ -126,6 +127,8 @@ class DistributedMF:
             raise ValueError(f"user_update must be 'store', 'sc1' or 'atomic', not {cfg.user_update!r}")
         self.user_atomic = cfg.user_update == "atomic"
         self.user_sc1 = cfg.user_update == "sc1" and dev.type == "cuda"
+        #: tiled kernel's user-row mode (ops.USER_MODES): plain / write-through / atomic deltas
+        self.user_mode = ops.USER_MODES[cfg.user_update] if dev.type == "cuda" or cfg.user_update == "atomic" else 0
         exchange = cfg.exchange
         if exchange == "auto":
             exchange = "ps" if cfg.force_ps_path else ("rotate" if Wn > 1 else "local")
@@ -146,11 +149,15 @@ class DistributedMF:
         block_rows = cfg.num_items if exchange == "ps" else max(block_rows_of(cfg.num_items, tile_w))
         tile_R = ops.tile_rows_for(cfg.dim, block_rows, tile_w)
         mode = cfg.sgd_mode
+        # exact user rows in the tiled kernel: 8-B records (< 2^24 users per shard) and a
+        # user table < 4 GiB (32-bit offsets); otherwise the flat atomic kernel
+        users_local = -(-cfg.num_users // Wn)
+        tiled_atomic_ok = users_local < (1 << 24) and users_local * cfg.dim * 4 < 0xFFFFFFFF
         if mode == "auto":
-            mode = "tiled" if (tile_R is not None and not self.user_atomic) else "flat"
-        if mode == "tiled" and (tile_R is None or self.user_atomic):
+            mode = "tiled" if (tile_R is not None and (not self.user_atomic or tiled_atomic_ok)) else "flat"
+        if mode == "tiled" and (tile_R is None or (self.user_atomic and not tiled_atomic_ok)):
             raise ValueError("sgd_mode 'tiled' needs dim in ops.TILED_DIMS, a table small enough for the LDS "
-                             "bucket counters and user_update='store'")
+                             "bucket counters and (user_update='atomic') < 2^24 users and < 4 GiB per shard")
         if mode == "grouped" and exchange == "rotate":
             raise ValueError("sgd_mode 'grouped' is not available with the rotation exchange")
         self.sgd_mode = mode
@@ -405,7 +412,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):  # both item blocks of a phase in one launch
                     ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, 2 * p, self.tile_T, self.tile_R,
-                                          c.learning_rate, c.lam, user_sc1=self.user_sc1)
+                                          c.learning_rate, c.lam, user_mode=self.user_mode)
             return
         nb = 2 * self.rot_w  # item blocks per user phase in the partition layout
 
@@ -415,11 +422,11 @@ class DistributedMF:
                 if len(act) == 2:  # one block of each ring: disjoint items, one launch
                     (g0, b0), (g1, b1) = act
                     ops.mf_sgd_tiled_pair(self.U, b0, b1, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                          c.learning_rate, c.lam, block1=p * nb + g1, user_sc1=self.user_sc1)
+                                          c.learning_rate, c.lam, block1=p * nb + g1, user_mode=self.user_mode)
                 else:
                     (g0, b0), = act
                     ops.mf_sgd_tiled(self.U, b0, rec, ptr, p * nb + g0, self.tile_T, self.tile_R,
-                                     c.learning_rate, c.lam, user_sc1=self.user_sc1)
+                                     c.learning_rate, c.lam, user_mode=self.user_mode)
 
         if not self._overlap:
             for _ in range(self.rot.K):
@@ -482,7 +489,7 @@ class DistributedMF:
             with stage("mf.sgd", self.timer):
                 for p in range(self.user_phases):
                     ops.mf_sgd_tiled(self.U, rows, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate,
-                                     c.lam, delta=delta, delta_init=p == 0, user_sc1=self.user_sc1)
+                                     c.lam, delta=delta, delta_init=p == 0, user_mode=self.user_mode)
             return delta
         with stage("mf.sgd", self.timer):
             if self.sgd_mode == "grouped":

@@ -546,8 +546,13 @@ class TilePartitioner:
         return uid, row.to(torch.int32), rec[:, 1].contiguous().view(torch.float32)
 
 
+#: user-row modes of the tiled SGD (``mf_sgd_tiled(user_mode=...)``)
+USER_MODES = {"store": 0, "sc1": 1, "atomic": 2}
+
+
 def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
-                 delta: Optional[torch.Tensor] = None, delta_init: bool = True, user_sc1: bool = False):
+                 delta: Optional[torch.Tensor] = None, delta_init: bool = True, user_sc1: bool = False,
+                 user_mode: int = 0):
     """MF SGD of the ratings of item block ``block`` (tiles ``ptr[block*T : (block+1)*T + 1]``,
     records from ``TilePartitioner``): one workgroup per tile, every item row owned
     by one lane group (registers), item deltas summed per row -- no item atomics.
@@ -556,7 +561,10 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
     ``delta_init=False`` adds to the deltas of an earlier launch over the same rows
     (the rows then continue from ``I_block + delta``).  ``user_sc1``: user rows loaded /
     stored write-through (``sc1``; 8-B records, user table < 4 GiB) -- about half the
-    Hogwild lost user updates of plain accesses (``profiles/r4_hogwild.md``)."""
+    Hogwild lost user updates of plain accesses (``profiles/r4_hogwild.md``).
+    ``user_mode`` (``USER_MODES``): 0 plain (Hogwild), 1 = ``user_sc1``, 2 = exact: every
+    user delta added with float atomics (no update lost; same constraints as sc1)."""
+    user_mode = max(int(user_mode), 1 if user_sc1 else 0)
     if delta is not None and (delta.shape != I_block.shape or delta.dtype != torch.float32):
         raise ValueError("mf_sgd_tiled: delta must be an fp32 tensor shaped like the item block")
     if _on_gpu(U):
@@ -565,37 +573,38 @@ def mf_sgd_tiled(U, I_block, rec, ptr, block: int, T: int, tile_rows: int, lr: f
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I_block).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), p0, T, tile_rows, I_block.shape[0], None, None, 0, 1,
                                      U.shape[1], lr, lam, None if delta is None else _c(delta).data_ptr(),
-                                     int(delta_init), U.numel() * 4, int(user_sc1), N.stream_ptr(U.device)),
+                                     int(delta_init), U.numel() * 4, user_mode, N.stream_ptr(U.device)),
                 "mf_sgd_tiled")
         return
     uid, row, r = rec
     a, b = int(ptr[block * T]), int(ptr[(block + 1) * T])
     if delta is None:
-        R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam)
+        R.mf_sgd_local(U, I_block, uid[a:b], row[a:b], r[a:b], lr, lam, user_atomic=user_mode == 2)
         return
     work = I_block.clone() if delta_init else I_block + delta
-    R.mf_sgd_local(U, work, uid[a:b], row[a:b], r[a:b], lr, lam)
+    R.mf_sgd_local(U, work, uid[a:b], row[a:b], r[a:b], lr, lam, user_atomic=user_mode == 2)
     torch.sub(work, I_block, out=delta)
 
 
 def mf_sgd_tiled_pair(U, I0, I1, rec, ptr, block: int, T: int, tile_rows: int, lr: float, lam: float = 0.0,
-                      block1: Optional[int] = None, user_sc1: bool = False):
+                      block1: Optional[int] = None, user_sc1: bool = False, user_mode: int = 0):
     """``mf_sgd_tiled`` of item blocks ``block`` (rows ``I0``) and ``block1`` (default
     ``block + 1``; rows ``I1``) in one launch of 2T workgroups: the blocks share no
     item row, so they need no ordering, and one launch instead of two halves the
     tail of partly filled waves."""
     block1 = block + 1 if block1 is None else block1
+    user_mode = max(int(user_mode), 1 if user_sc1 else 0)
     if _on_gpu(U):
         lib = N.require()
         base = _c(ptr).data_ptr()
         N.check(lib.fps_mf_sgd_tiled(_c(U).data_ptr(), _c(I0).data_ptr(), _c(rec).data_ptr(),
                                      int(rec.shape[1] == 2), base + 4 * block * T, T, tile_rows, I0.shape[0],
                                      _c(I1).data_ptr(), base + 4 * block1 * T, I1.shape[0], 2, U.shape[1], lr, lam,
-                                     None, 1, U.numel() * 4, int(user_sc1), N.stream_ptr(U.device)),
+                                     None, 1, U.numel() * 4, user_mode, N.stream_ptr(U.device)),
                 "mf_sgd_tiled_pair")
         return
-    mf_sgd_tiled(U, I0, rec, ptr, block, T, tile_rows, lr, lam, user_sc1=user_sc1)
-    mf_sgd_tiled(U, I1, rec, ptr, block1, T, tile_rows, lr, lam, user_sc1=user_sc1)
+    mf_sgd_tiled(U, I0, rec, ptr, block, T, tile_rows, lr, lam, user_mode=user_mode)
+    mf_sgd_tiled(U, I1, rec, ptr, block1, T, tile_rows, lr, lam, user_mode=user_mode)
 
 
 PAIR_LOSSES = {"logistic": 0, "squared": 1}

@@ -27,16 +27,34 @@ def test_lost_user_updates_bounded():
 
     store = lost_updates(**GEO)
     assert store["updates_checked"] == int(GEO["users"] * GEO["per_user"])
-    assert store["lost_update_fraction"] < 0.10, store
-    assert store["lost_user_fraction"] < 0.45, store
+    # measured 6.97 % of the updates / 33.8 % of the users (round 4): the bound is that + 1 point
+    assert store["lost_update_fraction"] < 0.0797, store
+    assert store["lost_user_fraction"] < 0.348, store
     sc1 = lost_updates(**GEO, user_update="sc1")
     assert sc1["lost_update_fraction"] < store["lost_update_fraction"], (sc1, store)
 
 
 def test_atomic_user_updates_lose_nothing():
+    """``user_update="atomic"``: the tiled kernel adds every user delta with float atomics
+    (item rows still one lane group each): no update is lost."""
     from probe_hogwild import lost_updates
 
     at = lost_updates(users=200_000, items=20_000, per_user=6.4, phases=1, user_update="atomic")
+    assert at["users_with_lost_update"] == 0 and at["lost_update_fraction"] < 1e-3, at
+    at4 = lost_updates(**dict(GEO, phases=4), user_update="atomic")  # more phases: more concurrency per user
+    assert at4["users_with_lost_update"] == 0 and at4["lost_update_fraction"] < 1e-3, at4
+
+
+def test_rotation_geometry_losses_bounded_and_atomic_exact():
+    """The N = 8 rotation geometry of rank 0 (emulated: the same 16 sub-steps, blocks and
+    overlapping sub-step streams as one GPU of the 8-GPU job), scaled to 1/8 of the
+    users: Hogwild rows lose a bounded share, the atomic mode loses nothing."""
+    from probe_hogwild import lost_updates
+
+    geo = dict(users=156_250, items=125_000, per_user=51.2, phases=1, world=8)
+    store = lost_updates(**geo)
+    assert 0.0 < store["lost_update_fraction"] < 0.12, store
+    at = lost_updates(**geo, user_update="atomic")
     assert at["users_with_lost_update"] == 0 and at["lost_update_fraction"] < 1e-3, at
 
 
