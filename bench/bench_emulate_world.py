@@ -44,6 +44,7 @@ def main():
                     help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
                          "timing, a one-wave device sleep for the link time + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
+    ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"])
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="sub-steps on alternating compute streams (MFConfig.overlap_substeps; auto: from 4 ranks)")
     a = ap.parse_args()
@@ -60,7 +61,8 @@ def main():
         cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=0.01,
                        exchange="local" if W == 1 else "rotate", rotation=a.rotation, emulate_world=W if W > 1 else 0,
                        emulate_link_gbps=a.link_gbps, emulate_latency_us=a.latency_us,
-                       overlap_substeps={"auto": "auto", "on": True, "off": False}[a.overlap])
+                       overlap_substeps={"auto": "auto", "on": True, "off": False}[a.overlap],
+                       user_update=a.user_update)
         m = DistributedMF(cfg, comm)
         data = SyntheticRatings(a.users, a.items, a.batch * a.pool, 0, W, device=dev)
         s = 0

@@ -26,4 +26,12 @@ for N in 8; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pa8 -- python bench/bench_pa.py --ps-path --emulate-world 8 --steps 6 --warmup 2 > $O/prof_pa8.log 2>&1 || { tail -20 $O/prof_pa8.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_w2v8 -- python bench/bench_w2v.py --ps-path --emulate-world 8 --steps 6 --warmup 2 > $O/prof_w2v8.log 2>&1 || { tail -20 $O/prof_w2v8.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_hogwild_gpu.py -x -v --timeout 500 --timeout-method thread > $O/hogwild.log 2>&1 || { tail -40 $O/hogwild.log; exit 1; }
+grep -E "PASS|FAIL" $O/hogwild.log
+for uu in atomic store; do
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --user-update $uu > $O/bench_$uu.log 2>&1 || { tail -20 $O/bench_$uu.log; exit 1; }
+  tail -1 $O/bench_$uu.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["config"]["user_update"], round(d["ms_per_step"],3), "%.4e" % d["value"], d["config"]["lost_user_update_fraction"], d["effective_updates_per_s"])'
+  timeout -k 10 300 python bench/bench_emulate_world.py --ws 8 --steps 10 --warmup 3 --user-update $uu > $O/emu8_$uu.log 2>&1 || { tail -20 $O/emu8_$uu.log; exit 1; }
+  tail -1 $O/emu8_$uu.log | cut -c1-300
+done
 echo ALLDONE
