@@ -156,103 +156,144 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
 #pragma unroll
   for (int b = 0; b < QB; ++b) lc[b] = 0;
   int scored = 0, skipped = 0;
-  // software pipeline: block i0 + 32 is requested before block i0's MFMAs
-  uint4 xv[S];
-  float xl;        // the next block's longest item (wave-uniform)
-  float2 cbv[QB];  // COORD: this block's range of each query's focus coordinate (prefetched with xv)
-  {
-    const int i = i_begin + r;
-    const bool ok = i < i_end;
-    const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
+  // Item tiles are staged in LDS, double-buffered: the workgroup loads each stage of
+  // ST items ONCE (16-B loads, every thread 2 at D = 64) and its four waves read their
+  // MFMA A operands from LDS.  Before, every wave loaded the same item rows from L2
+  // itself (4x the L2 traffic of the workgroup) and half the waves stood waiting on
+  // them (r4 counters: ~23 % MFMA busy, profiles/r4_counters_late.md).  The next
+  // stage's loads are issued before this stage's MFMAs and land in the other buffer
+  // after them; one barrier per stage.  Rows are padded to 2D + 16 bytes: the 16
+  // lanes of each ds_read_b128 group then hit 16 distinct 4-bank groups (row stride
+  // / 16 is odd).
+  constexpr int ST = 64;               // items per stage: two 32-item MFMA blocks
+  constexpr int ROWB = 2 * D + 16;     // padded bytes per bf16 item row in LDS
+  constexpr int CPR = D / 8;           // 16-B chunks per row
+  constexpr int LPT = ST * CPR / 256;  // chunks per thread per stage
+  static_assert(ST * CPR % 256 == 0, "stage chunks must divide over the workgroup");
+  __shared__ __attribute__((aligned(16))) unsigned char xs[2][ST * ROWB];
+  const uint4* __restrict__ X16 = reinterpret_cast<const uint4*>(Xb);
+  uint4 ldv[LPT];
+  auto gload = [&](int s0) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
-    xl = xbm[i_begin >> 5];
+    for (int u = 0; u < LPT; ++u) {
+      const int c = tid + 256 * u, row = c / CPR, col = c % CPR;
+      const int i = s0 + row;
+      ldv[u] = i < i_end ? X16[(int64_t)i * CPR + col] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int c = tid + 256 * u, row = c / CPR, col = c % CPR;
+      *reinterpret_cast<uint4*>(&xs[buf][row * ROWB + col * 16]) = ldv[u];
+    }
+  };
+  // the longest item of each of a stage's two blocks and (COORD) their coordinate
+  // ranges, prefetched one stage ahead with the rows
+  float2 cbs[2][QB], cbn[2][QB];
+  float bms[2], bmn[2];
+  auto cload = [&](int s0, float2 (&dst)[2][QB]) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) bmn[bi] = xbm[min((s0 + 32 * bi) >> 5, (N - 1) >> 5)];
     if (COORD && use_coord) {
 #pragma unroll
-      for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)(i_begin / 32) * D + fq[b]];
-    }
-  }
-  for (int i0 = i_begin; i0 < i_end; i0 += 32) {
-    uint4 cur[S];
+      for (int bi = 0; bi < 2; ++bi) {
+        const int blk = min((s0 + 32 * bi) / 32, (N - 1) / 32);
 #pragma unroll
-    for (int s = 0; s < S; ++s) cur[s] = xv[s];
-    float2 cbc[QB];
+        for (int b = 0; b < QB; ++b) dst[bi][b] = cb[(int64_t)blk * D + fq[b]];
+      }
+    }
+  };
+  gload(i_begin);
+  cload(i_begin, cbn);
+  lstore(0);
+  __syncthreads();
+  for (int s0 = i_begin, st = 0; s0 < i_end; s0 += ST, ++st) {
+    const int buf = st & 1;
+    const bool more = s0 + ST < i_end;
+    bms[0] = bmn[0];
+    bms[1] = bmn[1];
     if (COORD && use_coord) {
 #pragma unroll
-      for (int b = 0; b < QB; ++b) cbc[b] = cbv[b];
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int b = 0; b < QB; ++b) cbs[bi][b] = cbn[bi][b];
     }
-    const float bm = xl;  // longest item of this block
-    if (i0 + 32 < i_end) {
-      const int i = i0 + 32 + r;
-      const bool ok = i < i_end;
-      const uint4* src = reinterpret_cast<const uint4*>(Xb + (int64_t)i * D + h * HALF);
-#pragma unroll
-      for (int s = 0; s < S; ++s) xv[s] = ok ? src[s] : make_uint4(0, 0, 0, 0);
-      xl = xbm[(i0 + 32) >> 5];
-      if (COORD && use_coord) {  // the next block's coordinate ranges: no dependent load before the bound
-#pragma unroll
-        for (int b = 0; b < QB; ++b) cbv[b] = cb[(int64_t)((i0 + 32) / 32) * D + fq[b]];
-      }
+    if (more) {  // the next stage's rows are in flight during this stage's MFMAs
+      gload(s0 + ST);
+      cload(s0 + ST, cbn);
     }
 #pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
-        const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
-        const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbc[b]);
-        if (!__any(pass)) {  // wave-uniform
-          // counted only when the length bound alone would have scored the pair: the
-          // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
-          // adds over LENGTH, not what the length bound skips anyway
-          if (__any(lpass)) ++skipped;
-          continue;
-        }
-        ++scored;
-      }
-      floatx16 acc = {0};
+    for (int bi = 0; bi < 2; ++bi) {
+      const int i0 = s0 + 32 * bi;
+      if (i0 >= i_end) break;  // uniform
+      uint4 cur[S];
+      const unsigned char* rowp = &xs[buf][(32 * bi + r) * ROWB + h * D];  // half h = bytes [h D, h D + D)
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
-                                                      __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
-      const float thr = theta[b] - margin * ql[b] * bm;
-      float m = acc[0];
+      for (int s = 0; s < S; ++s) cur[s] = *reinterpret_cast<const uint4*>(rowp + 16 * s);
+      const float bm = bms[bi];  // longest item of this block
 #pragma unroll
-      for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
-      if (MASK && m > thr) {  // passing registers as a bit mask, walked by ctz
-        uint32_t bits = 0;
+        for (int b = 0; b < QB; ++b) {
+          if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
+            const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
+            const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbs[bi][b]);
+            if (!__any(pass)) {  // wave-uniform
+              // counted only when the length bound alone would have scored the pair: the
+              // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
+              // adds over LENGTH, not what the length bound skips anyway
+              if (__any(lpass)) ++skipped;
+              continue;
+            }
+            ++scored;
+          }
+          floatx16 acc = {0};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) bits |= acc[j] > thr ? (1u << j) : 0u;
-        while (bits) {
-          const int j = __builtin_ctz(bits);
-          bits &= bits - 1;
-          const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-          if (item < i_end) {
-            if (lc[b] < SB_SLOTS) {
-              lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
-              ++lc[b];
-            } else {
-              const int q = qrow[b];
-              const int slot = atomicAdd(cnt + q, 1);
-              if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
+          for (int s = 0; s < S; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
+                                                          __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
+          const float thr = theta[b] - margin * ql[b] * bm;
+          float m = acc[0];
+#pragma unroll
+          for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
+          if (MASK && m > thr) {  // passing registers as a bit mask, walked by ctz
+            uint32_t bits = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) bits |= acc[j] > thr ? (1u << j) : 0u;
+            while (bits) {
+              const int j = __builtin_ctz(bits);
+              bits &= bits - 1;
+              const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+              if (item < i_end) {
+                if (lc[b] < SB_SLOTS) {
+                  lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+                  ++lc[b];
+                } else {
+                  const int q = qrow[b];
+                  const int slot = atomicAdd(cnt + q, 1);
+                  if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
+                }
+              }
+            }
+          } else if (!MASK && m > thr) {  // ~k ln(1 + n / s) passes per query and segment
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+              if (acc[j] > thr && item < i_end) {
+                if (lc[b] < SB_SLOTS) {
+                  lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+                  ++lc[b];
+                } else {
+                  const int q = qrow[b];
+                  const int slot = atomicAdd(cnt + q, 1);
+                  if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
+                }
+              }
             }
           }
         }
-      } else if (!MASK && m > thr) {  // ~k ln(1 + n / s) passes per query and segment
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-          if (acc[j] > thr && item < i_end) {
-            if (lc[b] < SB_SLOTS) {
-              lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
-              ++lc[b];
-            } else {
-              const int q = qrow[b];
-              const int slot = atomicAdd(cnt + q, 1);
-              if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
-            }
-          }
-        }
-      }
     }
+    if (more) lstore(buf ^ 1);  // every wave finished reading buf ^ 1 at the previous barrier
+    __syncthreads();
   }
   if (COORD && use_coord && stats != nullptr && lane == 0) {
     atomicAdd(stats, scored);
