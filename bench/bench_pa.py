@@ -36,6 +36,9 @@ def main(argv=None):
     ap.add_argument("--no-fuse-local-push", action="store_true",
                     help="PS path at one rank: push a delta buffer and apply it (default: the kernel adds its push "
                          "into the owner's table)")
+    ap.add_argument("--staleness", type=int, default=None,
+                    help="PS path: micro-batches in flight (default: 1 at N > 1 -- pulls of batch k+1 overlap batch "
+                         "k -- and 0 at N = 1)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="N > 1: run rank 0 of an N-rank PS job on this one GPU under rank symmetry "
                          "(parallel/emulated.py: every all-to-all answered by this rank's own send buffer, "
@@ -58,7 +61,8 @@ def main(argv=None):
         comm = Comm.init_from_env()
     dev = comm.device
     m = DistributedPA(PAConfig(feature_count=a.features, kind=a.kind, label_count=a.labels, wire_dtype=a.wire,
-                               local_direct=not a.ps_path, fuse_local_push=not a.no_fuse_local_push),
+                               local_direct=not a.ps_path, fuse_local_push=not a.no_fuse_local_push,
+                               staleness=a.staleness if a.staleness is not None else int(comm.world > 1)),
                       comm)
     batches = [synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=comm.rank + 1, step=s, label_count=a.labels,
                                       device=dev, zipf=a.zipf) for s in range(4)]
@@ -77,6 +81,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for s in range(a.steps):
         m.train_step(*batches[s % 4])
+    m.flush()  # the last batches' pushes land inside the timed region
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
@@ -95,7 +100,7 @@ def main(argv=None):
             "exposed_wait_ms_per_step": wait_ms if emu else None, "link_gbps": a.link_gbps if emu else None,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": "range", "wire_dtype": a.wire,
-                       "exchange": "local-direct" if m._direct else "ps",
+                       "exchange": "local-direct" if m._direct else "ps", "staleness": m.cfg.staleness,
                        "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1)},
         }), flush=True)
 

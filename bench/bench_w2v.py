@@ -29,7 +29,10 @@ def main(argv=None):
     ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU per step")
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--lr", type=float, default=0.005)
-    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--wire", default=None, choices=["fp32", "bf16"],
+                    help="PS-path row dtype on the wire (pulled rows and pushed deltas; the owner accumulates in "
+                         "fp32).  Default: bf16 at N > 1 -- dim-300 rows make the all-to-alls link-bound "
+                         "(profiles/r5_ps_paths_emulated.md) -- fp32 at N = 1")
     ap.add_argument("--neg-group", type=int, default=None, choices=[1, 2, 4],
                     help="32-pair blocks sharing one set of negatives (default: SGNSConfig)")
     ap.add_argument("--ps-path", action="store_true",
@@ -65,6 +68,8 @@ def main(argv=None):
     else:
         comm = Comm.init_from_env()
     dev = comm.device
+    if a.wire is None:
+        a.wire = "bf16" if comm.world > 1 else "fp32"
     m = DistributedSGNS(SGNSConfig(vocab_size=a.vocab, dim=a.dim, window=a.window, learning_rate=a.lr,
                                    wire_dtype=a.wire, shared_negatives=a.shared_negatives,
                                    local_direct=not a.ps_path, mode=a.mode, negatives=a.negatives,

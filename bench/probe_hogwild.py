@@ -112,7 +112,8 @@ def lost_updates(users: int, items: int, per_user: float, phases: int, seed: int
            "overlap_substeps": bool(getattr(m, "_overlap", False)) if world > 1 else None,
            "phases": getattr(m, "user_phases", None), "tile_rows": getattr(m, "tile_R", None), "user_update": cfg.user_update, "users_with_lost_update": int(lost.sum()),
            "rated_users": int(rated.sum()), "lost_user_fraction": float(lost.sum()) / max(int(rated.sum()), 1),
-           "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())}
+           "max_rel_err_clean": float((err / want.norm(dim=1).clamp_min(1e-30))[rated & ~lost].max())
+           if bool((rated & ~lost).any()) else None}
     if count_updates:
         # users with more ratings than the solver's width are not counted (reported in updates_checked)
         nmax = max(24, min(64, int(cnt.max())))

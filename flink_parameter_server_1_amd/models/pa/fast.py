@@ -43,6 +43,11 @@ class PAConfig:
     #: plans (``TensorPS.capacity``: no split sizes on the host, capturable steps)
     capacity: Optional[int] = None
     fuse_local_push: bool = True  # W = 1 PS path: the kernel adds its pushes into the table (no delta buffer)
+    #: PS path: micro-batches in flight (the reference's asynchronous pulls under a pull
+    #: limit, ``PassiveAggressiveParameterServer.scala:283-338``; ``tensor_engine.
+    #: staleness_for_pull_limit``): 1 = the pulls of batch k+1 overlap batch k's step and
+    #: its pushes (the row all-to-alls hide behind compute at N > 1); ``flush()`` drains
+    staleness: int = 0
 
 
 class DistributedPA:
@@ -73,7 +78,8 @@ class DistributedPA:
             Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
         self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
         self.worker.fuse_local_push = cfg.fuse_local_push
-        self.runtime = TensorRuntime(self.comm, staleness=0, capacity=cfg.capacity).start(self.worker, logic)
+        self.runtime = TensorRuntime(self.comm, staleness=cfg.staleness, capacity=cfg.capacity).start(self.worker,
+                                                                                                     logic)
         self.timer = None  # utils.metrics.StageTimer (optional)
 
     @property
@@ -104,12 +110,17 @@ class DistributedPA:
             if train:
                 self.examples += indptr.numel() - 1
             return pred, loss
-        # one micro-batch through the engine (staleness 0: done inside submit); a
-        # predict-only call skips the push round (collective: every rank predicts)
+        # one micro-batch through the engine (staleness 0: done inside submit; staleness s:
+        # the batch submitted s calls earlier completes); a predict-only call drains the
+        # pipeline first and skips the push round (collective: every rank predicts)
+        if not train:
+            self.flush()
         self.worker.with_loss = with_loss
         self.worker.pushes = train
         with stage("pa.step", self.timer):
             self.runtime.submit((indptr, indices, values, labels))
+        if not train:
+            self.flush()  # the predictions of THIS batch
         if train:
             self.examples += indptr.numel() - 1
         return self.worker.last
@@ -125,7 +136,13 @@ class DistributedPA:
              else torch.full((B,), -1, dtype=torch.int32, device=dev))
         return self._run(indptr, indices, values, y, False)[0]
 
+    def flush(self) -> None:
+        """Complete every micro-batch in flight (their pushes applied)."""
+        if self.runtime.pipe is not None:
+            self.runtime.pipe.drain()
+
     def dump(self, only_touched=True):
+        self.flush()
         return self.table.dump(only_touched)
 
 
