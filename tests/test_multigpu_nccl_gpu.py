@@ -127,6 +127,24 @@ def _pa_restore(comm, directory):
     return ids[o].cpu(), w[o].reshape(-1).cpu()
 
 
+def _pair_emb(comm, optimizer):
+    """Config #5 scaled down: the range-sharded pair-embedding table under bounded
+    staleness 2 (pushes of up to two later micro-batches in flight before a pull)."""
+    from flink_parameter_server_1_amd.models.emb import DistributedPairEmbedding, PairEmbeddingConfig, \
+        synthetic_pairs
+
+    cfg = PairEmbeddingConfig(num_ids=2_000_000, dim=64, staleness=2, optimizer=optimizer, learning_rate=0.05)
+    m = DistributedPairEmbedding(cfg, comm)
+    batches = [synthetic_pairs(cfg.num_ids, 1 << 14, seed=comm.rank + 1, step=s, device=comm.device, zipf=3.0)
+               for s in range(4)]
+    loss0 = m.mean_loss(*batches[0])
+    for s in range(12):
+        m.step(*batches[s % 4])
+    m.flush()
+    loss1 = m.mean_loss(*batches[0])
+    return m.table.weight.cpu().clone(), loss0, loss1, m.rows_pushed
+
+
 def _model_load_wp(comm, wp, pp, capacity):
     from test_tensor_engine import _model_load
 
@@ -220,6 +238,21 @@ def test_checkpoint_saved_at_n_restores_at_half(backend, tmp_path):
     oa, ob = torch.argsort(ids_a), torch.argsort(ids_b)
     assert ids_a.numel() > 0 and torch.equal(ids_a[oa], ids_b[ob])
     assert torch.equal(w_a[oa], w_b[ob])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("optimizer", ["add", "adagrad"])
+def test_capacity_table_bounded_staleness_equals_host_synchronous_world(backend, optimizer):
+    """BASELINE config #5 (the sharded embedding table with bounded staleness 2) on N
+    ranks vs the host-synchronous world: the same shards to fp32 summation order and
+    the same pushed rows; the loss falls."""
+    W = _world(backend) if backend == "nccl" else 8
+    res = _run(backend, _pair_emb, W, optimizer)
+    ref = run_virtual(_pair_emb, W, optimizer, mode="sync")
+    for (wa, l0a, l1a, ra), (wb, l0b, l1b, rb) in zip(res, ref):
+        assert ra == rb and l1a < l0a
+        torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.timeout(600)
