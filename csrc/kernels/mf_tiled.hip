@@ -729,9 +729,12 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
 
 // Build-time knobs of the tile SGD (A/B variants: csrc/build.py --variant NAME -D ...):
 // user rows in flight per lane group, and the minimum waves per SIMD the register
-// allocation must leave room for (2 = two 512-thread workgroups per CU)
+// allocation must leave room for (2 = two 512-thread workgroups per CU).  4 rows in
+// flight: 79 VGPRs, three 512-thread workgroups per CU (8 rows: 109 VGPRs, two) --
+// 0.5 % faster on the headline in two same-box A/Bs; 6 or 10 rows, or a forced 3rd /
+// 4th workgroup with spills, were slower (profiles/r5_tile_sgd_variants_ab.txt)
 #ifndef FPS_TG_PF
-#define FPS_TG_PF 8
+#define FPS_TG_PF 4
 #endif
 #ifndef FPS_TG_MINW
 #define FPS_TG_MINW 2
