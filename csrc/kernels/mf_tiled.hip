@@ -693,11 +693,20 @@ __device__ __forceinline__ void tilegroup_tile(TgShared<REC8>& sh, const int t, 
             nu.z = u.z + lr * (e * i.z - lambda * u.z);
             nu.w = u.w + lr * (e * i.w - lambda * u.w);
             if constexpr (UM == 2) {
-              float* up = reinterpret_cast<float*>(Ug + ur[q] + j + v * TPR);
-              atomic_add_noret(up + 0, nu.x - u.x);
-              atomic_add_noret(up + 1, nu.y - u.y);
-              atomic_add_noret(up + 2, nu.z - u.z);
-              atomic_add_noret(up + 3, nu.w - u.w);
+              // the delta added with contiguous float atomics: lane j of the group holds
+              // elements 4j .. 4j+3 of this 4*TPR-float chunk; atomic instruction c adds
+              // element TPR*c + j, fetched from lane (TPR*c + j) / 4 -- every instruction then
+              // covers 4*TPR contiguous bytes of the row (one 64-B request per row at
+              // TPR = 16) instead of 4-B lanes at a 16-B stride (4x the atomic requests)
+              const float dx = nu.x - u.x, dy = nu.y - u.y, dz = nu.z - u.z, dw = nu.w - u.w;
+              float* up = reinterpret_cast<float*>(Ug + ur[q] + v * TPR);
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                const int src = (TPR * c + j) >> 2, comp = j & 3;
+                const float a0 = __shfl(dx, src, TPR), a1 = __shfl(dy, src, TPR);
+                const float a2 = __shfl(dz, src, TPR), a3 = __shfl(dw, src, TPR);
+                atomic_add_noret(up + TPR * c + j, comp == 0 ? a0 : comp == 1 ? a1 : comp == 2 ? a2 : a3);
+              }
             } else if constexpr (UM == 1)
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tg_u4, nu), urs,
                                                      (int)((uint32_t)(ur[q] + j + v * TPR) * 16u), 0, 16);

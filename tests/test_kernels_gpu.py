@@ -373,6 +373,45 @@ def test_mf_sgd_tiled_unique_rows(D, rec8):
 
 
 @pytest.mark.parametrize("rec8", [False, True])
+def test_mf_sgd_tiled_user_modes_match_reference_rmw_and_atomic_sums():
+    """User-row modes of the tiled kernel vs the fp32 reference: sc1 / atomic equal the
+    plain kernel on unique users; with every user repeated 8 times in one launch the
+    atomic mode (exact: float-atomic user deltas) equals the reference's summed user
+    deltas (``R.mf_sgd_local(user_atomic=True)``), D = 16 / 64 / 128 (the lane transposition
+    of the contiguous atomics at 4, 16 and 16 x 2 lanes per chunk)."""
+    for D in (16, 64, 128):
+        nu, ni, B = 6000, 5000, 3000
+        U0 = torch.rand(nu, D, device=DEV) * 0.1
+        I0 = torch.rand(ni, D, device=DEV) * 0.1
+        uid = torch.randperm(nu, device=DEV)[:B].to(torch.int32)
+        iid = torch.randperm(ni, device=DEV)[:B].to(torch.int32)
+        r = torch.rand(B, device=DEV)
+        Rt = ops.tile_rows_for(D, ni, 1)
+        T = -(-ni // Rt)
+        ptr, rec = ops.TilePartitioner(1, [ni], Rt, T, DEV, rec8=True).run(uid, iid, r)
+        out = []
+        for mode in (0, 1, 2):
+            U, I = U0.clone(), I0.clone()
+            ops.mf_sgd_tiled(U, I, rec, ptr, 0, T, Rt, 0.05, 0.01, user_mode=mode)
+            out.append((U, I))
+        for U, I in out[1:]:
+            torch.testing.assert_close(U, out[0][0], rtol=1e-6, atol=1e-7)
+            torch.testing.assert_close(I, out[0][1], rtol=1e-6, atol=1e-7)
+        # repeated users, distinct items: users get 8 deltas each in one launch
+        uid8 = (torch.arange(B, device=DEV) % (B // 8)).to(torch.int32)
+        ptr, rec = ops.TilePartitioner(1, [ni], Rt, T, DEV, rec8=True).run(uid8, iid, r)
+        U, I = U0.clone(), I0.clone()
+        ops.mf_sgd_tiled(U, I, rec, ptr, 0, T, Rt, 0.05, 0.0, user_mode=2)
+        Ur, Ir = U0.cpu().clone(), I0.cpu().clone()
+        R.mf_sgd_local(Ur, Ir, uid8.cpu(), iid.cpu(), r.cpu(), 0.05, 0.0, user_atomic=True)
+        # a user's 8 ratings may read its row before or after the others' adds landed
+        # (second order: ~1e-5 here); a LOST delta would be ~1e-3
+        assert float((U.cpu() - Ur).abs().max()) < 5e-5
+        assert float((I.cpu() - Ir).abs().max()) < 5e-5
+        assert float((U.cpu() - U0.cpu()).abs().max()) > 1e-3  # the deltas did land
+
+
+@pytest.mark.parametrize("rec8", [False, True])
 def test_mf_sgd_tiled_pair_matches_two_launches(rec8):
     """Both item blocks in one launch (``mf_sgd_tiled_pair``): unique users and items,
     so it equals the batch reference; blocks of unequal size."""
