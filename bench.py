@@ -106,6 +106,9 @@ def main(argv=None):
                     help="tiled SGD: user-range phases per step (0 = auto, ~2.5M users per phase)")
     ap.add_argument("--force-ps-path", action="store_true",
                     help="run dedup/pull/push even at N=1 (measures the N>1 step minus RCCL)")
+    ap.add_argument("--no-fuse-local-push", action="store_true",
+                    help="--force-ps-path at N=1: push the delta buffer through the PS apply instead of letting the "
+                         "tiled kernel update the served shard in place")
     ap.add_argument("--watchdog-s", type=float, default=0.0,
                     help="fail fast: end this rank (exit 17) when a step makes no progress for this long (0 = off)")
     ap.add_argument("--no-hogwild-probe", action="store_true",
@@ -165,7 +168,7 @@ def main(argv=None):
     cfg = MFConfig(num_users=a.users, num_items=a.items, dim=a.dim, learning_rate=a.lr, wire_dtype=a.wire,
                    user_update=a.user_update, force_ps_path=a.force_ps_path, sgd_mode=a.sgd_mode,
                    pipeline=not a.no_pipeline, exchange=a.exchange, prefetch_partition=not a.no_prefetch,
-                   user_phases=a.user_phases, rotation=a.rotation)
+                   user_phases=a.user_phases, rotation=a.rotation, fuse_local_push=not a.no_fuse_local_push)
     model = DistributedMF(cfg, comm)
     data = SyntheticRatings(a.users, a.items, a.batch * a.pool, comm.rank, n, device=comm.device)
 
@@ -267,6 +270,7 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{n} (users by user%W) + ps{n} (items hash-sharded, exchange={model.exchange})",
                 "exchange": model.exchange,
+                "fuse_local_push": cfg.fuse_local_push if model.exchange == "ps" else None,
                 "wire_dtype": a.wire if model.exchange == "ps" else "none (fp32 parameters stay resident or travel "
                                                                      "whole)",
                 "sgd_mode": model.sgd_mode,

@@ -112,12 +112,18 @@ class BatchedPSClient:
     def push(self, deltas: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         raise NotImplementedError
 
-    def local_push_target(self):
+    def local_push_target(self, in_place: bool = False):
         """``(table, row_map)`` when the answered pull's push may be applied by the
         worker itself -- the owner is this rank (world 1), the PS rule is a plain
         additive one and the pulled rows are a snapshot, not the table -- else None.
         Adding the delta of pulled row ``r`` to ``table[row_map[r]]`` (float atomics)
-        is then the push; call ``push_applied()`` afterwards instead of ``push*``."""
+        is then the push; call ``push_applied()`` afterwards instead of ``push*``.
+
+        ``in_place=True``: the pulled rows may also BE the table (a zero-copy serve).
+        The worker declares that it reads a row it has started updating only as
+        "pulled row + what this micro-batch added so far" -- so updating the table row
+        in place computes exactly what pushing the summed delta would (the MF tiled
+        kernel's delta mode: a chunk continues from ``I + Dl``)."""
         return None
 
     def push_applied(self) -> None:

@@ -185,7 +185,7 @@ class _Client(BatchedPSClient):
             self._acc += d.to(self._acc.dtype) * mask.view(-1, 1).to(self._acc.dtype)
         self._mask |= mask
 
-    def local_push_target(self):
+    def local_push_target(self, in_place: bool = False):
         plan = self._plan
         if plan is None:
             raise RuntimeError("local_push_target() is only valid inside on_pull_recv_batch")
@@ -196,7 +196,8 @@ class _Client(BatchedPSClient):
         t = ps.table
         if (logic.op != "add" or logic.combine != "sum" or logic.emit == "push" or ps.masked_push
                 or getattr(t, "optimizer", "") != "add" or getattr(t, "sparse", False) or plan.fixed
-                or t.weight.dtype != torch.float32 or plan.recv_rows is None or self._served_is_table(plan)):
+                or t.weight.dtype != torch.float32 or plan.recv_rows is None
+                or (self._served_is_table(plan) and not in_place)):
             return None
         return t.weight, plan.recv_rows
 

@@ -70,6 +70,9 @@ class MFConfig:
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
     pipeline: bool = True             # overlap pull(k+1) all-to-all with SGD(k) (remote PS path)
+    fuse_local_push: bool = True      # PS path, world 1, identity plan: the tiled SGD updates the served
+                                      # shard rows in place -- the push applied by the kernel (no delta
+                                      # buffer, second row read or apply pass); False: delta mode + apply
     prefetch_partition: bool = True   # tiled: bucket batch k+1 on a side stream during the SGD of k
     negative_sample_rate: int = 0     # implicit feedback: negatives (rating 0) per rating
     user_memory: int = 128            # per-user ring of recent items excluded from the negatives
@@ -502,6 +505,18 @@ class DistributedMF:
                                   self.user_atomic)
         return delta
 
+    def _item_sgd_in_place(self, table: torch.Tensor, staged):
+        """PS path, world 1 (``_MFPSWorker``): the tiled SGD of one micro-batch on the
+        served shard itself, its push (the rows' summed deltas) added in place."""
+        c = self.cfg
+        ptr, rec, ev = staged
+        if ev is not None:
+            torch.cuda.current_stream(self.U.device).wait_event(ev)
+        with stage("mf.sgd", self.timer):
+            for p in range(self.user_phases):
+                ops.mf_sgd_tiled(self.U, table, rec, ptr, 2 * p, self.tile_T, self.tile_R, c.learning_rate, c.lam,
+                                 user_mode=self.user_mode)
+
     def flush(self):
         """Complete the in-flight micro-batch of the pipelined path / bring the
         rotating item blocks back to their PS shards."""
@@ -621,9 +636,19 @@ class _MFPSWorker(BatchedWorkerLogic):
 
     def on_pull_recv_batch(self, pulled, ps):
         uid_local, rating, staged = pulled.payload
+        m = self.m
         if staged is not None and not getattr(pulled, "identity", False):
             raise RuntimeError("MF PS path: a partition was staged for an identity plan that did not happen")
-        ps.push_unique(self.m._item_deltas(pulled.rows, pulled.pos, pulled.n_unique, uid_local, rating, staged))
+        if staged is not None and m.cfg.fuse_local_push:
+            # world 1, zero-copy identity serve: the pulled rows ARE the shard.  The
+            # delta-mode kernel continues every row from "pulled + added so far", which
+            # is the row updated in place -- so the kernel adds the push itself
+            target = ps.local_push_target(in_place=True)
+            if target is not None and target[0].data_ptr() == pulled.rows.data_ptr():
+                m._item_sgd_in_place(pulled.rows, staged)
+                ps.push_applied()
+                return
+        ps.push_unique(m._item_deltas(pulled.rows, pulled.pos, pulled.n_unique, uid_local, rating, staged))
 
 
 @dataclass

@@ -7,6 +7,14 @@ O=gpurun_out/r5h
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_hogwild_gpu.py -k "user_modes or atomic" -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 grep -E "PASS|FAIL" $O/tests.log
+timeout -k 10 300 python -u -m pytest tests/test_tensor_engine_gpu.py -k "mf_ps" -x -v --timeout 200 --timeout-method thread > $O/tests_ps.log 2>&1 || { tail -40 $O/tests_ps.log; exit 1; }
+grep -E "PASS|FAIL" $O/tests_ps.log
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --force-ps-path --no-hogwild-probe > $O/ps_fused_$i.log 2>&1 || { tail -20 $O/ps_fused_$i.log; exit 1; }
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --force-ps-path --no-hogwild-probe --no-fuse-local-push > $O/ps_delta_$i.log 2>&1 || { tail -20 $O/ps_delta_$i.log; exit 1; }
+  for v in fused delta; do tail -1 $O/ps_${v}_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("ps", sys.argv[1], round(d["ms_per_step"],3), "%.4e" % d["value"])' $v; done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_ps_fused -- python bench.py --steps 5 --warmup 2 --force-ps-path --no-hogwild-probe > $O/prof_ps_fused.log 2>&1 || { tail -20 $O/prof_ps_fused.log; exit 1; }
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --user-update atomic > $O/bench_atomic.log 2>&1 || { tail -20 $O/bench_atomic.log; exit 1; }
 tail -1 $O/bench_atomic.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["config"]["user_update"], round(d["ms_per_step"],3), "%.4e" % d["value"], d["config"]["lost_user_update_fraction"], d["effective_updates_per_s"])'
 timeout -k 10 300 python bench/bench_emulate_world.py --ws 8 --steps 6 --warmup 2 --user-update atomic > $O/emu8_atomic.log 2>&1 || { tail -20 $O/emu8_atomic.log; exit 1; }

@@ -372,7 +372,6 @@ def test_mf_sgd_tiled_unique_rows(D, rec8):
     torch.testing.assert_close(I.cpu(), Ir, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("rec8", [False, True])
 def test_mf_sgd_tiled_user_modes_match_reference_rmw_and_atomic_sums():
     """User-row modes of the tiled kernel vs the fp32 reference: sc1 / atomic equal the
     plain kernel on unique users; with every user repeated 8 times in one launch the

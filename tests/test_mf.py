@@ -204,3 +204,4 @@ def test_ps_path_tiled_on_pulled_rows_converges_cpu(mode):
     for s in range(30):
         m.step(*data.batch(s, 6000))
     assert m.rmse(uid, iid, r) < 0.5 * before
+
