@@ -138,16 +138,17 @@ class LempTopK:
         return self.lengths[s:].max()
 
     def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None, start: int = 0,
-              state=None):
+              state=None, unfused: bool = False):
         """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
         use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering.  ``start`` /
         ``state = (best_s, best_i)``: continue a scan whose items ``[0, start)`` are
-        already merged into ``state``."""
+        already merged into ``state``.  ``unfused``: the score-matrix scan (the rescan
+        of a batch whose fused scan overflowed)."""
         Q = Q.float().contiguous()
         B = Q.shape[0]
         dev = Q.device
         N = self.vecs.shape[0]
-        fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K
+        fused = self.fused and dev.type == "cuda" and k <= ops.TOPK_MAX_K and not unfused
         if fused and self.sync_free and N > max(self.seed_items, start) and state is None and start == 0 \
                 and (Q.shape[0], int(k)) in self._graph and not self._coord_active() and not ops.DEBUG:
             if self._uses_coord():  # COORD switched off for this batch (the per-batch switch)
@@ -231,6 +232,35 @@ class LempTopK:
                 cand_i = torch.cat([best_i, self.ids[s:e].expand(B, n)], 1)
                 best_s, best_i = top_s, torch.gather(cand_i, 1, top_j)
         return best_s, best_i
+
+    def query_async(self, Q: torch.Tensor, k: int) -> "TopKFuture":
+        """``query`` without the end-of-scan host sync: the scan of a fresh batch is
+        replayed from its hipGraph, its result copied out on the device and its
+        overflow flag copied to pinned host memory behind an event -- nothing waits.
+        ``TopKFuture.result()`` reads the flag, so a caller that enqueues batch k + 1
+        before asking for batch k's result never drains the device (an overflowed
+        batch is rescanned then: ``query(..., unfused=True)``, the same exact top-K).
+        ``Q`` must not be modified before ``result()``.  Batches the graph does not
+        cover (first of a shape, COORD scans, continued scans, CPU) run ``query``."""
+        Q = Q.float().contiguous()
+        key = (Q.shape[0], int(k))
+        if not (Q.is_cuda and self.fused and self.sync_free and self.graphs and k <= ops.TOPK_MAX_K
+                and self.vecs.shape[0] > self.seed_items and key in self._graph and not self._coord_active()
+                and not ops.DEBUG):
+            return TopKFuture(value=self.query(Q, k))
+        if self._uses_coord():  # COORD switched off for this batch (the per-batch switch)
+            self.coord_off_batches -= 1
+            self.coord_batches["off"] += 1
+        graph, q_in, best_s, best_i, ovf, scanned = self._graph[key]
+        q_in.copy_(Q)
+        graph.replay()
+        self.buckets_scanned += scanned
+        flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        flag.copy_(ovf, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        # the graph's buffers are rewritten by the next replay: the result is a copy
+        return TopKFuture(raw=(best_s.clone(), best_i.clone()), index=self, Q=Q, k=int(k), flag=flag, event=ev)
 
     def _query_graph(self, Q: torch.Tensor, qlen: torch.Tensor, k: int):
         """The fused scan of a fresh query batch as one hipGraph replay: the seed
@@ -433,14 +463,50 @@ class LempTopK:
         return not (float(self._len_host[s]) > float(self._len_host[e - 1]) * self.strategy.algorithm_switch_threshold)
 
 
+class TopKFuture:
+    """The top-K of one query batch, completed on the host only when asked
+    (``LempTopK.query_async``): ``result()`` waits for the batch's event -- long
+    done when later batches were enqueued first -- reads its overflow flag from
+    pinned memory, rescans the batch if it overflowed, and applies ``finish``
+    (the cross-shard merge) once."""
+
+    def __init__(self, value=None, raw=None, index=None, Q=None, k: int = 0, flag=None, event=None, finish=None):
+        self._value, self._raw, self._index, self._Q, self._k = value, raw, index, Q, k
+        self._flag, self._event, self._finish = flag, event, finish
+        if value is not None and finish is not None:
+            self._value, self._finish = finish(value), None
+
+    def then(self, finish) -> "TopKFuture":
+        """Apply ``finish(best_s, best_i) -> result`` to the result (now if it is ready)."""
+        if self._value is not None:
+            self._value = finish(self._value)
+        else:
+            self._finish = finish
+        return self
+
+    def done(self) -> bool:
+        return self._value is not None or self._event is None or self._event.query()
+
+    def result(self):
+        if self._value is None:
+            self._event.synchronize()
+            res = self._raw
+            if int(self._flag[0]):  # some query passed more than the candidate cap: rescan
+                self._index.overflows += 1
+                res = self._index.query(self._Q, self._k, unfused=True)
+            self._value = self._finish(res) if self._finish is not None else res
+            self._raw = self._Q = self._index = None
+        return self._value
+
+
 def merge_top_k(scores: torch.Tensor, ids: torch.Tensor, k: int, exclude_ids: Optional[torch.Tensor] = None):
     """Merge partial top-K lists ``[B, m]`` into the best ``k``; ``exclude_ids`` [B, E]
-    (padded with -1) are dropped first (K13)."""
+    (padded with -1) are dropped first (K13).  No host sync."""
     s = scores.clone()
     if exclude_ids is not None and exclude_ids.numel():
         hit = (ids[:, :, None] == exclude_ids[:, None, :]).any(-1)
-        s[hit] = float("-inf")
-    s[ids < 0] = float("-inf")
+        s.masked_fill_(hit, float("-inf"))
+    s.masked_fill_(ids < 0, float("-inf"))
     top_s, j = torch.topk(s, min(k, s.shape[1]), dim=1)
     return top_s, torch.gather(ids, 1, j)
 
@@ -465,3 +531,13 @@ class DistributedTopK:
         else:
             ss, ii = s, i
         return merge_top_k(ss, ii, K, exclude_ids)
+
+    def query_async(self, Q: torch.Tensor, K: int, worker_k: Optional[int] = None,
+                    exclude_ids: Optional[torch.Tensor] = None) -> TopKFuture:
+        """``query`` whose overflow check is deferred to ``result()`` (``LempTopK.query_async``):
+        enqueue batch k + 1, then take batch k's result -- no host sync per batch on one
+        rank.  Across ranks the partial lists are merged after every rank's flag is known,
+        so world > 1 completes synchronously."""
+        if self.comm.world > 1:
+            return TopKFuture(value=self.query(Q, K, worker_k, exclude_ids))
+        return self.local.query_async(Q, worker_k or K).then(lambda r: merge_top_k(r[0], r[1], K, exclude_ids))
