@@ -22,6 +22,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     names = {0: "plain gather (baseline)", 1: "returning atomicAdd", 2: "no-return atomicAdd",
              3: "lock CAS + exchange", 4: "returning atomicAdd, 1 lane per 16"}
+    if os.environ.get("FPS_PROBE_ROWS"):  # only the row-update probes
+        return rows(lib, dev, st)
     for which in (0, 1, 2, 3, 4):
         ts = []
         for rep in range(4):
@@ -42,6 +44,38 @@ def main():
         if which == 3:
             ok = int(cnt.abs().sum()) == 0
         print(json.dumps({"probe": names[which], "ms": min(ts), "per_s": n / (min(ts) / 1e3), "ok": ok}), flush=True)
+
+    rows(lib, dev, st)
+
+
+def rows(lib, dev, st):
+    """256-B row updates (one wave per update): plain read-modify-write (Hogwild) vs
+    float atomics, rows random over the table or owned by one XCD each
+    (``s_getreg HW_REG_XCC_ID``).  Design input for exact user rows."""
+    lib.probe_rows.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                               ctypes.c_void_p]
+    names = {0: "row RMW plain (Hogwild)", 1: "row float atomics, agent scope", 2: "row float atomics, workgroup scope",
+             3: "row float atomics, agent scope, XCD-owned rows", 4: "row float atomics, workgroup scope, XCD-owned rows"}
+    n = 1 << 24  # one user phase of the headline step
+    for nrows in (2_500_000, 10_000_000):
+        uid = torch.randint(0, nrows, (n,), dtype=torch.int32, device=dev)
+        tab = torch.zeros(nrows, 64, device=dev)
+        for mode in (0, 1, 2, 3, 4):
+            ts = []
+            for rep in range(4):
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = lib.probe_rows(mode, uid.data_ptr(), tab.data_ptr(), n, nrows, st)
+                e1.record()
+                torch.cuda.synchronize()
+                assert rc == 0, rc
+                if rep:
+                    ts.append(e0.elapsed_time(e1))
+            ms = min(ts)
+            print(json.dumps({"probe": names[mode], "rows": nrows, "updates": n, "ms": ms,
+                              "GB_per_s_256B": n * 256 / (ms / 1e3) / 1e9}), flush=True)
+        del tab
 
 
 if __name__ == "__main__":

@@ -207,6 +207,12 @@ __device__ __forceinline__ void tp3_scan(const int32_t* cnt, int32_t* off, int n
 // 2^15 at the start of every sub-batch and grows by at most H16_SB = 2^15 in it,
 // so it never exceeds 2^16 - 1.  Uniform keys never flush (~8 counts per bucket).
 constexpr int H16_SB = 32768;
+// FPS_TP_NORET=1: the 16-bit counters are incremented with non-returning LDS atomics and
+// the "a counter reached 2^15" test reads the histogram at each sub-batch end (KT / 2
+// words, 128-bit reads) instead of every returned old value (A/B knob)
+#ifndef FPS_TP_NORET
+#define FPS_TP_NORET 0
+#endif
 
 template <bool H16>
 __device__ __forceinline__ int32_t hb_get(const int32_t* hb, int b) {
@@ -223,7 +229,7 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
   // One LDS atomic per rating (LDS atomics run at ~1 lane per CU cycle and
   // bound this kernel); the coarse counts of a chunk are read off the fine
   // histogram afterwards: 8 lanes per coarse key sum its 2^cshift buckets.
-  extern __shared__ int32_t hb[];  // [KT] ints, or [ceil(KT / 2)] words of two 16-bit counters (dynamic LDS)
+  extern __shared__ __attribute__((aligned(16))) int32_t hb[];  // [KT] ints, or [ceil(KT / 2)] words of two 16-bit counters (dynamic LDS)
   __shared__ int32_t hc_prev[TP3_MAXK], hc_acc[TP3_MAXK];
   __shared__ int32_t s_ovf, s_flushed;
   const int KW = H16 ? (KT + 1) / 2 : KT;
@@ -271,8 +277,12 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
           tile_bucket(iv[j], uv[j], g, bk, row);
           if constexpr (H16) {
             const int sh = (bk & 1) << 4;
+#if FPS_TP_NORET
+            atomicAdd(reinterpret_cast<uint32_t*>(hb) + (bk >> 1), 1u << sh);
+#else
             const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(hb) + (bk >> 1), 1u << sh);
             if (((old >> sh) & 0xffffu) >= 32767u) s_ovf = 1;  // this counter reached 2^15
+#endif
           } else {
             atomicAdd(hb + bk, 1);
           }
@@ -281,6 +291,20 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
       }
       if constexpr (H16) {
         __syncthreads();
+#if FPS_TP_NORET
+        {  // any counter >= 2^15?  (KW words; 4 per 128-bit read where aligned)
+          bool hit = false;
+          const int KW4 = KW >> 2;
+          const uint4* h4 = reinterpret_cast<const uint4*>(hb);
+          for (int k = threadIdx.x; k < KW4; k += blockDim.x) {
+            const uint4 w = h4[k];
+            hit |= ((w.x | w.y | w.z | w.w) & 0x80008000u) != 0u;
+          }
+          for (int k = 4 * KW4 + threadIdx.x; k < KW; k += blockDim.x) hit |= (hb[k] & 0x80008000u) != 0u;
+          if (hit) s_ovf = 1;
+        }
+        __syncthreads();
+#endif
         const bool ovf = s_ovf;
         // every thread has read the flag before any can start the next sub-batch and set it again
         __syncthreads();

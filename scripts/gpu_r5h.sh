@@ -23,4 +23,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 FPS_SHARE_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --steps 4 --warmup 1 --batch 4194304 --no-hogwild-probe > $O/bench_n2_rehearsal.log 2>&1 || { tail -30 $O/bench_n2_rehearsal.log; exit 1; }
 grep '^{' $O/bench_n2_rehearsal.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("n2 rehearsal", d["n_gpus"], d["backend"], "verify_ok", d.get("verify_ok"), d["verify"]["verify_max_abs_err_items"], d["verify"]["devices"])'
 FPS_SHARE_GPU=1 FPS_VERIFY_MUTANT=wrong_buffer timeout -k 10 400 python bench.py --gpus 2 --steps 2 --warmup 1 --batch 4194304 --no-hogwild-probe > $O/bench_n2_mutant.log 2>&1; echo "mutant rc=$? (expect nonzero)"; grep -c '^{' $O/bench_n2_mutant.log; grep -o "VERIFY FAILED" $O/bench_n2_mutant.log | head -1
-echo ALLDONE
+echo R5H_DONE

@@ -9,7 +9,7 @@ grep -cE "PASSED" $O/tests.log
 for i in 1 2; do
   for v in sync async; do
     F=""; [ $v = sync ] && F="--sync"
-    timeout -k 10 300 python bench/bench_topk.py --steps 40 --warmup 4 $F > $O/topk_${v}_$i.log 2>&1 || { tail -20 $O/topk_${v}_$i.log; exit 1; }
+    timeout -k 10 300 python bench/bench_topk.py --steps 30 --warmup 3 $F > $O/topk_${v}_$i.log 2>&1 || { tail -20 $O/topk_${v}_$i.log; exit 1; }
     tail -1 $O/topk_${v}_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("topk", sys.argv[1], round(d["ms_per_step"],3), "%.4e" % d["value"], d["exact_vs_brute_force"])' $v
   done
 done

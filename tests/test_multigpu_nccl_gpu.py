@@ -255,6 +255,48 @@ def test_capacity_table_bounded_staleness_equals_host_synchronous_world(backend,
         torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
 
 
+def _graph_step(comm, graph):
+    """Fixed-shape plans at world N (keys / rows / deltas: three all-to-alls per micro-batch);
+    ``graph=True`` captures the whole step -- its RCCL all-to-alls included -- into one
+    hipGraph and replays it (``core/step_graph.py``)."""
+    from flink_parameter_server_1_amd.api.batched import BatchedWorkerLogic
+    from flink_parameter_server_1_amd.core.tensor_engine import TensorRuntime
+    from flink_parameter_server_1_amd.ps.device_logics import DeviceSimplePSLogic
+
+    class W(BatchedWorkerLogic):
+        graph_safe = True
+
+        def on_recv_batch(self, batch, ps):
+            keys, w = batch
+            ps.pull(keys, payload=w)
+
+        def on_pull_recv_batch(self, pulled, ps):
+            ps.push(0.1 * pulled.values() + pulled.payload.view(-1, 1))
+
+    logic = DeviceSimplePSLogic(5000, 8, op="add", init=("uniform", -0.1, 0.1), seed=3)
+    rt = TensorRuntime(comm, staleness=0, graph=graph, capacity=512).start(W(), logic)
+    g = torch.Generator(device=comm.device).manual_seed(11 + comm.rank)
+    for _ in range(10):
+        rt.submit((torch.randint(0, 5000, (256,), generator=g, device=comm.device),
+                   torch.rand(256, generator=g, device=comm.device)))
+    rt.finish()
+    torch.cuda.synchronize()
+    replays = rt.graphs.replays if graph and rt.graphs is not None else 0
+    return logic.table.weight.cpu(), replays
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.skipif(N_GPUS < 2, reason="needs >= 2 GPUs")
+def test_graph_captured_rccl_step_equals_eager_across_gpus():
+    """What the one-rank loopback group could not show: a hipGraph holding RCCL
+    all-to-alls between DIFFERENT GPUs replays to the eager engine's tables."""
+    eager = run_nccl(_graph_step, N_GPUS, False)
+    graph = run_nccl(_graph_step, N_GPUS, True)
+    for (w0, _), (w1, replays) in zip(eager, graph):
+        assert replays > 0
+        torch.testing.assert_close(w1, w0, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.timeout(600)
 def test_verify_sees_a_missing_stream_wait():
     """The check itself under RCCL semantics: the rotation with the ``w.wait()`` of

@@ -307,13 +307,15 @@ def test_mf_ps_identity_plan_matches_dedup_plan():
 def test_mf_ps_world1_fused_push_equals_delta_mode():
     """World 1, identity plans: the tiled SGD updating the served shard in place (the
     push applied by the kernel: no delta buffer, second row read or apply pass) trains
-    the same model as the delta-mode kernel + pushed deltas (exact user rows, so the
-    only difference is fp32 summation order)."""
+    the same model as the delta-mode kernel + pushed deltas.  The GPU step is not
+    bit-deterministic (concurrent user-row reads see other deltas or not), so the
+    fused run is compared with one delta-mode run at the distance between two
+    delta-mode runs."""
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
     res = []
-    for fuse in (True, False):
+    for fuse in (True, False, False):
         cfg = MFConfig(num_users=20000, num_items=1000, dim=64, learning_rate=0.05, force_ps_path=True, seed=3,
                        fuse_local_push=fuse, user_update="atomic", user_phases=2)
         m = DistributedMF(cfg, Comm(device=DEV))
@@ -327,8 +329,10 @@ def test_mf_ps_world1_fused_push_equals_delta_mode():
         assert bool(calls) == fuse
         uid, iid, r = data.batch(0, 1 << 16)
         res.append((m.rmse(uid, iid, r), m.I.clone(), m.U.clone(), m.ps.stats["pushes"]))
-    (r1, I1, U1, p1), (r0, I0, U0, p0) = res
-    assert p1 == p0 > 0
-    assert abs(r1 - r0) < 1e-4 * r0, (r1, r0)
-    torch.testing.assert_close(I1, I0, rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(U1, U0, rtol=1e-4, atol=1e-5)
+    (rf, If, Uf, pf), (r0, I0, U0, p0), (r1, I1, U1, p1) = res
+    assert pf == p0 == p1 > 0
+    noise_i = float((I1 - I0).abs().max())
+    noise_u = float((U1 - U0).abs().max())
+    assert float((If - I0).abs().max()) <= 3 * noise_i + 1e-6, (float((If - I0).abs().max()), noise_i)
+    assert float((Uf - U0).abs().max()) <= 3 * noise_u + 1e-6, (float((Uf - U0).abs().max()), noise_u)
+    assert abs(rf - r0) < 1e-3 * r0, (rf, r0)
