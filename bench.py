@@ -96,10 +96,11 @@ def main(argv=None):
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="tiled SGD: partition each batch on the main stream instead of prefetching it")
-    ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"],
+    ap.add_argument("--user-update", default="auto", choices=["auto", "store", "sc1", "atomic"],
                     help="store: Hogwild user rows (plain accesses); sc1: write-through user rows (about half the lost "
                          "user updates); atomic: exact -- the tiled kernel adds every user delta with float atomics "
-                         "(none lost)")
+                         "(none lost, ~2x the step: float atomics run at ~1.25 TB/s, profiles/r5_exact_user_rows.md); "
+                         "auto (default): atomic at N > 1, store at N = 1")
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--user-phases", type=int, default=0,
@@ -237,7 +238,7 @@ def main(argv=None):
         n_loc = model.users.n_local
         try:  # a side measurement: its failure must not cost the timed result
             hog = lost_updates(n_loc, a.items, a.batch / n_loc, getattr(model, "user_phases", 1),
-                               user_update=a.user_update, world=n if model.exchange == "rotate" else 1)
+                               user_update=model.user_update, world=n if model.exchange == "rotate" else 1)
         except Exception as e:  # noqa: BLE001 -- reported, the bench line still prints
             print(f"hogwild side probe failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
             hog = None
@@ -287,7 +288,7 @@ def main(argv=None):
                 "users_per_rank": [int(x) for x in n_local],
                 "bytes_sent_per_rank": bytes_per_rank,
                 "bytes_per_peer_rank0": list(comm.peer_bytes),
-                "user_update": a.user_update,
+                "user_update": model.user_update,
                 # Hogwild race of the user rows (side probe on rank 0's geometry, not timed):
                 # fraction of rated users that lost >= 1 update, fraction of rating updates lost
                 "lost_user_fraction": None if hog is None else hog["lost_user_fraction"],
@@ -298,7 +299,7 @@ def main(argv=None):
         # updates that survive the Hogwild user-row race (value counts every rating's update;
         # user_update="atomic" loses none): value x (1 - lost fraction), None when unmeasured
         out["effective_updates_per_s"] = value * (1.0 - lf) if lf is not None else \
-            (value if a.user_update == "atomic" else None)
+            (value if model.user_update == "atomic" else None)
         if verify is not None:
             out["verify_ok"] = verify["verify_ok"]
             out["verify"] = verify

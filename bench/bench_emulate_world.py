@@ -44,7 +44,8 @@ def main():
                     help="model each sub-step's transfers on links of this rate (EmulatedRotation: rank-symmetric "
                          "timing, a one-wave device sleep for the link time + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
-    ap.add_argument("--user-update", default="store", choices=["store", "sc1", "atomic"])
+    ap.add_argument("--user-update", default="auto", choices=["auto", "store", "sc1", "atomic"],
+                    help="auto = what bench.py runs at this world size (atomic at N > 1)")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="sub-steps on alternating compute streams (MFConfig.overlap_substeps; auto: from 4 ranks)")
     a = ap.parse_args()
@@ -86,7 +87,7 @@ def main():
                           "updates_per_s_per_gpu": a.batch / ms * 1e3, "ratio_to_n1": ms / base,
                           "users_per_gpu": m.users.n_local, "sub_steps": m.rot.K if W > 1 else 1,
                           "tile_rows": getattr(m, "tile_R", None), "tiles_per_block": getattr(m, "tile_T", None),
-                          "user_phases": getattr(m, "user_phases", None),
+                          "user_phases": getattr(m, "user_phases", None), "user_update": m.user_update,
                           "link_gbps": a.link_gbps if W > 1 else None, "latency_us": a.latency_us if W > 1 else None,
                           "comm_wait_ms_per_step": wait, "exposed_fraction": wait / ms,
                           "overlap_substeps": bool(getattr(m, "_overlap", False)),

@@ -62,10 +62,12 @@ class MFConfig:
     range_min: float = -0.01
     range_max: float = 0.01
     seed: int = 0
-    user_update: str = "store"        # "store" (Hogwild, plain accesses) | "sc1" (Hogwild, write-through user
+    user_update: str = "auto"         # "store" (Hogwild, plain accesses) | "sc1" (Hogwild, write-through user
                                       # rows: ~half the lost user updates, profiles/r4_hogwild.md) | "atomic"
                                       # (exact: no lost update -- the tiled kernel adds every user delta with
-                                      # float atomics; the flat kernel where the tiled one does not apply)
+                                      # float atomics; the flat kernel where the tiled one does not apply) |
+                                      # "auto": "atomic" on a job of N > 1 ranks (real or emulated), "store"
+                                      # on one (profiles/r5_exact_user_rows.md)
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
@@ -126,12 +128,21 @@ class DistributedMF:
         # PS item shard
         self.items = ShardedTable(cfg.num_items, cfg.dim, r, W, "hash", init, cfg.item_seed(), dev, optimizer="add")
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
-        if cfg.user_update not in ("store", "sc1", "atomic"):
-            raise ValueError(f"user_update must be 'store', 'sc1' or 'atomic', not {cfg.user_update!r}")
-        self.user_atomic = cfg.user_update == "atomic"
-        self.user_sc1 = cfg.user_update == "sc1" and dev.type == "cuda"
+        uu = cfg.user_update
+        if uu == "auto":
+            # exact user rows wherever the job has several ranks: the reference updates a
+            # user's vector sequentially inside its one worker
+            # (M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-55);
+            # one rank keeps the Hogwild kernel, its losses published by bench.py
+            uu = "atomic" if Wn > 1 else "store"
+        if uu not in ("store", "sc1", "atomic"):
+            raise ValueError(f"user_update must be 'auto', 'store', 'sc1' or 'atomic', not {cfg.user_update!r}")
+        #: the resolved user-row update mode
+        self.user_update = uu
+        self.user_atomic = uu == "atomic"
+        self.user_sc1 = uu == "sc1" and dev.type == "cuda"
         #: tiled kernel's user-row mode (ops.USER_MODES): plain / write-through / atomic deltas
-        self.user_mode = ops.USER_MODES[cfg.user_update] if dev.type == "cuda" or cfg.user_update == "atomic" else 0
+        self.user_mode = ops.USER_MODES[uu] if dev.type == "cuda" or uu == "atomic" else 0
         exchange = cfg.exchange
         if exchange == "auto":
             exchange = "ps" if cfg.force_ps_path else ("rotate" if Wn > 1 else "local")
