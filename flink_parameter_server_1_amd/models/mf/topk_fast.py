@@ -525,6 +525,8 @@ class DistributedTopK:
               exclude_ids: Optional[torch.Tensor] = None):
         wk = worker_k or K
         s, i = self.local.query(Q, wk)
+        if self.comm.world == 1 and exclude_ids is None and wk == K:
+            return s, i  # one shard, nothing to exclude: the local list is the answer (sorted, -inf pads)
         if self.comm.world > 1:
             ss = torch.cat(self.comm.all_gather(s.contiguous()), 1)
             ii = torch.cat(self.comm.all_gather(i.contiguous()), 1)
@@ -540,4 +542,7 @@ class DistributedTopK:
         so world > 1 completes synchronously."""
         if self.comm.world > 1:
             return TopKFuture(value=self.query(Q, K, worker_k, exclude_ids))
-        return self.local.query_async(Q, worker_k or K).then(lambda r: merge_top_k(r[0], r[1], K, exclude_ids))
+        wk = worker_k or K
+        if exclude_ids is None and wk == K:  # the local list is the answer (as ``query``)
+            return self.local.query_async(Q, K)
+        return self.local.query_async(Q, wk).then(lambda r: merge_top_k(r[0], r[1], K, exclude_ids))
