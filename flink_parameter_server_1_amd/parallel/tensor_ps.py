@@ -83,6 +83,8 @@ class PullPlan:
     fixed: bool = False
     #: the serve handed out the shard itself (``zero_copy_identity``), not a snapshot
     zero_copy: bool = False
+    #: static plans: ``valid.sum()`` on the device (counted once for pulls and pushes)
+    n_valid: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -180,19 +182,30 @@ class TensorPS:
         idles while the host waits (``plan()`` back to back, or a pipeline without
         lookahead)."""
         if self._lazy:
-            for k, t in self._lazy.items():
-                self._stats[k] += int(t.item())
+            for k, parts in self._lazy.items():
+                self._stats[k] += int(torch.stack(parts).sum().item())
             self._lazy = {}
         return self._stats
 
-    def _count_lazy(self, key: str, valid: torch.Tensor, bound: Optional[int] = None) -> None:
+    #: per-step device counts stay 0-dim tensors (no accumulate kernel per step), folded
+    #: into one every ``_LAZY_FOLD`` steps
+    _LAZY_FOLD = 256
+
+    def _count_lazy(self, key: str, valid: torch.Tensor, bound: Optional[int] = None,
+                    total: Optional[torch.Tensor] = None):
+        """Add ``valid.sum()`` (or the precomputed ``total``) to ``stats[key]`` without a
+        host sync; returns the device count (None while a graph is captured)."""
         if valid.is_cuda and torch.cuda.is_current_stream_capturing():
             # a captured step (core.step_graph) replays its host-side increments: count the
             # bound there (a device counter inside the graph would not be read per replay)
             self._stats[key] += valid.numel() if bound is None else bound
-            return
-        n = valid.sum()
-        self._lazy[key] = n if key not in self._lazy else self._lazy[key] + n
+            return None
+        n = valid.sum() if total is None else total
+        parts = self._lazy.setdefault(key, [])
+        parts.append(n)
+        if len(parts) >= self._LAZY_FOLD:
+            self._lazy[key] = [torch.stack(parts).sum()]
+        return n
 
     #: key space / batch ratio above which ``dedup_mode = None`` ships requests undeduplicated
     REQUEST_PLAN_RATIO = 64
@@ -381,13 +394,15 @@ class TensorPS:
             if pp.ready is not None and self.table.device.type == "cuda":
                 torch.cuda.current_stream(self.table.device).wait_event(pp.ready)
             self._stats["pulls"] += pp.n
+            n_valid = None
             if pp.valid is not None:
-                self._count_lazy("unique", pp.valid)
+                n_valid = self._count_lazy("unique", pp.valid)
             else:
                 self._stats["unique"] += pp.n_bound
             self._stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
-                            valid=pp.valid, identity=pp.identity, unique=pp.unique, ready=pp.ready)
+                            valid=pp.valid, identity=pp.identity, unique=pp.unique, ready=pp.ready,
+                            n_valid=n_valid)
         if pp.event is not None:
             if not pp.event.query():
                 self._stats["host_waits"] += 1
@@ -542,7 +557,7 @@ class TensorPS:
             recv_keys = torch.where(valid, recv_keys, torch.full_like(recv_keys, -1))
         opt = op or self.table.optimizer
         if plan.valid is not None:
-            self._count_lazy("pushes", plan.valid)
+            self._count_lazy("pushes", plan.valid, total=plan.n_valid)
         elif plan.fixed:
             self._count_lazy("pushes", recv_keys >= 0)
         else:
@@ -607,7 +622,7 @@ class TensorPS:
         if self.comm.world != 1 or getattr(self.table, "optimizer", "") != "add":
             raise ValueError("local pushes need world 1 and an additive table")
         if plan.valid is not None:  # static plan: its padding rows are never pushed
-            self._count_lazy("pushes", plan.valid)
+            self._count_lazy("pushes", plan.valid, total=plan.n_valid)
         else:
             self._stats["pushes"] += plan.n_unique
 
