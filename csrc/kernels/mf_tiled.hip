@@ -432,16 +432,18 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
   __shared__ int32_t cnt[TP3_MAXK], off[TP3_MAXK], base[TP3_MAXK];
   __shared__ int32_t s_item[3];  // level 2: lo, hi, key base of the current work item
   const int tid = threadIdx.x;
-  const int nwork = LEVEL == 1 ? 1 : wptr[NC];
-  for (int w = LEVEL == 1 ? 0 : blockIdx.x; w < nwork; w += (LEVEL == 1 ? 1 : gridDim.x)) {
+  // level 1: one work item per chunk (a grid smaller than the chunk count loops);
+  // level 2: the work items of wptr
+  const int nwork = LEVEL == 1 ? (int)((n + chunk - 1) / chunk) : wptr[NC];
+  for (int w = blockIdx.x; w < nwork; w += gridDim.x) {
     int64_t lo, hi;
     int kb, nk;
     if (LEVEL == 1) {
-      lo = (int64_t)blockIdx.x * chunk;
+      lo = (int64_t)w * chunk;
       hi = min(n, lo + chunk);
       kb = 0;
       nk = NC;
-      if (tid < nk) base[tid] = H1[(int64_t)blockIdx.x * NC + tid];  // this workgroup's run starts
+      if (tid < nk) base[tid] = H1[(int64_t)w * NC + tid];  // this chunk's run starts
     } else {
       if (tid == 0) {
         int c = 0;
@@ -830,6 +832,10 @@ FPS_API int64_t fps_tile_partition_ws_ints(int W, int T, int P) {
 // above 16k buckets always 16-bit)
 static int g_tp_h16 = 1;
 FPS_API void fps_tile_partition_set_h16(int v) { g_tp_h16 = v; }
+// most workgroups per partition launch (0 = as many as there is work): fewer, looping
+// workgroups occupy fewer CUs beside the SGD of the previous batch (A/B knob, FPS_TP_GRID)
+static int g_tp_grid = 0;
+FPS_API void fps_tile_partition_set_grid(int v) { g_tp_grid = v; }
 
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                                const int32_t* half, int R, int T, int P, int upp, int32_t* ws, int4* tmp, int32_t* ptr,
@@ -852,7 +858,8 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   if (e != hipSuccess) return (int)e;
   const int G = tp3_groups(n, KT);
   const int64_t chunk = (n + G - 1) / G;
-  const int sub = (G + 511) / 512;  // <= 512 count workgroups (2 per CU)
+  const int cmax = g_tp_grid > 0 ? min(512, g_tp_grid) : 512;
+  const int sub = (G + cmax - 1) / cmax;  // <= 512 count workgroups (2 per CU)
   const int Gc = (G + sub - 1) / sub;
   int32_t* bhist = H1 + 1024 * (int64_t)NC;  // [1 + Gc][KT]: totals, then one row per count workgroup
   // 16-bit LDS counters (<= 64 KiB at 31k buckets, the default dynamic-LDS ceiling,
@@ -877,11 +884,13 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   if (n > 0) {
     int64_t g2 = n / TP3_CH + NC + 1;  // >= the number of work items
     if (g2 > 1024) g2 = 1024;
+    if (g_tp_grid > 0 && g2 > g_tp_grid) g2 = g_tp_grid;
+    const int g1 = g_tp_grid > 0 ? min(G, g_tp_grid) : G;
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
     hipLaunchKernelGGL((tp3_scatter_kernel<L, R8>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, TMP, n, chunk, \
                        g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT)
-    if (rec8) { FPS_TP3(1, true, G, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
-    else { FPS_TP3(1, false, G, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
+    if (rec8) { FPS_TP3(1, true, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
+    else { FPS_TP3(1, false, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
     if (rec8) { FPS_TP3(2, true, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }
     else { FPS_TP3(2, false, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }
 #undef FPS_TP3

@@ -516,6 +516,9 @@ class TilePartitioner:
         h16 = os.environ.get("FPS_TP_H16")  # A/B switch of the count kernel's counter width
         if h16 is not None:
             lib.fps_tile_partition_set_h16(int(h16))
+        grid = os.environ.get("FPS_TP_GRID")  # A/B switch: most workgroups per partition launch
+        if grid is not None:
+            lib.fps_tile_partition_set_grid(int(grid))
         n = uid.numel()
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))
