@@ -329,6 +329,43 @@ def R_tile(*a):
     return R.tile_partition(*a)
 
 
+@pytest.mark.parametrize("grid", [3, 40])
+def test_tile_partition_capped_grid_loops_over_chunks(grid, monkeypatch):
+    """FPS_TP_GRID caps every partition launch's workgroups: level-1 workgroups loop over
+    the chunks, count workgroups take several chunks each -- same partition (per bucket,
+    as a multiset) as the reference."""
+    monkeypatch.setenv("FPS_TP_GRID", str(grid))
+    try:
+        NI, NU, R, n, P = 100_000, 200_000, 64, 1 << 23, 2  # 8M ratings: 32 level-1 chunks
+        T = -(-NI // R)
+        half_t = torch.tensor([NI], dtype=torch.int32)
+        g = torch.Generator().manual_seed(grid)
+        uid = torch.randint(0, NU, (n,), dtype=torch.int32, generator=g)
+        iid = torch.randint(0, NI, (n,), dtype=torch.int32, generator=g)
+        r = torch.rand(n, generator=g)
+        upp = -(-NU // P)
+        part = ops.TilePartitioner(1, [NI], R, T, DEV, rec8=True, phases=P, users_per_phase=upp)
+        ptr, rec = part.run(uid.to(DEV), iid.to(DEV), r.to(DEV))
+        p_ref, u_ref, row_ref, r_ref = R_tile(uid, iid, r, 1, half_t, R, T, P, upp)
+        assert torch.equal(ptr.cpu(), p_ref)
+        u, row, rr = part.unpack(rec, ptr)
+        bucket = torch.repeat_interleave(torch.arange(p_ref.numel() - 1), (p_ref[1:] - p_ref[:-1]).long())
+        def canon(b, uu, ro, ra):  # lexicographic (bucket, user, row, rating bits) order
+            hi = (b.long() * (1 << 21) + uu.long()) * 256 + ro.long()
+            bits = ra.float().view(torch.int32).long()
+            o = torch.argsort(bits, stable=True)
+            o = o[torch.argsort(hi[o], stable=True)]
+            return hi[o], bits[o]
+
+        gh, gb = canon(bucket, u.cpu(), row.cpu(), rr.cpu())
+        wh, wb = canon(bucket, u_ref, row_ref, r_ref)
+        assert torch.equal(gh, wh) and torch.equal(gb, wb)
+    finally:
+        from flink_parameter_server_1_amd.ops import _native
+
+        _native.require().fps_tile_partition_set_grid(0)
+
+
 def test_tile_partition_16bit_counters_survive_one_hot_bucket():
     """Every rating on ONE item: one bucket gets all n = 1M counts, four times the
     16-bit range per count workgroup -- the flushes must keep the counts exact."""
