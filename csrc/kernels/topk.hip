@@ -127,7 +127,8 @@ template <bool REG>
 __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restrict__ S, int64_t ldS, int n,
                                                            const int64_t* __restrict__ ids,
                                                            float* __restrict__ best_s, int64_t* __restrict__ best_i,
-                                                           int k) {
+                                                           int k, const uint8_t* __restrict__ only) {
+  if (only != nullptr && only[blockIdx.x] == 0) return;  // fps_topk_select: rows the wave kernel did
   constexpr int SORT = REG ? TK_SORT_R : TK_SORT;
   __shared__ uint32_t hist[TK_BINS];
   __shared__ uint32_t skey[SORT];
@@ -481,7 +482,124 @@ __global__ void __launch_bounds__(RP_NT) round_plan_kernel(const int64_t* __rest
   }
 }
 
+// ---- fresh top-k of a short row: one wave per query (the seed segment of a scan).
+// The block kernel above spent ~100 us on the 4096 x 4096 seed merge (its three radix
+// levels and the bitonic sort each cost a dozen block barriers per row).  With an empty
+// running list the merge is a plain selection, and a row of <= 4096 scores fits one
+// wave's registers: the exact k-th key by three radix levels (11 + 11 + 10 bits) over a
+// per-wave LDS histogram, the keys >= it compacted by a wave scan, and a bitonic sort
+// of those <= TS_SORT entries (key desc, then id asc -- the block kernel's order).  A row
+// whose ties at the k-th key overflow TS_SORT is left to the block kernel (redo[row]).
+constexpr int TS_NPL = 64;    // keys per lane (n <= 64 * TS_NPL = 4096)
+constexpr int TS_SORT = 256;  // candidates sorted per row (>= k + ties)
+
+__global__ void __launch_bounds__(64) topk_select_wave_kernel(const float* __restrict__ S, int64_t ldS, int n,
+                                                              const int64_t* __restrict__ ids,
+                                                              float* __restrict__ best_s,
+                                                              int64_t* __restrict__ best_i, int k,
+                                                              uint8_t* __restrict__ redo) {
+  __shared__ __attribute__((aligned(16))) uint32_t hist[TK_BINS];
+  __shared__ uint32_t skey[TS_SORT];
+  __shared__ int64_t sid[TS_SORT];
+  __shared__ uint32_t above;
+  __shared__ int bin_sel;
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const float* s = S + (int64_t)row * ldS;
+  uint32_t kr[TS_NPL];
+#pragma unroll
+  for (int q = 0; q < TS_NPL; ++q) {  // all loads in flight; j = lane + 64 q (coalesced)
+    const int j = lane + 64 * q;
+    kr[q] = j < n ? fkey(s[j]) : 0u;
+  }
+  // the exact k-th largest key T, digit by digit; need = how many keys == prefix's
+  // range are still to take below the digits fixed so far
+  uint32_t need = (uint32_t)k, prefix = 0;
+  for (int lvl = 0; lvl < 3; ++lvl) {
+    const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);
+    const int psh = lvl == 1 ? 21 : 10;
+    const uint32_t dmask = lvl == 2 ? 1023u : 2047u;
+    uint4* h4 = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+    for (int i = lane; i < TK_BINS / 4; i += 64) h4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < TS_NPL; ++q) {
+      const uint32_t kk = kr[q];
+      if (lvl == 0 || (kk >> psh) == (prefix >> psh)) atomicAdd(&hist[(kk >> sh) & dmask], 1u);
+    }
+    __syncthreads();
+    const int b = select_bin(hist, need, &above, &bin_sel);
+    prefix |= (uint32_t)b << sh;
+    need -= above;  // keys above bin b (at this level) are in for sure
+    __syncthreads();
+  }
+  const uint32_t T = prefix;  // the k-th largest key; (k - need) keys are > T
+  // compact every key >= T (wave scan of the per-lane counts)
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < TS_NPL; ++q) c += kr[q] >= T;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  const uint32_t m = __shfl(inc, 63, 64);
+  if (m > (uint32_t)TS_SORT) {  // ties at T beyond the sort: the block kernel redoes this row
+    if (lane == 0) redo[row] = 1;
+    return;
+  }
+  uint32_t o = inc - c;
+#pragma unroll
+  for (int q = 0; q < TS_NPL; ++q) {
+    if (kr[q] >= T) {
+      skey[o] = kr[q];
+      sid[o] = ids[lane + 64 * q];
+      ++o;
+    }
+  }
+  int P = 64;
+  while (P < (int)m) P <<= 1;
+  for (int i = (int)m + lane; i < P; i += 64) { skey[i] = 0u; sid[i] = INT64_MAX; }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = lane; p < P / 2; p += 64) {  // pair p: (i, i + stride)
+        const int i = 2 * stride * (p / stride) + (p % stride), j = i + stride;
+        const bool desc = (i & size) == 0;
+        const uint32_t ki = skey[i], kj = skey[j];
+        const int64_t ii = sid[i], ij = sid[j];
+        const bool i_first = ki > kj || (ki == kj && ii < ij);
+        if (desc != i_first) { skey[i] = kj; skey[j] = ki; sid[i] = ij; sid[j] = ii; }
+      }
+      __syncthreads();
+    }
+  }
+  float* bs = best_s + (int64_t)row * k;
+  int64_t* bi = best_i + (int64_t)row * k;
+  for (int i = lane; i < k; i += 64) {
+    bs[i] = kfloat(skey[i]);
+    bi[i] = skey[i] == 0u ? -1 : sid[i];
+  }
+}
+
 }  // namespace
+
+// The top-k of every row of S[B, n] into EMPTY running lists best_s / best_i [B, k]
+// (-inf / -1: a fresh scan's first segment): one wave per row (n <= 4096, k <= 128);
+// rows whose ties at the k-th key overflow its sort (redo[row] = 1, redo: B zeroed bytes)
+// are redone by the block kernel.  Same result as fps_topk_merge on empty lists.
+FPS_API int fps_topk_select(const float* S, int64_t ldS, int B, int n, const int64_t* ids, float* best_s,
+                            int64_t* best_i, int k, uint8_t* redo, void* stream) {
+  if (B <= 0 || n <= 0) return 0;
+  if (k <= 0 || k > 128 || n > 64 * TS_NPL || n < k || redo == nullptr) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(topk_select_wave_kernel, dim3(B), dim3(64), 0, st, S, ldS, n, ids, best_s, best_i, k, redo);
+  hipLaunchKernelGGL(topk_merge_kernel<true>, dim3(B), dim3(TK_NT), 0, st, S, ldS, n, ids, best_s, best_i, k,
+                     (const uint8_t*)redo);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
 
 // best_s / best_i: [B, k] sorted descending (start: -inf / -1); S: [B, n] with row stride ldS
 FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int64_t* ids, float* best_s,
@@ -490,10 +608,10 @@ FPS_API int fps_topk_merge(const float* S, int64_t ldS, int B, int n, const int6
   if (k <= 0 || k > TK_MAXK) return (int)hipErrorInvalidValue;
   if (n <= TK_NT * TK_REG)
     hipLaunchKernelGGL(topk_merge_kernel<true>, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s,
-                       best_i, k);
+                       best_i, k, (const uint8_t*)nullptr);
   else
     hipLaunchKernelGGL(topk_merge_kernel<false>, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, S, ldS, n, ids, best_s,
-                       best_i, k);
+                       best_i, k, (const uint8_t*)nullptr);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -352,7 +352,7 @@ class LempTopK:
             seed = min(N, -(-start // 32) * 32)  # fused segments start on 32-item blocks
         if seed > start:
             S = ops.score_gemm(Q, self.vecs[start:seed])
-            ops.topk_merge(S, self.ids[start:seed], best_s, best_i)
+            ops.topk_merge(S, self.ids[start:seed], best_s, best_i, fresh=state is None)
             del S
             self.buckets_scanned += 1
         if seed >= N:

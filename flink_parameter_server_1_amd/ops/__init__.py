@@ -871,9 +871,12 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
 TOPK_MAX_K = 256
 
 
-def topk_merge(S: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, best_i: torch.Tensor) -> None:
+def topk_merge(S: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, best_i: torch.Tensor,
+               fresh: bool = False) -> None:
     """Merge each row of ``S[B, n]`` (item ids ``ids[n]``) into the running top-k
-    ``best_s``/``best_i`` ``[B, k]`` (sorted descending; start -inf / -1) in place (K13)."""
+    ``best_s``/``best_i`` ``[B, k]`` (sorted descending; start -inf / -1) in place (K13).
+    ``fresh``: the running lists are still empty (-inf / -1) -- a plain selection, one
+    wave per row on the GPU for ``n <= 4096`` (``fps_topk_select``, same result)."""
     B, n = S.shape
     k = best_s.shape[1]
     if _on_gpu(S):
@@ -881,6 +884,12 @@ def topk_merge(S: torch.Tensor, ids: torch.Tensor, best_s: torch.Tensor, best_i:
             raise ValueError(f"topk_merge: k <= {TOPK_MAX_K}")
         if S.stride(1) != 1:
             raise ValueError("topk_merge: S needs unit column stride")
+        if fresh and k <= 128 and k <= n <= 4096:
+            redo = torch.zeros(B, dtype=torch.uint8, device=S.device)
+            N.check(N.require().fps_topk_select(S.data_ptr(), S.stride(0), B, n, _c(ids.long()).data_ptr(),
+                                                _c(best_s).data_ptr(), _c(best_i).data_ptr(), k, redo.data_ptr(),
+                                                N.stream_ptr(S.device)), "topk_select")
+            return
         N.check(N.require().fps_topk_merge(S.data_ptr(), S.stride(0), B, n, _c(ids.long()).data_ptr(),
                                            _c(best_s).data_ptr(), _c(best_i).data_ptr(), k, N.stream_ptr(S.device)),
                 "topk_merge")

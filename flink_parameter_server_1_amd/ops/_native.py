@@ -67,6 +67,7 @@ _SIGNATURES = {
     "fps_lock_acquire": [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp],
     "fps_lock_release": [c_vp, c_vp, c_i64, c_vp, c_vp],
     "fps_topk_merge": [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    "fps_topk_select": [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "fps_bucketize": [c_vp, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp],
     "fps_mf_sgd_local": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],
     "fps_mf_sgd_pulled": [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_f32, c_f32, c_int, c_vp],

@@ -554,3 +554,32 @@ def test_mf_sgd_tiled_delta_mode_equals_in_place(phases, rec8):
     assert torch.equal(delta[ni - 600:], torch.zeros_like(delta[ni - 600:]))
     torch.testing.assert_close(U2, U1, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(I0 + delta, I1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,k", [(4096, 100), (4096, 128), (1000, 100), (300, 37)])
+def test_topk_select_fresh_equals_block_merge(n, k):
+    """``topk_merge(fresh=True)`` (one wave per row, ``fps_topk_select``) == the block
+    merge into empty lists, bit for bit: distinct scores, ties at the k-th key broken by
+    smaller id, and rows whose ties overflow the wave's sort (redone by the block kernel)."""
+    g = torch.Generator(device=DEV).manual_seed(n + k)
+    B = 777
+    S = torch.randn(B, n, device=DEV, generator=g)
+    S[1::5] = torch.round(S[1::5] * 4) / 4  # heavy ties, some at the k-th key
+    # > 256 keys tied at the k-th key: the wave's sort cannot hold them, the block kernel
+    # redoes those rows (within its own exact range, < 924 ties)
+    a, t = k // 2, min(600, n - k // 2)
+    S[2::9] = -torch.rand(S[2::9].shape, device=DEV, generator=g) - 2.0
+    S[2::9, :a] = 5.0
+    S[2::9, a:a + t] = 1.0
+    S[3, : n // 2] = float("-inf")
+    ids = torch.randperm(10 * n, device=DEV, generator=g)[:n]
+    out = []
+    for fresh in (True, False):
+        bs = torch.full((B, k), float("-inf"), device=DEV)
+        bi = torch.full((B, k), -1, dtype=torch.long, device=DEV)
+        ops.topk_merge(S, ids, bs, bi, fresh=fresh)
+        out.append((bs, bi))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    ref = torch.topk(S, k, dim=1).values
+    assert torch.equal(out[0][0], ref)
