@@ -80,11 +80,12 @@ __global__ void __launch_bounds__(256) ht_assign_kernel(const int32_t* __restric
   constexpr int TILE = 256 * HT_AU;
   for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < n; t0 += (int64_t)gridDim.x * TILE) {  // block-uniform
     uint32_t fm = 0;  // which of this thread's HT_AU requests are fresh (coalesced: stride 256)
+    uint8_t fv[HT_AU];  // unconditional clamped loads, all in flight (a guarded one waited each)
 #pragma unroll
-    for (int j = 0; j < HT_AU; ++j) {
-      const int64_t b = t0 + j * 256 + threadIdx.x;
-      if (b < n && fresh[b]) fm |= 1u << j;
-    }
+    for (int j = 0; j < HT_AU; ++j) fv[j] = fresh[min(t0 + j * 256 + threadIdx.x, n - 1)];
+#pragma unroll
+    for (int j = 0; j < HT_AU; ++j)
+      if (t0 + j * 256 + threadIdx.x < n && fv[j]) fm |= 1u << j;
     const int c = __popc(fm);
     int x = c;  // inclusive wave scan
 #pragma unroll

@@ -358,21 +358,33 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
   const int64_t base = (int64_t)blockIdx.x * blockDim.x * DEDUP_ITEMS;
   int32_t slot_l[DEDUP_ITEMS];
   int dd[DEDUP_ITEMS];
+  // loads first, all in flight (clamped indices, masked after: a load guarded by
+  // b < n compiled to a branch and a full wait per item), then the slot allocation
+  int32_t kv[DEDUP_ITEMS];
+#pragma unroll
+  for (int it = 0; it < DEDUP_ITEMS; ++it) kv[it] = keys[min(base + (int64_t)it * blockDim.x + threadIdx.x, n - 1)];
+  uint32_t ov[DEDUP_ITEMS];  // dense: the claim's owner; hashed: the hash slot word
+  if (HASHED && hslot == nullptr) {
+#pragma unroll
+    for (int it = 0; it < DEDUP_ITEMS; ++it) ov[it] = 0x80000000u;
+  } else {
+#pragma unroll
+    for (int it = 0; it < DEDUP_ITEMS; ++it) {
+      const int64_t bc = min(base + (int64_t)it * blockDim.x + threadIdx.x, n - 1);
+      if (HASHED) ov[it] = (uint32_t)hslot[bc];
+      else ov[it] = 0xffffffffu - (uint32_t)(map[kv[it]] & 0xffffffffull);
+    }
+  }
 #pragma unroll
   for (int it = 0; it < DEDUP_ITEMS; ++it) {
     const int64_t b = base + (int64_t)it * blockDim.x + threadIdx.x;
     bool own = false;
     int d = 0;
     if (b < n) {
-      const int32_t k = keys[b];
       int32_t local;
-      key_dest(k, W, part_kind, block, d, local);
-      if (HASHED) {
-        own = hslot == nullptr || hslot[b] < 0;  // no hslot: every request owns its own slot b
-      } else {
-        const uint32_t owner = 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull);
-        own = owner == (uint32_t)b;
-      }
+      key_dest(kv[it], W, part_kind, block, d, local);
+      // hashed without hslot: every request owns its own slot b
+      own = HASHED ? (int32_t)ov[it] < 0 : ov[it] == (uint32_t)b;
     }
     dd[it] = own ? d : -1;
     slot_l[it] = wave_alloc(own, d, lds_cnt);  // LDS atomics: cheap
@@ -386,7 +398,7 @@ __global__ void __launch_bounds__(256) dedup_assign_kernel(const int32_t* __rest
     if (dd[it] < 0) continue;
     const int64_t b = base + (int64_t)it * blockDim.x + threadIdx.x;
     // dense: indexed by the owner's request index; hashed: by the key's hash slot
-    owner_slot[HASHED && hslot != nullptr ? (int64_t)(hslot[b] & 0x7fffffff) : b] = lds_base[dd[it]] + slot_l[it];
+    owner_slot[HASHED && hslot != nullptr ? (int64_t)(ov[it] & 0x7fffffffu) : b] = lds_base[dd[it]] + slot_l[it];
   }
 }
 
@@ -414,18 +426,30 @@ __global__ void dedup_resolve_kernel(const int32_t* __restrict__ keys, const int
     int64_t at[DEDUP_HU];
     bool own[DEDUP_HU], act[DEDUP_HU];
     int d[DEDUP_HU];
+    // unconditional loads of clamped indices (masked after): guarded loads compiled to a
+    // branch and a full wait each
+    int32_t kv[DEDUP_HU];
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) kv[u] = keys[min(b0 + u * stride, n - 1)];
+    uint64_t mv[DEDUP_HU];
+    int32_t hv[DEDUP_HU];
+#pragma unroll
+    for (int u = 0; u < DEDUP_HU; ++u) {
+      if (HASHED) hv[u] = hslot != nullptr ? hslot[min(b0 + u * stride, n - 1)] : 0;
+      else mv[u] = map[kv[u]];
+    }
 #pragma unroll
     for (int u = 0; u < DEDUP_HU; ++u) {
       const int64_t b = b0 + u * stride;
       act[u] = b < n;
-      const int32_t k = act[u] ? keys[b] : 0;
+      const int32_t k = act[u] ? kv[u] : 0;
       key_dest(k, W, part_kind, block, d[u], local[u]);
       if (HASHED) {
-        const int32_t hs = !act[u] ? 0 : (hslot != nullptr ? hslot[b] : (int32_t)((uint32_t)b | 0x80000000u));
+        const int32_t hs = !act[u] ? 0 : (hslot != nullptr ? hv[u] : (int32_t)((uint32_t)b | 0x80000000u));
         at[u] = hs & 0x7fffffff;
         own[u] = hs < 0;
       } else {
-        const uint32_t owner = act[u] ? 0xffffffffu - (uint32_t)(map[k] & 0xffffffffull) : 0u;
+        const uint32_t owner = act[u] ? 0xffffffffu - (uint32_t)(mv[u] & 0xffffffffull) : 0u;
         at[u] = owner;
         own[u] = owner == (uint32_t)b;
       }

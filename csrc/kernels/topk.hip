@@ -142,11 +142,13 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
   const uint32_t cap = REG ? (uint32_t)(TK_SORT_R - k) : (uint32_t)TK_CAP;  // candidates kept
   uint32_t kr[REG ? TK_REG : 1];
   if constexpr (REG) {
+    // all loads in flight at once: unconditional loads of a clamped index, masked after
+    // (a guarded load compiled to a branch and a full wait per load: 16 round trips)
+    float sv[TK_REG];
 #pragma unroll
-    for (int q = 0; q < TK_REG; ++q) {  // all loads in flight at once
-      const int j = tid + q * TK_NT;
-      kr[q] = j < n ? fkey(s[j]) : 0u;
-    }
+    for (int q = 0; q < TK_REG; ++q) sv[q] = s[min(tid + q * TK_NT, n - 1)];
+#pragma unroll
+    for (int q = 0; q < TK_REG; ++q) kr[q] = tid + q * TK_NT < n ? fkey(sv[q]) : 0u;
   }
   // body(j, key) over this thread's entries of the row
   auto for_keys = [&](auto&& body) {

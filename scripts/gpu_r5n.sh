@@ -3,7 +3,7 @@
 # LEMP + MF/top-K benches; the capped-grid partition test.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r5n
+O=gpurun_out/r5o
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "topk_select or capped_grid" -x -v --timeout 300 --timeout-method thread > $O/tests_k.log 2>&1 || { tail -40 $O/tests_k.log; exit 1; }
 grep -cE "PASSED" $O/tests_k.log
