@@ -66,18 +66,6 @@ __device__ __forceinline__ float4 ld4(const void* rows, int64_t row, int D, int 
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// a 4-aligned in-range quad (D % 4 == 0, c + 3 < D): one 16-B (8-B bf16) load, no branch
-template <bool BF16>
-__device__ __forceinline__ float4 ld4_aligned(const void* rows, int64_t row, int D, int c) {
-  const int64_t o = row * D + c;
-  if (BF16) {
-    const uint2 u = *(const uint2*)((const uint16_t*)rows + o);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-                       __uint_as_float(u.y & 0xffff0000u));
-  }
-  return *(const float4*)((const float*)rows + o);
-}
-
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // C/D map of the 32x32 MFMA: lane l, reg r -> row (col = l & 31)
@@ -251,10 +239,6 @@ __global__ void __launch_bounds__(NT) sgns_block_kernel(const void* __restrict__
 // profiles/r1_w2v_v4.md).  The dH run reduction gathers a tile column's 32
 // rows in registers with one half-wave swap instead of a wave-private LDS tile,
 // and dN = G^T H is a 32x32x2 MFMA whose rows 16-31 are zero.
-// FPS_SGNS_GUARDED_LOADS=1: the round-4 staging loads (guarded, one wait each) -- A/B knob
-#ifndef FPS_SGNS_GUARDED_LOADS
-#define FPS_SGNS_GUARDED_LOADS 0
-#endif
 constexpr int K4 = 16;
 constexpr int NT4 = 512;
 constexpr int NW4 = NT4 / 64;
@@ -342,40 +326,16 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
       }
       {
         float4 v[RPW][2];
-        if (!FPS_SGNS_GUARDED_LOADS && (D & 3) == 0) {
-          // every load unconditional (row and column clamped, the value masked after): a
-          // guarded load compiled to a branch and a full wait each -- 12 round trips
 #pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            const int r = wave + NW4 * j;
-            const bool is_h = r < M;
-            const int32_t rr = is_h ? pc[r] : (sb == 0 ? pn[r - M] : -1);  // N rows: once per group
+        for (int j = 0; j < RPW; ++j) {
+          const int r = wave + NW4 * j;
+          const bool is_h = r < M;
+          const int32_t rr = is_h ? pc[r] : (sb == 0 ? pn[r - M] : -1);  // N rows: once per group
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int c = lane * 4 + 256 * h;
-              v[j][h] = ld4_aligned<BF16>(is_h ? rows_in : rows_out, rr < 0 ? 0 : rr, D, min(c, D - 4));
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            const int r = wave + NW4 * j;
-            const int32_t rr = r < M ? pc[r] : (sb == 0 ? pn[r - M] : -1);
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-              if (rr < 0 || lane * 4 + 256 * h >= D) v[j][h] = make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            const int r = wave + NW4 * j;
-            const bool is_h = r < M;
-            const int32_t rr = is_h ? pc[r] : (sb == 0 ? pn[r - M] : -1);  // N rows: once per group
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int c = lane * 4 + 256 * h;
-              v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+          for (int h = 0; h < 2; ++h) {
+            const int c = lane * 4 + 256 * h;
+            v[j][h] = (rr >= 0 && c < Dp) ? ld4<BF16>(is_h ? rows_in : rows_out, rr, D, c)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
 #pragma unroll
@@ -418,7 +378,6 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
         constexpr int KP = (M + NW4 - 3) / (NW4 - 2), JP = 5;
         const int w2 = wave - 2;
         float ov[KP][JP];
-#if FPS_SGNS_GUARDED_LOADS
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
           const int m = w2 + (NW4 - 2) * k;
@@ -428,22 +387,6 @@ __global__ void __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(4, 8))
             ov[k][j] = (m < npairs && c < D) ? ld1<BF16>(rows_out, (int64_t)po[m] * D + c) : 0.f;
           }
         }
-#else
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {  // unconditional clamped loads, masked after (see the staging)
-          const int m = w2 + (NW4 - 2) * k;
-          const int64_t row = m < npairs ? po[m] : 0;
-#pragma unroll
-          for (int j = 0; j < JP; ++j) ov[k][j] = ld1<BF16>(rows_out, row * D + min(lane + 64 * j, D - 1));
-        }
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-          const int m = w2 + (NW4 - 2) * k;
-#pragma unroll
-          for (int j = 0; j < JP; ++j)
-            if (m >= npairs || lane + 64 * j >= D) ov[k][j] = 0.f;
-        }
-#endif
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
           const int m = w2 + (NW4 - 2) * k;
