@@ -61,22 +61,37 @@ def _write_stamp(target: str, digest: str):
 PER_FILE_FLAGS = {"score_bf16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
-def build_kernels(force: bool = False, verbose: bool = True, variant: str = None, defines=()) -> str:
+def build_kernels(force: bool = False, verbose: bool = True, variant: str = None, defines=(), rev: str = None) -> str:
     """One object per source (compiled in parallel, each with its own digest stamp:
     a change rebuilds only its file), linked into one shared object.  ``variant`` +
     ``defines`` (``NAME=VALUE``): an A/B build of the library with extra macros, into
-    ``_lib/ab/<variant>/libfps_kernels.so`` (select it with ``FPS_KERNELS_SO``)."""
+    ``_lib/ab/<variant>/libfps_kernels.so`` (select it with ``FPS_KERNELS_SO``);
+    ``rev``: the variant's kernel sources as of that git revision (an A/B against
+    earlier code)."""
     from concurrent.futures import ThreadPoolExecutor
 
     out = OUT if variant is None else os.path.join(OUT, "ab", variant)
     os.makedirs(out, exist_ok=True)
     objdir = os.path.join(out, "obj")
     os.makedirs(objdir, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    kdir = os.path.join(CSRC, "kernels")
+    if rev is not None:
+        if variant is None:
+            raise ValueError("rev needs a variant (the main library is always built from the working tree)")
+        kdir = os.path.join(out, "src")
+        os.makedirs(kdir, exist_ok=True)
+        root = os.path.dirname(CSRC)
+        names = subprocess.run(["git", "-C", root, "ls-tree", "--name-only", rev, "csrc/kernels/"], check=True,
+                               capture_output=True, text=True).stdout.split()
+        for nm in names:
+            body = subprocess.run(["git", "-C", root, "show", f"{rev}:{nm}"], check=True, capture_output=True).stdout
+            with open(os.path.join(kdir, os.path.basename(nm)), "wb") as f:
+                f.write(body)
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(kdir, "*.h")))
     target = os.path.join(out, "libfps_kernels.so")
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics", "-Wno-unused-result",
-             "-I", os.path.join(CSRC, "kernels")] + [f"-D{d}" for d in defines]
+             "-I", kdir] + [f"-D{d}" for d in defines]
 
     def obj(src):
         extra = PER_FILE_FLAGS.get(os.path.basename(src), [])
@@ -150,13 +165,14 @@ def main(argv=None):
     ap.add_argument("--only", choices=["kernels", "host"])
     ap.add_argument("--variant", default=None, help="A/B build name (with -D NAME=VALUE macros)")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--rev", default=None, help="--variant: kernel sources as of this git revision")
     ap.add_argument("--asan-selftest", action="store_true",
                     help="build + run the host runtime self-test under ASan/UBSan, then exit")
     a = ap.parse_args(argv)
     if a.asan_selftest:
         return asan_selftest()
     if a.variant:
-        print(build_kernels(a.force, variant=a.variant, defines=a.defines))
+        print(build_kernels(a.force, variant=a.variant, defines=a.defines, rev=a.rev))
         return 0
     if a.only in (None, "kernels"):
         print(build_kernels(a.force))
