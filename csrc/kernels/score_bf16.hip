@@ -41,7 +41,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int SB_WAVES = 4;     // waves per workgroup
-constexpr int SB_ITEMS = 1024;  // items per workgroup (32 MFMA blocks of 32)
+constexpr int SB_ITEMS = 1024;  // most items per workgroup (32 MFMA blocks of 32); fewer on short segments
 constexpr int SB_SLOTS = 16;    // LDS candidate slots per (query block, lane)
 
 __device__ __forceinline__ uint32_t sb_key(float f) {  // order-preserving float -> uint32 (as topk.hip)
@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xbm,
     float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
     const int32_t* __restrict__ qf, const float* __restrict__ qbf, const float2* __restrict__ cb,
-    int32_t* __restrict__ stats, const int32_t* __restrict__ gate) {
+    int32_t* __restrict__ stats, const int32_t* __restrict__ gate, int ipw) {
   constexpr int S = D / 16;   // k-steps of 16; also 16-B loads per lane per row
   // COORD gate (device flag, nullable): off when the bound stopped paying on earlier
   // segments of this scan (coord_gate_kernel) -- the bound costs VALU per block pair
@@ -92,12 +92,12 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   constexpr int GQ = SB_WAVES * WQ;
   __shared__ float red[SB_WAVES];
   const int nqt = (B + GQ - 1) / GQ;
-  const int nit = (N + SB_ITEMS - 1) / SB_ITEMS;
+  const int nit = (N + ipw - 1) / ipw;  // ipw: items per workgroup, a multiple of 64, <= SB_ITEMS
   // query tiles fastest: the workgroups reading one item range are consecutive
   // logical ids, i.e. on one XCD (one L2 holds the range)
   const int wg = xcd_remap(blockIdx.x, nqt * nit);
   const int qt = wg % nqt, it = wg / nqt;
-  const int i_begin = it * SB_ITEMS, i_end = min(N, i_begin + SB_ITEMS);
+  const int i_begin = it * ipw, i_end = min(N, i_begin + ipw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
 
@@ -398,6 +398,11 @@ FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, i
 // COORD bound (optional, all or none): qf [B] focus coordinates, qbf [B] = q_f / |q|,
 // cb [N / 32][D] float2 coordinate ranges of the 32-item blocks (N a multiple of 32
 // or the last block's range over its items); stats (optional) = 2 counters.
+// fewest workgroups a scorer launch aims for (items per workgroup shrink to reach it);
+// 0: always SB_ITEMS items per workgroup (A/B knob, FPS_SB_MIN_WGS)
+static int g_sb_min_wgs = 1024;
+FPS_API void fps_score_set_min_wgs(int v) { g_sb_min_wgs = v; }
+
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xbm, float margin, float slack,
                                   int64_t* cand_pos, int32_t* cnt, int cap, const int32_t* qf, const float* qbf,
@@ -405,20 +410,26 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
   if (B <= 0 || N <= 0) return 0;
   if (k <= 0 || cap <= 0 || qlen == nullptr || xbm == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t nit = (N + SB_ITEMS - 1) / SB_ITEMS;
   const bool coord = qf != nullptr && qbf != nullptr && cb != nullptr;
+  // items per workgroup: 1024, halved (down to one 64-item stage) while the launch would
+  // have fewer than g_sb_min_wgs workgroups -- the short first segments of a geometric
+  // scan ran on 32-256 workgroups, 98 / 70 / 63 / 56 us on a mostly idle GPU
+  // (profiles/r5_topk_segments.md)
 #define FPS_SB(D_, QB_, MASK_)                                                                              \
   {                                                                                                         \
     const int64_t nqt = (B + SB_WAVES * 32 * QB_ - 1) / (SB_WAVES * 32 * QB_);                              \
+    int ipw = SB_ITEMS;                                                                                     \
+    while (ipw > 64 && nqt * ((N + ipw - 1) / ipw) < g_sb_min_wgs) ipw >>= 1;                             \
+    const int64_t nit = (N + ipw - 1) / ipw;                                                                \
     if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
     if (coord)                                                                                              \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true>), dim3((unsigned)(nqt * nit)),    \
                          dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
-                         cap, qf, qbf, cb, stats, gate);                                                    \
+                         cap, qf, qbf, cb, stats, gate, ipw);                                               \
     else                                                                                                    \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false>), dim3((unsigned)(nqt * nit)),   \
                          dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
-                         cap, qf, qbf, cb, stats, gate);                                                    \
+                         cap, qf, qbf, cb, stats, gate, ipw);                                               \
   }
   // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4
   // blocks with branch or mask epilogues, same-box A/B, profiles/r2_bf16_topk.md)

@@ -1013,6 +1013,9 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
             check_index(qf, D, "score_filter_bf16 qf")
         qf, qbf, cb = _c(qf), _c(qbf.float()), _c(cb.float())
     slack = 1.0 + 1e-4 + D * 2.4e-7
+    mw = os.environ.get("FPS_SB_MIN_WGS")  # A/B switch: fewest workgroups per scorer launch (0: 1024 items each)
+    if mw is not None:
+        N.require().fps_score_set_min_wgs(int(mw))
     N.check(N.require().fps_score_filter_bf16(
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
         _c(qlen.float()).data_ptr(), _c(xbm.float()).data_ptr(), bf16_score_margin(D), slack,
