@@ -250,9 +250,14 @@ def test_capacity_table_bounded_staleness_equals_host_synchronous_world(backend,
     W = _world(backend) if backend == "nccl" else 8
     res = _run(backend, _pair_emb, W, optimizer)
     ref = run_virtual(_pair_emb, W, optimizer, mode="sync")
+    # adagrad: a hot key's accumulated squares differ in the last bits between runs (float
+    # atomics sum its per-source gradients in any order), and 1 / sqrt(G) amplifies that in
+    # its later steps (measured: 2 of 16M elements at 2e-5); a lost or doubled push moves a
+    # row by ~lr = 5e-2
+    tol = dict(rtol=1e-3, atol=1e-4) if optimizer == "adagrad" else dict(rtol=1e-4, atol=1e-5)
     for (wa, l0a, l1a, ra), (wb, l0b, l1b, rb) in zip(res, ref):
         assert ra == rb and l1a < l0a
-        torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(wa, wb, **tol)
 
 
 def _graph_step(comm, graph):
