@@ -492,10 +492,15 @@ __global__ void __launch_bounds__(RP_NT) round_plan_kernel(const int64_t* __rest
 // per-wave LDS histogram, the keys >= it compacted by a wave scan, and a bitonic sort
 // of those <= TS_SORT entries (key desc, then id asc -- the block kernel's order).  A row
 // whose ties at the k-th key overflow TS_SORT is left to the block kernel (redo[row]).
+// waves per SIMD the register allocation must allow: 3 (168 VGPRs, no spills; 197 and
+// two waves unconstrained) -- A/B knob
+#ifndef FPS_TS_WPE
+#define FPS_TS_WPE 3
+#endif
 constexpr int TS_NPL = 64;    // keys per lane (n <= 64 * TS_NPL = 4096)
 constexpr int TS_SORT = 256;  // candidates sorted per row (>= k + ties)
 
-__global__ void __launch_bounds__(64) topk_select_wave_kernel(const float* __restrict__ S, int64_t ldS, int n,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FPS_TS_WPE, 8))) topk_select_wave_kernel(const float* __restrict__ S, int64_t ldS, int n,
                                                               const int64_t* __restrict__ ids,
                                                               float* __restrict__ best_s,
                                                               int64_t* __restrict__ best_i, int k,
@@ -509,12 +514,13 @@ __global__ void __launch_bounds__(64) topk_select_wave_kernel(const float* __res
   const float* s = S + (int64_t)row * ldS;
   uint32_t kr[TS_NPL];
   // all loads in flight (j = lane + 64 q, coalesced): unconditional loads of a clamped
-  // index, masked after -- a guarded load compiled to a branch and a full wait per key
-  float sv[TS_NPL];
+  // index, masked after -- a guarded load compiled to a branch and a full wait per key.
+  // The raw bits land in kr itself (a separate float array doubled the live registers)
+  const uint32_t* su = reinterpret_cast<const uint32_t*>(s);
 #pragma unroll
-  for (int q = 0; q < TS_NPL; ++q) sv[q] = s[min(lane + 64 * q, n - 1)];
+  for (int q = 0; q < TS_NPL; ++q) kr[q] = su[min(lane + 64 * q, n - 1)];
 #pragma unroll
-  for (int q = 0; q < TS_NPL; ++q) kr[q] = lane + 64 * q < n ? fkey(sv[q]) : 0u;
+  for (int q = 0; q < TS_NPL; ++q) kr[q] = lane + 64 * q < n ? fkey(__uint_as_float(kr[q])) : 0u;
   // the exact k-th largest key T, digit by digit; need = how many keys == prefix's
   // range are still to take below the digits fixed so far
   uint32_t need = (uint32_t)k, prefix = 0;
