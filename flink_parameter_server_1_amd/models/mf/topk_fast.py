@@ -74,6 +74,10 @@ class LempTopK:
         self.break_check = int(os.environ.get("FPS_TOPK_BREAK_CHECK", "8"))
         #: fused path: segments double from ``seed_items`` up to ``max_segment`` items
         self.geometric = True
+        #: fused path: each segment is ``growth - 1`` times the items scanned before it (2 =
+        #: doubling); a segment passes ~k ln(growth) candidates per query, and every segment
+        #: costs a re-score + merge launch pair whatever its size (FPS_TOPK_GROWTH: A/B knob)
+        self.growth = int(os.environ.get("FPS_TOPK_GROWTH", "2"))
         self.overflows = 0
         self._suffix = None  # False once rows were updated out of order
         #: fused GPU scan on bf16 MFMA (``ops.score_filter_bf16``: candidates within a
@@ -374,7 +378,7 @@ class LempTopK:
             cuts |= {b for b in range(self.bucket, N, self.bucket) if b > seed}
         while c < N:
             cuts.add(c)
-            c += min(c, cap_seg)
+            c += min(c * (self.growth - 1), cap_seg)
         bounds = sorted(cuts) + [N]
         cap = ops.TOPK_CAND_CAP
         ck = torch.empty((B, cap), dtype=torch.int32, device=dev)
