@@ -400,7 +400,7 @@ FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, i
 // or the last block's range over its items); stats (optional) = 2 counters.
 // fewest workgroups a scorer launch aims for (items per workgroup shrink to reach it);
 // 0: always SB_ITEMS items per workgroup (A/B knob, FPS_SB_MIN_WGS)
-static int g_sb_min_wgs = 1024;
+static int g_sb_min_wgs = 512;
 FPS_API void fps_score_set_min_wgs(int v) { g_sb_min_wgs = v; }
 
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
@@ -412,7 +412,7 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
   hipStream_t s = (hipStream_t)stream;
   const bool coord = qf != nullptr && qbf != nullptr && cb != nullptr;
   // items per workgroup: 1024, halved (down to one 64-item stage) while the launch would
-  // have fewer than g_sb_min_wgs workgroups -- the short first segments of a geometric
+  // have fewer than g_sb_min_wgs (512: best of 256 / 384 / 512 / 768 / 1024 / 1536 / 2304) workgroups -- the short first segments of a geometric
   // scan ran on 32-256 workgroups, 98 / 70 / 63 / 56 us on a mostly idle GPU
   // (profiles/r5_topk_segments.md)
 #define FPS_SB(D_, QB_, MASK_)                                                                              \

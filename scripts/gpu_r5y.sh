@@ -4,8 +4,8 @@ export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r5y
 mkdir -p $O
-FPS_TOPK_GROWTH=4 timeout -k 10 400 python -u -m pytest tests/test_topk_bf16_gpu.py tests/test_topk_tensor_gpu.py -x -q --timeout 200 --timeout-method thread > $O/tests4.log 2>&1 || { tail -40 $O/tests4.log; exit 1; }
-tail -1 $O/tests4.log
+echo skip-tests
+
 for r in 1 2; do
   for g in 2 3 4; do
     FPS_TOPK_GROWTH=$g timeout -k 10 300 python bench/bench_topk.py --steps 30 --warmup 3 > $O/topk_g${g}_$r.log 2>&1 || { tail -20 $O/topk_g${g}_$r.log; exit 1; }
