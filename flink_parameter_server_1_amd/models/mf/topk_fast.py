@@ -74,10 +74,28 @@ class LempTopK:
         self.break_check = int(os.environ.get("FPS_TOPK_BREAK_CHECK", "8"))
         #: fused path: segments double from ``seed_items`` up to ``max_segment`` items
         self.geometric = True
-        #: fused path: each segment is ``growth - 1`` times the items scanned before it (2 =
-        #: doubling); a segment passes ~k ln(growth) candidates per query, and every segment
-        #: costs a re-score + merge launch pair whatever its size (FPS_TOPK_GROWTH: A/B knob)
-        self.growth = int(os.environ.get("FPS_TOPK_GROWTH", "2"))
+        #: fused path: each segment is ``growth - 1`` times the items scanned before it.  A
+        #: segment passes ~k ln(growth) candidates per query that the length bound does not
+        #: cut, and every segment costs a re-score + merge launch pair whatever its size: with
+        #: long-tailed item lengths (the longest items 1.5x+ the median) the bound cuts the
+        #: late segments and fewer, larger segments win (growth 4: LEMP 6.4 -> 6.8e6 q/s);
+        #: with near-equal lengths (random-init factors) doubling keeps the candidate lists
+        #: short (MF + top-K 2.2 vs 2.1e6; profiles/r5_topk_growth_ab.txt).  FPS_TOPK_GROWTH
+        #: overrides.
+        env_growth = os.environ.get("FPS_TOPK_GROWTH")
+        if env_growth is not None:
+            self.growth = int(env_growth)
+        else:
+            n = self.lengths.numel()
+            spread = 1.0
+            if n > 2 * self.seed_items:
+                pair = self.lengths[torch.tensor([self.seed_items, n // 2], device=self.lengths.device)].tolist()
+                spread = pair[0] / max(pair[1], 1e-30)
+            # (COORD / LC choose their bound per segment from its length spread, which the
+            # short doubling segments keep small)
+            from .pruning import COORD, LC
+            coordish = isinstance(strategy, (COORD, LC))
+            self.growth = 4 if spread > 1.5 and not coordish else 2
         self.overflows = 0
         self._suffix = None  # False once rows were updated out of order
         #: fused GPU scan on bf16 MFMA (``ops.score_filter_bf16``: candidates within a
