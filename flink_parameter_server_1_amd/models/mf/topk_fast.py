@@ -46,7 +46,8 @@ class LempTopK:
     #: largest fused segment (segments double from ``seed_items``)
     max_segment = 1 << 19
 
-    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536, strategy=None):
+    def __init__(self, item_ids: torch.Tensor, item_vecs: torch.Tensor, bucket_size: int = 65536, strategy=None,
+                 growth: Optional[int] = None):
         """``strategy`` (a ``pruning`` LEMP strategy; None = LENGTH): the bounds the
         device scan applies per block of 32 items before scoring.  LENGTH (and LI /
         INCR, whose incremental per-candidate bound has no work to skip on MFMA
@@ -85,6 +86,8 @@ class LempTopK:
         env_growth = os.environ.get("FPS_TOPK_GROWTH")
         if env_growth is not None:
             self.growth = int(env_growth)
+        elif growth is not None:  # the caller knows its index (e.g. one updated in place: 2)
+            self.growth = int(growth)
         else:
             n = self.lengths.numel()
             spread = 1.0
