@@ -38,6 +38,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Optional
 
+import os
+
 import torch
 import torch.distributed
 
@@ -278,6 +280,7 @@ class DistributedMF:
             self._known = torch.zeros(cfg.num_items, dtype=torch.int32, device=dev)
             self._known_count = torch.zeros(1, dtype=torch.int32, device=dev)
             self._neg_counter = 0
+        self._part_delay_us = float(os.environ.get("FPS_PART_DELAY_US", "0"))
         self.updates = 0
         #: observability: ``timer`` (a ``utils.metrics.StageTimer``, set by
         #: bench.py --metrics-jsonl) times every stage with HIP events; the counters
@@ -406,6 +409,12 @@ class DistributedMF:
         main = torch.cuda.current_stream(self.U.device)
         self._side.wait_stream(main)  # inputs written, and this buffer's previous SGD done
         with torch.cuda.stream(self._side):
+            if self._part_delay_us > 0:
+                # A/B knob (FPS_PART_DELAY_US): let the SGD launch that starts with this
+                # partition fill the CUs first
+                from ...parallel.vworld import _Sleep
+
+                _Sleep.us(self.U.device, self._part_delay_us)
             if self._presence is not None:
                 seen.zero_()
             with stage("mf.partition", self.timer):  # timed on the side stream
