@@ -60,12 +60,22 @@ static FastDiv make_fastdiv(int d) {
 
 struct TileGeo {
   int W, R, T;
-  FastDiv dW, dR, dU;
+  FastDiv dW, dR, dU, dT, d2W;
   const int32_t* half;
 };
 
 static TileGeo make_geo(int W, const int32_t* half, int R, int T, int upp) {
-  return TileGeo{W, R, T, make_fastdiv(W), make_fastdiv(R), make_fastdiv(upp), half};
+  return TileGeo{W, R, T, make_fastdiv(W), make_fastdiv(R), make_fastdiv(upp), make_fastdiv(T), make_fastdiv(2 * W),
+                 half};
+}
+
+// the global item of a record from its bucket and row in block (tile_bucket's inverse)
+__device__ __forceinline__ int32_t tile_item(int bucket, int32_t row_in_block, const TileGeo& g) {
+  const int32_t a = g.dT.div(bucket);                // user phase * 2W + 2q + h
+  const int32_t b = a - g.d2W.div(a) * (2 * g.W);    // 2q + h
+  const int q = b >> 1;
+  const int32_t loc = row_in_block + ((b & 1) ? g.half[q] : 0);
+  return loc * g.W + q;
 }
 
 __device__ __forceinline__ void tile_bucket(int32_t i, int32_t u, const TileGeo& g, int& bucket, int32_t& row) {
@@ -286,7 +296,6 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
           } else {
             atomicAdd(hb + bk, 1);
           }
-          if (seen != nullptr) seen[iv[j]] = 1;
         }
       }
       if constexpr (H16) {
@@ -426,7 +435,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ cptr,
                                                            const int32_t* __restrict__ wptr,
                                                            const int32_t* __restrict__ H1,
-                                                           void* __restrict__ out) {
+                                                           void* __restrict__ out, uint8_t* __restrict__ seen) {
   constexpr int E = TP3_B / 1024;
   __shared__ int4 srt[TP3_B];
   __shared__ int32_t cnt[TP3_MAXK], off[TP3_MAXK], base[TP3_MAXK];
@@ -516,6 +525,15 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         } else if (LEVEL == 1) tp_st<true>(reinterpret_cast<tp_i4*>(out) + o, tp_i4{x.x, x.y, x.z, x.w});
         else if (REC8) tp_st<true>(reinterpret_cast<tp_i2*>(out) + o, tp_i2{x.x, x.y});
         else put_rec<false>(out, o, x.x, x.y, __int_as_float(x.z), x.w, g.R);
+        if (LEVEL == 2 && seen != nullptr) {
+          // the batch's items (presence / touched flags), marked here rather than in the
+          // count pass: the records leave the sort grouped by tile, so a wave's 64 byte
+          // stores fall in a tile's few hundred bytes instead of 64 random lines (the count
+          // pass's per-rating random byte stores slowed the SGD beside it:
+          // profiles/r5_presence_ab.txt)
+          const int32_t rib = REC8 ? (int32_t)(bk - g.dT.div(bk) * g.T) * g.R + (int32_t)((uint32_t)x.x >> 24) : x.y;
+          seen[tile_item(bk, rib, g)] = 1;
+        }
       }
       __syncthreads();  // LDS reused by the next batch
       if (LEVEL == 1 && tid < nk) base[tid] += cnt[tid];  // same thread zeroes cnt[tid] next
@@ -871,10 +889,10 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   const size_t hb_bytes = sizeof(int32_t) * (size_t)(h16 ? (KT + 1) / 2 : KT);
   if (h16) {
     hipLaunchKernelGGL(tp3_count_kernel<true>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
-                       cshift, NC, KT, ccount, bhist, seen, H1);
+                       cshift, NC, KT, ccount, bhist, (uint8_t*)nullptr, H1);
   } else {
     hipLaunchKernelGGL(tp3_count_kernel<false>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
-                       cshift, NC, KT, ccount, bhist, seen, H1);
+                       cshift, NC, KT, ccount, bhist, (uint8_t*)nullptr, H1);
   }
   hipLaunchKernelGGL(tp3_colsum_kernel, dim3((KT + 63) / 64), dim3(1024), 0, s, bhist, Gc, KT);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)ccount, NC, cptr);
@@ -888,7 +906,8 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
     const int g1 = g_tp_grid > 0 ? min(G, g_tp_grid) : G;
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
     hipLaunchKernelGGL((tp3_scatter_kernel<L, R8>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, TMP, n, chunk, \
-                       g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT)
+                       g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT,         \
+                       L == 2 ? seen : (uint8_t*)nullptr)
     if (rec8) { FPS_TP3(1, true, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
     else { FPS_TP3(1, false, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
     if (rec8) { FPS_TP3(2, true, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }
