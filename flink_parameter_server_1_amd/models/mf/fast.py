@@ -224,7 +224,9 @@ class DistributedMF:
             # the partition of batch k+1 runs on a side stream beside the SGD of batch k
             # (a priority stream for the SGD and CU-masked streams splitting the CUs
             # between them were measured slower and removed, profiles/r2_partition.md)
-            self._side = torch.cuda.Stream(dev) if (self._prefetch or ps_spec) else None
+            # FPS_PART_PRIORITY (A/B knob): the partition's side-stream priority (-1: high)
+            prio = int(os.environ.get("FPS_PART_PRIORITY", "0"))
+            self._side = torch.cuda.Stream(dev, priority=prio) if (self._prefetch or ps_spec) else None
             # rotation sub-steps on alternating streams (``MFConfig.overlap_substeps``)
             ov = cfg.overlap_substeps
             if ov == "auto":
