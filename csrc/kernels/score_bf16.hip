@@ -32,6 +32,13 @@
 // rows (reg & 3) + 8 (reg >> 2) + 4h are items.
 #include "common.h"
 
+// 32-query blocks per wave at D = 64: 2 (118 VGPRs, 4 waves / SIMD) scores the online
+// MF + top-K batches 4 % faster than 4 (164 VGPRs, 3 waves / SIMD) and LEMP the same
+// (profiles/r5_scorer_qb_ab.txt)
+#ifndef FPS_SB_QB64
+#define FPS_SB_QB64 2
+#endif
+
 
 using namespace fps;
 
@@ -232,65 +239,78 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
 #pragma unroll
       for (int s = 0; s < S; ++s) cur[s] = *reinterpret_cast<const uint4*>(rowp + 16 * s);
       const float bm = bms[bi];  // longest item of this block
+      // the passing scores of one (query block, 32-item block) into the block's LDS list
+      auto emit = [&](int b, const floatx16& acc, float thr) {
+        if (MASK) {  // passing registers as a bit mask, walked by ctz
+          uint32_t bits = 0;
 #pragma unroll
-        for (int b = 0; b < QB; ++b) {
-          if (COORD && use_coord) {  // LEMP length + coordinate bounds of this 32 x 32 pair of blocks
-            const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
-            const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbs[bi][b]);
-            if (!__any(pass)) {  // wave-uniform
-              // counted only when the length bound alone would have scored the pair: the
-              // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
-              // adds over LENGTH, not what the length bound skips anyway
-              if (__any(lpass)) ++skipped;
-              continue;
-            }
-            ++scored;
-          }
-          floatx16 acc = {0};
-#pragma unroll
-          for (int s = 0; s < S; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
-                                                          __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
-          const float thr = theta[b] - margin * ql[b] * bm;
-          float m = acc[0];
-#pragma unroll
-          for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
-          if (MASK && m > thr) {  // passing registers as a bit mask, walked by ctz
-            uint32_t bits = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) bits |= acc[j] > thr ? (1u << j) : 0u;
-            while (bits) {
-              const int j = __builtin_ctz(bits);
-              bits &= bits - 1;
-              const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-              if (item < i_end) {
-                if (lc[b] < SB_SLOTS) {
-                  lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
-                  ++lc[b];
-                } else {
-                  const int q = qrow[b];
-                  const int slot = atomicAdd(cnt + q, 1);
-                  if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
-                }
+          for (int j = 0; j < 16; ++j) bits |= acc[j] > thr ? (1u << j) : 0u;
+          while (bits) {
+            const int j = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            if (item < i_end) {
+              if (lc[b] < SB_SLOTS) {
+                lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+                ++lc[b];
+              } else {
+                const int q = qrow[b];
+                const int slot = atomicAdd(cnt + q, 1);
+                if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
               }
             }
-          } else if (!MASK && m > thr) {  // ~k ln(1 + n / s) passes per query and segment
+          }
+        } else {  // ~k ln(1 + n / s) passes per query and segment
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-              if (acc[j] > thr && item < i_end) {
-                if (lc[b] < SB_SLOTS) {
-                  lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
-                  ++lc[b];
-                } else {
-                  const int q = qrow[b];
-                  const int slot = atomicAdd(cnt + q, 1);
-                  if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
-                }
+          for (int j = 0; j < 16; ++j) {
+            const int item = i0 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            if (acc[j] > thr && item < i_end) {
+              if (lc[b] < SB_SLOTS) {
+                lst[wave][b][lc[b]][lane] = (uint16_t)(item - i_begin);
+                ++lc[b];
+              } else {
+                const int q = qrow[b];
+                const int slot = atomicAdd(cnt + q, 1);
+                if (slot < cap) cand_pos[(int64_t)q * cap + slot] = item;
               }
             }
           }
         }
+      };
+      // LEMP length + coordinate bounds of one 32 x 32 pair of blocks: false = skip
+      // (wave-uniform)
+      auto block_live = [&](int b) {
+        if (!(COORD && use_coord)) return true;
+        const bool lpass = qrow[b] < B && !(theta[b] > -INFINITY && ql[b] * bm * slack <= theta[b]);
+        const bool pass = lpass && coord_pass(theta[b], ql[b], bm, qb[b], cbs[bi][b]);
+        if (!__any(pass)) {
+          // counted only when the length bound alone would have scored the pair: the
+          // gates (coord_gate_kernel, LempTopK's per-batch switch) weigh what COORD
+          // adds over LENGTH, not what the length bound skips anyway
+          if (__any(lpass)) ++skipped;
+          return false;
+        }
+        ++scored;
+        return true;
+      };
+      auto mfma_block = [&](int b) {
+        floatx16 acc = {0};
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
+                                                        __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
+        return acc;
+      };
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        if (!block_live(b)) continue;
+        const floatx16 acc = mfma_block(b);
+        const float thr = theta[b] - margin * ql[b] * bm;
+        float m = acc[0];
+#pragma unroll
+        for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
+        if (m > thr) emit(b, acc, thr);
+      }
     }
     if (more) lstore(buf ^ 1);  // every wave finished reading buf ^ 1 at the previous barrier
     __syncthreads();
@@ -431,11 +451,13 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
                          dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
                          cap, qf, qbf, cb, stats, gate, ipw);                                               \
   }
-  // D = 64: 4 query blocks per wave + the bit-mask epilogue (the fastest of 1/2/4
-  // blocks with branch or mask epilogues, same-box A/B, profiles/r2_bf16_topk.md)
+  // D = 64: FPS_SB_QB64 query blocks per wave + the bit-mask epilogue (round 2: 4
+  // blocks, the fastest of 1/2/4 with branch or mask epilogues, profiles/r2_bf16_topk.md;
+  // round 5, with the LDS-staged items and the workgroup floor: 2,
+  // profiles/r5_scorer_qb_ab.txt)
   switch (D) {
     case 32: FPS_SB(32, 2, true); break;
-    case 64: FPS_SB(64, 4, true); break;
+    case 64: FPS_SB(64, FPS_SB_QB64, true); break;
     case 128: FPS_SB(128, 1, true); break;
     default: return (int)hipErrorInvalidValue;
   }
