@@ -243,12 +243,13 @@ def test_lemp_topk_sync_free_equals_synced_scan():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nc_max", [40, 256, 900])  # rank path, its edge, bitonic path
-def test_topk_merge_cand_exact(nc_max):
+@pytest.mark.parametrize("k", [75, 200])  # <= 64 / > 128 running entries per lane of the wave kernel
+def test_topk_merge_cand_exact(nc_max, k):
     """Candidate merge == a (key desc, id asc) sort of running list + candidates, ties included."""
     from flink_parameter_server_1_amd.models.mf.topk_tensor import _fkey
 
-    torch.manual_seed(nc_max)
-    B, k, cap = 96, 75, 1024
+    torch.manual_seed(nc_max + k)
+    B, cap = 96, 1024
     best_s = torch.sort(torch.round(torch.randn(B, k) * 4) / 4, dim=1, descending=True)[0]
     best_s[:8, 40:] = float("-inf")  # rows still filling
     best_i = torch.randint(0, 10**6, (B, k))
