@@ -365,21 +365,28 @@ __global__ void __launch_bounds__(256) cand_rescore_kernel(const float* __restri
     qh[2 * m + 1] = h ? v.w : v.z;
   }
   const uint32_t ktau = sb_key(best_s[(int64_t)q * k + k - 1]);
+  // every load of a chunk is unconditional (a clamped candidate for lanes past n, whose
+  // column is computed and dropped): the guarded row loads compiled to a branch and a
+  // full memory wait each -- 16 dependent round trips per 32 candidates
   for (int c0 = 0; c0 < n; c0 += 32) {
     const bool ok = c0 + c < n;
-    const int64_t pos = ok ? cand_id[(int64_t)q * cap + c0 + c] : 0;
+    const int64_t pos = cand_id[(int64_t)q * cap + min(c0 + c, n - 1)];
+    const int64_t id = ids[pos];
     const float4* xr = reinterpret_cast<const float4*>(X + pos * D);
+    float4 xv[D / 4];
+#pragma unroll
+    for (int m = 0; m < D / 4; ++m) xv[m] = xr[m];
     floatx16 acc = {0};
 #pragma unroll
     for (int m = 0; m < D / 4; ++m) {
-      const float4 v = ok ? xr[m] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = xv[m];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[2 * m], h ? v.y : v.x, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qh[2 * m + 1], h ? v.w : v.z, acc, 0, 0, 0);
     }
     if (ok && h == 0) {  // lanes 0..31: column c
       const uint32_t key = sb_key(acc[0]);
       cand_key[(int64_t)q * cap + c0 + c] = key > ktau ? key : 0u;
-      cand_id[(int64_t)q * cap + c0 + c] = ids[pos];
+      cand_id[(int64_t)q * cap + c0 + c] = id;
     }
   }
 }
