@@ -318,6 +318,127 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* 
   }
 }
 
+#ifndef FPS_MR_NT
+#define FPS_MR_NT 0
+#endif
+// The same rank merge on NT <= TK_NT threads per row: TK_NT / NT candidates and
+// TK_MAXK / NT running entries per thread, every load issued before any is used.
+// A/B knob FPS_MR_NT (0 = the kernel above; one wave per row measured slower,
+// profiles/r5_merge_rank_wave_ab.txt).
+template <int NT>
+__global__ void __launch_bounds__(NT) topk_merge_rank_nt_kernel(const uint32_t* __restrict__ cand_key,
+                                                                const int64_t* __restrict__ cand_id,
+                                                                const int32_t* __restrict__ cnt, int cap,
+                                                                float* __restrict__ best_s,
+                                                                int64_t* __restrict__ best_i, int k,
+                                                                int32_t* __restrict__ ovf) {
+  static_assert(NT >= 64 && TK_NT % NT == 0 && TK_MAXK % NT == 0, "threads per row");
+  constexpr int CPT = TK_NT / NT, EPT = TK_MAXK / NT;
+  __shared__ uint32_t ckey[TK_NT];
+  __shared__ int64_t cid[TK_NT];
+  __shared__ uint32_t bkey[TK_MAXK];
+  __shared__ int64_t bid[TK_MAXK];
+  __shared__ int32_t hpre[TK_MAXK];
+  __shared__ float out_s[TK_MAXK];
+  __shared__ int64_t out_i[TK_MAXK];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int c = cnt[row];
+  if (ovf != nullptr && c > cap && tid == 0) ovf[0] = 1;
+  const int nc = min(min(c, cap), TK_CAP);
+  if (nc == 0 || nc > TK_NT) return;  // nothing to merge / the bitonic kernel's row
+  float* bs = best_s + (int64_t)row * k;
+  int64_t* bi = best_i + (int64_t)row * k;
+  uint32_t kq[CPT];
+  int64_t iq[CPT];
+  float ev[EPT];
+  int64_t ei[EPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int64_t j = (int64_t)row * cap + min(tid + NT * q, nc - 1);
+    kq[q] = cand_key[j];
+    iq[q] = cand_id[j];
+  }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int i = min(tid + NT * q, k - 1);
+    ev[q] = bs[i];
+    ei[q] = bi[i];
+  }
+#pragma unroll
+  for (int q = 0; q < CPT; ++q)
+    if (tid + NT * q < nc) { ckey[tid + NT * q] = kq[q]; cid[tid + NT * q] = iq[q]; }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int i = tid + NT * q;
+    hpre[i] = 0;
+    if (i < k) { bkey[i] = fkey(ev[q]); bid[i] = ei[q]; }
+  }
+  __syncthreads();
+  int pos[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {  // running entries ahead of candidate j (binary search)
+    const int j = tid + NT * q;
+    int lo = 0, hi = k;
+    if (j < nc) {
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t km = bkey[mid];
+        if (km > kq[q] || (km == kq[q] && bid[mid] <= iq[q])) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < k) atomicAdd(&hpre[lo], 1);  // ahead of running entries lo .. k-1
+    }
+    pos[q] = lo;
+  }
+  for (int t = 0; t < nc; ++t) {  // + the candidates ahead of it
+    const uint32_t kt = ckey[t];
+    const int64_t it = cid[t];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q)
+      pos[q] += kt > kq[q] || (kt == kq[q] && (it < iq[q] || (it == iq[q] && t < tid + NT * q)));
+  }
+#pragma unroll
+  for (int q = 0; q < CPT; ++q)
+    if (tid + NT * q < nc && pos[q] < k) { out_s[pos[q]] = kfloat(kq[q]); out_i[pos[q]] = iq[q]; }
+  __syncthreads();
+  if (tid < 64) {  // inclusive prefix of hpre[0..k): 4 counters per lane + a wave scan
+    int32_t c4[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * tid + q;
+      c4[q] = i < k ? hpre[i] : 0;
+      sum += c4[q];
+    }
+    int32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += y;
+    }
+    int32_t run = inc - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * tid + q;
+      run += c4[q];
+      if (i < k) hpre[i] = run;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {  // running entry i: its index + the candidates ahead of it
+    const int i = tid + NT * q;
+    if (i < k) {
+      const int p = i + hpre[i];
+      if (p < k) { out_s[p] = ev[q]; out_i[p] = ei[q]; }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < k; i += NT) {
+    bs[i] = out_s[i];
+    bi[i] = out_i[i];
+  }
+}
+
 // bitonic merge of the rows with more than TK_NT candidates (<= TK_CAP kept)
 // reset (the second of the two kernels, so both read the count first): cnt[row] = 0
 // for the next segment's filter -- no fill launch per segment
@@ -640,8 +761,12 @@ FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id
                                 float* best_s, int64_t* best_i, int k, int32_t* ovf, int reset_cnt, void* stream) {
   if (B <= 0) return 0;
   if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(topk_merge_rank_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
-                     best_s, best_i, k, ovf);
+  if (FPS_MR_NT > 0)
+    hipLaunchKernelGGL(topk_merge_rank_nt_kernel<(FPS_MR_NT > 0 ? FPS_MR_NT : TK_NT)>, dim3(B), dim3(FPS_MR_NT), 0,
+                       (hipStream_t)stream, cand_key, cand_id, cnt, cap, best_s, best_i, k, ovf);
+  else
+    hipLaunchKernelGGL(topk_merge_rank_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt,
+                       cap, best_s, best_i, k, ovf);
   FPS_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
                      best_s, best_i, k, reset_cnt);
