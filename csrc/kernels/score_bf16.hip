@@ -38,6 +38,10 @@
 #ifndef FPS_SB_QB64
 #define FPS_SB_QB64 2
 #endif
+// items per LDS stage (a multiple of 64; one barrier per stage)
+#ifndef FPS_SB_ST
+#define FPS_SB_ST 64
+#endif
 
 
 using namespace fps;
@@ -172,7 +176,8 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   // after them; one barrier per stage.  Rows are padded to 2D + 16 bytes: the 16
   // lanes of each ds_read_b128 group then hit 16 distinct 4-bank groups (row stride
   // / 16 is odd).
-  constexpr int ST = 64;               // items per stage: two 32-item MFMA blocks
+  constexpr int ST = FPS_SB_ST;        // items per stage: ST / 32 32-item MFMA blocks
+  constexpr int NB = ST / 32;
   constexpr int ROWB = 2 * D + 16;     // padded bytes per bf16 item row in LDS
   constexpr int CPR = D / 8;           // 16-B chunks per row
   constexpr int LPT = ST * CPR / 256;  // chunks per thread per stage
@@ -197,14 +202,14 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   };
   // the longest item of each of a stage's two blocks and (COORD) their coordinate
   // ranges, prefetched one stage ahead with the rows
-  float2 cbs[2][QB], cbn[2][QB];
-  float bms[2], bmn[2];
-  auto cload = [&](int s0, float2 (&dst)[2][QB]) {
+  float2 cbs[NB][QB], cbn[NB][QB];
+  float bms[NB], bmn[NB];
+  auto cload = [&](int s0, float2 (&dst)[NB][QB]) {
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi) bmn[bi] = xbm[min((s0 + 32 * bi) >> 5, (N - 1) >> 5)];
+    for (int bi = 0; bi < NB; ++bi) bmn[bi] = xbm[min((s0 + 32 * bi) >> 5, (N - 1) >> 5)];
     if (COORD && use_coord) {
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
+      for (int bi = 0; bi < NB; ++bi) {
         const int blk = min((s0 + 32 * bi) / 32, (N - 1) / 32);
 #pragma unroll
         for (int b = 0; b < QB; ++b) dst[bi][b] = cb[(int64_t)blk * D + fq[b]];
@@ -218,11 +223,11 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   for (int s0 = i_begin, st = 0; s0 < i_end; s0 += ST, ++st) {
     const int buf = st & 1;
     const bool more = s0 + ST < i_end;
-    bms[0] = bmn[0];
-    bms[1] = bmn[1];
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) bms[bi] = bmn[bi];
     if (COORD && use_coord) {
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
         for (int b = 0; b < QB; ++b) cbs[bi][b] = cbn[bi][b];
     }
@@ -231,7 +236,7 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
       cload(s0 + ST, cbn);
     }
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi) {
+    for (int bi = 0; bi < NB; ++bi) {
       const int i0 = s0 + 32 * bi;
       if (i0 >= i_end) break;  // uniform
       uint4 cur[S];

@@ -232,101 +232,16 @@ __global__ void __launch_bounds__(TK_NT) topk_merge_kernel(const float* __restri
 // walked all k entries per candidate and all candidates per entry (~27 us per
 // 4096-row launch, profiles/r2_bf16_topk.md).
 // Also flags overflowed rows (cnt > cap: merged incompletely) in ovf.
-__global__ void __launch_bounds__(TK_NT) topk_merge_rank_kernel(const uint32_t* __restrict__ cand_key,
-                                                                const int64_t* __restrict__ cand_id,
-                                                                const int32_t* __restrict__ cnt, int cap,
-                                                                float* __restrict__ best_s,
-                                                                int64_t* __restrict__ best_i, int k,
-                                                                int32_t* __restrict__ ovf) {
-  __shared__ uint32_t ckey[TK_NT];
-  __shared__ int64_t cid[TK_NT];
-  __shared__ uint32_t bkey[TK_MAXK];
-  __shared__ int64_t bid[TK_MAXK];
-  __shared__ int32_t hpre[TK_MAXK];  // histogram of r_c, then its inclusive prefix
-  __shared__ float out_s[TK_MAXK];
-  __shared__ int64_t out_i[TK_MAXK];
-  const int row = blockIdx.x, tid = threadIdx.x;
-  const int c = cnt[row];
-  // an overflowed row (more than cap passed the filter) is merged incompletely: flag it
-  // for the caller, which checks once per query batch (no host sync per segment)
-  if (ovf != nullptr && c > cap && tid == 0) ovf[0] = 1;
-  const int nc = min(min(c, cap), TK_CAP);
-  if (nc == 0 || nc > TK_NT) return;  // nothing to merge / the bitonic kernel's row
-  float* bs = best_s + (int64_t)row * k;
-  int64_t* bi = best_i + (int64_t)row * k;
-  if (tid < nc) {
-    ckey[tid] = cand_key[(int64_t)row * cap + tid];
-    cid[tid] = cand_id[(int64_t)row * cap + tid];
-  }
-  if (tid < k) {
-    bkey[tid] = fkey(bs[tid]);
-    bid[tid] = bi[tid];
-  }
-  if (tid < TK_MAXK) hpre[tid] = 0;
-  __syncthreads();
-  if (tid < nc) {  // candidate tid: running entries (binary search) and candidates ahead of it
-    const uint32_t kc = ckey[tid];
-    const int64_t ic = cid[tid];
-    int lo = 0, hi = k;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      const uint32_t km = bkey[mid];
-      if (km > kc || (km == kc && bid[mid] <= ic)) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo < k) atomicAdd(&hpre[lo], 1);  // ahead of running entries lo .. k-1
-    int pos = lo;
-#pragma unroll 4
-    for (int j = 0; j < nc; ++j) {
-      const uint32_t kj = ckey[j];
-      pos += kj > kc || (kj == kc && (cid[j] < ic || (cid[j] == ic && j < tid)));
-    }
-    if (pos < k) { out_s[pos] = kfloat(kc); out_i[pos] = ic; }
-  }
-  __syncthreads();
-  if (tid < 64) {  // inclusive prefix of hpre[0..k): 4 counters per lane + a wave scan
-    int32_t c4[4], sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 4 * tid + q;
-      c4[q] = i < k ? hpre[i] : 0;
-      sum += c4[q];
-    }
-    int32_t inc = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t y = __shfl_up(inc, o, 64);
-      if (tid >= o) inc += y;
-    }
-    int32_t run = inc - sum;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 4 * tid + q;
-      run += c4[q];
-      if (i < k) hpre[i] = run;
-    }
-  }
-  __syncthreads();
-  if (tid < k) {  // running entry tid: its index + the candidates ahead of it
-    const int pos = tid + hpre[tid];
-    if (pos < k) { out_s[pos] = bs[tid]; out_i[pos] = bid[tid]; }
-  }
-  __syncthreads();
-  if (tid < k) {
-    bs[tid] = out_s[tid];
-    bi[tid] = out_i[tid];
-  }
-}
-
+// NT threads per row (TK_NT / NT candidates and TK_MAXK / NT running entries per
+// thread), every load issued before any is used (the guarded loads of the first
+// version compiled to a branch and a full wait each: -5 % kernel time on the online
+// MF + top-K scan, profiles/r5_merge_rank_nt_ab.txt).  NT = 64 (one wave per row) and
+// 128 measured slower or mixed (profiles/r5_merge_rank_wave_ab.txt) -- A/B knob.
 #ifndef FPS_MR_NT
-#define FPS_MR_NT 0
+#define FPS_MR_NT 256
 #endif
-// The same rank merge on NT <= TK_NT threads per row: TK_NT / NT candidates and
-// TK_MAXK / NT running entries per thread, every load issued before any is used.
-// A/B knob FPS_MR_NT (0 = the kernel above; one wave per row measured slower,
-// profiles/r5_merge_rank_wave_ab.txt).
 template <int NT>
-__global__ void __launch_bounds__(NT) topk_merge_rank_nt_kernel(const uint32_t* __restrict__ cand_key,
+__global__ void __launch_bounds__(NT) topk_merge_rank_kernel(const uint32_t* __restrict__ cand_key,
                                                                 const int64_t* __restrict__ cand_id,
                                                                 const int32_t* __restrict__ cnt, int cap,
                                                                 float* __restrict__ best_s,
@@ -761,12 +676,8 @@ FPS_API int fps_topk_merge_cand(const uint32_t* cand_key, const int64_t* cand_id
                                 float* best_s, int64_t* best_i, int k, int32_t* ovf, int reset_cnt, void* stream) {
   if (B <= 0) return 0;
   if (k <= 0 || k > TK_MAXK || cap <= 0 || cap > TK_CAP) return (int)hipErrorInvalidValue;
-  if (FPS_MR_NT > 0)
-    hipLaunchKernelGGL(topk_merge_rank_nt_kernel<(FPS_MR_NT > 0 ? FPS_MR_NT : TK_NT)>, dim3(B), dim3(FPS_MR_NT), 0,
-                       (hipStream_t)stream, cand_key, cand_id, cnt, cap, best_s, best_i, k, ovf);
-  else
-    hipLaunchKernelGGL(topk_merge_rank_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt,
-                       cap, best_s, best_i, k, ovf);
+  hipLaunchKernelGGL(topk_merge_rank_kernel<FPS_MR_NT>, dim3(B), dim3(FPS_MR_NT), 0, (hipStream_t)stream, cand_key,
+                     cand_id, cnt, cap, best_s, best_i, k, ovf);
   FPS_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_cand_kernel, dim3(B), dim3(TK_NT), 0, (hipStream_t)stream, cand_key, cand_id, cnt, cap,
                      best_s, best_i, k, reset_cnt);
