@@ -414,6 +414,45 @@ __global__ void __launch_bounds__(TK_NT) seen_merge_kernel(
   for (int j = tid; j < r; j += TK_NT)
     if (j >= r - M) win[(int)((c + j) % M)] = (int32_t)items[by_user[p0 + j]];
   __syncthreads();
+  if (m <= TK_NT) {
+    // one partial list already in the merge order (key desc, then id asc; invalid entries
+    // only at its end -- a single shard's sorted top-K): dropping the seen items keeps
+    // that order, so a stable compaction replaces the sort (~28 block barriers per row)
+    const int t = tid;
+    const int64_t id = t < m ? ii[(int64_t)e * m + t] : -1;
+    const float sc = t < m ? ss[(int64_t)e * m + t] : -INFINITY;
+    const int64_t id1 = t + 1 < m ? ii[(int64_t)e * m + t + 1] : -1;
+    const float sc1 = t + 1 < m ? ss[(int64_t)e * m + t + 1] : -INFINITY;
+    const bool valid = id >= 0 && isfinite(sc), valid1 = id1 >= 0 && isfinite(sc1);
+    const uint32_t k0 = fkey(sc), k1 = fkey(sc1);
+    const bool in_order = !valid1 || (valid && (k0 > k1 || (k0 == k1 && id < id1)));
+    if (__syncthreads_and(in_order)) {  // uniform
+      bool keep = valid;
+      if (keep)
+        for (int q = 0; q < M; ++q)
+          if (win[q] == (int32_t)id) { keep = false; break; }
+      __shared__ int32_t wsum[TK_NT / 64];
+      const int lane = tid & 63, wv = tid >> 6;
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) wsum[wv] = __popcll(bal);
+      __syncthreads();
+      int pos = __popcll(bal & ((1ull << lane) - 1ull)), total = 0;
+#pragma unroll
+      for (int w = 0; w < TK_NT / 64; ++w) {
+        if (w < wv) pos += wsum[w];
+        total += wsum[w];
+      }
+      if (keep && pos < K) {
+        best_s[(int64_t)e * K + pos] = sc;
+        best_i[(int64_t)e * K + pos] = id;
+      }
+      for (int i = total + tid; i < K; i += TK_NT) {
+        best_s[(int64_t)e * K + i] = -INFINITY;
+        best_i[(int64_t)e * K + i] = -1;
+      }
+      return;
+    }
+  }
   for (int t = tid; t < m; t += TK_NT) {
     const int64_t id = ii[(int64_t)e * m + t];
     const float sc = ss[(int64_t)e * m + t];
