@@ -36,6 +36,27 @@ def main():
         for s in range(4):
             rt.submit(data[s])
         torch.cuda.synchronize()
+    # which package lines issue the aten ops of one batch (a dispatch-mode log)
+    import collections
+    import traceback
+
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    seen = collections.Counter()
+
+    class _Log(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            fr = [f for f in traceback.extract_stack()[:-1] if "flink_parameter_server_1_amd" in f.filename]
+            where = " < ".join(f"{f.filename.split('flink_parameter_server_1_amd/')[-1]}:{f.lineno}" for f in fr[-3:][::-1])
+            seen[(str(func.overloadpacket.__name__), where)] += 1
+            return func(*args, **(kwargs or {}))
+
+    with _Log():
+        rt.submit(data[0])
+    torch.cuda.synchronize()
+    print("aten ops of one batch by call site:", sum(seen.values()))
+    for (op, where), n in sorted(seen.items(), key=lambda x: -x[1]):
+        print(f"{n:4d} {op:24s} {where}")
     ka = prof.key_averages(group_by_stack_n=6)
     rows = [e for e in ka if e.device_time_total > 0 and not e.key.startswith("fps") and e.count >= 4
             and any(t in e.key for t in ("fill", "copy", "zero", "full", "add", "mul", "where", "remainder",
