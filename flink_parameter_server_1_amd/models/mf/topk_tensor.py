@@ -645,25 +645,28 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self._serve(U, None, users, items, ts, ps, plan)
         # learning: the owner of each rated item (non-owned rows masked, not compacted)
         n = self.items.n_local
-        if self.W == 1:  # every item is local, row = id
-            own = torch.ones(items.shape, dtype=torch.bool, device=items.device)
+        if self.W == 1:  # every item is local, row = id (no ownership mask: every row is pushed)
+            own = None
             loc = items.long()
         else:
             own = (items.long() % self.W) == self.rank
             loc = torch.where(own, items.long() // self.W, torch.zeros_like(items, dtype=torch.long))
         if not self.prefill_items:
             # a first rating initialises the item: the index must take it in (one sync)
-            if bool((own & ~self.valid[loc]).any()):
+            fresh = ~self.valid[loc] if own is None else own & ~self.valid[loc]
+            if bool(fresh.any()):
                 self._stale = True
-            self._valid_buf[torch.where(own, loc, torch.full_like(loc, n))] = True
+            self._valid_buf[loc if own is None else torch.where(own, loc, torch.full_like(loc, n))] = True
         du = torch.zeros_like(U)
         lr = self.lr
         W_ = self.items.weight
         touched = [loc]
         if self.fused and U.is_cuda and W_.dtype == torch.float32 and self.dim <= 256:
             self._learn_fused(U, users, items, rating, own, loc, du)
-            ps.push(du, mask=own)
+            ps.push(du, mask=own)  # None at W == 1: the engine's unmasked accumulate (fewer launches)
             return
+        if own is None:
+            own = torch.ones(items.shape, dtype=torch.bool, device=items.device)
         if self.neg_rate > 0:
             rows_own = torch.arange(users.numel(), device=U.device) if self.W == 1 else torch.nonzero(own).flatten()
             ou, oi = users[rows_own].to(torch.int32), items[rows_own].to(torch.int32)
