@@ -70,6 +70,24 @@ def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: flo
     return R.init_rows(table, id_base, id_stride, lo, hi, seed)
 
 
+def static_plan(uniq: torch.Tensor, prefix: torch.Tensor, nb: int, pos: torch.Tensor):
+    """The world-1 static de-duplicated plan: ``(gkeys[nb], valid[nb], pos copy)`` with
+    slot ``j`` serving ``uniq[j]`` for ``j < U = prefix[1]`` and the real key
+    ``uniq[j mod U]`` as padding after (``valid[j] = j < U``).  One launch on the GPU."""
+    if _on_gpu(uniq) and uniq.dtype == torch.int32 and pos.dtype == torch.int32 and prefix.dtype == torch.int32:
+        gkeys = torch.empty(nb, dtype=torch.int32, device=uniq.device)
+        valid = torch.empty(nb, dtype=torch.bool, device=uniq.device)
+        pos_c = torch.empty_like(pos)
+        N.check(N.require().fps_static_plan(_c(uniq).data_ptr(), _c(prefix).data_ptr(), int(nb), _c(pos).data_ptr(),
+                                            pos.numel(), gkeys.data_ptr(), valid.data_ptr(), pos_c.data_ptr(),
+                                            N.stream_ptr(uniq.device)), "static_plan")
+        return gkeys, valid, pos_c
+    j = torch.arange(nb, device=uniq.device)
+    valid = j < prefix[1]
+    gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
+    return gkeys, valid, pos.clone()
+
+
 def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
     """``touched[rows] = 1`` (uint8 flags, int32 rows): the dump bookkeeping of the
     in-place (``local_direct``) update paths, one byte store per request."""

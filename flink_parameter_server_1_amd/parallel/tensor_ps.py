@@ -332,15 +332,13 @@ class TensorPS:
             counts, prefix, uniq, pos = self.dedup.run(keys)
         if W == 1 and self.static and not getattr(self.table, "sparse", False):
             nb = min(n, int(self.table.key_space))
-            j = torch.arange(nb, device=keys.device)
-            valid = j < prefix[1]
             # padding slot j serves the real key uniq[j mod U]: real rows only (the
             # close-time dump stays exact) and spread over all of them (a single padding
             # row shared by millions of slots serialised the gather on one cache line)
-            gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
+            gkeys, valid, pos_c = ops.static_plan(uniq, prefix, nb, pos)
             if self.dedup.clear_after:
                 self.dedup.reset_claims(gkeys)
-            return PendingPlan(n, counts, gkeys, pos.clone(), None, None, int(flag), valid=valid, n_bound=nb,
+            return PendingPlan(n, counts, gkeys, pos_c, None, None, int(flag), valid=valid, n_bound=nb,
                                static=True)
         return n, counts, uniq, pos, True
 
