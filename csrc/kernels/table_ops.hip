@@ -693,30 +693,33 @@ FPS_API int fps_dedup_flags(const int32_t* keys, int64_t n, uint32_t* flag, int3
 // The world-1 static de-duplicated plan in one launch (it was seven torch ops per
 // micro-batch): slot j < nb serves uniq[j] when j < U = prefix[1] (the unique keys)
 // and the real key uniq[j mod U] as padding otherwise (valid[j] = j < U); pos_out = a
-// copy of the request positions (the dedup workspace reuses pos for the next plan).
+// copy of the request positions (the dedup workspace reuses pos for the next plan);
+// push_rows[j] = gkeys[j] for the real keys, -1 for the padding (the rows a push applies).
 __global__ void static_plan_kernel(const int32_t* __restrict__ uniq, const int32_t* __restrict__ prefix,
                                    int64_t nb, const int32_t* __restrict__ pos, int64_t n,
                                    int32_t* __restrict__ gkeys, uint8_t* __restrict__ valid,
-                                   int32_t* __restrict__ pos_out) {
+                                   int32_t* __restrict__ pos_out, int32_t* __restrict__ push_rows) {
   const int64_t U = prefix[1];
   const int64_t Uc = U > 0 ? U : 1;
   const int64_t m = nb > n ? nb : n;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     if (j < nb) {
       const bool v = j < U;
+      const int32_t key = uniq[v ? j : j % Uc];
       valid[j] = v;
-      gkeys[j] = uniq[v ? j : j % Uc];
+      gkeys[j] = key;
+      push_rows[j] = v ? key : -1;
     }
     if (j < n) pos_out[j] = pos[j];
   }
 }
 
 FPS_API int fps_static_plan(const int32_t* uniq, const int32_t* prefix, int64_t nb, const int32_t* pos, int64_t n,
-                            int32_t* gkeys, uint8_t* valid, int32_t* pos_out, void* stream) {
+                            int32_t* gkeys, uint8_t* valid, int32_t* pos_out, int32_t* push_rows, void* stream) {
   const int64_t m = nb > n ? nb : n;
   if (m <= 0) return 0;
   hipLaunchKernelGGL(static_plan_kernel, dim3(grid_for(m, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, uniq,
-                     prefix, nb, pos, n, gkeys, valid, pos_out);
+                     prefix, nb, pos, n, gkeys, valid, pos_out, push_rows);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -583,7 +583,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         self._stale = True      # the index must be (re)built before the next query
         self._since_sort = 0
         if self.neg_rate > 0:
-            n_u = 1 << 20  # per-user rings are keyed by user id modulo this (bounded state)
+            n_u = 1 << 20  # per-user rings are keyed by user id modulo this (bounded state; a power of 2)
             self._ring_users = n_u
             self._ring = torch.full((n_u * self.neg_memory,), -1, dtype=torch.int32, device=self.device)
             self._ring_cur = torch.zeros(n_u, dtype=torch.int32, device=self.device)
@@ -670,7 +670,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
         if self.neg_rate > 0:
             rows_own = torch.arange(users.numel(), device=U.device) if self.W == 1 else torch.nonzero(own).flatten()
             ou, oi = users[rows_own].to(torch.int32), items[rows_own].to(torch.int32)
-            uring = (ou.long() % self._ring_users).to(torch.int32)
+            uring = ou & (self._ring_users - 1)  # user id mod 2^20 (ids >= 0): one op, not three
             ops.ring_push(self._ring, self._ring_cur, uring, oi, self.neg_memory)
             ops.known_append(self._known_flag, self._known, self._known_cnt, oi)
             negs = ops.sample_uniform_reject(ou.numel(), self.neg_rate, self.num_items, oi, uring, self._ring,
@@ -711,7 +711,7 @@ class OnlineMFTopKWorker(BatchedWorkerLogic, _TopKServing):
             ou = users if rows_own is None else users[rows_own]
             oi = items if rows_own is None else items[rows_own]
             ou, oi = ou.to(torch.int32), oi.to(torch.int32)
-            uring = (ou.long() % self._ring_users).to(torch.int32)
+            uring = ou & (self._ring_users - 1)  # user id mod 2^20 (ids >= 0): one op, not three
             ops.ring_push(self._ring, self._ring_cur, uring, oi, self.neg_memory)
             ops.known_append(self._known_flag, self._known, self._known_cnt, oi)
             negs = ops.sample_uniform_reject(ou.numel(), self.neg_rate, self.num_items, oi, uring, self._ring,

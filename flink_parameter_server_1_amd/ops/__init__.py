@@ -71,21 +71,23 @@ def init_rows(table: torch.Tensor, id_base: int = 0, id_stride: int = 1, lo: flo
 
 
 def static_plan(uniq: torch.Tensor, prefix: torch.Tensor, nb: int, pos: torch.Tensor):
-    """The world-1 static de-duplicated plan: ``(gkeys[nb], valid[nb], pos copy)`` with
-    slot ``j`` serving ``uniq[j]`` for ``j < U = prefix[1]`` and the real key
-    ``uniq[j mod U]`` as padding after (``valid[j] = j < U``).  One launch on the GPU."""
+    """The world-1 static de-duplicated plan: ``(gkeys[nb], valid[nb], pos copy,
+    push_rows[nb])`` with slot ``j`` serving ``uniq[j]`` for ``j < U = prefix[1]`` and the
+    real key ``uniq[j mod U]`` as padding after (``valid[j] = j < U``); ``push_rows`` =
+    ``gkeys`` with -1 on the padding (the rows a push applies).  One launch on the GPU."""
     if _on_gpu(uniq) and uniq.dtype == torch.int32 and pos.dtype == torch.int32 and prefix.dtype == torch.int32:
         gkeys = torch.empty(nb, dtype=torch.int32, device=uniq.device)
         valid = torch.empty(nb, dtype=torch.bool, device=uniq.device)
         pos_c = torch.empty_like(pos)
+        push_rows = torch.empty(nb, dtype=torch.int32, device=uniq.device)
         N.check(N.require().fps_static_plan(_c(uniq).data_ptr(), _c(prefix).data_ptr(), int(nb), _c(pos).data_ptr(),
                                             pos.numel(), gkeys.data_ptr(), valid.data_ptr(), pos_c.data_ptr(),
-                                            N.stream_ptr(uniq.device)), "static_plan")
-        return gkeys, valid, pos_c
+                                            push_rows.data_ptr(), N.stream_ptr(uniq.device)), "static_plan")
+        return gkeys, valid, pos_c, push_rows
     j = torch.arange(nb, device=uniq.device)
     valid = j < prefix[1]
     gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
-    return gkeys, valid, pos.clone()
+    return gkeys, valid, pos.clone(), torch.where(valid, gkeys, torch.full_like(gkeys, -1))
 
 
 def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:

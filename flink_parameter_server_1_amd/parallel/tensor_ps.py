@@ -85,6 +85,9 @@ class PullPlan:
     zero_copy: bool = False
     #: static plans: ``valid.sum()`` on the device (counted once for pulls and pushes)
     n_valid: Optional[torch.Tensor] = None
+    #: static dense plans: ``recv_keys`` with -1 on the padding slots (the rows a push
+    #: applies), built with the plan instead of per push
+    push_rows: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -111,6 +114,8 @@ class PendingPlan:
     cols: tuple = (0, 1, 2, 3)
     #: fixed-shape plan: the received ``[W, C + 2]`` header + key slots
     fixed: Optional[torch.Tensor] = None
+    push_rows: Optional[torch.Tensor] = None  # static dense plan: recv keys, -1 on the padding
+
 
 
 class TensorPS:
@@ -335,11 +340,11 @@ class TensorPS:
             # padding slot j serves the real key uniq[j mod U]: real rows only (the
             # close-time dump stays exact) and spread over all of them (a single padding
             # row shared by millions of slots serialised the gather on one cache line)
-            gkeys, valid, pos_c = ops.static_plan(uniq, prefix, nb, pos)
+            gkeys, valid, pos_c, push_rows = ops.static_plan(uniq, prefix, nb, pos)
             if self.dedup.clear_after:
                 self.dedup.reset_claims(gkeys)
             return PendingPlan(n, counts, gkeys, pos_c, None, None, int(flag), valid=valid, n_bound=nb,
-                               static=True)
+                               static=True, push_rows=push_rows)
         return n, counts, uniq, pos, True
 
     @staticmethod
@@ -400,7 +405,7 @@ class TensorPS:
             self._stats["steps"] += 1
             return PullPlan([pp.n_bound], [pp.n_bound], pp.uniq, pp.pos, pp.n_bound, [pp.flag], pp.n,
                             valid=pp.valid, identity=pp.identity, unique=pp.unique, ready=pp.ready,
-                            n_valid=n_valid)
+                            n_valid=n_valid, push_rows=pp.push_rows)
         if pp.event is not None:
             if not pp.event.query():
                 self._stats["host_waits"] += 1
@@ -548,7 +553,10 @@ class TensorPS:
             rows, fresh = self.table.rows_for(plan.recv_keys, push=True)
         recv_keys = rows
         if plan.valid is not None:  # static plan: the padding rows are never applied
-            recv_keys = torch.where(plan.valid, recv_keys, torch.full_like(recv_keys, -1))
+            if plan.push_rows is not None and rows is plan.recv_keys:  # dense: built with the plan
+                recv_keys = plan.push_rows
+            else:
+                recv_keys = torch.where(plan.valid, recv_keys, torch.full_like(recv_keys, -1))
         if self.masked_push:
             valid = recv[:, D] > 0.5
             recv = recv[:, :D].contiguous()

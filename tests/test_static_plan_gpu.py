@@ -17,10 +17,11 @@ def test_static_plan_equals_torch(n, U, nb):
     uniq = torch.randint(0, 10**6, (max(n, nb),), generator=g, device=DEV, dtype=torch.int32)
     prefix = torch.tensor([0, U], dtype=torch.int32, device=DEV)
     pos = torch.randint(0, max(U, 1), (n,), generator=g, device=DEV, dtype=torch.int32)
-    gk, va, pc = ops.static_plan(uniq, prefix, nb, pos)
+    gk, va, pc, pr = ops.static_plan(uniq, prefix, nb, pos)
     j = torch.arange(nb, device=DEV)
     valid = j < prefix[1]
     gkeys = torch.where(valid, uniq[:nb], uniq[j % prefix[1].clamp_min(1)])
     assert torch.equal(va, valid)
     assert torch.equal(gk, gkeys)
     assert torch.equal(pc, pos) and pc.data_ptr() != pos.data_ptr()
+    assert torch.equal(pr, torch.where(valid, gkeys, torch.full_like(gkeys, -1)))
