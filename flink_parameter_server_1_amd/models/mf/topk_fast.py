@@ -163,9 +163,12 @@ class LempTopK:
         return self.lengths[s:].max()
 
     def query(self, Q: torch.Tensor, k: int, exclude: Optional[torch.Tensor] = None, start: int = 0,
-              state=None, unfused: bool = False):
+              state=None, unfused: bool = False, copy: bool = True):
         """Exact top-``k`` inner products. ``exclude`` = bool mask [B, N_sorted-order-free] not supported;
-        use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering.  ``start`` /
+        use ``exclude_ids`` in ``DistributedTopK`` for seen-item filtering.  ``copy=False``: a
+        replayed scan may hand out its graph's own result buffers, valid until the next
+        query of that shape is enqueued (a caller that consumes them on the stream before
+        then saves two copies per batch).  ``start`` /
         ``state = (best_s, best_i)``: continue a scan whose items ``[0, start)`` are
         already merged into ``state``.  ``unfused``: the score-matrix scan (the rescan
         of a batch whose fused scan overflowed)."""
@@ -179,7 +182,7 @@ class LempTopK:
             if self._uses_coord():  # COORD switched off for this batch (the per-batch switch)
                 self.coord_off_batches -= 1
                 self.coord_batches["off"] += 1
-            res = self._query_graph(Q, None, k)  # the captured scan computes the norms itself
+            res = self._query_graph(Q, None, k, copy)  # the captured scan computes the norms itself
             if res is not None:
                 return res
             self.overflows += 1
@@ -206,7 +209,7 @@ class LempTopK:
                     inv[perm] = torch.arange(perm.numel(), device=perm.device)
                     res = (res[0][inv], res[1][inv])
             elif st is None and start == 0 and self.graphs and not self._coord_active() and not ops.DEBUG:
-                res = self._query_graph(Q, qlen, k)
+                res = self._query_graph(Q, qlen, k, copy)
             else:
                 res = self._query_fused(Q, qlen, k, start, st)
             if res is not None:
@@ -287,7 +290,7 @@ class LempTopK:
         # the graph's buffers are rewritten by the next replay: the result is a copy
         return TopKFuture(raw=(best_s.clone(), best_i.clone()), index=self, Q=Q, k=int(k), flag=flag, event=ev)
 
-    def _query_graph(self, Q: torch.Tensor, qlen: torch.Tensor, k: int):
+    def _query_graph(self, Q: torch.Tensor, qlen: torch.Tensor, k: int, copy: bool = True):
         """The fused scan of a fresh query batch as one hipGraph replay: the seed
         segment, every segment's zero / filter / re-score / merge chain and the norms
         (~35 launches at 1M items) from one host call -- the scan's launches had been
@@ -311,8 +314,9 @@ class LempTopK:
         self.buckets_scanned += scanned
         if int(ovf.item()):  # the scan's one sync, as the eager path's
             return None
-        # the graph's buffers are rewritten by the next replay: hand out copies
-        return best_s.clone(), best_i.clone()
+        # the graph's buffers are rewritten by the next replay: hand out copies (unless the
+        # caller consumes them before it)
+        return (best_s.clone(), best_i.clone()) if copy else (best_s, best_i)
 
     def _capture(self, Q: torch.Tensor, k: int):
         import gc

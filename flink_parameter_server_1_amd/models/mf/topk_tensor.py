@@ -316,9 +316,9 @@ class PrunedLempTopK(LempTopK):
         self.pruned = 0
         self.scored = 0
 
-    def query(self, Q: torch.Tensor, k: int, exclude=None):
+    def query(self, Q: torch.Tensor, k: int, exclude=None, copy: bool = True):
         if self.strategy is None:
-            return super().query(Q, k)
+            return super().query(Q, k, copy=copy)
         Q = Q.float().contiguous()
         best_s, best_i, s0 = self._mask_scan(Q, k, settle=not self.quirks)
         if s0 < self.vecs.shape[0]:
@@ -435,7 +435,9 @@ class _TopKServing:
     def _serve(self, Q, valid, users, items, ts, ps, plan: Optional[RoundPlan] = None):
         with stage("topk.score", None):
             if self.index is not None and self.index.vecs.shape[0] > 0:
-                s, i = self.index.query(Q, self.worker_k)
+                # the partial lists are consumed on the stream within this batch (merge,
+                # seen merge), before the next replay of the scan rewrites them: no copies
+                s, i = self.index.query(Q, self.worker_k, copy=False)
             else:
                 s = torch.full((Q.shape[0], self.worker_k), float("-inf"), device=Q.device)
                 i = torch.full((Q.shape[0], self.worker_k), -1, dtype=torch.long, device=Q.device)
