@@ -61,6 +61,10 @@ class PulledBatch:
     def values(self) -> torch.Tensor:
         """``[B, D]`` parameter of every request, in request order (fp32; fp64
         when the rows travel as fp64, the bit-parity configuration)."""
+        if self.rows.is_cuda and self.rows.dtype == torch.float32 and self.rows.dim() == 2:
+            from .. import ops  # one native gather launch (the torch index took a cast + a gather)
+
+            return ops.gather_rows(self.rows, self.pos)
         r = self.rows if self.rows.dtype == torch.float64 else self.rows.float()
         return r[self.pos.long()]
 
