@@ -99,8 +99,12 @@ def main(argv=None):
     ap.add_argument("--user-update", default="auto", choices=["auto", "store", "sc1", "atomic"],
                     help="store: Hogwild user rows (plain accesses); sc1: write-through user rows (about half the lost "
                          "user updates); atomic: exact -- the tiled kernel adds every user delta with float atomics "
-                         "(none lost, ~2x the step: float atomics run at ~1.25 TB/s, profiles/r5_exact_user_rows.md); "
-                         "auto (default): atomic at N > 1, store at N = 1")
+                         "(none lost, ~2x the step: float atomics run at ~1.29 TB/s at every working set, "
+                         "profiles/r6_exact_user_rows.md); auto (default): store at every N -- one semantics for "
+                         "the whole scaling curve; the exact mode is timed beside it (--exact-steps)")
+    ap.add_argument("--exact-steps", type=int, default=5,
+                    help="after the timed loop, time this many steps of the exact user-row mode (atomic) on the same "
+                         "model and report exact_updates_per_s / exact_ms_per_step (0 = skip; tiled SGD only)")
     ap.add_argument("--sgd-mode", default="auto", choices=["auto", "tiled", "grouped", "flat"],
                     help="auto = tiled (tile-grouped kernel, no item atomics) where it applies")
     ap.add_argument("--user-phases", type=int, default=0,
@@ -143,12 +147,26 @@ def main(argv=None):
         import torch.distributed as dist
         from flink_parameter_server_1_amd.parallel import verify as V
 
-        ex = a.exchange if a.exchange in ("rotate", "ps") else ("rotate" if n > 1 else "local")
+        # the exchange MFConfig picks for this job (force_ps_path -> the PS protocol)
+        ex = a.exchange if a.exchange in ("rotate", "ps") else \
+            ("ps" if a.force_ps_path else ("rotate" if n > 1 else "local"))
         if ex == "local":
             ex = "rotate"  # world 1: the rotation path without peers
         mut = os.environ.get("FPS_VERIFY_MUTANT")  # fault injection: the check's own tests
         verify = V.rotation_check(comm, schedule=a.rotation, exchange=ex, pipeline=not a.no_pipeline, wire=a.wire,
-                                  rotation_cls=V.mutant_rotation(mut) if mut else None)
+                                  rotation_cls=V.mutant_rotation(mut) if mut else None, user_update=a.user_update,
+                                  sgd_mode=a.sgd_mode, dim=a.dim)
+        if verify["verify_ok"] and ex == "rotate" and (a.user_update == "atomic" or a.exact_steps > 0):
+            # the exact user-row mode this job times, in the collision regime (users repeated
+            # 8 times per step, under the real rotation and sub-step overlap)
+            col = V.rotation_check(comm, schedule=a.rotation, exchange=ex, user_update="atomic", sgd_mode=a.sgd_mode,
+                                   dim=a.dim, repeated_users=True,
+                                   rotation_cls=V.mutant_rotation(mut) if mut else None)
+            verify["collision"] = col
+            if a.user_update == "atomic":  # the timed mode itself: a failure ends the job
+                verify["verify_ok"] = bool(col["verify_ok"])
+            elif not col["verify_ok"]:  # only the side measurement's mode: it is not reported
+                a.exact_steps = 0
         ids = [V.device_identity(comm)]
         if n > 1:
             ids = [None] * n
@@ -222,6 +240,34 @@ def main(argv=None):
     sent = float(comm.bytes_sent + (model.rot.bytes_sent if model.exchange == "rotate" else 0))
     bytes_per_rank = comm.gather_floats(sent)
     import torch.distributed as dist
+
+    # the exact user-row mode on the same model, data and schedule (outside the headline's
+    # timed region, timed the same way): every rating's user delta added with float atomics
+    exact = None
+    if a.exact_steps > 0 and model.sgd_mode == "tiled" and model.user_update != "atomic" and dev.type == "cuda":
+        mode0 = model.user_update
+        model.set_user_update("atomic")
+        model.step(*data.batch(step, a.batch))  # one untimed step in the mode
+        step += 1
+        model.flush()
+        sync()
+        comm.barrier()
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(a.exact_steps):
+            model.step(*data.batch(step, a.batch))
+            step += 1
+        model.flush()
+        sync()
+        comm.barrier()
+        sync()
+        dte = comm.max_over_ranks(time.perf_counter() - t1)
+        model.set_user_update(mode0)
+        exact = {"exact_updates_per_s": a.batch * a.exact_steps * n / dte, "exact_ms_per_step": dte / a.exact_steps * 1e3,
+                 "exact_steps": a.exact_steps}
+    elif model.user_update == "atomic":
+        exact = {"exact_updates_per_s": a.batch * a.steps * n / dt_max, "exact_ms_per_step": dt_max / a.steps * 1e3,
+                 "exact_steps": a.steps}
 
     # side probe (outside the timed region): the Hogwild user-row race of the tiled SGD
     # measured on this rank's geometry -- users per GPU, the same batch and user phases
@@ -300,6 +346,8 @@ def main(argv=None):
         # user_update="atomic" loses none): value x (1 - lost fraction), None when unmeasured
         out["effective_updates_per_s"] = value * (1.0 - lf) if lf is not None else \
             (value if model.user_update == "atomic" else None)
+        if exact is not None:  # the exact mode (0 lost user updates), timed on the same job
+            out.update(exact)
         if verify is not None:
             out["verify_ok"] = verify["verify_ok"]
             out["verify"] = verify

@@ -57,8 +57,18 @@ def rows(lib, dev, st):
     names = {0: "row RMW plain (Hogwild)", 1: "row float atomics, agent scope", 2: "row float atomics, workgroup scope",
              3: "row float atomics, agent scope, XCD-owned rows", 4: "row float atomics, workgroup scope, XCD-owned rows"}
     n = 1 << 24  # one user phase of the headline step
-    for nrows in (2_500_000, 10_000_000):
-        uid = torch.randint(0, nrows, (n,), dtype=torch.int32, device=dev)
+    # working sets (rows of 256 B): 4 MB (one XCD's L2), 16 / 64 MB (the rotation's active
+    # item block at N = 8 / 2), 200 MB (inside the 256 MiB Infinity Cache), then the round-5
+    # sets 640 MB / 2.5 GB; FPS_PROBE_ROW_SETS="16384,65536" picks others
+    sets = [int(x) for x in os.environ.get("FPS_PROBE_ROW_SETS", "16384,65536,262144,819200,2500000,10000000")
+            .split(",")]
+    for nrows, layout in [(r, lay) for r in sets for lay in ("random", "tile")]:
+        if layout == "random":
+            uid = torch.randint(0, nrows, (n,), dtype=torch.int32, device=dev)
+        else:  # tile-clustered: each run of 4096 updates stays inside one 256-row tile (a tile SGD chunk)
+            tiles = max(1, nrows // 256)
+            t = torch.randint(0, tiles, (n // 4096 + 1,), dtype=torch.int32, device=dev).repeat_interleave(4096)[:n]
+            uid = (t * 256 + torch.randint(0, min(256, nrows), (n,), dtype=torch.int32, device=dev)).clamp_(max=nrows - 1)
         tab = torch.zeros(nrows, 64, device=dev)
         for mode in (0, 1, 2, 3, 4):
             ts = []
@@ -73,7 +83,8 @@ def rows(lib, dev, st):
                 if rep:
                     ts.append(e0.elapsed_time(e1))
             ms = min(ts)
-            print(json.dumps({"probe": names[mode], "rows": nrows, "updates": n, "ms": ms,
+            print(json.dumps({"probe": names[mode], "rows": nrows, "MB": nrows * 256 / 2**20, "layout": layout,
+                              "updates": n, "ms": ms,
                               "GB_per_s_256B": n * 256 / (ms / 1e3) / 1e9}), flush=True)
         del tab
 

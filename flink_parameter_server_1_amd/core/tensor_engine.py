@@ -274,7 +274,9 @@ class TensorRuntime:
             ps_logic.ps_parallelism = self.ps_parallelism
         ps_logic.open(c)
         ps_logic.ps.timer = self.timer
-        worker_logic.open(RuntimeContext(min(c.rank, self.worker_parallelism - 1), self.worker_parallelism, c.rank,
+        # a rank past worker_parallelism runs no worker subtask: its context index is its
+        # own rank (>= worker_parallelism), which no real subtask uses
+        worker_logic.open(RuntimeContext(c.rank, self.worker_parallelism, c.rank,
                                          c.world, self.device, "worker", comm=c))
         self.client = _Client(self)
         if ps_logic.locking:
@@ -347,7 +349,11 @@ class TensorRuntime:
 
     def submit(self, batch: Any, flag: int = 0) -> None:
         """One micro-batch of this rank (collective: all ranks submit in lockstep;
-        ``batch=None`` takes part without data)."""
+        ``batch=None`` takes part without data).  A rank ``>= worker_parallelism`` has
+        no worker subtask and must submit ``None``."""
+        if batch is not None and self.comm.rank >= self.worker_parallelism:
+            raise ValueError(f"rank {self.comm.rank} runs no worker (worker_parallelism="
+                             f"{self.worker_parallelism}): submit None here and give its input to a worker rank")
         if self.graphs is not None and self.graphs.submit(batch, flag):
             return
         self._submit_eager(batch, flag)
@@ -566,7 +572,16 @@ class TensorRuntime:
             raise NotImplementedError("execute() with a locking PS logic: drive it with submit()/finish()")
         self.start(worker_logic, ps_logic)
         if self.comm.rank >= self.worker_parallelism:
-            source = ()  # no worker subtask on this rank: it serves its shard and joins the collectives
+            # no worker subtask on this rank: it serves its shard and joins the collectives.
+            # Each rank passes its OWN input (SPMD), so data given here would be dropped --
+            # the reference's workerParallelism spreads input over the worker subtasks
+            # instead; the caller must partition it over ranks < worker_parallelism
+            it = iter(source)
+            if next(it, _END) is not _END:
+                raise ValueError(f"rank {self.comm.rank} runs no worker (worker_parallelism="
+                                 f"{self.worker_parallelism}) but was given input: partition the input over ranks "
+                                 f"0..{self.worker_parallelism - 1}")
+            source = ()
         if model is not None or worker_model is not None:
             self.load_model(model, worker_model)
         if self.iteration_wait_time is not None:

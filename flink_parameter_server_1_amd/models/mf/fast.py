@@ -68,8 +68,9 @@ class MFConfig:
                                       # rows: ~half the lost user updates, profiles/r4_hogwild.md) | "atomic"
                                       # (exact: no lost update -- the tiled kernel adds every user delta with
                                       # float atomics; the flat kernel where the tiled one does not apply) |
-                                      # "auto": "atomic" on a job of N > 1 ranks (real or emulated), "store"
-                                      # on one (profiles/r5_exact_user_rows.md)
+                                      # "auto" = "store" at EVERY world size: one semantics for the whole
+                                      # 1 -> N curve (bench.py reports the lost fraction and the exact
+                                      # rate beside it; profiles/r6_exact_user_rows.md)
     wire_dtype: str = "fp32"          # "fp32" | "bf16" (pull answers + pushed deltas)
     force_ps_path: bool = False       # run the pull/push protocol even when the shard is local
     sgd_mode: str = "auto"            # "auto" | "tiled" | "flat" | "grouped"
@@ -132,11 +133,14 @@ class DistributedMF:
         self.ps = TensorPS(self.items, self.comm, _WIRE[cfg.wire_dtype])
         uu = cfg.user_update
         if uu == "auto":
-            # exact user rows wherever the job has several ranks: the reference updates a
-            # user's vector sequentially inside its one worker
-            # (M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-55);
-            # one rank keeps the Hogwild kernel, its losses published by bench.py
-            uu = "atomic" if Wn > 1 else "store"
+            # the same user-row semantics at every world size (round 5 switched to the exact
+            # mode at N > 1, so a scaling curve measured a mode change).  The reference updates
+            # a user's vector sequentially inside its one worker
+            # (M/matrix/factorization/workers/PSOnlineMatrixFactorizationWorker.scala:41-55):
+            # "atomic" loses no user update and costs ~2x the step on MI355X (float atomics are
+            # executed memory-side at ~1.3 TB/s whatever the working set,
+            # profiles/r6_exact_user_rows.md); bench.py times both modes on every line
+            uu = "store"
         if uu not in ("store", "sc1", "atomic"):
             raise ValueError(f"user_update must be 'auto', 'store', 'sc1' or 'atomic', not {cfg.user_update!r}")
         #: the resolved user-row update mode
@@ -297,6 +301,23 @@ class DistributedMF:
     @property
     def I(self):
         return self.items.weight
+
+    def set_user_update(self, mode: str) -> None:
+        """Switch the tiled kernel's user-row mode between steps ("store" / "sc1" /
+        "atomic"): the same model, partition and schedule, only the user-row write differs
+        (bench.py times the exact mode beside the Hogwild one).  Call after ``flush()``."""
+        if self.sgd_mode != "tiled":
+            raise ValueError("set_user_update switches the tiled kernel's user-row mode")
+        if mode not in ("store", "sc1", "atomic"):
+            raise ValueError(f"user_update must be 'store', 'sc1' or 'atomic', not {mode!r}")
+        dev = self.comm.device
+        if mode in ("sc1", "atomic") and dev.type == "cuda" and not (
+                self.users.n_local < (1 << 24) and self.U.numel() * 4 < 0xFFFFFFFF):
+            raise ValueError(f"user_update={mode!r} needs < 2^24 users and < 4 GiB per shard")
+        self.user_update = mode
+        self.user_atomic = mode == "atomic"
+        self.user_sc1 = mode == "sc1" and dev.type == "cuda"
+        self.user_mode = ops.USER_MODES[mode] if dev.type == "cuda" or mode == "atomic" else 0
 
     def step(self, uid_local: torch.Tensor, iid: torch.Tensor, rating: torch.Tensor):
         """One micro-batch. ``uid_local`` = row in this worker's user shard,

@@ -126,7 +126,13 @@ class DistributedPA:
         return self.worker.last
 
     def train_step(self, indptr, indices, values, labels, with_loss=False):
-        """Labels: binary +1/-1 (int8, 0 = predict only); multiclass class id (int32, -1 = predict only)."""
+        """Labels: binary +1/-1 (int8, 0 = predict only); multiclass class id (int32, -1 = predict only).
+
+        Returns ``(predictions, loss)`` of the micro-batch that COMPLETES during this call:
+        this one at ``staleness == 0`` (and on the local-direct path); with the PS path's
+        pipeline (``staleness = s > 0``) the batch submitted ``s`` calls earlier -- ``None``
+        for the first ``s`` calls -- and ``with_loss`` applies to that completing batch
+        (``flush()`` completes the rest; ``predict`` drains first and returns its own)."""
         return self._run(indptr, indices, values, labels, True, with_loss)
 
     def predict(self, indptr, indices, values):

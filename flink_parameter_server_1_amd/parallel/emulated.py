@@ -17,7 +17,22 @@ of every shard) -- while each all-to-all's transfer is modelled on the device:
   compute stream waited with nothing else to run.
 
 Counts / flags / reductions are the symmetric ones (``exchange_counts`` returns
-what was sent, ``sum_over_ranks(x) = N x``).  Values computed from the exchanged
+what was sent, ``sum_over_ranks(x) = N x``).
+
+**Hot-owner mode** (``hot_owner=True``, the default of the benches since round 6).
+Rank symmetry holds for the WORKER side (every rank's micro-batch is drawn from
+the same distribution) but not for the OWNER side when keys are skewed: under
+range partitioning of Zipf features, shard 0 receives 71 / 50 / 35 % of all
+requests at N = 2 / 4 / 8.  The job then runs at the pace of the hottest owner,
+so the emulated rank ``rank`` plays an OWNER as every peer sees it: peer j sends
+shard s what this rank sends shard s (the worker-side symmetry), hence this rank
+receives ``split[rank]`` rows from EVERY peer -- ``N x split[rank]`` rows to
+serve / apply -- and its busiest incoming link carries ``split[rank]``.  Each
+received segment is this rank's own self-segment (keys of its shard, valid rows),
+tiled or cut to the expected size; a link's time is the larger of its outgoing
+and incoming bytes (full-duplex links, one per peer).  The benches pick the
+hottest shard as ``rank`` (``bench/bench_pa.py --emulate-rank``; range: shard 0)
+and report every shard's share of the keys.  Values computed from the exchanged
 rows are NOT those of a real job (rank 0 serves its own shard for every peer): the
 emulation is for timing (``bench/bench_pa.py`` / ``bench_w2v.py --emulate-world``),
 like ``rotation.EmulatedRotation`` is for the MF rotation.  Real multi-rank
@@ -46,11 +61,18 @@ class _LinkWork:
 class SymmetricComm(Comm):
     """Rank 0 of a ``world``-rank job under rank symmetry (module docstring)."""
 
-    def __init__(self, world: int, device=None, link_gbps: float = 50.0, latency_us: float = 5.0):
+    def __init__(self, world: int, device=None, link_gbps: float = 50.0, latency_us: float = 5.0,
+                 hot_owner: bool = False, rank: int = 0):
         super().__init__(device=device, local=True)
         if world < 1:
             raise ValueError("world must be >= 1")
-        self.world, self.rank, self.backend = int(world), 0, "emulated"
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside a world of {world}")
+        self.world, self.rank, self.backend = int(world), int(rank), "emulated"
+        #: owner-side model: every peer sends this rank what it sends itself (module docstring)
+        self.hot_owner = bool(hot_owner)
+        #: rows received per all-to-all (the owner-side load the model produced), for tests
+        self.recv_rows: List[int] = []
         self.peer_bytes = [0] * self.world
         self.link_gbps, self.latency_us = float(link_gbps), float(latency_us)
         self.cuda = self.device.type == "cuda"
@@ -59,15 +81,48 @@ class SymmetricComm(Comm):
         self.transfers = 0
 
     # ------------------------------------------------------------- link model
-    def _post(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int]) -> Optional[object]:
-        """Model one all-to-all: latency + busiest peer's bytes / link rate, then the
+    def _fill(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
+              recv_splits: Sequence[int]) -> None:
+        """The received buffer: this rank's own send buffer (symmetric), or every
+        incoming segment = this rank's self-segment tiled / cut (hot owner)."""
+        if not self.hot_owner:
+            n = int(sum(send_splits))
+            out[:n].copy_(send[:n], non_blocking=True)
+            return
+        a = int(sum(send_splits[: self.rank]))
+        own = send[a: a + int(send_splits[self.rank])]
+        off = 0
+        for m in recv_splits:
+            m = int(m)
+            done = 0
+            while done < m:
+                k = min(m - done, own.shape[0]) if own.shape[0] else 0
+                if k == 0:  # nothing to mirror: any valid rows of the send buffer
+                    src = send if send.shape[0] else None
+                    if src is None:
+                        out[off + done: off + m].zero_()
+                        break
+                    k = min(m - done, src.shape[0])
+                    out[off + done: off + done + k].copy_(src[:k], non_blocking=True)
+                else:
+                    out[off + done: off + done + k].copy_(own[:k], non_blocking=True)
+                done += k
+            off += m
+
+    def _post(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
+              recv_splits: Optional[Sequence[int]] = None) -> Optional[object]:
+        """Model one all-to-all: latency + busiest link's bytes / link rate, then the
         receive's device copy; returns the completion event (None on the CPU)."""
+        if recv_splits is None:
+            recv_splits = send_splits
         row_bytes = send.element_size() * (send[0].numel() if send.dim() > 1 and send.shape[0] else 1)
         peer = [int(n) * row_bytes for j, n in enumerate(send_splits) if j != self.rank]
+        if self.hot_owner:  # full-duplex links: the busier direction of each
+            peer += [int(n) * row_bytes for j, n in enumerate(recv_splits) if j != self.rank]
         self._count(send, send_splits)
-        n = int(sum(send_splits))
+        self.recv_rows.append(int(sum(recv_splits)))
         if not self.cuda:
-            out[:n].copy_(send[:n])
+            self._fill(send, out, send_splits, recv_splits)
             return None
         from .vworld import _Sleep
 
@@ -77,7 +132,7 @@ class SymmetricComm(Comm):
         self._link.wait_event(posted)
         with torch.cuda.stream(self._link):
             _Sleep.us(self.device, us)
-            out[:n].copy_(send[:n], non_blocking=True)
+            self._fill(send, out, send_splits, recv_splits)
             done = torch.cuda.Event()
             done.record(self._link)
         send.record_stream(self._link)
@@ -107,6 +162,8 @@ class SymmetricComm(Comm):
         pass
 
     def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
+        if self.hot_owner:  # every peer sends this rank what it sends itself
+            return send_counts[self.rank: self.rank + 1].expand_as(send_counts).clone()
         return send_counts.clone()
 
     def all_to_all(self, send: torch.Tensor, send_splits: Sequence[int], recv_splits: Sequence[int],
@@ -114,13 +171,13 @@ class SymmetricComm(Comm):
         n_out = int(sum(recv_splits))
         if out is None:
             out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-        self._wait(self._post(send, out, send_splits))
+        self._wait(self._post(send, out, send_splits, recv_splits))
         return out
 
     def all_to_all_async(self, send: torch.Tensor, send_splits: Sequence[int], recv_splits: Sequence[int]):
         n_out = int(sum(recv_splits))
         out = torch.empty((n_out,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-        return out, _LinkWork(self, self._post(send, out, send_splits), None)
+        return out, _LinkWork(self, self._post(send, out, send_splits, recv_splits), None)
 
     def all_reduce(self, t: torch.Tensor, op=None) -> torch.Tensor:
         import torch.distributed as dist
@@ -143,3 +200,21 @@ class SymmetricComm(Comm):
 
     def sum_over_ranks(self, x: float) -> float:
         return x * self.world
+
+
+def shard_shares(keys: torch.Tensor, partitioner, unique: bool = True) -> List[float]:
+    """Each shard's share of ``keys`` (de-duplicated first, as a micro-batch's pull plan
+    does) under ``partitioner`` (``core.partitioners``): the owner-side load split."""
+    k = keys.reshape(-1).to(torch.int64)
+    if unique:
+        k = torch.unique(k)
+    sh = partitioner.shard_tensor(k).to(torch.int64)
+    c = torch.bincount(sh.cpu(), minlength=partitioner.n).double()
+    tot = float(c.sum()) or 1.0
+    return [float(x) / tot for x in c]
+
+
+def hottest_shard(keys: torch.Tensor, partitioner) -> int:
+    """The shard receiving the most de-duplicated keys: the owner a job waits for."""
+    sh = shard_shares(keys, partitioner)
+    return max(range(len(sh)), key=lambda j: sh[j])

@@ -46,6 +46,36 @@ def unique_batches(rank: int, steps: int, n_users_local: int, n_items: int, batc
     return out
 
 
+def repeated_user_batches(rank: int, steps: int, n_users_local: int, n_items: int, batch: int, repeat: int = 8,
+                          seed: int = 11, device="cpu") -> List[tuple]:
+    """The collision regime: per step ``batch // repeat`` distinct local users, each rating
+    ``repeat`` distinct items (``batch`` distinct items per step), shuffled -- every user row
+    gets ``repeat`` deltas inside one launch, as the headline's ~6.4 ratings per user do."""
+    g = torch.Generator(device="cpu").manual_seed(seed * 7919 + rank)
+    out = []
+    for _ in range(steps):
+        nu = max(1, batch // repeat)
+        u = torch.randperm(n_users_local, generator=g)[:nu].repeat(repeat)
+        i = torch.randperm(n_items, generator=g)[: u.numel()]
+        p = torch.randperm(u.numel(), generator=g)
+        r = torch.rand(u.numel(), generator=g)
+        out.append((u[p].to(torch.int32).to(device), i[p].to(torch.int32).to(device), r.to(device)))
+    return out
+
+
+def _occurrence_rounds(uid: torch.Tensor) -> torch.Tensor:
+    """k for the k-th occurrence of each user in ``uid`` (0-based, in input order)."""
+    order = torch.argsort(uid.long(), stable=True)
+    su = uid.long()[order]
+    start = torch.ones_like(su, dtype=torch.bool)
+    start[1:] = su[1:] != su[:-1]
+    idx = torch.arange(su.numel())
+    first = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
+    k = torch.empty_like(idx)
+    k[order] = idx - first
+    return k
+
+
 def active_blocks(rank: int, substep: int, world: int, schedule: str) -> List[int]:
     """Partition-layout blocks rank ``rank`` updates in sub-step ``substep``
     (``_Ring.order``: ring 0 direction +1; bidir ring 1 direction -1, base 2W)."""
@@ -56,9 +86,16 @@ def active_blocks(rank: int, substep: int, world: int, schedule: str) -> List[in
     return out
 
 
-def replay_rotation(world: int, schedule: str, cfg, batches: List[List[tuple]]):
+def replay_rotation(world: int, schedule: str, cfg, batches: List[List[tuple]], users_mode: str = "jacobi"):
     """Sequential fp32 CPU replay of ``len(batches[0])`` rotation steps of ``world``
-    ranks: returns ``(items [num_items, D], [user shard of rank r])``."""
+    ranks: returns ``(items [num_items, D], [user shard of rank r])``.
+
+    ``users_mode`` -- how a user rated several times in one (rank, sub-step) is updated:
+    "jacobi" sums the deltas all computed from the row at the sub-step's start (what the
+    exact ``user_update="atomic"`` kernel does when every read lands before any add);
+    "sequential" applies them one after another, in input order (the reference worker's
+    order: ``PSOnlineMatrixFactorizationWorker.scala:41-55``).  With distinct users per
+    sub-step both equal the kernel exactly."""
     from ..ops import reference as R
     from .table import ShardedTable
 
@@ -76,7 +113,16 @@ def replay_rotation(world: int, schedule: str, cfg, batches: List[List[tuple]]):
                 u, i, rt = (x.cpu() for x in batches[r][s])
                 blk, _ = R.rot_block_of(i, Wv, half)
                 sel = torch.isin(blk, torch.tensor(active_blocks(r, t, world, schedule)))
-                R.mf_sgd_local(users[r], items, u[sel], i[sel], rt[sel], cfg.learning_rate, cfg.lam)
+                u, i, rt = u[sel], i[sel], rt[sel]
+                if users_mode == "sequential":
+                    # k-th occurrence of each user in round k: users distinct inside a round,
+                    # so the rounds in order are a sequential schedule (items are distinct)
+                    k = _occurrence_rounds(u)
+                    for q in range(int(k.max()) + 1 if k.numel() else 0):
+                        m = k == q
+                        R.mf_sgd_local(users[r], items, u[m], i[m], rt[m], cfg.learning_rate, cfg.lam)
+                else:
+                    R.mf_sgd_local(users[r], items, u, i, rt, cfg.learning_rate, cfg.lam, user_atomic=True)
     return items, users
 
 
@@ -171,26 +217,40 @@ def mutant_rotation(name: str):
 
 def rotation_check(comm: Comm, schedule: str = "bidir", overlap="auto", steps: int = VERIFY_STEPS,
                    rotation_cls=None, sgd_mode: str = "auto", exchange: str = "rotate",
-                   pipeline: bool = True, wire: str = "fp32") -> Dict[str, object]:
+                   pipeline: bool = True, wire: str = "fp32", user_update: str = "auto",
+                   repeated_users: bool = False, dim: int = VERIFY_DIM) -> Dict[str, object]:
     """Run ``steps`` steps of a small MF job on ``comm`` (the real world) and compare every
     rank's user rows and the whole item table with the sequential replay: the rotation
     schedule (``exchange="rotate"``) or the pull / push protocol with the pipeline's
     staleness (``"ps"``; bf16 on the wire is compared at bf16 tolerance).  Returns the
     same report on every rank (``verify_ok`` agreed by all ranks).  ``rotation_cls``
-    replaces ``RingRotation`` (mutation tests)."""
+    replaces ``RingRotation`` (mutation tests).
+
+    ``repeated_users`` (rotation only): the collision regime -- every user rated 8 times
+    per step (``repeated_user_batches``), so user rows get several deltas inside one
+    launch and across the overlapped sub-steps.  A lost user delta is first order in the
+    learning rate; which reads see which adds is not deterministic, a second-order effect,
+    so the tolerance is measured: 4x the gap between the two exact orders of the replay
+    (summed deltas from one read vs one user delta after another) -- and the check asserts
+    that a lost delta would exceed it.  ``user_update="atomic"`` must pass; "store" (Hogwild)
+    loses deltas and fails."""
     from ..models.mf.fast import DistributedMF, MFConfig
 
     if exchange not in ("rotate", "ps"):
         raise ValueError(f"verify: exchange must be 'rotate' or 'ps', not {exchange!r}")
-    cfg = MFConfig(num_users=VERIFY_USERS, num_items=VERIFY_ITEMS, dim=VERIFY_DIM, learning_rate=0.05,
+    if repeated_users and exchange != "rotate":
+        raise ValueError("verify: the collision regime checks the rotation exchange")
+    lr = 0.01 if repeated_users else 0.05
+    cfg = MFConfig(num_users=VERIFY_USERS, num_items=VERIFY_ITEMS, dim=dim, learning_rate=lr,
                    range_min=0.0, range_max=0.2, exchange=exchange, rotation=schedule, overlap_substeps=overlap,
-                   sgd_mode=sgd_mode, pipeline=pipeline, wire_dtype=wire)
+                   sgd_mode=sgd_mode, pipeline=pipeline, wire_dtype=wire, user_update=user_update)
     m = DistributedMF(cfg, comm)
     if rotation_cls is not None:
         m.rot = rotation_cls(comm, m.items.weight, cfg.num_items, schedule)
     rtol, atol = (RTOL, ATOL) if wire == "fp32" else (2e-2, 2e-3)
     W, r = comm.world, comm.rank
-    for u, i, rt in unique_batches(r, steps, m.users.n_local, cfg.num_items, VERIFY_BATCH, device=comm.device):
+    make = repeated_user_batches if repeated_users else unique_batches
+    for u, i, rt in make(r, steps, m.users.n_local, cfg.num_items, VERIFY_BATCH, device=comm.device):
         m.step(u, i, rt)
     m.flush()
     ids, vals = m.item_vectors(only_touched=False)
@@ -199,9 +259,11 @@ def rotation_check(comm: Comm, schedule: str = "bidir", overlap="auto", steps: i
     all_users = _gather_rows(comm, m.U.contiguous())
     bad = 0.0
     report = {"verify_world": W, "verify_exchange": exchange, "verify_schedule": schedule, "verify_steps": steps,
-              "verify_sgd_mode": m.sgd_mode, "verify_overlap_substeps": bool(getattr(m, "_overlap", False))}
+              "verify_sgd_mode": m.sgd_mode, "verify_overlap_substeps": bool(getattr(m, "_overlap", False)),
+              "verify_user_update": m.user_update, "verify_dim": dim, "verify_wire": wire,
+              "verify_repeated_users": repeated_users}
     if r == 0:
-        batches = [unique_batches(q, steps, (cfg.num_users - q + W - 1) // W, cfg.num_items, VERIFY_BATCH)
+        batches = [make(q, steps, (cfg.num_users - q + W - 1) // W, cfg.num_items, VERIFY_BATCH)
                    for q in range(W)]
         if exchange == "rotate":
             ref_items, ref_users = replay_rotation(W, schedule, cfg, batches)
@@ -212,9 +274,24 @@ def rotation_check(comm: Comm, schedule: str = "bidir", overlap="auto", steps: i
         err_i = float((got_items - ref_items).abs().max())
         err_u = max(float((all_users[q].cpu() - ref_users[q]).abs().max()) for q in range(W))
         moved = float((ref_items - ShardedInit.items(cfg)).abs().max())
-        ok = (torch.allclose(got_items, ref_items, rtol=rtol, atol=atol)
-              and all(torch.allclose(all_users[q].cpu(), ref_users[q], rtol=rtol, atol=atol) for q in range(W))
-              and moved > 100 * atol)
+        if repeated_users:
+            # measured tolerance: the gap between the two exact orders, x 4; a lost delta
+            # (the smallest user delta of the replay's first sub-step) must exceed it
+            seq_items, seq_users = replay_rotation(W, schedule, cfg, batches, users_mode="sequential")
+            gap_u = max(float((seq_users[q] - ref_users[q]).abs().max()) for q in range(W))
+            gap_i = float((seq_items - ref_items).abs().max())
+            tol_u, tol_i = 4 * gap_u + atol, 4 * gap_i + atol
+            u0 = [ShardedInit.users(cfg, q, W) for q in range(W)]
+            # a user's whole-job delta, median over the rated users: losing 7 of its 8
+            # per-step deltas moves it by most of that
+            moved_u = torch.cat([(ref_users[q] - u0[q]).abs().amax(1) for q in range(W)])
+            moved_u = float(moved_u[moved_u > 0].median()) if bool((moved_u > 0).any()) else 0.0
+            ok = (err_u <= tol_u and err_i <= tol_i and moved_u > 4 * tol_u)
+            report.update(verify_tol_users=tol_u, verify_tol_items=tol_i, verify_user_delta_median=moved_u)
+        else:
+            ok = (torch.allclose(got_items, ref_items, rtol=rtol, atol=atol)
+                  and all(torch.allclose(all_users[q].cpu(), ref_users[q], rtol=rtol, atol=atol) for q in range(W)))
+        ok = ok and moved > 100 * atol
         bad = 0.0 if ok else 1.0
         report.update(verify_max_abs_err_items=err_i, verify_max_abs_err_users=err_u, verify_ref_moved=moved)
     bad = comm.max_over_ranks(bad)  # every rank learns rank 0's verdict
@@ -231,3 +308,10 @@ class ShardedInit:
 
         return ShardedTable(cfg.num_items, cfg.dim, 0, 1, "hash", ("uniform", cfg.range_min, cfg.range_max),
                             cfg.item_seed(), "cpu", track_touched=False).weight
+
+    @staticmethod
+    def users(cfg, rank: int, world: int) -> torch.Tensor:
+        from .table import ShardedTable
+
+        return ShardedTable(cfg.num_users, cfg.dim, rank, world, "hash", ("uniform", cfg.range_min, cfg.range_max),
+                            cfg.user_seed(), "cpu", track_touched=False).weight

@@ -113,10 +113,9 @@ def _emulate(world, steps, dim=D, phases=0, schedule="bidir"):
                 for p in range(P):  # the phases of a sub-step run in order on the resident blocks
                     for b, (gid, blk) in blks.items():
                         a, e = int(ptr[p * KB + b]), int(ptr[p * KB + b + 1])
-                        # user rows: summed deltas at world > 1 (user_update "auto" = exact "atomic"
-                        # there), last writer at world 1 ("store")
+                        # user rows: last writer (user_update "auto" = "store" at every world size)
                         R.mf_sgd_local(users[r].weight, blk, u[a:e], row[a:e], rr[a:e], cfg.learning_rate,
-                                       user_atomic=world > 1)
+                                       user_atomic=False)
                 for b, (gid, blk) in blks.items():
                     items[gid] = blk
     return users, items, seen

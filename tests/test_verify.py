@@ -50,3 +50,32 @@ def test_replay_schedule_covers_every_block_once_per_step():
             for t in range(K):  # no block is held by two ranks in one sub-step
                 held = [b for r in range(world) for b in active_blocks(r, t, world, schedule)]
                 assert len(held) == len(set(held))
+
+
+def _collision(rank, world, user_update):
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.parallel.verify import rotation_check
+
+    return rotation_check(Comm(device=torch.device("cpu")), schedule="bidir", user_update=user_update,
+                          repeated_users=True)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_collision_check_passes_exact_user_rows_and_fails_hogwild(world):
+    """The collision regime (every user rated 8 times per step): the exact user-row mode
+    sums every delta and passes at the measured second-order tolerance; the Hogwild
+    ``store`` mode (last writer wins on the CPU twin) loses 7 of 8 deltas and fails on every rank."""
+    ok = run_ranks(_collision, world, "atomic")
+    assert all(r["verify_ok"] for r in ok), ok[0]
+    assert ok[0]["verify_repeated_users"] and ok[0]["verify_user_update"] == "atomic"
+    assert ok[0]["verify_user_delta_median"] > 4 * ok[0]["verify_tol_users"]
+    bad = run_ranks(_collision, world, "store")
+    assert not any(r["verify_ok"] for r in bad)
+    assert bad[0]["verify_max_abs_err_users"] > bad[0]["verify_tol_users"]
+
+
+def test_occurrence_rounds_are_a_sequential_schedule():
+    from flink_parameter_server_1_amd.parallel.verify import _occurrence_rounds
+
+    u = torch.tensor([5, 3, 5, 5, 7, 3, 9])
+    assert _occurrence_rounds(u).tolist() == [0, 0, 1, 2, 0, 1, 0]
