@@ -288,7 +288,8 @@ class TensorRuntime:
             ps_logic.ps.static = c.world == 1 and self.device.type == "cuda" and \
                 (self.capacity is None or not getattr(c, "loopback", False))
             self.pipe = BoundedStalenessPipeline(ps_logic.ps, self._compute, self.staleness,
-                                                 lookahead=self.lookahead)
+                                                 lookahead=self.lookahead,
+                                                 owner_stream=False if self.graph else None)
         self._started = True
         if self.graph:
             self.graphs = StepGraphs(self)

@@ -158,7 +158,10 @@ def synthetic_sparse_batch(B: int, nnz: int, feature_count: int, seed: int, step
     so a PA learner has signal.  Features drawn ``F * u^(1+zipf)`` (skewed toward low ids)."""
     g = torch.Generator(device=device)
     g.manual_seed((seed * 1_000_003 + step) & 0x7FFFFFFF)
-    u = torch.rand(B * nnz, generator=g, device=device)
+    # fp64 draws: an fp32 u has a 24-bit mantissa, so F * u at F = 1e9 reached only ~2^24
+    # ids, nearly all multiples of 64 -- hash sharding (id % N) then sent ~95 % of the keys
+    # to shard 0 (round 6, profiles/r6_ps_paths_hot_owner.md)
+    u = torch.rand(B * nnz, generator=g, device=device, dtype=torch.float64)
     idx = torch.clamp((u ** (1.0 + zipf) * feature_count).long(), max=feature_count - 1)
     vals = torch.rand(B * nnz, generator=g, device=device) + 0.1
     indptr = torch.arange(0, B * nnz + 1, nnz, dtype=torch.int64, device=device)

@@ -106,6 +106,17 @@ class Comm:
         dist.all_to_all_single(recv, send_counts, group=self.group)
         return recv
 
+    def exchange_counts_async(self, send_counts: torch.Tensor):
+        """``exchange_counts`` without blocking the caller's stream: ``(recv, work)``;
+        ``work.wait()`` (None: already complete) orders a stream after the exchange.  A
+        synchronous exchange would make the compute stream wait for every transfer
+        queued on the communicator before it (one RCCL stream per rank)."""
+        if self.world == 1 or self._staged(send_counts):
+            return self.exchange_counts(send_counts), None
+        recv = torch.empty_like(send_counts)
+        work = dist.all_to_all_single(recv, send_counts, group=self.group, async_op=True)
+        return recv, work
+
     def all_to_all(self, send: torch.Tensor, send_splits: Sequence[int], recv_splits: Sequence[int],
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Variable-split all-to-all along dim 0 (rows of any trailing shape)."""

@@ -77,6 +77,9 @@ class SymmetricComm(Comm):
         self.link_gbps, self.latency_us = float(link_gbps), float(latency_us)
         self.cuda = self.device.type == "cuda"
         self._link = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
+        #: exposed waits are those of this (compute) stream; an owner stream waiting for a
+        #: transfer (``TensorPS.owner_stream``) idles no compute
+        self._main = torch.cuda.current_stream(self.device) if self.cuda else None
         self._events: List[tuple] = []  # (wait start, wait end) events of every exposed wait
         self.transfers = 0
 
@@ -91,6 +94,11 @@ class SymmetricComm(Comm):
             return
         a = int(sum(send_splits[: self.rank]))
         own = send[a: a + int(send_splits[self.rank])]
+        n_out = int(sum(recv_splits))
+        if own.shape[0] and n_out:  # one gather: segment j = own tiled / cut to recv_splits[j]
+            idx = torch.cat([torch.arange(int(m), device=send.device) % own.shape[0] for m in recv_splits])
+            torch.index_select(own, 0, idx, out=out[:n_out])
+            return
         off = 0
         for m in recv_splits:
             m = int(m)
@@ -143,6 +151,9 @@ class SymmetricComm(Comm):
     def _wait(self, done) -> None:
         if done is None:
             return
+        if torch.cuda.current_stream(self.device) != self._main:
+            torch.cuda.current_stream(self.device).wait_event(done)
+            return
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
         torch.cuda.current_stream(self.device).wait_event(done)
@@ -160,6 +171,9 @@ class SymmetricComm(Comm):
     # ------------------------------------------------------------- collectives
     def barrier(self):
         pass
+
+    def exchange_counts_async(self, send_counts: torch.Tensor):
+        return self.exchange_counts(send_counts), None
 
     def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
         if self.hot_owner:  # every peer sends this rank what it sends itself

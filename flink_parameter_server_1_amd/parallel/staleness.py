@@ -29,6 +29,15 @@ rows per micro-batch); ``submit`` then takes one key tensor per table, their
 plans share ONE count exchange (``TensorPS.plan_begin_multi``), and ``compute``
 receives / returns lists (rows, plans, deltas) in table order.
 
+Owner stream (``owner_stream=True``, world > 1 on the GPU over RCCL / the virtual or
+emulated world): the owner side -- the serve of every pull and the apply of every
+push -- runs on a second stream, each after its all-to-all, and every exchange is
+posted asynchronously.  The compute stream then waits only for the answer rows of
+the batch it computes; the key, push and count transfers and the owner's random
+gather / apply passes overlap the worker's compute (``TensorPS.owner_stream``).  The
+enqueue order is unchanged, so the owner stream holds serve(k) behind apply(k-s-1):
+the staleness bound is the same.  ``drain`` joins the owner stream.
+
 End of input: every ``submit`` carries a ``flag`` that reaches all peers with
 the counts; ``all_flagged`` turns True on every rank at the same micro-batch once
 every rank flagged it (the ``FlinkEOF`` barrier, ``M/utils/FlinkEOF.scala:97-107``,
@@ -50,15 +59,24 @@ ComputeFn = Callable[[torch.Tensor, PullPlan, Any], Tuple[Optional[torch.Tensor]
 
 class BoundedStalenessPipeline:
     def __init__(self, ps, compute: ComputeFn, staleness: int = 1, lr: float = 0.0,
-                 lookahead: Optional[bool] = None):
+                 lookahead: Optional[bool] = None, owner_stream: Optional[bool] = None):
         """``lookahead`` (default: ``staleness > 0``): stage B of a batch waits for
         the next ``submit``, so its counts are never waited for on an idle device.
         Without it (the default of the synchronous ``staleness = 0`` mode) a
-        batch is pulled, computed and pushed inside its own ``submit``."""
+        batch is pulled, computed and pushed inside its own ``submit``.
+        ``owner_stream`` (default: where it applies -- ``owner_stream_ok``; env
+        ``FPS_OWNER_STREAM=0`` turns it off): serve / apply on a second stream."""
         if staleness < 0:
             raise ValueError("staleness must be >= 0")
         self.multi = isinstance(ps, (list, tuple))
         self.pss: List[TensorPS] = list(ps) if self.multi else [ps]
+        if owner_stream is None:
+            owner_stream = owner_stream_ok(self.pss[0].comm, self.pss[0].table.device)
+        self.owner = None
+        if owner_stream:
+            self.owner = torch.cuda.Stream(self.pss[0].table.device)
+            for p in self.pss:  # one owner stream for every table of the pipeline
+                p.owner_stream = self.owner
         self.ps, self.compute, self.staleness, self.lr = ps, compute, int(staleness), lr
         self.lookahead = staleness > 0 if lookahead is None else bool(lookahead)
         self._planned: deque = deque()  # (pending plan, payload) after stage A
@@ -125,6 +143,8 @@ class BoundedStalenessPipeline:
                 out.append(self._finish(self._pulled.popleft()))
         while self._pulled:
             out.append(self._finish(self._pulled.popleft()))
+        if self.owner is not None:  # every apply done before the caller reads the tables
+            self.pss[0].owner_sync()
         return out
 
     @property
@@ -155,6 +175,11 @@ class BoundedStalenessPipeline:
         for w in works:
             if w is not None:
                 w.wait()
+        if self.owner is not None:  # answer rows allocated on the owner stream, read here
+            cur = torch.cuda.current_stream(self.pss[0].table.device)
+            for r in rows:
+                if r is not None and r.is_cuda:
+                    r.record_stream(cur)
         if self.multi:
             deltas, result = self.compute(rows, plans, payload)
             for ps, plan, d in zip(self.pss, plans, deltas or [None] * len(plans)):
@@ -165,3 +190,16 @@ class BoundedStalenessPipeline:
         if deltas is not None:
             self.ps.push(plans[0], deltas, lr=self.lr)
         return result
+
+
+def owner_stream_ok(comm, device) -> bool:
+    """Does an owner stream apply?  World > 1 on the GPU with an asynchronous transport
+    (RCCL, the virtual world, the emulated world); not gloo (host-staged, synchronous)
+    and not inside a graph capture.  ``FPS_OWNER_STREAM=0`` disables it (A/B)."""
+    import os
+
+    if os.environ.get("FPS_OWNER_STREAM", "1") == "0":
+        return False
+    dev = torch.device(device)
+    return (dev.type == "cuda" and comm.world > 1 and getattr(comm, "backend", "") in ("nccl", "virtual", "emulated")
+            and not torch.cuda.is_current_stream_capturing())

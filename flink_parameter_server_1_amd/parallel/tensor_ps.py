@@ -88,6 +88,9 @@ class PullPlan:
     #: static dense plans: ``recv_keys`` with -1 on the padding slots (the rows a push
     #: applies), built with the plan instead of per push
     push_rows: Optional[torch.Tensor] = None
+    #: owner stream (``TensorPS.owner_stream``): the key all-to-all's work -- the serve
+    #: waits for it on the owner stream instead of the compute stream
+    key_work: Optional[object] = None
 
 
 @dataclass
@@ -116,6 +119,19 @@ class PendingPlan:
     fixed: Optional[torch.Tensor] = None
     push_rows: Optional[torch.Tensor] = None  # static dense plan: recv keys, -1 on the padding
 
+
+
+class _EventWork:
+    """A ``Work``-like handle over a device event: ``wait()`` orders the caller's stream."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.event)
+
+    def is_completed(self) -> bool:
+        return self.event.query()
 
 
 class TensorPS:
@@ -176,6 +192,16 @@ class TensorPS:
         #: ``plan_begin`` (the pipelined path); ``plan()`` keeps dynamic plans.
         self.capacity: Optional[int] = None
         self._slots: Optional[torch.Tensor] = None
+        #: the OWNER side on its own stream (``BoundedStalenessPipeline(owner_stream=True)``
+        #: at world > 1 on the GPU): the serve of a pull and the apply of a push run there,
+        #: each after its all-to-all, so the compute stream never waits for a key or push
+        #: transfer -- only for the answer rows it is about to compute on.  Every
+        #: all-to-all (and the count exchange) is posted asynchronously; the counts reach
+        #: the host through ``_aux_stream``.  Stream order on the owner stream keeps the
+        #: staleness bound (serve k is enqueued after apply k - s - 1, as before).
+        self.owner_stream = None
+        self._aux_stream = None
+        self._compute_stream = None
 
     @property
     def stats(self) -> dict:
@@ -372,18 +398,44 @@ class TensorPS:
             return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
         send = torch.cat([self._wire_counts(counts, W, unique), flags], dim=1).contiguous()  # [W, 2]
-        with stage("ps.count-a2a", self.timer):
-            recv = self.comm.exchange_counts(send)
-        both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 4]
-        if self._pinned:
-            host = torch.empty((W, 4), dtype=torch.int32, pin_memory=True)
-            host.copy_(both, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+        if self.owner_stream is not None and self._pinned:
+            host, ev = self._counts_async(send)
         else:
-            host, ev = both.to("cpu"), None
+            with stage("ps.count-a2a", self.timer):
+                recv = self.comm.exchange_counts(send)
+            both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 4]
+            if self._pinned:
+                host = torch.empty((W, 4), dtype=torch.int32, pin_memory=True)
+                host.copy_(both, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host, ev = both.to("cpu"), None
         self._plan_seq += 1
         return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
+
+    def _counts_async(self, send: torch.Tensor):
+        """Owner-stream mode: the count exchange posted asynchronously; the pinned host
+        copy of ``[send | recv]`` runs on the aux stream behind it (a synchronous
+        exchange would make the compute stream wait for every row transfer queued on the
+        communicator before it).  Returns ``(pinned host tensor, event)``."""
+        with stage("ps.count-a2a", self.timer):
+            recv, work = self.comm.exchange_counts_async(send)
+        cur = torch.cuda.current_stream(send.device)
+        if self._aux_stream is None:
+            self._aux_stream = torch.cuda.Stream(send.device)
+        aux = self._aux_stream
+        host = torch.empty((send.shape[0], 2 * send.shape[1]), dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(aux):
+            aux.wait_stream(cur)  # send was written on the compute stream
+            if work is not None:
+                work.wait()
+            send.record_stream(aux)
+            recv.record_stream(aux)
+            host.copy_(torch.cat([send, recv], dim=1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(aux)
+        return host, ev
 
     def plan_end(self, pp: PendingPlan) -> PullPlan:
         """Stage B: split sizes from the host copy, key all-to-all."""
@@ -424,13 +476,17 @@ class TensorPS:
             recv_unique = not any(int(r[rc]) & 1 for r in h)
             peer_flags = [int(r[rf]) for r in h]
         n_unique = int(sum(send_splits))
+        kw = None
         with stage("ps.key-a2a", self.timer):
-            recv_keys = self.comm.all_to_all(pp.uniq[:n_unique], send_splits, recv_splits)
+            if self.owner_stream is not None:  # the serve waits for the keys on the owner stream
+                recv_keys, kw = self.comm.all_to_all_async(pp.uniq[:n_unique], send_splits, recv_splits)
+            else:
+                recv_keys = self.comm.all_to_all(pp.uniq[:n_unique], send_splits, recv_splits)
         self._stats["pulls"] += pp.n
         self._stats["unique"] += n_unique
         self._stats["steps"] += 1
         return PullPlan(send_splits, recv_splits, recv_keys, pp.pos, n_unique, peer_flags, pp.n, unique=pp.unique,
-                        recv_unique=recv_unique)
+                        recv_unique=recv_unique, key_work=kw)
 
     @staticmethod
     def plan_begin_multi(pss: Sequence["TensorPS"], keys_list: Sequence[torch.Tensor], flag: int = 0,
@@ -458,10 +514,16 @@ class TensorPS:
             cols = [TensorPS._wire_counts(c, W, staged[j][4]) for c, j in zip(counts, dyn)]
             cols.append(torch.full((W, 1), int(flag), dtype=torch.int32, device=dev))
             send = torch.cat(cols, dim=1).contiguous()  # [W, T + 1]
-            with stage("ps.count-a2a", pss[0].timer):
-                recv = comm.exchange_counts(send)
-            both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 2T + 2]
-        if dev.type == "cuda":
+            if pss[0].owner_stream is not None and dev.type == "cuda":
+                both = None
+                host, ev = pss[0]._counts_async(send)
+            else:
+                with stage("ps.count-a2a", pss[0].timer):
+                    recv = comm.exchange_counts(send)
+                both = torch.cat([send, recv.to(send.device)], dim=1)  # [W, 2T + 2]
+        if both is None:
+            pass
+        elif dev.type == "cuda":
             host = torch.empty(tuple(both.shape), dtype=torch.int32, pin_memory=True)
             host.copy_(both, non_blocking=True)
             ev = torch.cuda.Event()
@@ -503,8 +565,45 @@ class TensorPS:
                 touched |= plan.valid.view(torch.uint8)
             return out
 
+    def _owner_enter(self, work, *tensors) -> None:
+        """On the owner stream (current): order it after ``work`` (an all-to-all whose
+        output it is about to read) or, without one, after the compute stream; keep the
+        ``tensors`` (allocated on the compute stream) alive for its reads."""
+        O = self.owner_stream
+        if work is not None:
+            work.wait()
+        else:
+            O.wait_stream(self._compute_stream)
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(O)
+
+    def owner_sync(self) -> None:
+        """The compute stream waits for every serve / apply enqueued on the owner stream
+        (end of a pipeline drain: the caller then reads the table)."""
+        if self.owner_stream is not None:
+            torch.cuda.current_stream(self.table.device).wait_stream(self.owner_stream)
+
     def pull_planned(self, plan: PullPlan, async_op: bool = False):
-        """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``."""
+        """Serve + answer all-to-all of a planned pull: ``rows`` or ``(rows, work)``.
+        Owner-stream mode (``async_op``): both run on the owner stream."""
+        if async_op and self.owner_stream is not None:
+            self._compute_stream = torch.cuda.current_stream(self.table.device)
+            with torch.cuda.stream(self.owner_stream):
+                self._owner_enter(plan.key_work, plan.recv_keys, plan.valid, plan.push_rows)
+                plan.key_work = None
+                served = self.serve(plan)
+                with stage("ps.answer-a2a", self.timer):
+                    rows, work = self.comm.all_to_all_async(served, plan.recv_splits, plan.send_splits)
+                if work is None:  # no transfer (world 1): the compute stream waits for the serve
+                    ev = torch.cuda.Event()
+                    ev.record(self.owner_stream)
+                    work = _EventWork(ev)
+            return rows, work
+        self.owner_sync()  # a serve on the compute stream: after every owner-stream apply
+        if plan.key_work is not None:  # keys of an owner-stream plan served here instead
+            plan.key_work.wait()
+            plan.key_work = None
         served = self.serve(plan)
         with stage("ps.answer-a2a", self.timer):
             if async_op:
@@ -542,11 +641,43 @@ class TensorPS:
         elif mask is not None:
             deltas = deltas * mask.reshape(-1, 1).to(deltas.dtype)
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
+        opt = op or self.table.optimizer
+        if (self.owner_stream is not None and not plan.fixed and plan.valid is None and not return_updated
+                and opt != "fn" and self.table.device.type == "cuda"):
+            # owner-stream mode: the push travels while the compute stream goes on; the
+            # owner stream waits for it and applies (after every earlier serve / apply)
+            self._compute_stream = torch.cuda.current_stream(self.table.device)
+            with stage("ps.push-a2a", self.timer):
+                recv, work = self.comm.all_to_all_async(wire.contiguous(), plan.send_splits, plan.recv_splits)
+            with torch.cuda.stream(self.owner_stream):
+                if plan.key_work is not None:  # a push without a pull: its keys' transfer
+                    plan.key_work.wait()
+                    plan.key_work = None
+                self._owner_enter(work, recv, plan.recv_keys)
+                self._apply_pushed(plan, recv, opt, lr, mark=plan.recv_rows is None)
+            return None
         with stage("ps.push-a2a", self.timer):
             recv = self.comm.all_to_all(wire.contiguous(), plan.send_splits, plan.recv_splits)
+        self.owner_sync()  # an apply on the compute stream: after every owner-stream serve / apply
+        if plan.key_work is not None:
+            plan.key_work.wait()
+            plan.key_work = None
+        recv_keys = self._apply_pushed(plan, recv, op or self.table.optimizer, lr, mark=plan.recv_rows is None)
+        if return_updated:
+            if not sum(plan.recv_splits):  # nothing arrived at this shard (host-known sizes)
+                return None
+            if self.masked_push or plan.fixed:  # skipped / padding rows drop out when the consumer reads
+                k = recv_keys.long().clamp_min(0)
+                return MaskedPair(self.table.global_ids(k), self.table.weight[k], recv_keys >= 0)
+            return self.table.global_ids(recv_keys), self.table.weight[recv_keys.long()]
+        return None
+
+    def _apply_pushed(self, plan: PullPlan, recv: torch.Tensor, opt: str, lr: float, mark: bool) -> torch.Tensor:
+        """Apply one push's received rows (stage 9); returns the local rows written (-1:
+        skipped)."""
+        D = self.table.dim
         fresh = None
-        # served by this plan: the rows exist and were marked touched when served
-        mark = plan.recv_rows is None
+        # served by this plan: the rows exist and were marked touched when served (mark)
         if plan.recv_rows is not None:
             rows = plan.recv_rows
         else:  # a push without a pull (push_keys, model load)
@@ -561,7 +692,6 @@ class TensorPS:
             valid = recv[:, D] > 0.5
             recv = recv[:, :D].contiguous()
             recv_keys = torch.where(valid, recv_keys, torch.full_like(recv_keys, -1))
-        opt = op or self.table.optimizer
         if plan.valid is not None:
             self._count_lazy("pushes", plan.valid, total=plan.n_valid)
         elif plan.fixed:
@@ -595,14 +725,7 @@ class TensorPS:
                     off += n
             else:
                 self.table.apply_rows(recv_keys, recv, lr=lr, op=opt, mark=mark)
-        if return_updated:
-            if not sum(plan.recv_splits):  # nothing arrived at this shard (host-known sizes)
-                return None
-            if self.masked_push or plan.fixed:  # skipped / padding rows drop out when the consumer reads
-                k = recv_keys.long().clamp_min(0)
-                return MaskedPair(self.table.global_ids(k), self.table.weight[k], recv_keys >= 0)
-            return self.table.global_ids(recv_keys), self.table.weight[recv_keys.long()]
-        return None
+        return recv_keys
 
     @staticmethod
     def _first_fresh(rows: torch.Tensor, fresh: torch.Tensor) -> torch.Tensor:

@@ -94,8 +94,9 @@ def replay_rotation(world: int, schedule: str, cfg, batches: List[List[tuple]], 
     "jacobi" sums the deltas all computed from the row at the sub-step's start (what the
     exact ``user_update="atomic"`` kernel does when every read lands before any add);
     "sequential" applies them one after another, in input order (the reference worker's
-    order: ``PSOnlineMatrixFactorizationWorker.scala:41-55``).  With distinct users per
-    sub-step both equal the kernel exactly."""
+    order: ``PSOnlineMatrixFactorizationWorker.scala:41-55``); "store" keeps only one of
+    them (last writer: what a lost-update race leaves).  With distinct users per sub-step
+    all three equal the kernel exactly."""
     from ..ops import reference as R
     from .table import ShardedTable
 
@@ -121,8 +122,9 @@ def replay_rotation(world: int, schedule: str, cfg, batches: List[List[tuple]], 
                     for q in range(int(k.max()) + 1 if k.numel() else 0):
                         m = k == q
                         R.mf_sgd_local(users[r], items, u[m], i[m], rt[m], cfg.learning_rate, cfg.lam)
-                else:
-                    R.mf_sgd_local(users[r], items, u, i, rt, cfg.learning_rate, cfg.lam, user_atomic=True)
+                else:  # "jacobi" sums the deltas; "store" keeps the last writer's (a lost-update model)
+                    R.mf_sgd_local(users[r], items, u, i, rt, cfg.learning_rate, cfg.lam,
+                                   user_atomic=users_mode != "store")
     return items, users
 
 
@@ -232,7 +234,7 @@ def rotation_check(comm: Comm, schedule: str = "bidir", overlap="auto", steps: i
     learning rate; which reads see which adds is not deterministic, a second-order effect,
     so the tolerance is measured: 4x the gap between the two exact orders of the replay
     (summed deltas from one read vs one user delta after another) -- and the check asserts
-    that a lost delta would exceed it.  ``user_update="atomic"`` must pass; "store" (Hogwild)
+    that the replay with lost updates (one writer per user and sub-step) lies beyond 2x it.  ``user_update="atomic"`` must pass; "store" (Hogwild)
     loses deltas and fails."""
     from ..models.mf.fast import DistributedMF, MFConfig
 
@@ -281,13 +283,11 @@ def rotation_check(comm: Comm, schedule: str = "bidir", overlap="auto", steps: i
             gap_u = max(float((seq_users[q] - ref_users[q]).abs().max()) for q in range(W))
             gap_i = float((seq_items - ref_items).abs().max())
             tol_u, tol_i = 4 * gap_u + atol, 4 * gap_i + atol
-            u0 = [ShardedInit.users(cfg, q, W) for q in range(W)]
-            # a user's whole-job delta, median over the rated users: losing 7 of its 8
-            # per-step deltas moves it by most of that
-            moved_u = torch.cat([(ref_users[q] - u0[q]).abs().amax(1) for q in range(W)])
-            moved_u = float(moved_u[moved_u > 0].median()) if bool((moved_u > 0).any()) else 0.0
-            ok = (err_u <= tol_u and err_i <= tol_i and moved_u > 4 * tol_u)
-            report.update(verify_tol_users=tol_u, verify_tol_items=tol_i, verify_user_delta_median=moved_u)
+            # what lost updates look like: the replay keeping one writer per user and sub-step
+            _, lost_users = replay_rotation(W, schedule, cfg, batches, users_mode="store")
+            lost_u = max(float((lost_users[q] - ref_users[q]).abs().max()) for q in range(W))
+            ok = (err_u <= tol_u and err_i <= tol_i and lost_u > 2 * tol_u)
+            report.update(verify_tol_users=tol_u, verify_tol_items=tol_i, verify_lost_update_err=lost_u)
         else:
             ok = (torch.allclose(got_items, ref_items, rtol=rtol, atol=atol)
                   and all(torch.allclose(all_users[q].cpu(), ref_users[q], rtol=rtol, atol=atol) for q in range(W)))

@@ -523,6 +523,15 @@ class VirtualComm(Comm):
         self._a2a_post(send_counts.contiguous(), [1] * W, [1] * W, recv).wait()
         return recv
 
+    def exchange_counts_async(self, send_counts: torch.Tensor):
+        if self.world == 1:
+            return send_counts.clone(), None
+        recv = torch.empty_like(send_counts)
+        W = self.world
+        if send_counts.shape[0] != W:
+            raise ValueError("exchange_counts: one row per rank")
+        return recv, self._a2a_post(send_counts.contiguous(), [1] * W, [1] * W, recv)
+
     def _a2a_post(self, send, send_splits, recv_splits, out) -> VWork:
         ss = [int(x) for x in send_splits]
         rs = [int(x) for x in recv_splits]

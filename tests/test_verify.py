@@ -68,7 +68,7 @@ def test_collision_check_passes_exact_user_rows_and_fails_hogwild(world):
     ok = run_ranks(_collision, world, "atomic")
     assert all(r["verify_ok"] for r in ok), ok[0]
     assert ok[0]["verify_repeated_users"] and ok[0]["verify_user_update"] == "atomic"
-    assert ok[0]["verify_user_delta_median"] > 4 * ok[0]["verify_tol_users"]
+    assert ok[0]["verify_lost_update_err"] > 2 * ok[0]["verify_tol_users"]
     bad = run_ranks(_collision, world, "store")
     assert not any(r["verify_ok"] for r in bad)
     assert bad[0]["verify_max_abs_err_users"] > bad[0]["verify_tol_users"]
