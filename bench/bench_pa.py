@@ -28,6 +28,10 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=1 << 16, help="examples per GPU per step")
     ap.add_argument("--nnz", type=int, default=64)
     ap.add_argument("--zipf", type=float, default=1.0)
+    ap.add_argument("--dedup", default="auto", choices=["auto", "on", "off"],
+                    help="PS path: de-duplicate each micro-batch's features (on: unique keys per peer segment, the "
+                         "owner applies with plain read-modify-writes) or ship every request (off: atomic apply); "
+                         "auto: TensorPS's choice from the key space / batch ratio")
     ap.add_argument("--partition", default="range", choices=["range", "hash"],
                     help="feature table sharding (the reference's rangePartitionerPS, or hash)")
     ap.add_argument("--kind", default="binary", choices=["binary", "ova", "pb", "ml"])
@@ -84,6 +88,8 @@ def main(argv=None):
                                local_direct=not a.ps_path, fuse_local_push=not a.no_fuse_local_push,
                                staleness=a.staleness if a.staleness is not None else int(comm.world > 1)),
                       comm)
+    if a.dedup != "auto":
+        m.ps.dedup_mode = a.dedup == "on"
     batches = [synthetic_sparse_batch(a.batch, a.nnz, a.features, seed=comm.rank + 1, step=s, label_count=a.labels,
                                       device=dev, zipf=a.zipf) for s in range(4)]
 
@@ -130,6 +136,7 @@ def main(argv=None):
             "exposed_wait_ms_per_step": wait_ms if emu else None, "link_gbps": a.link_gbps if emu else None,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": a.partition, "zipf": a.zipf, "wire_dtype": a.wire,
+                       "dedup": a.dedup,
                        "exchange": "local-direct" if m._direct else "ps", "staleness": m.cfg.staleness,
                        "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1)},
         }), flush=True)

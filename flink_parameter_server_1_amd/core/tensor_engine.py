@@ -228,7 +228,7 @@ class TensorRuntime:
     def __init__(self, comm: Optional[Comm] = None, staleness: int = 0, iteration_wait_time: Optional[float] = None,
                  output_sink: Optional[Callable[[Any], None]] = None, lookahead: Optional[bool] = None,
                  graph: bool = False, capacity: Optional[int] = None, worker_parallelism: Optional[int] = None,
-                 ps_parallelism: Optional[int] = None):
+                 ps_parallelism: Optional[int] = None, owner_stream: Optional[bool] = None):
         """``graph``: replay fixed-shape micro-batch steps from captured hipGraphs
         (``core.step_graph``: static plans at world 1, fixed-shape plans over RCCL at
         world > 1, a ``graph_safe`` worker).  ``capacity``: the most keys this rank
@@ -260,6 +260,9 @@ class TensorRuntime:
         self._started = False
         self.graph = bool(graph)
         self.capacity = capacity
+        #: the PS pipeline's owner stream (``parallel.staleness``): None = where it applies;
+        #: False = the interleaved single-stream schedule (latency-bound workers)
+        self.owner_stream = owner_stream
         self.graphs: Optional[StepGraphs] = None
         self._capture_emits: Optional[List[Any]] = None
 
@@ -289,7 +292,8 @@ class TensorRuntime:
                 (self.capacity is None or not getattr(c, "loopback", False))
             self.pipe = BoundedStalenessPipeline(ps_logic.ps, self._compute, self.staleness,
                                                  lookahead=self.lookahead,
-                                                 owner_stream=False if self.graph else None)
+                                                 owner_stream=False if self.graph else self.owner_stream,
+                                                 interleave=False if self.graph else None)
         self._started = True
         if self.graph:
             self.graphs = StepGraphs(self)

@@ -48,6 +48,9 @@ class PAConfig:
     #: staleness_for_pull_limit``): 1 = the pulls of batch k+1 overlap batch k's step and
     #: its pushes (the row all-to-alls hide behind compute at N > 1); ``flush()`` drains
     staleness: int = 0
+    #: PS path at N > 1: serve / apply on a second stream (None: the pipeline's default where
+    #: it applies); False (default): the interleaved single-stream schedule (measured faster)
+    owner_stream: Optional[bool] = False
 
 
 class DistributedPA:
@@ -78,8 +81,11 @@ class DistributedPA:
             Logic(cfg.feature_count, self.L, partition=cfg.partition, **kw)
         self.worker = PAWorker(cfg.kind, self.L, cfg.variant, cfg.aggressiveness, self.cost, emit_predictions=False)
         self.worker.fuse_local_push = cfg.fuse_local_push
-        self.runtime = TensorRuntime(self.comm, staleness=cfg.staleness, capacity=cfg.capacity).start(self.worker,
-                                                                                                     logic)
+        # no owner stream: PA's worker side is a chain of short latency-bound kernels that
+        # a concurrent 4M-row atomic apply slows 2-5x; the interleaved schedule hides the
+        # transfers on one stream instead (profiles/r6_ps_paths_hot_owner.md)
+        self.runtime = TensorRuntime(self.comm, staleness=cfg.staleness, capacity=cfg.capacity,
+                                     owner_stream=cfg.owner_stream).start(self.worker, logic)
         self.timer = None  # utils.metrics.StageTimer (optional)
 
     @property

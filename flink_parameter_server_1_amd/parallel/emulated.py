@@ -95,9 +95,16 @@ class SymmetricComm(Comm):
         a = int(sum(send_splits[: self.rank]))
         own = send[a: a + int(send_splits[self.rank])]
         n_out = int(sum(recv_splits))
-        if own.shape[0] and n_out:  # one gather: segment j = own tiled / cut to recv_splits[j]
-            idx = torch.cat([torch.arange(int(m), device=send.device) % own.shape[0] for m in recv_splits])
-            torch.index_select(own, 0, idx, out=out[:n_out])
+        rs = [int(m) for m in recv_splits]
+        k = own.shape[0]
+        # one kernel per exchange (the transfer model must not cost more device time than
+        # the real receive): every peer sends the self-segment (requests / pushes), or a
+        # prefix of it (answers)
+        if k and n_out and all(m == k for m in rs):
+            out[:n_out].view((len(rs),) + tuple(own.shape)).copy_(own.unsqueeze(0).expand((len(rs),) + tuple(own.shape)))
+            return
+        if k and n_out and max(rs) <= k:
+            torch.cat([own[:m] for m in rs], out=out[:n_out])
             return
         off = 0
         for m in recv_splits:

@@ -38,6 +38,16 @@ gather / apply passes overlap the worker's compute (``TensorPS.owner_stream``). 
 enqueue order is unchanged, so the owner stream holds serve(k) behind apply(k-s-1):
 the staleness bound is the same.  ``drain`` joins the owner stream.
 
+Interleaved schedule (``interleave``, the default where an owner stream is not used
+but the transport is asynchronous): everything stays on the compute stream, but
+each ``submit(k)`` posts the key all-to-all of ``k-1``, computes and pushes (posted,
+not applied) the oldest batch, THEN waits for the keys and serves ``k-1``, and only
+then waits for the push and applies it -- the key transfer hides behind the compute
+and the push transfer behind the serve, without a concurrent owner stream (whose
+random-access apply slows the worker's latency-bound kernels: PA,
+``profiles/r6_ps_paths_hot_owner.md``).  Serve ``k-1`` still lands after apply
+``k-s-2`` and before apply ``k-s-1``: the same bound.
+
 End of input: every ``submit`` carries a ``flag`` that reaches all peers with
 the counts; ``all_flagged`` turns True on every rank at the same micro-batch once
 every rank flagged it (the ``FlinkEOF`` barrier, ``M/utils/FlinkEOF.scala:97-107``,
@@ -46,6 +56,7 @@ reach the host one ``submit`` later (``poll_flags``), the same micro-batch on ev
 """
 from __future__ import annotations
 
+import os
 from collections import deque
 from typing import Any, Callable, List, Optional, Tuple
 
@@ -59,7 +70,8 @@ ComputeFn = Callable[[torch.Tensor, PullPlan, Any], Tuple[Optional[torch.Tensor]
 
 class BoundedStalenessPipeline:
     def __init__(self, ps, compute: ComputeFn, staleness: int = 1, lr: float = 0.0,
-                 lookahead: Optional[bool] = None, owner_stream: Optional[bool] = None):
+                 lookahead: Optional[bool] = None, owner_stream: Optional[bool] = None,
+                 interleave: Optional[bool] = None):
         """``lookahead`` (default: ``staleness > 0``): stage B of a batch waits for
         the next ``submit``, so its counts are never waited for on an idle device.
         Without it (the default of the synchronous ``staleness = 0`` mode) a
@@ -70,13 +82,24 @@ class BoundedStalenessPipeline:
             raise ValueError("staleness must be >= 0")
         self.multi = isinstance(ps, (list, tuple))
         self.pss: List[TensorPS] = list(ps) if self.multi else [ps]
-        if owner_stream is None:
+        env = os.environ.get("FPS_OWNER_STREAM")  # A/B override: "0" off, "1" on where it applies
+        if env in ("0", "1"):
+            owner_stream = env == "1"
+        if owner_stream is None or owner_stream:
             owner_stream = owner_stream_ok(self.pss[0].comm, self.pss[0].table.device)
         self.owner = None
         if owner_stream:
             self.owner = torch.cuda.Stream(self.pss[0].table.device)
             for p in self.pss:  # one owner stream for every table of the pipeline
                 p.owner_stream = self.owner
+        self.lookahead = staleness > 0 if lookahead is None else bool(lookahead)
+        if interleave is None:
+            interleave = (self.owner is None and staleness > 0 and self.lookahead
+                          and async_transport(self.pss[0].comm, self.pss[0].table.device))
+        self.interleave = bool(interleave) and self.owner is None and staleness > 0 and self.lookahead
+        if self.interleave:
+            for p in self.pss:
+                p.async_exchange = True
         self.ps, self.compute, self.staleness, self.lr = ps, compute, int(staleness), lr
         self.lookahead = staleness > 0 if lookahead is None else bool(lookahead)
         self._planned: deque = deque()  # (pending plan, payload) after stage A
@@ -98,6 +121,24 @@ class BoundedStalenessPipeline:
             self._planned.append((self.ps.plan_begin(keys, flag, presence=presence), payload))
         self.submitted += 1
         out: List[Any] = []
+        if self.interleave:
+            # keys of the batches beyond the lookahead posted; the oldest pulled batches
+            # computed and their pushes posted; then the new ones served; then the pushes
+            # applied (module docstring: the same staleness bound)
+            ready = []
+            while len(self._planned) > 1:
+                ready.append(self._plan_next())
+            pend = []
+            while len(self._pulled) + len(ready) > self.staleness and self._pulled:
+                r, p = self._finish(self._pulled.popleft(), defer=True)
+                out.append(r)
+                pend.extend(p)
+            for item in ready:
+                self._serve(*item)
+            for ps, pp in pend:
+                ps.apply_pending(pp)
+            self.poll_flags()
+            return out
         while len(self._planned) > (1 if self.lookahead else 0):
             self._pull_next()
         while len(self._pulled) > self.staleness:
@@ -157,7 +198,8 @@ class BoundedStalenessPipeline:
     def planned(self) -> int:
         return len(self._planned)
 
-    def _pull_next(self):
+    def _plan_next(self):
+        """Stage B's first half: the plan's sizes from the host, its key all-to-all posted."""
         pps, payload = self._planned.popleft()
         if not self.multi:
             pps = [pps]
@@ -166,11 +208,18 @@ class BoundedStalenessPipeline:
             self._flags_dev = plans[0].flags_dev
         elif plans[0].peer_flags and all(f != 0 for f in plans[0].peer_flags):
             self.all_flagged = True
+        return plans, payload
+
+    def _serve(self, plans, payload):
+        """Stage B's second half: serve + answer all-to-all (async)."""
         pulled = [ps.pull_planned(plan, async_op=True) for ps, plan in zip(self.pss, plans)]
         self.max_observed = max(self.max_observed, len(self._pulled))
         self._pulled.append(([r for r, _ in pulled], [w for _, w in pulled], plans, payload))
 
-    def _finish(self, item) -> Any:
+    def _pull_next(self):
+        self._serve(*self._plan_next())
+
+    def _finish(self, item, defer: bool = False) -> Any:
         rows, works, plans, payload = item
         for w in works:
             if w is not None:
@@ -180,26 +229,42 @@ class BoundedStalenessPipeline:
             for r in rows:
                 if r is not None and r.is_cuda:
                     r.record_stream(cur)
-        if self.multi:
-            deltas, result = self.compute(rows, plans, payload)
-            for ps, plan, d in zip(self.pss, plans, deltas or [None] * len(plans)):
-                if d is not None:
-                    ps.push(plan, d, lr=self.lr)
-            return result
-        deltas, result = self.compute(rows[0], plans[0], payload)
-        if deltas is not None:
-            self.ps.push(plans[0], deltas, lr=self.lr)
-        return result
+        pend = []
+        if defer:
+            for ps in self.pss:  # the compute's own pushes (engine workers) are deferred too
+                ps._defer_into = pend
+        try:
+            if self.multi:
+                deltas, result = self.compute(rows, plans, payload)
+                for ps, plan, d in zip(self.pss, plans, deltas or [None] * len(plans)):
+                    if d is not None:
+                        pp = ps.push(plan, d, lr=self.lr, defer=defer)
+                        if pp is not None:
+                            pend.append((ps, pp))
+            else:
+                deltas, result = self.compute(rows[0], plans[0], payload)
+                if deltas is not None:
+                    pp = self.ps.push(plans[0], deltas, lr=self.lr, defer=defer)
+                    if pp is not None:
+                        pend.append((self.ps, pp))
+        finally:
+            if defer:
+                for ps in self.pss:
+                    ps._defer_into = None
+        return (result, pend) if defer else result
+
+
+def async_transport(comm, device) -> bool:
+    """World > 1 on the GPU over an asynchronous transport (RCCL, the virtual world, the
+    emulated world) -- not gloo (host-staged, synchronous)."""
+    return (torch.device(device).type == "cuda" and comm.world > 1
+            and getattr(comm, "backend", "") in ("nccl", "virtual", "emulated"))
 
 
 def owner_stream_ok(comm, device) -> bool:
     """Does an owner stream apply?  World > 1 on the GPU with an asynchronous transport
     (RCCL, the virtual world, the emulated world); not gloo (host-staged, synchronous)
-    and not inside a graph capture.  ``FPS_OWNER_STREAM=0`` disables it (A/B)."""
-    import os
-
-    if os.environ.get("FPS_OWNER_STREAM", "1") == "0":
-        return False
+    and not inside a graph capture."""
     dev = torch.device(device)
     return (dev.type == "cuda" and comm.world > 1 and getattr(comm, "backend", "") in ("nccl", "virtual", "emulated")
             and not torch.cuda.is_current_stream_capturing())

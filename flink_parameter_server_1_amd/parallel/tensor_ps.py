@@ -121,6 +121,16 @@ class PendingPlan:
 
 
 
+@dataclass
+class PendingPush:
+    """A push whose all-to-all is posted, not yet applied (``TensorPS.push(defer=True)``)."""
+    plan: PullPlan
+    recv: torch.Tensor
+    work: Optional[object]
+    opt: str
+    lr: float
+
+
 class _EventWork:
     """A ``Work``-like handle over a device event: ``wait()`` orders the caller's stream."""
 
@@ -202,6 +212,14 @@ class TensorPS:
         self.owner_stream = None
         self._aux_stream = None
         self._compute_stream = None
+        #: the exchanges are posted asynchronously on ONE stream (``BoundedStalenessPipeline``'s
+        #: interleaved schedule): the key all-to-all's work is waited for right before the
+        #: serve and a deferred push (``push(defer=True)``) right before its apply, so the
+        #: transfers overlap the compute enqueued in between without a second stream
+        self.async_exchange = False
+        #: set by the pipeline around a compute that pushes through the engine: deferrable
+        #: pushes are posted and appended here as ``(self, PendingPush)`` instead of applied
+        self._defer_into: Optional[list] = None
 
     @property
     def stats(self) -> dict:
@@ -398,7 +416,7 @@ class TensorPS:
             return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
         flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
         send = torch.cat([self._wire_counts(counts, W, unique), flags], dim=1).contiguous()  # [W, 2]
-        if self.owner_stream is not None and self._pinned:
+        if (self.owner_stream is not None or self.async_exchange) and self._pinned:
             host, ev = self._counts_async(send)
         else:
             with stage("ps.count-a2a", self.timer):
@@ -478,7 +496,7 @@ class TensorPS:
         n_unique = int(sum(send_splits))
         kw = None
         with stage("ps.key-a2a", self.timer):
-            if self.owner_stream is not None:  # the serve waits for the keys on the owner stream
+            if self.owner_stream is not None or self.async_exchange:  # the serve waits for the keys
                 recv_keys, kw = self.comm.all_to_all_async(pp.uniq[:n_unique], send_splits, recv_splits)
             else:
                 recv_keys = self.comm.all_to_all(pp.uniq[:n_unique], send_splits, recv_splits)
@@ -514,7 +532,7 @@ class TensorPS:
             cols = [TensorPS._wire_counts(c, W, staged[j][4]) for c, j in zip(counts, dyn)]
             cols.append(torch.full((W, 1), int(flag), dtype=torch.int32, device=dev))
             send = torch.cat(cols, dim=1).contiguous()  # [W, T + 1]
-            if pss[0].owner_stream is not None and dev.type == "cuda":
+            if (pss[0].owner_stream is not None or pss[0].async_exchange) and dev.type == "cuda":
                 both = None
                 host, ev = pss[0]._counts_async(send)
             else:
@@ -625,13 +643,15 @@ class TensorPS:
 
     # --------------------------------------------------------------------- push
     def push(self, plan: PullPlan, deltas: torch.Tensor, lr: float = 0.0, op: Optional[str] = None,
-             return_updated: bool = False, mask: Optional[torch.Tensor] = None):
+             return_updated: bool = False, mask: Optional[torch.Tensor] = None, defer: bool = False):
         """Send per-unique-key deltas ``[U, D]`` (fp32) to their owners and apply
         with ``op`` (default: the table's rule).  ``return_updated``: also return
         ``(global ids, new rows)`` of the keys applied on THIS shard -- the
         per-push ``(id, value)`` output of ``SimplePSLogic``
         (``M/server/SimplePSLogic.scala:24``).  ``mask[U]`` (bool) marks the keys
-        actually pushed; it travels only when ``masked_push`` is set."""
+        actually pushed; it travels only when ``masked_push`` is set.  ``defer``: post the
+        all-to-all and return a ``PendingPush`` -- ``apply_pending`` waits for it and
+        applies (None when the push had to complete here)."""
         D = self.table.dim
         deltas = deltas.reshape(plan.n_unique, D)
         if self.masked_push:
@@ -642,8 +662,18 @@ class TensorPS:
             deltas = deltas * mask.reshape(-1, 1).to(deltas.dtype)
         wire = deltas if deltas.dtype == self.wire_dtype else deltas.to(self.wire_dtype)
         opt = op or self.table.optimizer
-        if (self.owner_stream is not None and not plan.fixed and plan.valid is None and not return_updated
-                and opt != "fn" and self.table.device.type == "cuda"):
+        can_defer = (not plan.fixed and plan.valid is None and not return_updated and opt != "fn"
+                     and self.table.device.type == "cuda")
+        into = self._defer_into
+        if (defer or into is not None) and can_defer and self.owner_stream is None:
+            with stage("ps.push-a2a", self.timer):
+                recv, work = self.comm.all_to_all_async(wire.contiguous(), plan.send_splits, plan.recv_splits)
+            pp = PendingPush(plan, recv, work, opt, lr)
+            if into is not None and not defer:
+                into.append((self, pp))
+                return None
+            return pp
+        if self.owner_stream is not None and can_defer:
             # owner-stream mode: the push travels while the compute stream goes on; the
             # owner stream waits for it and applies (after every earlier serve / apply)
             self._compute_stream = torch.cuda.current_stream(self.table.device)
@@ -671,6 +701,15 @@ class TensorPS:
                 return MaskedPair(self.table.global_ids(k), self.table.weight[k], recv_keys >= 0)
             return self.table.global_ids(recv_keys), self.table.weight[recv_keys.long()]
         return None
+
+    def apply_pending(self, pp: "PendingPush") -> None:
+        """Wait (on the current stream) for a deferred push's transfer and apply it."""
+        if pp.work is not None:
+            pp.work.wait()
+        if pp.plan.key_work is not None:
+            pp.plan.key_work.wait()
+            pp.plan.key_work = None
+        self._apply_pushed(pp.plan, pp.recv, pp.opt, pp.lr, mark=pp.plan.recv_rows is None)
 
     def _apply_pushed(self, plan: PullPlan, recv: torch.Tensor, opt: str, lr: float, mark: bool) -> torch.Tensor:
         """Apply one push's received rows (stage 9); returns the local rows written (-1:
