@@ -81,6 +81,70 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
   }
 }
 
+// D = 1 rows (PA's weight per feature, 4 B): SC rows per thread, every index and value
+// load issued before the first dependent access, so a wave keeps SC random row accesses
+// in flight per lane instead of one (the one-row-per-lane loops above issue a dependent
+// idx -> row pair per trip: 96 us to gather and 218 us to add 4M scalars at N = 8,
+// profiles/r6_ps_paths_hot_owner.md).  Thread t covers rows base + t + k * 256.
+constexpr int SC = 8;
+
+template <bool OUT_BF16, typename IDX>
+__global__ void __launch_bounds__(256) gather_scalar_kernel(const float* __restrict__ table,
+                                                            const IDX* __restrict__ idx, int64_t n,
+                                                            void* __restrict__ out, uint8_t* __restrict__ touched,
+                                                            float* __restrict__ flip) {
+  const int64_t base = (int64_t)blockIdx.x * (256 * SC) + threadIdx.x;
+  int64_t row[SC];
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    const int64_t r = base + k * 256;
+    row[k] = r < n ? (int64_t)idx[r] : -2;
+  }
+  float v[SC];
+#pragma unroll
+  for (int k = 0; k < SC; ++k) v[k] = row[k] >= 0 ? table[row[k]] : 0.f;
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    const int64_t r = base + k * 256;
+    if (row[k] == -2) continue;  // past the end (a padding slot, row -1, serves zero)
+    if (OUT_BF16) ((uint16_t*)out)[r] = f32_to_bf16(v[k]);
+    else ((float*)out)[r] = v[k];
+    if (row[k] < 0) continue;
+    if (flip != nullptr && __float_as_uint(v[k]) == NEG0_BITS) flip_neg0(flip + row[k]);
+    if (touched != nullptr) touched[row[k]] = 1;
+  }
+}
+
+// OP 0: atomic add (keys may repeat), 4: plain read-modify-write (unique keys), 1: set
+template <int OP, bool IN_BF16>
+__global__ void __launch_bounds__(256) apply_scalar_kernel(float* __restrict__ table, const int32_t* __restrict__ idx,
+                                                           int64_t n, const void* __restrict__ delta,
+                                                           uint8_t* __restrict__ touched) {
+  const int64_t base = (int64_t)blockIdx.x * (256 * SC) + threadIdx.x;
+  int32_t row[SC];
+  float g[SC];
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    const int64_t r = base + k * 256;
+    row[k] = r < n ? idx[r] : -1;
+    g[k] = r < n ? (IN_BF16 ? bf16_to_f32(((const uint16_t*)delta)[r]) : ((const float*)delta)[r]) : 0.f;
+  }
+  float old[SC];
+  if (OP == 4) {
+#pragma unroll
+    for (int k = 0; k < SC; ++k) old[k] = row[k] >= 0 ? table[row[k]] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    if (row[k] < 0) continue;
+    const float d = pos0(g[k]);  // a -0.0 delta must not keep the sentinel
+    if (OP == 0) atomic_add_noret(table + row[k], d);
+    else if (OP == 4) table[row[k]] = old[k] + d;
+    else table[row[k]] = d;
+    if (touched != nullptr) touched[row[k]] = 1;
+  }
+}
+
 // op: 0 = add (atomic), 1 = set, 2 = sgd w -= lr*g (atomic), 3 = adagrad
 // (acc += g^2, w -= lr*g/sqrt(acc+eps); keys must be unique in the launch),
 // 4 = add (unique keys, plain RMW), 5 = add + renorm: w += g, then the row's
@@ -782,6 +846,18 @@ FPS_API int fps_gather_rows(const float* table, const void* idx, int idx_is_64, 
   float* flip = flip_sentinel ? const_cast<float*>(table) : nullptr;
   if (n <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (D == 1) {  // scalar rows: SC loads in flight per lane
+    const int64_t g = (n + 256 * SC - 1) / (256 * SC);
+    if (idx_is_64) {
+      if (out_bf16) hipLaunchKernelGGL((gather_scalar_kernel<true, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, out, touched, flip);
+      else hipLaunchKernelGGL((gather_scalar_kernel<false, int64_t>), dim3(g), dim3(256), 0, s, table, (const int64_t*)idx, n, out, touched, flip);
+    } else {
+      if (out_bf16) hipLaunchKernelGGL((gather_scalar_kernel<true, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, out, touched, flip);
+      else hipLaunchKernelGGL((gather_scalar_kernel<false, int32_t>), dim3(g), dim3(256), 0, s, table, (const int32_t*)idx, n, out, touched, flip);
+    }
+    FPS_CHECK_LAUNCH();
+    return 0;
+  }
   int tpr, nv;
   if (!out_bf16 && v4_shape(D, table, out, tpr, nv)) {
     const int D4 = D / 4;
@@ -840,6 +916,17 @@ FPS_API int fps_apply_rows(float* table, float* state, const int32_t* idx, int64
                            int delta_bf16, int op, float lr, float eps, uint8_t* touched, void* stream) {
   if (n <= 0) return 0;
   if ((op == 3 || op == 5) && state == nullptr) return (int)hipErrorInvalidValue;
+  if (D == 1 && (op == 0 || op == 1 || op == 4)) {  // scalar rows: SC loads in flight per lane
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t g = (n + 256 * SC - 1) / (256 * SC);
+#define FPS_APSC(OP_)                                                                                                  \
+    if (delta_bf16) hipLaunchKernelGGL((apply_scalar_kernel<OP_, true>), dim3(g), dim3(256), 0, s, table, idx, n, delta, touched); \
+    else hipLaunchKernelGGL((apply_scalar_kernel<OP_, false>), dim3(g), dim3(256), 0, s, table, idx, n, delta, touched);
+    if (op == 0) { FPS_APSC(0); } else if (op == 4) { FPS_APSC(4); } else { FPS_APSC(1); }
+#undef FPS_APSC
+    FPS_CHECK_LAUNCH();
+    return 0;
+  }
   int tpr, nv;
   if (!delta_bf16 && (op == 1 || op == 4) && v4_shape(D, table, delta, tpr, nv)) {
     const int D4 = D / 4;

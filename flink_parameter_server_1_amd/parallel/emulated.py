@@ -103,8 +103,9 @@ class SymmetricComm(Comm):
         if k and n_out and all(m == k for m in rs):
             out[:n_out].view((len(rs),) + tuple(own.shape)).copy_(own.unsqueeze(0).expand((len(rs),) + tuple(own.shape)))
             return
-        if k and n_out and max(rs) <= k:
-            torch.cat([own[:m] for m in rs], out=out[:n_out])
+        if k and n_out:
+            src = own if max(rs) <= k else torch.cat([own] * -(-max(rs) // k))
+            torch.cat([src[:m] for m in rs], out=out[:n_out])
             return
         off = 0
         for m in recv_splits:

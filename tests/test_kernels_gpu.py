@@ -21,7 +21,7 @@ def test_init_rows_matches_reference(D):
     torch.testing.assert_close(t.cpu(), ref, rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("D", [8, 64, 130])
+@pytest.mark.parametrize("D", [1, 8, 64, 130])
 @pytest.mark.parametrize("wire", [torch.float32, torch.bfloat16])
 def test_gather_rows(D, wire):
     tab = torch.randn(5000, D, device=DEV)
@@ -33,7 +33,7 @@ def test_gather_rows(D, wire):
 
 
 @pytest.mark.parametrize("op", ["add", "set", "sgd"])
-@pytest.mark.parametrize("D", [16, 64])
+@pytest.mark.parametrize("D", [1, 16, 64])
 def test_apply_rows(op, D):
     tab = torch.randn(300, D, device=DEV)
     idx = torch.randperm(300, device=DEV)[:100].to(torch.int32)  # unique for 'set'
@@ -48,7 +48,7 @@ def test_apply_rows(op, D):
 
 # 16-byte kernels (D % 4 == 0, aligned): NV = 1 at D <= 256, 2 at 300, 4 at 520;
 # D = 1028 and the misaligned view take the scalar kernels
-@pytest.mark.parametrize("D", [4, 64, 300, 520, 1028])
+@pytest.mark.parametrize("D", [1, 4, 64, 300, 520, 1028])
 @pytest.mark.parametrize("misaligned", [False, True])
 def test_gather_apply_v4_paths(D, misaligned):
     g = torch.Generator(device=DEV).manual_seed(D)
@@ -78,7 +78,7 @@ def test_gather_apply_v4_paths(D, misaligned):
 
 
 @pytest.mark.parametrize("D,out_dtype", [(64, torch.float32), (300, torch.float32), (7, torch.float32),
-                                         (64, torch.bfloat16)])
+                                         (64, torch.bfloat16), (1, torch.float32), (1, torch.bfloat16)])
 def test_gather_padding_slots_serve_zero_rows(D, out_dtype):
     """Fixed-shape plans pad with row -1: a zero row, no touched mark, no sentinel flip
     (16-byte, scalar and bf16-wire gathers) -- same as the torch twin."""
@@ -583,3 +583,21 @@ def test_topk_select_fresh_equals_block_merge(n, k):
     assert torch.equal(out[0][1], out[1][1])
     ref = torch.topk(S, k, dim=1).values
     assert torch.equal(out[0][0], ref)
+
+
+def test_scalar_rows_gather_apply_large():
+    """D = 1 (PA's weight vector): the scalar kernels (8 rows in flight per lane) over more
+    rows than one workgroup covers, with repeats (atomic add) and -1 padding, vs torch."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    tab = torch.randn(200_003, 1, device=DEV, generator=g)
+    idx = torch.randint(0, 200_003, (70_001,), device=DEV, dtype=torch.int32, generator=g)
+    idx[::9] = -1
+    out = ops.gather_rows(tab, idx)
+    ref = torch.where((idx >= 0).view(-1, 1), tab[idx.long().clamp_min(0)], torch.zeros_like(out))
+    assert torch.equal(out, ref)
+    delta = torch.randn(idx.numel(), 1, device=DEV, generator=g)
+    exp = tab.clone()
+    ok = idx >= 0
+    exp.index_add_(0, idx[ok].long(), delta[ok])
+    ops.apply_rows(tab, idx, delta, "add")
+    torch.testing.assert_close(tab, exp, rtol=1e-5, atol=1e-5)
