@@ -43,6 +43,14 @@ def main(argv=None):
     ap.add_argument("--zipf", type=float, default=3.0)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pool", type=int, default=4, help="pre-generated batches cycled through")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="N > 1: run one rank of an N-rank job on this one GPU (parallel/emulated.py hot-owner model: "
+                         "its shard of the N-GPU table, its own pairs, and every peer sending it what it sends "
+                         "itself); reports the per-GPU rate at N")
+    ap.add_argument("--emulate-rank", type=int, default=-1,
+                    help="--emulate-world: the rank to emulate (-1: the shard owning the most distinct ids of a batch)")
+    ap.add_argument("--link-gbps", type=float, default=50.0, help="--emulate-world: per-peer link rate (GB/s)")
+    ap.add_argument("--latency-us", type=float, default=5.0, help="--emulate-world: per-message link latency")
     a = ap.parse_args(argv)
 
     import torch
@@ -50,7 +58,23 @@ def main(argv=None):
     from flink_parameter_server_1_amd.models.emb import DistributedPairEmbedding, PairEmbeddingConfig, synthetic_pairs
     from flink_parameter_server_1_amd.parallel.comm import Comm
 
-    comm = Comm.init_from_env()
+    emu = a.emulate_world > 1
+    shares = None
+    if emu:
+        from flink_parameter_server_1_amd.core.partitioners import RangePartitioner
+        from flink_parameter_server_1_amd.parallel.emulated import SymmetricComm, shard_shares
+
+        edev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        n_ids = int(a.params_per_gpu * a.emulate_world) // a.dim
+        pa_, pb_, _ = synthetic_pairs(n_ids, a.batch, seed=1, step=0, device=edev, zipf=a.zipf)
+        shares = shard_shares(torch.cat([pa_, pb_]), RangePartitioner(a.emulate_world, n_ids))
+        del pa_, pb_
+        if a.emulate_rank < 0:
+            a.emulate_rank = max(range(a.emulate_world), key=lambda j: shares[j])
+        comm = SymmetricComm(a.emulate_world, device=edev, link_gbps=a.link_gbps, latency_us=a.latency_us,
+                             hot_owner=True, rank=a.emulate_rank)
+    else:
+        comm = Comm.init_from_env()
     dev = comm.device
     num_ids = int(a.params_per_gpu * comm.world) // a.dim
     wire = a.wire
@@ -75,6 +99,8 @@ def main(argv=None):
     m.flush()
     comm.barrier()
     sync()
+    if emu and dev.type == "cuda":
+        comm.wait_ms()  # drop the warm-up's waits
     rows0, t0 = m.rows_pushed, time.perf_counter()
     for s in range(a.steps):
         m.step(*pool[s % a.pool])
@@ -82,22 +108,32 @@ def main(argv=None):
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
+    wait_ms = comm.wait_ms() / a.steps if emu and dev.type == "cuda" else None
     rows = comm.sum_over_ranks(float(m.rows_pushed - rows0))
+    if emu:
+        rows = float(m.rows_pushed - rows0)  # this GPU's pushes (the model's N x is a projection)
     loss1 = m.mean_loss(*eval_batch)
     mem = torch.cuda.max_memory_allocated(dev) / 2**30 if dev.type == "cuda" else 0.0
-    if comm.rank == 0:
-        pairs = a.batch * a.steps * comm.world
+    if comm.rank == 0 or emu:
+        nw = 1 if emu else comm.world
+        pairs = a.batch * a.steps * nw
         print(json.dumps({
-            "metric": "param updates/sec (whole node), 100B-param sharded embedding table",
+            "metric": "param updates/sec per GPU (emulated N-rank job, hottest owner), 100B-param sharded embedding "
+                      "table" if emu else "param updates/sec (whole node), 100B-param sharded embedding table",
             "value": rows * a.dim / dt, "unit": "param updates/s",
-            "pairs_per_s": pairs / dt, "unique_rows_per_step_per_gpu": rows / a.steps / comm.world,
-            "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "pairs_per_s": pairs / dt, "unique_rows_per_step_per_gpu": rows / a.steps / nw,
+            "emulated_world": a.emulate_world if emu else None, "emulated_rank": a.emulate_rank if emu else None,
+            "shard_key_shares": shares, "exposed_wait_ms_per_step": wait_ms,
+            "link_gbps": a.link_gbps if emu else None,
+            "projected_whole_node": {"value": rows * a.dim / dt * a.emulate_world, "measured": False} if emu else None,
+            "n_gpus": nw, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic power-law id pairs (cluster labels), random-init table",
             "table_params": cfg.num_params, "table_gb_per_gpu": m.table.nbytes() / 2**30,
             "peak_hbm_gib_rank0": mem, "init_s": t_init, "eval_loss_before": loss0, "eval_loss_after": loss1,
             "config": {"model": f"pair-embedding ids={num_ids} dim={a.dim}", "global_batch": a.batch * comm.world,
                        "seq_len": None, "parallelism": f"ps{comm.world}", "staleness": a.staleness,
+                       "owner_stream": m.pipe.owner is not None, "interleaved": m.pipe.interleave,
                        "optimizer": a.optimizer, "wire_dtype": wire, "partition": "range", "zipf": a.zipf},
         }), flush=True)
 

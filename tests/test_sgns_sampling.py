@@ -129,6 +129,7 @@ def test_sgns_local_direct_matches_ps_path_on_one_rank():
 
     res = {}
     for direct in (True, False):
+        torch.manual_seed(0)  # skipgram_pairs' reduced windows: the same pairs for both paths
         m = DistributedSGNS(SGNSConfig(vocab_size=2000, dim=32, learning_rate=0.005, local_direct=direct))
         assert m._direct == direct
         c, o = skipgram_pairs(synthetic_corpus(40000, 2000, seed=0), 5)
@@ -140,7 +141,12 @@ def test_sgns_local_direct_matches_ps_path_on_one_rank():
         ids, _ = m.embeddings()
         res[direct] = (l0, l1, set(ids.tolist()))
     assert res[True][1] < res[True][0] and res[False][1] < res[False][0]
-    assert abs(res[True][1] - res[False][1]) < 0.05 * res[False][1]
+    # (no closeness claim between the two: on the GPU the direct path is the sequential
+    # in-place update -- it equals the sequential reference loop, see
+    # test_sgns_direct_path_equals_sequential_reference -- while the PS path reads one
+    # pulled snapshot per micro-batch; at 4096 pairs over 2000 words the sequential form
+    # learns ~10x faster per step (3.91 vs 4.14 from 4.15), so the round-5 5 % bound held
+    # only for lucky reduced-window draws)
     # both dumps cover every word that occurred; rows touched only as sampled negatives
     # may differ (the two paths draw their negatives from different streams)
     seen = set(c[:4096].tolist()) | set(o[:4096].tolist())
@@ -429,3 +435,34 @@ def test_sgns_standard_bf16_rows_equal_widened_rows(D):
     R.sgns_standard(rows_in.float(), rows_out.float(), pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r,
                     method="sorted")
     torch.testing.assert_close(out[0][1], d_out_r, rtol=1e-4, atol=5e-6)
+
+
+@pytest.mark.gpu
+def test_sgns_direct_path_equals_sequential_reference():
+    """The W = 1 direct path on the GPU (kernel updates the tables in place) trains like
+    the sequential reference loop (``reference.sgns_standard``, sorted output-row form,
+    in place) on the same pairs and negatives."""
+    from flink_parameter_server_1_amd.models.w2v.sgns import DistributedSGNS, SGNSConfig, skipgram_pairs, \
+        synthetic_corpus
+
+    torch.manual_seed(0)
+    m = DistributedSGNS(SGNSConfig(vocab_size=2000, dim=32, learning_rate=0.005, local_direct=True))
+    assert m._direct and m.w_in.weight.is_cuda
+    c, o = skipgram_pairs(synthetic_corpus(40000, 2000, seed=0), 5)
+    w_in, w_out = m.w_in.weight.cpu().clone(), m.w_out.weight.cpu().clone()
+    counter = m.counter
+    steps = [(0, True)] + [((i * 4096) % (c.numel() - 4096), False) for i in range(30)] + [(0, True)]
+    got, ref = [], []
+    for s, wl in steps:
+        cc, oo = c[s:s + 4096], o[s:s + 4096]
+        negs = ops.sample_alias(m.prob, m.alias, 4096 * 5, seed=m.cfg.seed, counter=counter).cpu().to(torch.int32)
+        counter += 1
+        d_out = torch.zeros_like(w_out)
+        lr_ = R.sgns_standard(w_in, w_out, cc, oo, negs, 5, 0.005, w_in, d_out, method="sorted")
+        w_out += d_out
+        lg = m.step(cc.cuda(), oo.cuda(), with_loss=wl)
+        if wl:
+            got.append(lg)
+            ref.append(lr_ / 4096)
+    assert abs(got[0] - ref[0]) < 1e-4 * ref[0]
+    assert abs(got[-1] - ref[-1]) < 0.01 * ref[-1], (got, ref)
