@@ -37,11 +37,6 @@ namespace {
 
 constexpr int SG = 4;  // rows per load group
 
-// rows read as fp32, or as bf16 (the PS path's wire dtype at N > 1: the pulled rows are
-// consumed as they arrived, no conversion pass; deltas stay fp32)
-__device__ __forceinline__ float ldr(const float* p) { return *p; }
-__device__ __forceinline__ float ldr(const uint16_t* p) { return bf16_to_f32(*p); }
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -57,9 +52,9 @@ __device__ __forceinline__ float softplusf(float x) { return x > 0.f ? x + log1p
 // output rows are not touched here; the pair's coefficient g_x goes to
 // gbuf[p * (k + 1) + x] and sgns_rows_kernel below applies sum_x g_x * h per
 // output row from the coefficients sorted by row (no atomics on the hot rows).
-template <int NPL, bool GOUT, typename RT = float>
-__global__ void __launch_bounds__(256) sgns_std_kernel(const RT* __restrict__ rows_in,
-                                                       const RT* __restrict__ rows_out,
+template <int NPL, bool GOUT>
+__global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__ rows_in,
+                                                       const float* __restrict__ rows_out,
                                                        const int32_t* __restrict__ pos_c,
                                                        const int32_t* __restrict__ pos_o,
                                                        const int32_t* __restrict__ pos_neg, int64_t P, int D, int k,
@@ -90,11 +85,11 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const RT* __restrict__ ro
     if (c != cur) {  // a new center run: push the previous run's change, load this center
       flush();
       cur = c;
-      const RT* src = rows_in + (int64_t)c * D;
+      const float* src = rows_in + (int64_t)c * D;
 #pragma unroll
       for (int m = 0; m < NPL; ++m) {
         const int j = lane + 64 * m;
-        h[m] = j < D ? ldr(src + j) : 0.f;
+        h[m] = j < D ? src[j] : 0.f;
         h0[m] = h[m];
       }
     }
@@ -113,11 +108,11 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const RT* __restrict__ ro
       }
 #pragma unroll
       for (int q = 0; q < SG; ++q) {  // all loads of the group in flight
-        const RT* src = rows_out + (int64_t)(row[q] < 0 ? 0 : row[q]) * D;
+        const float* src = rows_out + (int64_t)(row[q] < 0 ? 0 : row[q]) * D;
 #pragma unroll
         for (int m = 0; m < NPL; ++m) {
           const int j = lane + 64 * m;
-          xv[q][m] = (row[q] >= 0 && j < D) ? ldr(src + j) : 0.f;
+          xv[q][m] = (row[q] >= 0 && j < D) ? src[j] : 0.f;
         }
       }
 #pragma unroll
@@ -174,12 +169,12 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const RT* __restrict__ ro
 constexpr int SR_C = 256;  // sorted entries per wave
 constexpr int SR_G = 8;    // center rows in flight per lane
 
-template <int NPL, typename RT = float>
+template <int NPL>
 __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restrict__ srow,
                                                         const int64_t* __restrict__ perm,
                                                         const float* __restrict__ gbuf,
                                                         const int32_t* __restrict__ pos_c, int k1, int64_t n,
-                                                        const RT* __restrict__ rows_h, int D,
+                                                        const float* __restrict__ rows_h, int D,
                                                         float* __restrict__ d_out,
                                                         const int32_t* __restrict__ wmap_out) {
   __shared__ int32_t s_row[4][SR_C], s_cen[4][SR_C];
@@ -227,11 +222,11 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 #pragma unroll
     for (int q = 0; q < SR_G; ++q) {  // all SR_G center rows in flight
       const int i = min(i0 + q, m_n - 1);
-      const RT* src = rows_h + (int64_t)s_cen[wv][i] * D;
+      const float* src = rows_h + (int64_t)s_cen[wv][i] * D;
 #pragma unroll
       for (int m = 0; m < NPL; ++m) {
         const int j = lane + 64 * m;
-        hv[q][m] = j < D ? ldr(src + j) : 0.f;
+        hv[q][m] = j < D ? src[j] : 0.f;
       }
     }
 #pragma unroll
@@ -258,10 +253,9 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 // Sorted form, pass 1: centers as in fps_sgns_standard (d_in), output-row
 // coefficients into gbuf[P * (k + 1)] (zeroed by the caller; skipped negatives
 // stay 0).
-FPS_API int fps_sgns_standard_coef(const void* rows_in, const void* rows_out, const int32_t* pos_c,
+FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, const int32_t* pos_c,
                                    const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
-                                   float* d_in, const int32_t* wmap_in, float* loss, float* gbuf, int rows_bf16,
-                                   void* stream) {
+                                   float* d_in, const int32_t* wmap_in, float* loss, float* gbuf, void* stream) {
   if (P <= 0) return 0;
   if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
   const int chunk = 16;
@@ -269,19 +263,16 @@ FPS_API int fps_sgns_standard_coef(const void* rows_in, const void* rows_out, co
   const int64_t blocks = (waves + 3) / 4;
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-#define FPS_SGC_(NPL_, RT_)                                                                                      \
-  hipLaunchKernelGGL((sgns_std_kernel<NPL_, true, RT_>), dim3((unsigned)blocks), dim3(256), 0, s,                 \
-                     (const RT_*)rows_in, (const RT_*)rows_out, pos_c, pos_o, pos_neg, P, D, k, lr, d_in,          \
-                     (float*)nullptr, wmap_in, (const int32_t*)nullptr, loss, chunk, gbuf)
-#define FPS_SGC(NPL_) \
-  do { if (rows_bf16) { FPS_SGC_(NPL_, uint16_t); } else { FPS_SGC_(NPL_, float); } } while (0)
+#define FPS_SGC(NPL_)                                                                                            \
+  hipLaunchKernelGGL((sgns_std_kernel<NPL_, true>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
+                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, wmap_in, (const int32_t*)nullptr,  \
+                     loss, chunk, gbuf)
   if (D <= 64) FPS_SGC(1);
   else if (D <= 128) FPS_SGC(2);
   else if (D <= 256) FPS_SGC(4);
   else if (D <= 320) FPS_SGC(5);
   else FPS_SGC(8);
 #undef FPS_SGC
-#undef FPS_SGC_
   FPS_CHECK_LAUNCH();
   return 0;
 }
@@ -289,25 +280,22 @@ FPS_API int fps_sgns_standard_coef(const void* rows_in, const void* rows_out, co
 // Sorted form, pass 2: d_out[srow[t]] += gbuf[perm[t]] * rows_h[pos_c[perm[t] / k1]]
 // over the n = P * k1 entries sorted by output row.
 FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float* gbuf, const int32_t* pos_c, int k1,
-                          int64_t n, const void* rows_h, int D, float* d_out, const int32_t* wmap_out, int rows_bf16,
+                          int64_t n, const float* rows_h, int D, float* d_out, const int32_t* wmap_out,
                           void* stream) {
   if (n <= 0) return 0;
   if (D <= 0 || D > 512 || k1 <= 0) return (int)hipErrorInvalidValue;
   const int64_t blocks = (n + 4 * SR_C - 1) / (4 * SR_C);
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-#define FPS_SGR_(NPL_, RT_)                                                                                      \
-  hipLaunchKernelGGL((sgns_rows_kernel<NPL_, RT_>), dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf,    \
-                     pos_c, k1, n, (const RT_*)rows_h, D, d_out, wmap_out)
-#define FPS_SGR(NPL_) \
-  do { if (rows_bf16) { FPS_SGR_(NPL_, uint16_t); } else { FPS_SGR_(NPL_, float); } } while (0)
+#define FPS_SGR(NPL_)                                                                                            \
+  hipLaunchKernelGGL(sgns_rows_kernel<NPL_>, dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf, pos_c, k1, \
+                     n, rows_h, D, d_out, wmap_out)
   if (D <= 64) FPS_SGR(1);
   else if (D <= 128) FPS_SGR(2);
   else if (D <= 256) FPS_SGR(4);
   else if (D <= 320) FPS_SGR(5);
   else FPS_SGR(8);
 #undef FPS_SGR
-#undef FPS_SGR_
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -201,10 +201,7 @@ class DistributedSGNS:
         pos_neg = plan_out.pos[P:].contiguous()
         with stage("sgns.step", self.timer):
             if self.standard:
-                # bf16 wire rows go to the kernel as they arrived (it widens them as it loads)
-                bf = rows_in.dtype == torch.bfloat16 and rows_out.dtype == torch.bfloat16 and dev.type == "cuda"
-                loss = ops.sgns_standard(rows_in if bf else rows_in.float(), rows_out if bf else rows_out.float(),
-                                         plan_in.pos.contiguous(), pos_o, pos_neg,
+                loss = ops.sgns_standard(rows_in.float(), rows_out.float(), plan_in.pos.contiguous(), pos_o, pos_neg,
                                          c.negatives, lr, d_in, d_out, with_loss=with_loss, wmap_in=wm_in,
                                          wmap_out=wm_out)
             else:

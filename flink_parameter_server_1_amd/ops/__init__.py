@@ -840,14 +840,9 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
     if pos_neg.numel() != P * k:
         raise ValueError("sgns_standard: pos_neg needs k rows per pair")
     if rows_in.is_cuda:
-        for t in (d_in, d_out):
+        for t in (rows_in, rows_out, d_in, d_out):
             if t.dtype != torch.float32:
-                raise ValueError("sgns_standard: fp32 deltas")
-        rows_bf16 = rows_in.dtype == torch.bfloat16
-        if rows_in.dtype != rows_out.dtype or rows_in.dtype not in (torch.float32, torch.bfloat16):
-            raise ValueError("sgns_standard: rows_in / rows_out both fp32 or both bf16")
-        if rows_bf16 and (method or os.environ.get("FPS_SGNS_METHOD", "sorted")) != "sorted":
-            raise ValueError("sgns_standard: bf16 rows need the sorted method")
+                raise ValueError("sgns_standard: fp32 rows and deltas")
         if D > 512:
             raise ValueError("sgns_standard: D <= 512")
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
@@ -863,14 +858,12 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
             gbuf = torch.zeros(P * k1, dtype=torch.float32, device=rows_in.device)
             N.check(lib.fps_sgns_standard_coef(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                                _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
-                                               _c(d_in).data_ptr(), N.ptr(wmap_in), N.ptr(loss), gbuf.data_ptr(),
-                                               int(rows_bf16), s),
+                                               _c(d_in).data_ptr(), N.ptr(wmap_in), N.ptr(loss), gbuf.data_ptr(), s),
                     "sgns_coef")
             keys = torch.cat([pos_o.reshape(P, 1), pos_neg.reshape(P, int(k))], dim=1).reshape(-1)
             srow, perm = torch.sort(keys.to(torch.int32))
             N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
-                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out),
-                                      int(rows_bf16), s),
+                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out), s),
                     "sgns_rows")
             return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),

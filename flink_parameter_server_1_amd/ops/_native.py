@@ -93,8 +93,8 @@ _SIGNATURES = {
     "fps_sgns_standard": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_vp],
     "fps_sgns_standard_coef": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp,
-                               c_int, c_vp],
-    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_int, c_vp],
+                               c_vp],
+    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {}

@@ -409,35 +409,6 @@ def test_sgns_ps_path_fused_local_push_equals_pushed_deltas(device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D", [64, 300])
-def test_sgns_standard_bf16_rows_equal_widened_rows(D):
-    """PS path at N > 1 (bf16 wire): the sorted kernel reads bf16 rows as they arrived;
-    it must equal the same kernel on the rows widened to fp32 (the conversion pass it
-    replaces) -- and the fp32 reference on those widened rows."""
-    torch.manual_seed(D)
-    Uin, Uout, P, k = 300, 400, 3000, 5
-    rows_in = (torch.randn(Uin, D) * 0.3).to(torch.bfloat16)
-    rows_out = (torch.randn(Uout, D) * 0.3).to(torch.bfloat16)
-    pos_c = torch.sort(torch.randint(0, 60, (P,), dtype=torch.int32)).values
-    pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
-    pos_neg = torch.randint(0, Uout, (P * k,), dtype=torch.int32)
-    dev = "cuda"
-    out = []
-    for rin, rout in ((rows_in, rows_out), (rows_in.float(), rows_out.float())):
-        d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
-        loss = ops.sgns_standard(rin.to(dev), rout.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k, 0.05,
-                                 d_in, d_out, with_loss=True, method="sorted")
-        out.append((d_in.cpu(), d_out.cpu(), float(loss)))
-    torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-5, atol=1e-6)
-    assert abs(out[0][2] - out[1][2]) <= 1e-5 * abs(out[1][2])
-    d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
-    R.sgns_standard(rows_in.float(), rows_out.float(), pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r,
-                    method="sorted")
-    torch.testing.assert_close(out[0][1], d_out_r, rtol=1e-4, atol=5e-6)
-
-
-@pytest.mark.gpu
 def test_sgns_direct_path_equals_sequential_reference():
     """The W = 1 direct path on the GPU (kernel updates the tables in place) trains like
     the sequential reference loop (``reference.sgns_standard``, sorted output-row form,
