@@ -121,7 +121,7 @@ class BoundedStalenessPipeline:
             self._planned.append((self.ps.plan_begin(keys, flag, presence=presence), payload))
         self.submitted += 1
         out: List[Any] = []
-        if self.interleave:
+        if self.interleave and self.staleness > 0 and self.lookahead:  # (a synchronous call drops to the plain path)
             # keys of the batches beyond the lookahead posted; the oldest pulled batches
             # computed and their pushes posted; then the new ones served; then the pushes
             # applied (module docstring: the same staleness bound)
