@@ -45,7 +45,7 @@ def main():
                          "timing, a one-wave device sleep for the link time + a real device copy); 0 = no transfers")
     ap.add_argument("--latency-us", type=float, default=5.0)
     ap.add_argument("--user-update", default="auto", choices=["auto", "store", "sc1", "atomic"],
-                    help="auto = what bench.py runs at this world size (atomic at N > 1)")
+                    help="auto = what bench.py runs at every world size (store: Hogwild user rows)")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="sub-steps on alternating compute streams (MFConfig.overlap_substeps; auto: from 4 ranks)")
     a = ap.parse_args()
