@@ -1,0 +1,56 @@
+"""Probe: is the emulated link's device sleep (``vworld._Sleep``, calibrated on an idle
+GPU) accurate while the tiled SGD fills the GPU?  Times 160-us sleeps on a high-priority
+side stream, idle and beside the N = 8 rotation step (EmulatedRotation without links)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
+    from flink_parameter_server_1_amd.parallel.comm import Comm
+    from flink_parameter_server_1_amd.parallel.vworld import _Sleep
+
+    dev = torch.device("cuda", 0)
+    side = torch.cuda.Stream(dev, priority=-1)
+    cyc = _Sleep.calibrate(dev)
+
+    def sleeps(n, us):
+        out = []
+        for _ in range(n):
+            a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            with torch.cuda.stream(side):
+                a.record(side)
+                _Sleep.us(dev, us)
+                b.record(side)
+            out.append((a, b))
+        return out
+
+    idle = sleeps(20, 160.0)
+    torch.cuda.synchronize()
+    idle_ms = [a.elapsed_time(b) for a, b in idle]
+    m = DistributedMF(MFConfig(emulate_world=8, exchange="rotate"), Comm(device=dev))
+    data = SyntheticRatings(10_000_000, 1_000_000, 1 << 27, 0, 1, device=dev)
+    batch = [data.batch(s, 1 << 26) for s in range(2)]
+    for s in range(3):
+        m.step(*batch[s % 2])
+    torch.cuda.synchronize()
+    loaded = []
+    for s in range(4):
+        m.step(*batch[s % 2])
+        loaded += sleeps(10, 160.0)
+    m.flush()
+    torch.cuda.synchronize()
+    load_ms = [a.elapsed_time(b) for a, b in loaded]
+    print(json.dumps({"cycles_per_us": cyc, "requested_us": 160.0,
+                      "idle_us_median": sorted(idle_ms)[len(idle_ms) // 2] * 1e3,
+                      "loaded_us_median": sorted(load_ms)[len(load_ms) // 2] * 1e3,
+                      "loaded_us_max": max(load_ms) * 1e3, "loaded_us_min": min(load_ms) * 1e3}))
+
+
+if __name__ == "__main__":
+    main()
