@@ -34,7 +34,7 @@ def main():
     torch.cuda.synchronize()
     idle_ms = [a.elapsed_time(b) for a, b in idle]
     m = DistributedMF(MFConfig(emulate_world=8, exchange="rotate"), Comm(device=dev))
-    data = SyntheticRatings(10_000_000, 1_000_000, 1 << 27, 0, 1, device=dev)
+    data = SyntheticRatings(10_000_000, 1_000_000, 1 << 27, 0, 8, device=dev)  # rank 0 of 8: its 1.25M users
     batch = [data.batch(s, 1 << 26) for s in range(2)]
     for s in range(3):
         m.step(*batch[s % 2])

@@ -62,11 +62,18 @@ struct TileGeo {
   int W, R, T;
   FastDiv dW, dR, dU, dT, d2W;
   const int32_t* half;
+  int32_t nu, ni;  // valid local user / item ids: [0, nu) x [0, ni); a rating outside is dropped
 };
 
-static TileGeo make_geo(int W, const int32_t* half, int R, int T, int upp) {
+static TileGeo make_geo(int W, const int32_t* half, int R, int T, int upp, int nu, int ni) {
   return TileGeo{W, R, T, make_fastdiv(W), make_fastdiv(R), make_fastdiv(upp), make_fastdiv(T), make_fastdiv(2 * W),
-                 half};
+                 half, nu > 0 ? nu : INT32_MAX, ni > 0 ? ni : INT32_MAX};
+}
+
+// a rating the partition may bucket: an out-of-range id would index past the bucket
+// counters here and past the tables in the SGD (a device fault), so it is dropped
+__device__ __forceinline__ bool tile_valid(int32_t i, int32_t u, const TileGeo& g) {
+  return (uint32_t)i < (uint32_t)g.ni && (uint32_t)u < (uint32_t)g.nu;
 }
 
 // the global item of a record from its bucket and row in block (tile_bucket's inverse)
@@ -282,7 +289,7 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
         }
 #pragma unroll
         for (int j = 0; j < U4; ++j) {
-          if (iv[j] < 0) continue;
+          if (iv[j] < 0 || !tile_valid(iv[j], uv[j], g)) continue;
           int bk; int32_t row;
           tile_bucket(iv[j], uv[j], g, bk, row);
           if constexpr (H16) {
@@ -474,15 +481,19 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       if (tid < nk) cnt[tid] = 0;
       int4 r[E];
       int k[E], slot[E];
+      bool ok[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {  // this batch's records
         k[e] = 0;
         const int p = e * 1024 + tid;
+        ok[e] = p < nb;
         if (p >= nb) continue;
         const int64_t x = b0 + p;
         if (LEVEL == 1) {
           const int32_t u = tp_ld<true>(uid + x), i = tp_ld<true>(iid + x);
           const int32_t rb = __float_as_int(tp_ld<true>(rating + x));
+          ok[e] = tile_valid(i, u, g);  // the count pass skipped it too
+          if (!ok[e]) continue;
           int bk; int32_t row;
           tile_bucket(i, u, g, bk, row);
           if (REC8) r[e] = make_int4(u | ((row & (g.R - 1)) << 24), rb, bk, 0);
@@ -502,7 +513,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int p = e * 1024 + tid;
-        slot[e] = p < nb ? atomicAdd(cnt + k[e], 1) : -1;
+        slot[e] = ok[e] ? atomicAdd(cnt + k[e], 1) : -1;
       }
       __syncthreads();
       tp3_scan(cnt, off, nk);
@@ -512,7 +523,8 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       for (int e = 0; e < E; ++e)
         if (slot[e] >= 0) srt[off[k[e]] + slot[e]] = r[e];
       __syncthreads();
-      for (int p = tid; p < nb; p += 1024) {
+      const int nv = off[nk - 1] + cnt[nk - 1];  // records kept (level 1 drops invalid ones)
+      for (int p = tid; p < nv; p += 1024) {
         const int4 x = srt[p];
         const int bk = REC8 ? x.z : x.w;
         const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
@@ -856,14 +868,16 @@ static int g_tp_grid = 0;
 FPS_API void fps_tile_partition_set_grid(int v) { g_tp_grid = v; }
 
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
-                               const int32_t* half, int R, int T, int P, int upp, int32_t* ws, int4* tmp, int32_t* ptr,
-                               void* rec, int rec8, uint8_t* seen, void* stream) {
+                               const int32_t* half, int R, int T, int P, int upp, int nu, int ni, int32_t* ws,
+                               int4* tmp, int32_t* ptr, void* rec, int rec8, uint8_t* seen, void* stream) {
   const int KT = P * 2 * W * T;
   if (KT > TP_MAX_BUCKETS || R <= 0 || T <= 0) return (int)hipErrorInvalidValue;
   const int cshift = tp3_cshift(KT);
   const int NC = ((KT - 1) >> cshift) + 1;
   if (NC > TP3_MAXK || (1 << cshift) > TP3_MAXK) return (int)hipErrorInvalidValue;
-  const TileGeo g = make_geo(W, half, R, T, upp);
+  // user ids past the phases' range would land past the KT bucket counters
+  if (nu <= 0 || (int64_t)nu > (int64_t)P * upp) nu = (int)min((int64_t)P * upp, (int64_t)INT32_MAX);
+  const TileGeo g = make_geo(W, half, R, T, upp, nu, ni);
   hipStream_t s = (hipStream_t)stream;
   int32_t* ccount = ws;
   int32_t* ccursor = ccount + NC;

@@ -208,8 +208,9 @@ class DistributedMF:
             # two received batches wait for their compute -> three partition buffers
             ps_spec = exchange == "ps" and cfg.prefetch_partition and dev.type == "cuda"
             n_tilers = 2 if exchange != "ps" else (3 if ps_spec else 1)
+            bounds = dict(num_users=self.users.n_local, num_items=cfg.num_items)
             self._tilers = [ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8,
-                                                phases=self.user_phases, users_per_phase=upp)
+                                                phases=self.user_phases, users_per_phase=upp, **bounds)
                             for _ in range(n_tilers)]
             # PS path, identity plans: the partition's count pass marks the items a batch
             # rates (one flag array per partition buffer) -- the plan's presence flags, so
@@ -224,7 +225,7 @@ class DistributedMF:
             # the PS path's own partition (batches without an identity plan)
             self._ps_tiler = self._tilers[0] if not ps_spec else \
                 ops.TilePartitioner(tile_w, halves, tile_R, self.tile_T, dev, rec8=rec8, phases=self.user_phases,
-                                    users_per_phase=upp)
+                                    users_per_phase=upp, **bounds)
             # the partition of batch k+1 runs on a side stream beside the SGD of batch k
             # (a priority stream for the SGD and CU-masked streams splitting the CUs
             # between them were measured slower and removed, profiles/r2_partition.md)

@@ -507,8 +507,12 @@ class TilePartitioner:
     ``profiles/r2_tp4.md``) and were removed."""
 
     def __init__(self, W: int, half, R: int, T: int, device, rec8: bool = False, phases: int = 1,
-                 users_per_phase: Optional[int] = None):
+                 users_per_phase: Optional[int] = None, num_users: int = 0, num_items: int = 0):
+        """``num_users`` (local rows of the user shard) / ``num_items``: ratings with an id
+        outside are dropped by the partition instead of indexing past the bucket counters
+        and the tables (0 = no bound beyond the phases' user range)."""
         self.W, self.R, self.T = W, int(R), int(T)
+        self.nu, self.ni = int(num_users), int(num_items)
         self.P = max(1, int(phases))
         self.upp = int(users_per_phase) if (self.P > 1 and users_per_phase) else (1 << 30)
         if self.P > 1 and not users_per_phase:
@@ -527,6 +531,11 @@ class TilePartitioner:
 
     def run(self, uid, iid, rating, seen: Optional[torch.Tensor] = None):
         if self.device.type != "cuda":
+            nu = self.nu if self.nu > 0 else self.P * self.upp
+            ni = self.ni if self.ni > 0 else (1 << 31) - 1
+            keep = (uid >= 0) & (uid < nu) & (iid >= 0) & (iid < ni)  # as the kernels: drop, never index
+            if not bool(keep.all()):
+                uid, iid, rating = uid[keep], iid[keep], rating[keep]
             if seen is not None:
                 seen[iid.long()] = 1
             ptr, u, row, r = R.tile_partition(uid, iid, rating, self.W, self.half, self.R, self.T, self.P,
@@ -548,7 +557,8 @@ class TilePartitioner:
             self.ws = torch.empty(lib.fps_tile_partition_ws_ints(self.W, self.T, self.P), dtype=torch.int32,
                                   device=self.device)
         N.check(lib.fps_tile_partition(_c(uid).data_ptr(), _c(iid).data_ptr(), _c(rating).data_ptr(), n, self.W,
-                                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.ws.data_ptr(),
+                                       self.half.data_ptr(), self.R, self.T, self.P, self.upp, self.nu, self.ni,
+                                       self.ws.data_ptr(),
                                        self.tmp.data_ptr(), self.ptr.data_ptr(), self.rec.data_ptr(), int(self.rec8),
                                        N.ptr(seen), N.stream_ptr(self.device)), "tile_partition")
         return self.ptr, self.rec[:n]

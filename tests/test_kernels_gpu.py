@@ -307,6 +307,40 @@ def test_tile_partition_matches_reference(W, R, rec8, skew, phases):
     assert torch.equal(seen.cpu().bool(), torch.bincount(iid.long(), minlength=NI) > 0)
 
 
+@pytest.mark.parametrize("rec8", [False, True])
+@pytest.mark.parametrize("W,phases", [(1, 1), (8, 3)])
+def test_tile_partition_drops_out_of_range_ids(W, phases, rec8):
+    """Ratings whose user or item id lies outside the tables (negative, or at / past the
+    bound) are dropped by the partition -- the count and level-1 passes skip them alike --
+    instead of indexing past the bucket counters and, in the SGD, past the tables: the
+    result equals the partition of the valid ratings alone."""
+    from flink_parameter_server_1_amd.parallel.rotation import block_rows, shard_halves
+
+    NI, NU, n, R = 50_003, 9_000, 300_000, 64
+    half = [NI] if W == 1 else shard_halves(NI, W)
+    T = -(-(NI if W == 1 else max(block_rows(NI, W))) // R)
+    upp = -(-NU // phases)
+    g = torch.Generator().manual_seed(W + phases)
+    uid = torch.randint(0, NU, (n,), dtype=torch.int32, generator=g)
+    iid = torch.randint(0, NI, (n,), dtype=torch.int32, generator=g)
+    bad = torch.rand(n, generator=g)
+    uid = torch.where(bad < 0.02, NU + (uid % 7), uid)          # past the user shard (inside the phases' range
+    uid = torch.where((bad >= 0.02) & (bad < 0.03), -1 - uid % 5, uid)  # at phases * upp >= NU) / negative
+    iid = torch.where((bad >= 0.03) & (bad < 0.05), NI + (iid % 11), iid)
+    r = torch.rand(n, generator=g)
+    keep = (uid >= 0) & (uid < NU) & (iid < NI)
+    part = ops.TilePartitioner(W, half, R, T, DEV, rec8=rec8, phases=phases, users_per_phase=upp,
+                               num_users=NU, num_items=NI)
+    ptr, rec = part.run(uid.to(DEV), iid.to(DEV), r.to(DEV))
+    p_ref, u_ref, row_ref, r_ref = R_tile(uid[keep], iid[keep], r[keep], W, torch.tensor(half, dtype=torch.int32), R,
+                                          T, phases, upp)
+    assert torch.equal(ptr.cpu(), p_ref) and int(p_ref[-1]) == int(keep.sum()) < n
+    u, row, rr = part.unpack(rec[: int(p_ref[-1])], ptr)
+    bucket = torch.repeat_interleave(torch.arange(p_ref.numel() - 1), (p_ref[1:] - p_ref[:-1]).long())
+    key = lambda U_, Rw, Rt: sorted(zip(bucket.tolist(), U_.tolist(), Rw.tolist(), Rt.tolist()))  # noqa: E731
+    assert key(u.cpu(), row.cpu(), rr.cpu()) == key(u_ref, row_ref, r_ref)
+
+
 @pytest.mark.parametrize("W,R,skew", [(1, 128, True), (8, 64, False), (1, 16, True)])
 def test_tile_partition_32bit_counters_match_reference(W, R, skew, monkeypatch):
     """The 32-bit counter path of the count kernel (``FPS_TP_H16=0``; 16-bit packed
