@@ -56,6 +56,8 @@ def main(argv=None):
     ap.add_argument("--emulate-rank", type=int, default=-1,
                     help="--emulate-world: the rank to emulate (-1: the shard owning the most de-duplicated keys of "
                          "the first batch -- the owner the job waits for)")
+    ap.add_argument("--host-profile", default=None,
+                    help="write a cProfile summary of the timed loop's host (Python) time to this file")
     ap.add_argument("--link-gbps", type=float, default=50.0, help="--emulate-world: per-peer link rate (GB/s)")
     ap.add_argument("--latency-us", type=float, default=5.0, help="--emulate-world: per-message link latency")
     a = ap.parse_args(argv)
@@ -104,13 +106,31 @@ def main(argv=None):
     emu = a.emulate_world > 1
     if emu and dev.type == "cuda":
         comm.wait_ms()  # drop the warm-up's waits
+    prof = None
+    if a.host_profile:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for s in range(a.steps):
         m.train_step(*batches[s % 4])
+    t_host = time.perf_counter() - t0  # host time to enqueue the steps
     m.flush()  # the last batches' pushes land inside the timed region
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
+    if prof is not None:
+        import io
+        import pstats
+
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+        with open(a.host_profile, "w") as f:
+            f.write(f"host enqueue time per step: {t_host / a.steps * 1e3:.3f} ms; wall per step "
+                    f"{dt / a.steps * 1e3:.3f} ms\n")
+            f.write(buf.getvalue())
     wait_ms = comm.wait_ms() / a.steps if emu and dev.type == "cuda" else 0.0
     ip, idx, val, lab = batches[0]  # accuracy on a trained batch (1B features: held-out rows share few features)
     pred = m.predict(ip, idx, val)
