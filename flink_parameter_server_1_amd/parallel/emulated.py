@@ -71,8 +71,8 @@ class SymmetricComm(Comm):
         self.world, self.rank, self.backend = int(world), int(rank), "emulated"
         #: owner-side model: every peer sends this rank what it sends itself (module docstring)
         self.hot_owner = bool(hot_owner)
-        #: rows received per all-to-all (the owner-side load the model produced), for tests
-        self.recv_rows: List[int] = []
+        #: rows received over all all-to-alls (the owner-side load the model produced)
+        self.recv_rows_total = 0
         self.peer_bytes = [0] * self.world
         self.link_gbps, self.latency_us = float(link_gbps), float(latency_us)
         self.cuda = self.device.type == "cuda"
@@ -136,16 +136,14 @@ class SymmetricComm(Comm):
         if self.hot_owner:  # full-duplex links: the busier direction of each
             peer += [int(n) * row_bytes for j, n in enumerate(recv_splits) if j != self.rank]
         self._count(send, send_splits)
-        self.recv_rows.append(int(sum(recv_splits)))
+        self.recv_rows_total += int(sum(recv_splits))
         if not self.cuda:
             self._fill(send, out, send_splits, recv_splits)
             return None
         from .vworld import _Sleep
 
         us = (self.latency_us + (max(peer) if peer else 0) * 1e-3 / self.link_gbps) if self.world > 1 else 0.0
-        posted = torch.cuda.Event()
-        posted.record()
-        self._link.wait_event(posted)
+        self._link.wait_stream(torch.cuda.current_stream(self.device))  # the send is ready in post order
         with torch.cuda.stream(self._link):
             _Sleep.us(self.device, us)
             self._fill(send, out, send_splits, recv_splits)
