@@ -126,7 +126,10 @@ def main(argv=None):
 
         prof.disable()
         buf = io.StringIO()
-        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+        st = pstats.Stats(prof, stream=buf)
+        st.sort_stats("tottime").print_stats(40)
+        st.sort_stats("cumulative").print_stats(60)
+        st.print_callers("current_stream|_get_device_index|is_available|Event.record|__init__.py.*stream")
         with open(a.host_profile, "w") as f:
             f.write(f"host enqueue time per step: {t_host / a.steps * 1e3:.3f} ms; wall per step "
                     f"{dt / a.steps * 1e3:.3f} ms\n")
