@@ -237,12 +237,20 @@ __device__ __forceinline__ int32_t hb_get(const int32_t* hb, int b) {
   else return hb[b];
 }
 
-template <bool H16>
-__global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restrict__ uid,
-                                                         const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
-                                                         int G, int sub, TileGeo g, int cshift, int NC, int KT,
-                                                         int32_t* __restrict__ ccount, int32_t* __restrict__ bcount,
-                                                         uint8_t* __restrict__ seen, int32_t* __restrict__ H1) {
+// The partition kernels come in two shapes (``fps_tile_partition_set_slim``):
+//  * fat: 1024-thread workgroups (the round-1..5 shape), fastest alone;
+//  * slim: 256-thread workgroups of <= 32 VGPRs and <= ~35 KiB of LDS.  The tile SGD
+//    beside which the partition of the next batch runs holds 3 workgroups per CU at
+//    80 VGPRs (6 of 8 waves per SIMD, 480 of 512 registers, 114 KiB of LDS); a fat
+//    partition workgroup fits only where one of them left, so every one displaced a
+//    third of a CU's SGD.  A slim one fits in what the three leave free (one wave per
+//    SIMD, 32 registers, 46 KiB): the partition then takes memory bandwidth from the SGD
+//    but no occupancy.
+template <bool H16, int BS, int U4>
+__device__ __forceinline__ void tp3_count_body(const int32_t* __restrict__ uid, const int32_t* __restrict__ iid,
+                                               int64_t n, int64_t chunk, int G, int sub, const TileGeo& g, int cshift,
+                                               int NC, int KT, int32_t* __restrict__ ccount,
+                                               int32_t* __restrict__ bcount, int32_t* __restrict__ H1) {
   // One LDS atomic per rating (LDS atomics run at ~1 lane per CU cycle and
   // bound this kernel); the coarse counts of a chunk are read off the fine
   // histogram afterwards: 8 lanes per coarse key sum its 2^cshift buckets.
@@ -250,16 +258,16 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
   __shared__ int32_t hc_prev[TP3_MAXK], hc_acc[TP3_MAXK];
   __shared__ int32_t s_ovf, s_flushed;
   const int KW = H16 ? (KT + 1) / 2 : KT;
-  for (int k = threadIdx.x; k < KW; k += blockDim.x) hb[k] = 0;
-  if (threadIdx.x < NC) { hc_prev[threadIdx.x] = 0; hc_acc[threadIdx.x] = 0; }
+  for (int k = threadIdx.x; k < KW; k += BS) hb[k] = 0;
+  for (int k = threadIdx.x; k < NC; k += BS) { hc_prev[k] = 0; hc_acc[k] = 0; }
   if (threadIdx.x == 0) { s_ovf = 0; s_flushed = 0; }
   __syncthreads();
   int32_t* Hf = bcount + (int64_t)(blockIdx.x + 1) * KT;  // row 0 = the totals (tp3_colsum_kernel)
   const int span = 1 << cshift;
   const int per = (span + 7) / 8;
-  const int ck = threadIdx.x >> 3, cl = threadIdx.x & 7;  // coarse key, lane in its group of 8
-  // coarse key ck's count now (summed by its 8 lanes; every lane gets the total)
-  auto coarse_now = [&]() {
+  const int cl = threadIdx.x & 7;  // lane in a coarse key's group of 8
+  // coarse key ck's count now (summed by its 8 lanes; every lane of the group gets the total)
+  auto coarse_now = [&](int ck) {
     int32_t tot = 0;
     if (ck < NC)
       for (int q = 0; q < per; ++q) {
@@ -271,19 +279,21 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
     tot += __shfl_xor(tot, 4, 64);
     return tot;
   };
+  // the coarse keys of this thread's group of 8 (NC <= 256: one pass at BS = 1024 and NC <= 128)
+  constexpr int CKS = BS / 8;
   const int c0 = blockIdx.x * sub, c1 = min(G, c0 + sub);
   for (int c = c0; c < c1; ++c) {
     const int64_t lo = (int64_t)c * chunk, hi = min(n, lo + chunk);
-    constexpr int U4 = 8;  // loads in flight per thread (a lone dependent load pair per
-                           // iteration left the kernel latency-bound at ~1.7 TB/s)
-    const int64_t step = (int64_t)U4 * blockDim.x;
+    // U4: loads in flight per thread (a lone dependent load pair per iteration left the
+    // kernel latency-bound at ~1.7 TB/s)
+    const int64_t step = (int64_t)U4 * BS;
     for (int64_t s0 = lo; s0 < hi; s0 += (H16 ? H16_SB : hi - lo)) {
       const int64_t s1 = H16 ? min(hi, s0 + H16_SB) : hi;
       for (int64_t x0 = s0 + threadIdx.x; x0 < s1; x0 += step) {
         int32_t iv[U4], uv[U4];
 #pragma unroll
         for (int j = 0; j < U4; ++j) {
-          const int64_t x = x0 + (int64_t)j * blockDim.x;
+          const int64_t x = x0 + (int64_t)j * BS;
           iv[j] = x < s1 ? iid[x] : -1;
           uv[j] = x < s1 ? uid[x] : 0;
         }
@@ -312,11 +322,11 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
           bool hit = false;
           const int KW4 = KW >> 2;
           const uint4* h4 = reinterpret_cast<const uint4*>(hb);
-          for (int k = threadIdx.x; k < KW4; k += blockDim.x) {
+          for (int k = threadIdx.x; k < KW4; k += BS) {
             const uint4 w = h4[k];
             hit |= ((w.x | w.y | w.z | w.w) & 0x80008000u) != 0u;
           }
-          for (int k = 4 * KW4 + threadIdx.x; k < KW; k += blockDim.x) hit |= (hb[k] & 0x80008000u) != 0u;
+          for (int k = 4 * KW4 + threadIdx.x; k < KW; k += BS) hit |= (hb[k] & 0x80008000u) != 0u;
           if (hit) s_ovf = 1;
         }
         __syncthreads();
@@ -325,30 +335,53 @@ __global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restri
         // every thread has read the flag before any can start the next sub-batch and set it again
         __syncthreads();
         if (ovf) {  // uniform: flush the histogram into the global row and restart it at zero
-          const int32_t tot = coarse_now();
-          if (ck < NC && cl == 0) { hc_acc[ck] += tot - hc_prev[ck]; hc_prev[ck] = 0; }
+          for (int ck0 = 0; ck0 < NC; ck0 += CKS) {
+            const int ck = ck0 + (threadIdx.x >> 3);
+            const int32_t tot = coarse_now(ck);
+            if (ck < NC && cl == 0) { hc_acc[ck] += tot - hc_prev[ck]; hc_prev[ck] = 0; }
+          }
           const bool first = !s_flushed;
-          for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = (first ? 0 : Hf[k]) + hb_get<true>(hb, k);
+          for (int k = threadIdx.x; k < KT; k += BS) Hf[k] = (first ? 0 : Hf[k]) + hb_get<true>(hb, k);
           __syncthreads();
-          for (int k = threadIdx.x; k < KW; k += blockDim.x) hb[k] = 0;
+          for (int k = threadIdx.x; k < KW; k += BS) hb[k] = 0;
           if (threadIdx.x == 0) { s_ovf = 0; s_flushed = 1; }
           __syncthreads();
         }
       }
     }
     __syncthreads();
-    const int32_t tot = coarse_now();
-    if (ck < NC && cl == 0) {
-      const int32_t v = hc_acc[ck] + tot - hc_prev[ck];
-      hc_prev[ck] = tot;
-      hc_acc[ck] = 0;
-      if (v) atomicAdd(ccount + ck, v);
-      H1[(int64_t)c * NC + ck] = v;
+    for (int ck0 = 0; ck0 < NC; ck0 += CKS) {
+      const int ck = ck0 + (threadIdx.x >> 3);
+      const int32_t tot = coarse_now(ck);
+      if (ck < NC && cl == 0) {
+        const int32_t v = hc_acc[ck] + tot - hc_prev[ck];
+        hc_prev[ck] = tot;
+        hc_acc[ck] = 0;
+        if (v) atomicAdd(ccount + ck, v);
+        H1[(int64_t)c * NC + ck] = v;
+      }
     }
     __syncthreads();  // hb is read above before the next chunk adds to it
   }
   const bool flushed = s_flushed;
-  for (int k = threadIdx.x; k < KT; k += blockDim.x) Hf[k] = (flushed ? Hf[k] : 0) + hb_get<H16>(hb, k);
+  for (int k = threadIdx.x; k < KT; k += BS) Hf[k] = (flushed ? Hf[k] : 0) + hb_get<H16>(hb, k);
+}
+
+template <bool H16>
+__global__ void __launch_bounds__(1024) tp3_count_kernel(const int32_t* __restrict__ uid,
+                                                         const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                                                         int G, int sub, TileGeo g, int cshift, int NC, int KT,
+                                                         int32_t* __restrict__ ccount, int32_t* __restrict__ bcount,
+                                                         uint8_t* __restrict__ seen, int32_t* __restrict__ H1) {
+  tp3_count_body<H16, 1024, 8>(uid, iid, n, chunk, G, sub, g, cshift, NC, KT, ccount, bcount, H1);
+}
+
+template <bool H16>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32)))
+tp3_count_slim_kernel(const int32_t* __restrict__ uid, const int32_t* __restrict__ iid, int64_t n, int64_t chunk,
+                      int G, int sub, TileGeo g, int cshift, int NC, int KT, int32_t* __restrict__ ccount,
+                      int32_t* __restrict__ bcount, uint8_t* __restrict__ seen, int32_t* __restrict__ H1) {
+  tp3_count_body<H16, 256, 4>(uid, iid, n, chunk, G, sub, g, cshift, NC, KT, ccount, bcount, H1);
 }
 
 // bcount[k] = sum of the count workgroups' rows bcount[1 + g][k]: 64 columns x 16
@@ -430,21 +463,18 @@ __global__ void tp3_workptr_kernel(const int32_t* __restrict__ ccount, int NC, i
 // / Infinity Cache for the SGD's user rows (+2 % end to end, profiles/r2_partition.md;
 // a register prefetch of the next batch and 16-B level-1 slots were measured slower
 // and removed in round 3).
-template <int LEVEL, bool REC8>
-__global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
-                                                           const int32_t* __restrict__ iid,
-                                                           const float* __restrict__ rating,
-                                                           const int4* __restrict__ tmp, int64_t n, int64_t chunk,
-                                                           TileGeo g,
-                                                           int cshift, int NC, int KT,
-                                                           const int32_t* __restrict__ kptr,
-                                                           int32_t* __restrict__ cursor,
-                                                           const int32_t* __restrict__ cptr,
-                                                           const int32_t* __restrict__ wptr,
-                                                           const int32_t* __restrict__ H1,
-                                                           void* __restrict__ out, uint8_t* __restrict__ seen) {
-  constexpr int E = TP3_B / 1024;
-  __shared__ int4 srt[TP3_B];
+// BS threads, B records per LDS batch (fat: 1024 / TP3_B; slim: 256 / 1024)
+template <int LEVEL, bool REC8, int BS, int B>
+__device__ __forceinline__ void tp3_scatter_body(const int32_t* __restrict__ uid, const int32_t* __restrict__ iid,
+                                                 const float* __restrict__ rating, const int4* __restrict__ tmp,
+                                                 int64_t n, int64_t chunk, const TileGeo& g, int cshift, int NC,
+                                                 int KT, const int32_t* __restrict__ kptr,
+                                                 int32_t* __restrict__ cursor, const int32_t* __restrict__ cptr,
+                                                 const int32_t* __restrict__ wptr, const int32_t* __restrict__ H1,
+                                                 void* __restrict__ out, uint8_t* __restrict__ seen) {
+  static_assert(BS >= TP3_MAXK, "one thread per key of a batch sort (nk <= TP3_MAXK)");
+  constexpr int E = B / BS;
+  __shared__ int4 srt[B];
   __shared__ int32_t cnt[TP3_MAXK], off[TP3_MAXK], base[TP3_MAXK];
   __shared__ int32_t s_item[3];  // level 2: lo, hi, key base of the current work item
   const int tid = threadIdx.x;
@@ -476,8 +506,8 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       nk = min(1 << cshift, KT - kb);
       __syncthreads();  // s_item is rewritten for the next work item
     }
-    for (int64_t b0 = lo; b0 < hi; b0 += TP3_B) {
-      const int nb = (int)min((int64_t)TP3_B, hi - b0);
+    for (int64_t b0 = lo; b0 < hi; b0 += B) {
+      const int nb = (int)min((int64_t)B, hi - b0);
       if (tid < nk) cnt[tid] = 0;
       int4 r[E];
       int k[E], slot[E];
@@ -485,7 +515,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
 #pragma unroll
       for (int e = 0; e < E; ++e) {  // this batch's records
         k[e] = 0;
-        const int p = e * 1024 + tid;
+        const int p = e * BS + tid;
         ok[e] = p < nb;
         if (p >= nb) continue;
         const int64_t x = b0 + p;
@@ -512,7 +542,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       __syncthreads();  // cnt zeroed
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const int p = e * 1024 + tid;
+        const int p = e * BS + tid;
         slot[e] = ok[e] ? atomicAdd(cnt + k[e], 1) : -1;
       }
       __syncthreads();
@@ -524,7 +554,7 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
         if (slot[e] >= 0) srt[off[k[e]] + slot[e]] = r[e];
       __syncthreads();
       const int nv = off[nk - 1] + cnt[nk - 1];  // records kept (level 1 drops invalid ones)
-      for (int p = tid; p < nv; p += 1024) {
+      for (int p = tid; p < nv; p += BS) {
         const int4 x = srt[p];
         const int bk = REC8 ? x.z : x.w;
         const int kk = LEVEL == 1 ? (bk >> cshift) : bk - kb;
@@ -551,6 +581,37 @@ __global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __rest
       if (LEVEL == 1 && tid < nk) base[tid] += cnt[tid];  // same thread zeroes cnt[tid] next
     }
   }
+}
+
+
+template <int LEVEL, bool REC8>
+__global__ void __launch_bounds__(1024) tp3_scatter_kernel(const int32_t* __restrict__ uid,
+                                                           const int32_t* __restrict__ iid,
+                                                           const float* __restrict__ rating,
+                                                           const int4* __restrict__ tmp, int64_t n, int64_t chunk,
+                                                           TileGeo g, int cshift, int NC, int KT,
+                                                           const int32_t* __restrict__ kptr,
+                                                           int32_t* __restrict__ cursor,
+                                                           const int32_t* __restrict__ cptr,
+                                                           const int32_t* __restrict__ wptr,
+                                                           const int32_t* __restrict__ H1,
+                                                           void* __restrict__ out, uint8_t* __restrict__ seen) {
+  tp3_scatter_body<LEVEL, REC8, 1024, TP3_B>(uid, iid, rating, tmp, n, chunk, g, cshift, NC, KT, kptr, cursor, cptr,
+                                             wptr, H1, out, seen);
+}
+
+// slim shape (see tp3_count_body): 1024-record batches, 16 KiB of LDS
+constexpr int TP3_SLIM_B = 1024;
+template <int LEVEL, bool REC8>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(32)))
+tp3_scatter_slim_kernel(const int32_t* __restrict__ uid, const int32_t* __restrict__ iid,
+                        const float* __restrict__ rating, const int4* __restrict__ tmp, int64_t n, int64_t chunk,
+                        TileGeo g, int cshift, int NC, int KT, const int32_t* __restrict__ kptr,
+                        int32_t* __restrict__ cursor, const int32_t* __restrict__ cptr,
+                        const int32_t* __restrict__ wptr, const int32_t* __restrict__ H1, void* __restrict__ out,
+                        uint8_t* __restrict__ seen) {
+  tp3_scatter_body<LEVEL, REC8, 256, TP3_SLIM_B>(uid, iid, rating, tmp, n, chunk, g, cshift, NC, KT, kptr, cursor,
+                                                 cptr, wptr, H1, out, seen);
 }
 
 // ---------------------------------------------------------------- SGD
@@ -866,6 +927,11 @@ FPS_API void fps_tile_partition_set_h16(int v) { g_tp_h16 = v; }
 // workgroups occupy fewer CUs beside the SGD of the previous batch (A/B knob, FPS_TP_GRID)
 static int g_tp_grid = 0;
 FPS_API void fps_tile_partition_set_grid(int v) { g_tp_grid = v; }
+// partition kernel shape (tp3_count_body): 0 = fat (1024-thread workgroups), 1 = slim
+// (256 threads, <= 32 VGPRs: co-resident with the tile SGD's three workgroups per CU)
+static int g_tp_slim = 0;
+FPS_API void fps_tile_partition_set_slim(int v) { g_tp_slim = v; }
+FPS_API int fps_tile_partition_get_slim() { return g_tp_slim; }
 
 FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const float* rating, int64_t n, int W,
                                const int32_t* half, int R, int T, int P, int upp, int nu, int ni, int32_t* ws,
@@ -901,7 +967,12 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
   // (profiles/r4_count_width_ab.txt)
   const bool h16 = g_tp_h16 != 0 || KT > 16384;  // 32-bit counters only fit 16k buckets
   const size_t hb_bytes = sizeof(int32_t) * (size_t)(h16 ? (KT + 1) / 2 : KT);
-  if (h16) {
+  // slim: the 16-bit histogram within what three SGD workgroups leave of a CU's LDS
+  const bool slim = g_tp_slim != 0 && h16 && hb_bytes <= 40 * 1024;
+  if (slim) {
+    hipLaunchKernelGGL(tp3_count_slim_kernel<true>, dim3(Gc), dim3(256), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
+                       cshift, NC, KT, ccount, bhist, (uint8_t*)nullptr, H1);
+  } else if (h16) {
     hipLaunchKernelGGL(tp3_count_kernel<true>, dim3(Gc), dim3(1024), hb_bytes, s, uid, iid, n, chunk, G, sub, g,
                        cshift, NC, KT, ccount, bhist, (uint8_t*)nullptr, H1);
   } else {
@@ -919,9 +990,14 @@ FPS_API int fps_tile_partition(const int32_t* uid, const int32_t* iid, const flo
     if (g_tp_grid > 0 && g2 > g_tp_grid) g2 = g_tp_grid;
     const int g1 = g_tp_grid > 0 ? min(G, g_tp_grid) : G;
 #define FPS_TP3(L, R8, GRID, TMP, KPTR, CUR, H1P, OUT)                                                            \
-    hipLaunchKernelGGL((tp3_scatter_kernel<L, R8>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, TMP, n, chunk, \
-                       g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT,         \
-                       L == 2 ? seen : (uint8_t*)nullptr)
+    if (slim)                                                                                                        \
+      hipLaunchKernelGGL((tp3_scatter_slim_kernel<L, R8>), dim3(GRID), dim3(256), 0, s, uid, iid, rating, TMP, n,   \
+                         chunk, g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT, \
+                         L == 2 ? seen : (uint8_t*)nullptr);                                                         \
+    else                                                                                                             \
+      hipLaunchKernelGGL((tp3_scatter_kernel<L, R8>), dim3(GRID), dim3(1024), 0, s, uid, iid, rating, TMP, n, chunk, \
+                         g, cshift, NC, KT, KPTR, CUR, (const int32_t*)cptr, (const int32_t*)wptr, H1P, OUT,       \
+                         L == 2 ? seen : (uint8_t*)nullptr)
     if (rec8) { FPS_TP3(1, true, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
     else { FPS_TP3(1, false, g1, (const int4*)nullptr, (const int32_t*)cptr, ccursor, (const int32_t*)H1, (void*)tmp); }
     if (rec8) { FPS_TP3(2, true, (int)g2, (const int4*)tmp, (const int32_t*)ptr, bcursor, (const int32_t*)nullptr, rec); }

@@ -548,6 +548,9 @@ class TilePartitioner:
         grid = os.environ.get("FPS_TP_GRID")  # A/B switch: most workgroups per partition launch
         if grid is not None:
             lib.fps_tile_partition_set_grid(int(grid))
+        slim = os.environ.get("FPS_TP_SLIM")  # A/B switch: 256-thread partition kernels (mf_tiled.hip)
+        if slim is not None:
+            lib.fps_tile_partition_set_slim(int(slim))
         n = uid.numel()
         if n > self.cap:
             self.cap = max(n, int(self.cap * 1.25))

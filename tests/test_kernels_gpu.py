@@ -353,6 +353,22 @@ def test_tile_partition_32bit_counters_match_reference(W, R, skew, monkeypatch):
         N_lib().fps_tile_partition_set_h16(1)
 
 
+@pytest.mark.parametrize("rec8", [False, True])
+@pytest.mark.parametrize("W,R,skew,phases", [(1, 128, True, 3), (8, 64, False, 3), (2, 64, True, 1), (1, 256, False, 1)])
+def test_tile_partition_slim_kernels_match_reference(W, R, skew, phases, rec8, monkeypatch):
+    """The slim partition shape (``FPS_TP_SLIM=1``: 256-thread count / scatter workgroups,
+    1024-record LDS batches, co-resident with the tile SGD): same partition as the
+    reference, skewed coarse keys included."""
+    prev = N_lib().fps_tile_partition_get_slim()
+    monkeypatch.setenv("FPS_TP_SLIM", "1")
+    try:
+        test_tile_partition_matches_reference(W, R, rec8, skew, phases)
+        assert N_lib().fps_tile_partition_get_slim() == 1
+    finally:
+        monkeypatch.delenv("FPS_TP_SLIM")
+        N_lib().fps_tile_partition_set_slim(prev)
+
+
 def N_lib():
     from flink_parameter_server_1_amd.ops import _native
 
