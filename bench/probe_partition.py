@@ -34,6 +34,7 @@ def main(argv=None):
     ap.add_argument("--items", type=int, default=1_000_000)
     ap.add_argument("--batch", type=int, default=64 << 20)
     ap.add_argument("--only", default="part,sgd,step", help="comma list of part / sgd / step")
+    ap.add_argument("--user-phases", type=int, default=0, help="0: MFConfig's choice")
     a = ap.parse_args(argv)
 
     import torch
@@ -41,7 +42,7 @@ def main(argv=None):
     from flink_parameter_server_1_amd.models.mf.fast import DistributedMF, MFConfig, SyntheticRatings
 
     dev = torch.device("cuda", 0)
-    cfg = MFConfig(num_users=a.users, num_items=a.items, dim=64, learning_rate=0.01)
+    cfg = MFConfig(num_users=a.users, num_items=a.items, dim=64, learning_rate=0.01, user_phases=a.user_phases)
     model = DistributedMF(cfg)
     assert model.sgd_mode == "tiled" and model.exchange == "local", (model.sgd_mode, model.exchange)
     data = SyntheticRatings(a.users, a.items, a.batch * 2, 0, 1, device=dev)
