@@ -788,6 +788,64 @@ FPS_API int fps_static_plan(const int32_t* uniq, const int32_t* prefix, int64_t 
   return 0;
 }
 
+namespace {
+// ---- emulated all-to-all receive (parallel/emulated.py, hot-owner model): segment j of
+// the output is rows [0, m_j) of `src` (k rows), tiled as often as m_j needs, i.e.
+// out[off_j + i] = src[i mod k].  One launch over the output's 16-B (or smaller) words; the
+// segment of a word by a linear search over <= FPS_FILL_MAX_SEGS offsets.  (A torch.cat
+// of the prefixes ran at ~0.6 TB/s -- 300 us per SGNS exchange -- so the transfer model
+// cost more device time than the receive it models.)
+constexpr int FPS_FILL_MAX_SEGS = 64;
+struct SegOffsets {
+  int64_t off[FPS_FILL_MAX_SEGS + 1];  // output row offsets: off[0] = 0, off[nseg] = rows out
+};
+
+template <typename T>
+__global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_t wpr, T* __restrict__ out,
+                                    SegOffsets so, int nseg) {
+  const int64_t total = so.off[nseg] * wpr;  // words
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = w / wpr, col = w - row * wpr;
+    int j = 0;
+    while (j + 1 < nseg && so.off[j + 1] <= row) ++j;
+    const int64_t r = (row - so.off[j]) % k;
+    out[w] = src[r * wpr + col];
+  }
+}
+
+template <typename T>
+void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* out, const SegOffsets& so, int nseg,
+                         hipStream_t st) {
+  const int64_t wpr = row_bytes / (int64_t)sizeof(T);
+  hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(so.off[nseg] * wpr, 256, 256 * 8)), dim3(256), 0, st,
+                     (const T*)src, k, wpr, (T*)out, so, nseg);
+}
+}  // namespace
+
+// rows[nseg]: rows of each output segment (host array); src: k rows of row_bytes
+FPS_API int fps_segment_fill(const void* src, int64_t k, int64_t row_bytes, void* out, const int64_t* rows, int nseg,
+                             void* stream) {
+  if (nseg <= 0 || nseg > FPS_FILL_MAX_SEGS || row_bytes <= 0) return (int)hipErrorInvalidValue;
+  SegOffsets so;
+  so.off[0] = 0;
+  for (int j = 0; j < nseg; ++j) {
+    if (rows[j] < 0) return (int)hipErrorInvalidValue;
+    so.off[j + 1] = so.off[j] + rows[j];
+  }
+  if (so.off[nseg] == 0) return 0;
+  if (k <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  auto fits = [&](int64_t a) {
+    return row_bytes % a == 0 && (uintptr_t)src % a == 0 && (uintptr_t)out % a == 0;
+  };
+  if (fits(16)) segment_fill_launch<uint4>(src, k, row_bytes, out, so, nseg, st);
+  else if (fits(4)) segment_fill_launch<uint32_t>(src, k, row_bytes, out, so, nseg, st);
+  else if (fits(2)) segment_fill_launch<uint16_t>(src, k, row_bytes, out, so, nseg, st);
+  else segment_fill_launch<uint8_t>(src, k, row_bytes, out, so, nseg, st);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_mark_rows(uint8_t* touched, const int32_t* rows, int64_t n, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mark_rows_kernel, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream, touched,

@@ -101,6 +101,42 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
     touched[r[r >= 0]] = 1
 
 
+def segment_fill(src: torch.Tensor, rows, out: torch.Tensor) -> None:
+    """``out`` = the concatenation over ``j`` of ``src``'s first ``rows[j]`` rows, ``src``
+    tiled where ``rows[j] > len(src)`` (row ``i`` of segment ``j`` is ``src[i % len(src)]``):
+    the emulated all-to-all's receive (``parallel/emulated.py``), one launch on the GPU.
+    ``rows`` is a host sequence (<= 64 segments); ``out`` holds at least ``sum(rows)`` rows."""
+    rows = [int(m) for m in rows]
+    n_out, k = sum(rows), src.shape[0]
+    if n_out == 0:
+        return
+    if k == 0:
+        raise ValueError("segment_fill: nothing to tile (empty src)")
+    if out.shape[0] < n_out or tuple(out.shape[1:]) != tuple(src.shape[1:]) or out.dtype != src.dtype:
+        raise ValueError(f"segment_fill: out {tuple(out.shape)} {out.dtype} cannot take {n_out} rows of "
+                         f"{tuple(src.shape[1:])} {src.dtype}")
+    if _on_gpu(src):
+        import ctypes
+
+        if len(rows) > 64:
+            raise ValueError(f"segment_fill: {len(rows)} segments, the kernel takes <= 64")
+        _c(src), _c(out)
+
+        arr = (ctypes.c_int64 * len(rows))(*rows)
+        N.check(N.require().fps_segment_fill(src.data_ptr(), k, src[0].numel() * src.element_size(), out.data_ptr(),
+                                             ctypes.addressof(arr), len(rows), N.stream_ptr(src.device)),
+                "segment_fill")
+        return
+    off = 0
+    for m in rows:
+        done = 0
+        while done < m:
+            c = min(m - done, k)
+            out[off + done: off + done + c].copy_(src[:c], non_blocking=True)
+            done += c
+        off += m
+
+
 def gather_rows(table: torch.Tensor, idx: torch.Tensor, out: torch.Tensor = None, out_dtype=torch.float32,
                 touched: torch.Tensor = None, flip: bool = False) -> torch.Tensor:
     """Pull serve: ``out[r] = table[idx[r]]`` (optionally bf16 on the wire) (K2);

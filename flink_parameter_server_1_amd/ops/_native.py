@@ -49,6 +49,7 @@ _SIGNATURES = {
     "fps_tile_partition_set_h16": [c_int],
     "fps_tile_partition_set_grid": [c_int],
     "fps_tile_partition_set_slim": [c_int],
+    "fps_segment_fill": [c_vp, c_i64, c_i64, c_vp, c_vp, c_int, c_vp],
     "fps_tile_partition_get_slim": [],
     "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                            c_vp, c_vp, c_int, c_vp, c_vp],

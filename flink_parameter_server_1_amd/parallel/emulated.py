@@ -100,6 +100,11 @@ class SymmetricComm(Comm):
         # one kernel per exchange (the transfer model must not cost more device time than
         # the real receive): every peer sends the self-segment (requests / pushes), or a
         # prefix of it (answers)
+        if k and n_out and own.is_cuda:
+            from .. import ops
+
+            ops.segment_fill(own.contiguous(), rs, out[:n_out])
+            return
         if k and n_out and all(m == k for m in rs):
             out[:n_out].view((len(rs),) + tuple(own.shape)).copy_(own.unsqueeze(0).expand((len(rs),) + tuple(own.shape)))
             return

@@ -651,3 +651,28 @@ def test_scalar_rows_gather_apply_large():
     exp.index_add_(0, idx[ok].long(), delta[ok])
     ops.apply_rows(tab, idx, delta, "add")
     torch.testing.assert_close(tab, exp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,dtype", [((1000,), torch.int32), ((777, 1), torch.float32), ((513, 300), torch.bfloat16),
+                                         ((64, 7), torch.float32), ((90, 3), torch.bfloat16), ((50, 5), torch.uint8)])
+def test_segment_fill_matches_torch(shape, dtype):
+    """The emulated all-to-all's receive fill (``ops.segment_fill``): segment j = the first
+    rows[j] rows of src, tiled past its end -- 16-B, 4-B, 2-B and 1-B word kernels against
+    the torch loop on the CPU."""
+    g = torch.Generator().manual_seed(shape[0])
+    src = (torch.randint(0, 100, shape, generator=g).to(dtype) if dtype in (torch.int32, torch.uint8)
+           else torch.randn(shape, generator=g).to(dtype))
+    k = shape[0]
+    rows = [k, 0, k // 3, 2 * k + 5, 1, k - 1, 3 * k]
+    n = sum(rows)
+    ref = torch.empty((n,) + shape[1:], dtype=dtype)
+    ops.segment_fill(src, rows, ref)
+    off = 0
+    for m in rows:  # the definition, row by row
+        for i in range(0, m, max(1, m // 7)):
+            assert torch.equal(ref[off + i], src[i % k])
+        off += m
+    out = torch.full((n + 3,) + shape[1:], 7, dtype=dtype, device=DEV)
+    ops.segment_fill(src.to(DEV), rows, out)
+    assert torch.equal(out[:n].cpu(), ref)
+    assert bool((out[n:].cpu() == 7).all())  # nothing past the segments is written
