@@ -800,16 +800,34 @@ struct SegOffsets {
   int64_t off[FPS_FILL_MAX_SEGS + 1];  // output row offsets: off[0] = 0, off[nseg] = rows out
 };
 
-template <typename T>
+// source row of output row `row`: segment by a linear search (<= 64 offsets), then the
+// row inside the source (a modulo only where a segment tiles the source)
+__device__ __forceinline__ int64_t segment_src_row(const SegOffsets& so, int nseg, int64_t row, int64_t k) {
+  int j = 0;
+  while (j + 1 < nseg && so.off[j + 1] <= row) ++j;
+  int64_t r = row - so.off[j];
+  return r < k ? r : r % k;
+}
+
+// ROW_PER_THREAD: one thread per row (rows of a few words, e.g. PA's scalar weights); else
+// one wave per row, its lanes over the row's words (SGNS's 600-B rows)
+template <typename T, bool ROW_PER_THREAD>
 __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_t wpr, T* __restrict__ out,
                                     SegOffsets so, int nseg) {
-  const int64_t total = so.off[nseg] * wpr;  // words
-  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = w / wpr, col = w - row * wpr;
-    int j = 0;
-    while (j + 1 < nseg && so.off[j + 1] <= row) ++j;
-    const int64_t r = (row - so.off[j]) % k;
-    out[w] = src[r * wpr + col];
+  const int64_t rows = so.off[nseg];
+  if constexpr (ROW_PER_THREAD) {
+    for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < rows;
+         row += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t r = segment_src_row(so, nseg, row, k);
+      for (int64_t c = 0; c < wpr; ++c) out[row * wpr + c] = src[r * wpr + c];
+    }
+  } else {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < rows; row += waves) {
+      const int64_t r = segment_src_row(so, nseg, row, k);
+      for (int64_t c = lane; c < wpr; c += 64) out[row * wpr + c] = src[r * wpr + c];
+    }
   }
 }
 
@@ -817,8 +835,13 @@ template <typename T>
 void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* out, const SegOffsets& so, int nseg,
                          hipStream_t st) {
   const int64_t wpr = row_bytes / (int64_t)sizeof(T);
-  hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(so.off[nseg] * wpr, 256, 256 * 8)), dim3(256), 0, st,
-                     (const T*)src, k, wpr, (T*)out, so, nseg);
+  const int64_t rows = so.off[nseg];
+  if (wpr < 16)
+    hipLaunchKernelGGL((segment_fill_kernel<T, true>), dim3(grid_for(rows, 256, 256 * 16)), dim3(256), 0, st,
+                       (const T*)src, k, wpr, (T*)out, so, nseg);
+  else
+    hipLaunchKernelGGL((segment_fill_kernel<T, false>), dim3(grid_for(rows, 4, 256 * 16)), dim3(256), 0, st,
+                       (const T*)src, k, wpr, (T*)out, so, nseg);
 }
 }  // namespace
 
@@ -839,6 +862,7 @@ FPS_API int fps_segment_fill(const void* src, int64_t k, int64_t row_bytes, void
     return row_bytes % a == 0 && (uintptr_t)src % a == 0 && (uintptr_t)out % a == 0;
   };
   if (fits(16)) segment_fill_launch<uint4>(src, k, row_bytes, out, so, nseg, st);
+  else if (fits(8)) segment_fill_launch<uint2>(src, k, row_bytes, out, so, nseg, st);
   else if (fits(4)) segment_fill_launch<uint32_t>(src, k, row_bytes, out, so, nseg, st);
   else if (fits(2)) segment_fill_launch<uint16_t>(src, k, row_bytes, out, so, nseg, st);
   else segment_fill_launch<uint8_t>(src, k, row_bytes, out, so, nseg, st);
