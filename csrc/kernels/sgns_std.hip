@@ -48,13 +48,47 @@ __device__ __forceinline__ float sigmoidf(float s) { return 1.f / (1.f + __expf(
 // log(1 + exp(x)) without overflow
 __device__ __forceinline__ float softplusf(float x) { return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x)); }
 
+// Row layout in a wave.  fp32 rows: lane l owns coordinates l + 64 m (NPL = ceil(D / 64)
+// floats).  bf16 rows (BF, the PS path's wire rows read as pulled, even D): lane l owns
+// the coordinate PAIRS 128 m' + 2 l, + 1 (NPL = 2 ceil(D / 128) floats), one 4-B load per
+// pair widened in registers -- a 2-B load per coordinate (the fp32 map on bf16) ran the
+// kernels 2.5x slower (round 6), and a separate widening pass cost a full read + write
+// of every pulled row.  The fp32 delta buffers are addressed through the same map.
+template <bool BF>
+__device__ __forceinline__ int sg_coord(int lane, int m) {
+  if constexpr (BF) return 128 * (m >> 1) + 2 * lane + (m & 1);
+  else return lane + 64 * m;
+}
+
+template <int NPL, bool BF>
+__device__ __forceinline__ void sg_load_row(const void* __restrict__ base, int64_t row, int D, int lane, bool valid,
+                                            float (&v)[NPL]) {
+  if constexpr (BF) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(base) + row * D);
+#pragma unroll
+    for (int mp = 0; mp < NPL / 2; ++mp) {
+      const int j = 128 * mp + 2 * lane;
+      const uint32_t w = (valid && j < D) ? src[j >> 1] : 0u;
+      v[2 * mp] = __uint_as_float(w << 16);             // coordinate j (the low half)
+      v[2 * mp + 1] = __uint_as_float(w & 0xffff0000u);  // coordinate j + 1
+    }
+  } else {
+    const float* src = reinterpret_cast<const float*>(base) + row * D;
+#pragma unroll
+    for (int m = 0; m < NPL; ++m) {
+      const int j = lane + 64 * m;
+      v[m] = (valid && j < D) ? src[j] : 0.f;
+    }
+  }
+}
+
 // GOUT = false: output-row deltas by float atomics (above).  GOUT = true: the
 // output rows are not touched here; the pair's coefficient g_x goes to
 // gbuf[p * (k + 1) + x] and sgns_rows_kernel below applies sum_x g_x * h per
 // output row from the coefficients sorted by row (no atomics on the hot rows).
-template <int NPL, bool GOUT>
-__global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__ rows_in,
-                                                       const float* __restrict__ rows_out,
+template <int NPL, bool GOUT, bool BF = false>
+__global__ void __launch_bounds__(256) sgns_std_kernel(const void* __restrict__ rows_in,
+                                                       const void* __restrict__ rows_out,
                                                        const int32_t* __restrict__ pos_c,
                                                        const int32_t* __restrict__ pos_o,
                                                        const int32_t* __restrict__ pos_neg, int64_t P, int D, int k,
@@ -76,7 +110,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
     float* dst = d_in + (int64_t)(wmap_in != nullptr ? wmap_in[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
-      const int j = lane + 64 * m;
+      const int j = sg_coord<BF>(lane, m);
       if (j < D) atomic_add_noret(dst + j, h[m] - h0[m]);
     }
   };
@@ -85,13 +119,9 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
     if (c != cur) {  // a new center run: push the previous run's change, load this center
       flush();
       cur = c;
-      const float* src = rows_in + (int64_t)c * D;
+      sg_load_row<NPL, BF>(rows_in, c, D, lane, true, h);
 #pragma unroll
-      for (int m = 0; m < NPL; ++m) {
-        const int j = lane + 64 * m;
-        h[m] = j < D ? src[j] : 0.f;
-        h0[m] = h[m];
-      }
+      for (int m = 0; m < NPL; ++m) h0[m] = h[m];
     }
     const int32_t o = pos_o[p];
     float dh[NPL];
@@ -107,14 +137,8 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
         if (x > 0 && row[q] == o) row[q] = -1;  // word2vec skips a negative equal to the target
       }
 #pragma unroll
-      for (int q = 0; q < SG; ++q) {  // all loads of the group in flight
-        const float* src = rows_out + (int64_t)(row[q] < 0 ? 0 : row[q]) * D;
-#pragma unroll
-        for (int m = 0; m < NPL; ++m) {
-          const int j = lane + 64 * m;
-          xv[q][m] = (row[q] >= 0 && j < D) ? src[j] : 0.f;
-        }
-      }
+      for (int q = 0; q < SG; ++q)  // all loads of the group in flight
+        sg_load_row<NPL, BF>(rows_out, row[q] < 0 ? 0 : row[q], D, lane, row[q] >= 0, xv[q]);
 #pragma unroll
       for (int q = 0; q < SG; ++q) {
         float s = 0.f;
@@ -142,7 +166,7 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
           float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[row[q]] : row[q]) * D;
 #pragma unroll
           for (int m = 0; m < NPL; ++m) {
-            const int j = lane + 64 * m;
+            const int j = sg_coord<BF>(lane, m);
             if (j < D) atomic_add_noret(dst + j, g * h[m]);
             dh[m] += g * xv[q][m];
           }
@@ -169,12 +193,12 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const float* __restrict__
 constexpr int SR_C = 256;  // sorted entries per wave
 constexpr int SR_G = 8;    // center rows in flight per lane
 
-template <int NPL>
+template <int NPL, bool BF = false>
 __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restrict__ srow,
                                                         const int64_t* __restrict__ perm,
                                                         const float* __restrict__ gbuf,
                                                         const int32_t* __restrict__ pos_c, int k1, int64_t n,
-                                                        const float* __restrict__ rows_h, int D,
+                                                        const void* __restrict__ rows_h, int D,
                                                         float* __restrict__ d_out,
                                                         const int32_t* __restrict__ wmap_out) {
   __shared__ int32_t s_row[4][SR_C], s_cen[4][SR_C];
@@ -200,7 +224,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
     const float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
-      const int j = lane + 64 * m;
+      const int j = sg_coord<BF>(lane, m);
       acc[m] = 0.f;
       base[m] = (whole && j < D) ? dst[j] : 0.f;
     }
@@ -209,7 +233,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
     float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[cur] : cur) * D;
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
-      const int j = lane + 64 * m;
+      const int j = sg_coord<BF>(lane, m);
       if (j < D) {
         if (complete) dst[j] = base[m] + acc[m];
         else atomic_add_noret(dst + j, acc[m]);
@@ -222,12 +246,7 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 #pragma unroll
     for (int q = 0; q < SR_G; ++q) {  // all SR_G center rows in flight
       const int i = min(i0 + q, m_n - 1);
-      const float* src = rows_h + (int64_t)s_cen[wv][i] * D;
-#pragma unroll
-      for (int m = 0; m < NPL; ++m) {
-        const int j = lane + 64 * m;
-        hv[q][m] = j < D ? src[j] : 0.f;
-      }
+      sg_load_row<NPL, BF>(rows_h, s_cen[wv][i], D, lane, true, hv[q]);
     }
 #pragma unroll
     for (int q = 0; q < SR_G; ++q) {
@@ -253,25 +272,31 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
 // Sorted form, pass 1: centers as in fps_sgns_standard (d_in), output-row
 // coefficients into gbuf[P * (k + 1)] (zeroed by the caller; skipped negatives
 // stay 0).
-FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, const int32_t* pos_c,
+FPS_API int fps_sgns_standard_coef(const void* rows_in, const void* rows_out, const int32_t* pos_c,
                                    const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
-                                   float* d_in, const int32_t* wmap_in, float* loss, float* gbuf, void* stream) {
+                                   float* d_in, const int32_t* wmap_in, float* loss, float* gbuf, void* stream,
+                                   int rows_bf16) {
   if (P <= 0) return 0;
-  if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
+  if (D <= 0 || D > 512 || k < 0 || (rows_bf16 && D % 2)) return (int)hipErrorInvalidValue;
   const int chunk = 16;
   const int64_t waves = (P + chunk - 1) / chunk;
   const int64_t blocks = (waves + 3) / 4;
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-#define FPS_SGC(NPL_)                                                                                            \
-  hipLaunchKernelGGL((sgns_std_kernel<NPL_, true>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, wmap_in, (const int32_t*)nullptr,  \
-                     loss, chunk, gbuf)
-  if (D <= 64) FPS_SGC(1);
-  else if (D <= 128) FPS_SGC(2);
-  else if (D <= 256) FPS_SGC(4);
-  else if (D <= 320) FPS_SGC(5);
-  else FPS_SGC(8);
+#define FPS_SGC(NPL_, BF_)                                                                                       \
+  hipLaunchKernelGGL((sgns_std_kernel<NPL_, true, BF_>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in,         \
+                     rows_out, pos_c, pos_o, pos_neg, P, D, k, lr, d_in, (float*)nullptr, wmap_in,                 \
+                     (const int32_t*)nullptr, loss, chunk, gbuf)
+  if (rows_bf16) {
+    if (D <= 128) FPS_SGC(2, true);
+    else if (D <= 256) FPS_SGC(4, true);
+    else if (D <= 384) FPS_SGC(6, true);
+    else FPS_SGC(8, true);
+  } else if (D <= 64) FPS_SGC(1, false);
+  else if (D <= 128) FPS_SGC(2, false);
+  else if (D <= 256) FPS_SGC(4, false);
+  else if (D <= 320) FPS_SGC(5, false);
+  else FPS_SGC(8, false);
 #undef FPS_SGC
   FPS_CHECK_LAUNCH();
   return 0;
@@ -280,21 +305,26 @@ FPS_API int fps_sgns_standard_coef(const float* rows_in, const float* rows_out, 
 // Sorted form, pass 2: d_out[srow[t]] += gbuf[perm[t]] * rows_h[pos_c[perm[t] / k1]]
 // over the n = P * k1 entries sorted by output row.
 FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float* gbuf, const int32_t* pos_c, int k1,
-                          int64_t n, const float* rows_h, int D, float* d_out, const int32_t* wmap_out,
-                          void* stream) {
+                          int64_t n, const void* rows_h, int D, float* d_out, const int32_t* wmap_out,
+                          void* stream, int rows_bf16) {
   if (n <= 0) return 0;
-  if (D <= 0 || D > 512 || k1 <= 0) return (int)hipErrorInvalidValue;
+  if (D <= 0 || D > 512 || k1 <= 0 || (rows_bf16 && D % 2)) return (int)hipErrorInvalidValue;
   const int64_t blocks = (n + 4 * SR_C - 1) / (4 * SR_C);
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-#define FPS_SGR(NPL_)                                                                                            \
-  hipLaunchKernelGGL(sgns_rows_kernel<NPL_>, dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf, pos_c, k1, \
-                     n, rows_h, D, d_out, wmap_out)
-  if (D <= 64) FPS_SGR(1);
-  else if (D <= 128) FPS_SGR(2);
-  else if (D <= 256) FPS_SGR(4);
-  else if (D <= 320) FPS_SGR(5);
-  else FPS_SGR(8);
+#define FPS_SGR(NPL_, BF_)                                                                                       \
+  hipLaunchKernelGGL((sgns_rows_kernel<NPL_, BF_>), dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf,     \
+                     pos_c, k1, n, rows_h, D, d_out, wmap_out)
+  if (rows_bf16) {
+    if (D <= 128) FPS_SGR(2, true);
+    else if (D <= 256) FPS_SGR(4, true);
+    else if (D <= 384) FPS_SGR(6, true);
+    else FPS_SGR(8, true);
+  } else if (D <= 64) FPS_SGR(1, false);
+  else if (D <= 128) FPS_SGR(2, false);
+  else if (D <= 256) FPS_SGR(4, false);
+  else if (D <= 320) FPS_SGR(5, false);
+  else FPS_SGR(8, false);
 #undef FPS_SGR
   FPS_CHECK_LAUNCH();
   return 0;
@@ -303,12 +333,12 @@ FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float*
 // P pairs: centers pos_c[P] (rows of rows_in / d_in), contexts pos_o[P] and
 // k negatives per pair pos_neg[P * k] (rows of rows_out / d_out); fp32 rows,
 // D <= 512.  loss (optional, zeroed by the caller) receives the summed loss.
-FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const int32_t* pos_c,
+FPS_API int fps_sgns_standard(const void* rows_in, const void* rows_out, const int32_t* pos_c,
                               const int32_t* pos_o, const int32_t* pos_neg, int64_t P, int D, int k, float lr,
                               float* d_in, float* d_out, const int32_t* wmap_in, const int32_t* wmap_out, float* loss,
-                              void* stream) {
+                              void* stream, int rows_bf16) {
   if (P <= 0) return 0;
-  if (D <= 0 || D > 512 || k < 0) return (int)hipErrorInvalidValue;
+  if (D <= 0 || D > 512 || k < 0 || (rows_bf16 && D % 2)) return (int)hipErrorInvalidValue;
   // ~16 pairs per wave: long enough to reuse a center across its window, short
   // enough for >= 32k waves at 1M pairs (the GPU holds ~8k)
   const int chunk = 16;
@@ -316,14 +346,20 @@ FPS_API int fps_sgns_standard(const float* rows_in, const float* rows_out, const
   const int64_t blocks = (waves + 3) / 4;
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-#define FPS_SGS(NPL_)                                                                                            \
-  hipLaunchKernelGGL((sgns_std_kernel<NPL_, false>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in, rows_out,  \
-                     pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, wmap_in, wmap_out, loss, chunk, (float*)nullptr)
-  if (D <= 64) FPS_SGS(1);
-  else if (D <= 128) FPS_SGS(2);
-  else if (D <= 256) FPS_SGS(4);
-  else if (D <= 320) FPS_SGS(5);
-  else FPS_SGS(8);
+#define FPS_SGS(NPL_, BF_)                                                                                       \
+  hipLaunchKernelGGL((sgns_std_kernel<NPL_, false, BF_>), dim3((unsigned)blocks), dim3(256), 0, s, rows_in,        \
+                     rows_out, pos_c, pos_o, pos_neg, P, D, k, lr, d_in, d_out, wmap_in, wmap_out, loss, chunk,    \
+                     (float*)nullptr)
+  if (rows_bf16) {
+    if (D <= 128) FPS_SGS(2, true);
+    else if (D <= 256) FPS_SGS(4, true);
+    else if (D <= 384) FPS_SGS(6, true);
+    else FPS_SGS(8, true);
+  } else if (D <= 64) FPS_SGS(1, false);
+  else if (D <= 128) FPS_SGS(2, false);
+  else if (D <= 256) FPS_SGS(4, false);
+  else if (D <= 320) FPS_SGS(5, false);
+  else FPS_SGS(8, false);
 #undef FPS_SGS
   FPS_CHECK_LAUNCH();
   return 0;

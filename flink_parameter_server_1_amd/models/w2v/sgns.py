@@ -201,7 +201,9 @@ class DistributedSGNS:
         pos_neg = plan_out.pos[P:].contiguous()
         with stage("sgns.step", self.timer):
             if self.standard:
-                loss = ops.sgns_standard(rows_in.float(), rows_out.float(), plan_in.pos.contiguous(), pos_o, pos_neg,
+                # bf16 wire rows go to the kernels as pulled (read as bf16 pairs, widened in
+                # registers: ops.sgns_standard); fp32 rows as they are
+                loss = ops.sgns_standard(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg,
                                          c.negatives, lr, d_in, d_out, with_loss=with_loss, wmap_in=wm_in,
                                          wmap_out=wm_out)
             else:

@@ -889,9 +889,14 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
     if pos_neg.numel() != P * k:
         raise ValueError("sgns_standard: pos_neg needs k rows per pair")
     if rows_in.is_cuda:
-        for t in (rows_in, rows_out, d_in, d_out):
+        for t in (d_in, d_out):
             if t.dtype != torch.float32:
-                raise ValueError("sgns_standard: fp32 rows and deltas")
+                raise ValueError("sgns_standard: fp32 deltas")
+        # rows: fp32, or bf16 (both tables; the PS path's wire rows as pulled, even D) read
+        # directly by the kernels -- no widening pass over every pulled row
+        bf = rows_in.dtype == torch.bfloat16 and rows_out.dtype == torch.bfloat16 and D % 2 == 0
+        if not bf and (rows_in.dtype != torch.float32 or rows_out.dtype != torch.float32):
+            rows_in, rows_out = rows_in.float(), rows_out.float()
         if D > 512:
             raise ValueError("sgns_standard: D <= 512")
         loss = torch.zeros(1, dtype=torch.float32, device=rows_in.device) if with_loss else None
@@ -907,22 +912,26 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
             gbuf = torch.zeros(P * k1, dtype=torch.float32, device=rows_in.device)
             N.check(lib.fps_sgns_standard_coef(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                                _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
-                                               _c(d_in).data_ptr(), N.ptr(wmap_in), N.ptr(loss), gbuf.data_ptr(), s),
+                                               _c(d_in).data_ptr(), N.ptr(wmap_in), N.ptr(loss), gbuf.data_ptr(), s,
+                                               int(bf)),
                     "sgns_coef")
             keys = torch.cat([pos_o.reshape(P, 1), pos_neg.reshape(P, int(k))], dim=1).reshape(-1)
             srow, perm = torch.sort(keys.to(torch.int32))
             N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
-                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out), s),
+                                      k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out), s,
+                                      int(bf)),
                     "sgns_rows")
             return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
                                               _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(wmap_in),
-                                              N.ptr(wmap_out), N.ptr(loss), N.stream_ptr(rows_in.device)),
+                                              N.ptr(wmap_out), N.ptr(loss), N.stream_ptr(rows_in.device), int(bf)),
                 "sgns_standard")
         return loss
     # CPU: the mini-batch form (every pair reads the rows as of the call); the
     # kernel's exact per-wave order is ``reference.sgns_standard`` (numerics tests)
+    if rows_in.dtype != d_in.dtype or rows_out.dtype != d_out.dtype:  # bf16 wire rows: widened here
+        rows_in, rows_out = rows_in.to(d_in.dtype), rows_out.to(d_out.dtype)
     if wmap_in is not None or wmap_out is not None:
         tmp_in = torch.zeros((rows_in.shape[0], D), dtype=d_in.dtype)
         tmp_out = torch.zeros((rows_out.shape[0], D), dtype=d_out.dtype)

@@ -94,10 +94,10 @@ _SIGNATURES = {
                       c_int, c_f32, c_f32, c_u32, c_vp],
     "fps_ht_rehash": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp],
     "fps_sgns_standard": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp,
-                          c_vp],
+                          c_vp, c_int],
     "fps_sgns_standard_coef": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp,
-                               c_vp],
-    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_vp],
+                               c_vp, c_int],
+    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_int],
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {}

@@ -226,6 +226,32 @@ def test_sgns_standard_kernel_matches_reference(D, runs, k, method):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D", [16, 64, 100, 300, 512])
+@pytest.mark.parametrize("method", ["sorted", "atomic"])
+def test_sgns_standard_bf16_rows_match_reference(D, method):
+    """bf16 pulled rows (the PS path's bf16 wire) read by the kernels directly, as
+    coordinate pairs widened in registers: the same deltas as the sequential reference
+    on the widened rows (the per-lane summation order differs from the fp32 layout)."""
+    torch.manual_seed(D + 1)
+    k, Uin, Uout, P = 5, 300, 400, 3000
+    rows_in = (torch.randn(Uin, D) * 0.3).bfloat16()
+    rows_out = (torch.randn(Uout, D) * 0.3).bfloat16()
+    pos_c = torch.sort(torch.randint(0, 60, (P,), dtype=torch.int32)).values
+    pos_o = torch.randint(0, Uout, (P,), dtype=torch.int32)
+    pos_neg = torch.randint(0, Uout, (P * k,), dtype=torch.int32)
+    d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
+    loss_r = R.sgns_standard(rows_in.float(), rows_out.float(), pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r,
+                             method=method)
+    dev = "cuda"
+    d_in, d_out = torch.zeros(Uin, D, device=dev), torch.zeros(Uout, D, device=dev)
+    loss = ops.sgns_standard(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k,
+                             0.05, d_in, d_out, with_loss=True, method=method)
+    torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=5e-6)
+    torch.testing.assert_close(d_out.cpu(), d_out_r, rtol=1e-4, atol=5e-6)
+    assert abs(float(loss) - loss_r) / loss_r < 1e-4
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D", [64, 300])
 def test_sgns_standard_sorted_in_place_matches_reference(D):
     """Local path (d_in is rows_in, d_out is rows_out; a few very hot output rows
