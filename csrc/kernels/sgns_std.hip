@@ -48,6 +48,13 @@ __device__ __forceinline__ float sigmoidf(float s) { return 1.f / (1.f + __expf(
 // log(1 + exp(x)) without overflow
 __device__ __forceinline__ float softplusf(float x) { return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x)); }
 
+// float -> bf16, round to nearest even (torch's conversion; NaN stays a quiet NaN)
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
 // Row layout in a wave.  fp32 rows: lane l owns coordinates l + 64 m (NPL = ceil(D / 64)
 // floats).  bf16 rows (BF, the PS path's wire rows read as pulled, even D): lane l owns
 // the coordinate PAIRS 128 m' + 2 l, + 1 (NPL = 2 ceil(D / 128) floats), one 4-B load per
@@ -193,14 +200,21 @@ __global__ void __launch_bounds__(256) sgns_std_kernel(const void* __restrict__ 
 constexpr int SR_C = 256;  // sorted entries per wave
 constexpr int SR_G = 8;    // center rows in flight per lane
 
-template <int NPL, bool BF = false>
+// OB (bf16 push output, BF rows only, no wmap): d_out is scratch -- a run wholly inside
+// the range writes bf16(sum) straight into out_bf (the push's wire buffer: no zero-fill
+// of d_out, no widening of d_out afterwards); a run cut by a range end adds its sum with
+// float atomics into d_out, whose cut rows sgns_cut_rows_kernel zeroes before and
+// converts into out_bf after.
+template <int NPL, bool BF = false, bool OB = false>
 __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restrict__ srow,
                                                         const int64_t* __restrict__ perm,
                                                         const float* __restrict__ gbuf,
                                                         const int32_t* __restrict__ pos_c, int k1, int64_t n,
                                                         const void* __restrict__ rows_h, int D,
                                                         float* __restrict__ d_out,
-                                                        const int32_t* __restrict__ wmap_out) {
+                                                        const int32_t* __restrict__ wmap_out,
+                                                        uint16_t* __restrict__ out_bf) {
+  static_assert(!OB || BF, "bf16 push output pairs with the bf16 row layout");
   __shared__ int32_t s_row[4][SR_C], s_cen[4][SR_C];
   __shared__ float s_g[4][SR_C];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -226,11 +240,20 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
     for (int m = 0; m < NPL; ++m) {
       const int j = sg_coord<BF>(lane, m);
       acc[m] = 0.f;
-      base[m] = (whole && j < D) ? dst[j] : 0.f;
+      base[m] = (!OB && whole && j < D) ? dst[j] : 0.f;
     }
   };
   auto flush = [&](bool complete) {
     float* dst = d_out + (int64_t)(wmap_out != nullptr ? wmap_out[cur] : cur) * D;
+    if (OB && complete) {  // one 4-B store per coordinate pair
+      uint32_t* ob = reinterpret_cast<uint32_t*>(out_bf + (int64_t)cur * D);
+#pragma unroll
+      for (int mp = 0; mp < NPL / 2; ++mp) {
+        const int j = 128 * mp + 2 * lane;
+        if (j < D) ob[j >> 1] = (uint32_t)f32_to_bf16_rne(acc[2 * mp]) | ((uint32_t)f32_to_bf16_rne(acc[2 * mp + 1]) << 16);
+      }
+      return;
+    }
 #pragma unroll
     for (int m = 0; m < NPL; ++m) {
       const int j = sg_coord<BF>(lane, m);
@@ -265,6 +288,34 @@ __global__ void __launch_bounds__(256) sgns_rows_kernel(const int32_t* __restric
     }
   }
   flush(whole && (t0 + m_n == n || srow[t0 + m_n] != cur));
+}
+
+// The rows cut by a range end of sgns_rows_kernel (its SR_C-entry ranges): the first row
+// of a range that continues the previous range's last run, and the last row of a range
+// that the next range continues.  ZERO: zero them in d_out (before the OB pass: their
+// partial sums arrive by atomics); else write bf16(d_out) into out_bf (after).  A row cut
+// several times is handled by several waves with the same values.
+template <bool ZERO>
+__global__ void __launch_bounds__(256) sgns_cut_rows_kernel(const int32_t* __restrict__ srow, int64_t n, int D,
+                                                            float* __restrict__ d_out, uint16_t* __restrict__ out_bf) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t t0 = w * SR_C;
+  if (t0 >= n) return;
+  const int64_t t1 = min(n, t0 + SR_C) - 1;  // last entry of the range
+  const int32_t first = srow[t0], last = srow[t1];
+  const bool cut_first = t0 > 0 && srow[t0 - 1] == first;
+  const bool cut_last = t1 + 1 < n && srow[t1 + 1] == last;
+  for (int c = 0; c < 2; ++c) {
+    const bool cut = c == 0 ? cut_first : cut_last;
+    if (!cut) continue;  // wave-uniform
+    const int64_t r = c == 0 ? first : last;
+    float* dst = d_out + r * D;
+    for (int j = lane; j < D; j += 64) {
+      if (ZERO) dst[j] = 0.f;
+      else out_bf[r * D + j] = f32_to_bf16_rne(dst[j]);
+    }
+  }
 }
 
 }  // namespace
@@ -304,18 +355,34 @@ FPS_API int fps_sgns_standard_coef(const void* rows_in, const void* rows_out, co
 
 // Sorted form, pass 2: d_out[srow[t]] += gbuf[perm[t]] * rows_h[pos_c[perm[t] / k1]]
 // over the n = P * k1 entries sorted by output row.
+// out_bf16 (nullable; bf16 rows and no wmap only): the deltas leave as bf16 in out_bf16
+// (rows of the n entries' row ids) and d_out is scratch (see sgns_rows_kernel OB)
 FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float* gbuf, const int32_t* pos_c, int k1,
                           int64_t n, const void* rows_h, int D, float* d_out, const int32_t* wmap_out,
-                          void* stream, int rows_bf16) {
+                          void* stream, int rows_bf16, uint16_t* out_bf16) {
   if (n <= 0) return 0;
   if (D <= 0 || D > 512 || k1 <= 0 || (rows_bf16 && D % 2)) return (int)hipErrorInvalidValue;
+  if (out_bf16 != nullptr && (!rows_bf16 || wmap_out != nullptr)) return (int)hipErrorInvalidValue;
   const int64_t blocks = (n + 4 * SR_C - 1) / (4 * SR_C);
   if (blocks > INT32_MAX) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
 #define FPS_SGR(NPL_, BF_)                                                                                       \
   hipLaunchKernelGGL((sgns_rows_kernel<NPL_, BF_>), dim3((unsigned)blocks), dim3(256), 0, s, srow, perm, gbuf,     \
-                     pos_c, k1, n, rows_h, D, d_out, wmap_out)
-  if (rows_bf16) {
+                     pos_c, k1, n, rows_h, D, d_out, wmap_out, (uint16_t*)nullptr)
+#define FPS_SGRO(NPL_)                                                                                           \
+  hipLaunchKernelGGL((sgns_rows_kernel<NPL_, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, srow, perm,   \
+                     gbuf, pos_c, k1, n, rows_h, D, d_out, wmap_out, out_bf16)
+  if (out_bf16 != nullptr) {
+    const int64_t cut_blocks = ((n + SR_C - 1) / SR_C + 3) / 4;  // one wave per range
+    hipLaunchKernelGGL(sgns_cut_rows_kernel<true>, dim3((unsigned)cut_blocks), dim3(256), 0, s, srow, n, D, d_out,
+                       out_bf16);
+    if (D <= 128) FPS_SGRO(2);
+    else if (D <= 256) FPS_SGRO(4);
+    else if (D <= 384) FPS_SGRO(6);
+    else FPS_SGRO(8);
+    hipLaunchKernelGGL(sgns_cut_rows_kernel<false>, dim3((unsigned)cut_blocks), dim3(256), 0, s, srow, n, D, d_out,
+                       out_bf16);
+  } else if (rows_bf16) {
     if (D <= 128) FPS_SGR(2, true);
     else if (D <= 256) FPS_SGR(4, true);
     else if (D <= 384) FPS_SGR(6, true);
@@ -325,6 +392,7 @@ FPS_API int fps_sgns_rows(const int32_t* srow, const int64_t* perm, const float*
   else if (D <= 256) FPS_SGR(4, false);
   else if (D <= 320) FPS_SGR(5, false);
   else FPS_SGR(8, false);
+#undef FPS_SGRO
 #undef FPS_SGR
   FPS_CHECK_LAUNCH();
   return 0;

@@ -195,8 +195,16 @@ class DistributedSGNS:
             wm_in, wm_out = plan_in.recv_keys, plan_out.recv_keys
         else:
             d_in = torch.zeros((plan_in.n_unique, c.dim), dtype=torch.float32, device=dev)
-            d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
             wm_in = wm_out = None
+        # bf16 wire: the output-row deltas leave the kernel in bf16 (the push's wire rows),
+        # d_out is its scratch (no zero-fill, no narrowing pass: ops.sgns_standard)
+        out_bf = None
+        if not fused and self.standard and self.ps_out.wire_dtype == torch.bfloat16 and rows_out.is_cuda \
+                and not plan_out.fixed and plan_out.valid is None:
+            d_out = torch.empty((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
+            out_bf = torch.empty((plan_out.n_unique, c.dim), dtype=torch.bfloat16, device=dev)
+        elif not fused:
+            d_out = torch.zeros((plan_out.n_unique, c.dim), dtype=torch.float32, device=dev)
         pos_o = plan_out.pos[:P].contiguous()
         pos_neg = plan_out.pos[P:].contiguous()
         with stage("sgns.step", self.timer):
@@ -205,7 +213,7 @@ class DistributedSGNS:
                 # registers: ops.sgns_standard); fp32 rows as they are
                 loss = ops.sgns_standard(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg,
                                          c.negatives, lr, d_in, d_out, with_loss=with_loss, wmap_in=wm_in,
-                                         wmap_out=wm_out)
+                                         wmap_out=wm_out, d_out_bf16=out_bf)
             else:
                 loss = ops.sgns_step(rows_in, rows_out, plan_in.pos.contiguous(), pos_o, pos_neg, lr,
                                      c.negatives / c.shared_negatives, d_in, d_out, with_loss=with_loss,
@@ -215,7 +223,7 @@ class DistributedSGNS:
             for ps, plan in zip((self.ps_in, self.ps_out), plans):
                 ps.note_local_push(plan)
             return None, (float(loss.item()) / max(P, 1) if with_loss else None)
-        return [d_in, d_out], (float(loss.item()) / max(P, 1) if with_loss else None)
+        return [d_in, d_out if out_bf is None else out_bf], (float(loss.item()) / max(P, 1) if with_loss else None)
 
     def _fused_push(self, plans) -> bool:
         """World 1, additive tables, de-duplicating plans: the owner is this rank and each

@@ -863,7 +863,8 @@ SGNS_METHODS = ("sorted", "atomic")
 
 
 def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d_in, d_out,
-                  with_loss: bool = False, method: Optional[str] = None, wmap_in=None, wmap_out=None):
+                  with_loss: bool = False, method: Optional[str] = None, wmap_in=None, wmap_out=None,
+                  d_out_bf16=None):
     """Standard skip-gram negative sampling (K6, ``kernels/sgns_std.hip``): ``k``
     independent negatives per pair (``pos_neg[P * k]``), word2vec's objective.
     ``d_in`` / ``d_out`` receive the deltas (the tables themselves on the local
@@ -882,6 +883,11 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
       waves).  ``h`` = the center rows after this call's center updates
       (``rows_in``; on the PS path the pulled rows).
     * ``method="atomic"``: Hogwild float atomics per pair and row, inside the pass.
+
+    ``d_out_bf16`` (bf16, shaped as ``d_out``; the PS path's bf16 push): the output-row
+    deltas are returned there in bf16 and ``d_out`` is scratch (its content on entry
+    does not matter).  With bf16 rows and the sorted form on the GPU the rows kernel
+    writes them directly (no zero-fill of ``d_out``, no widening pass after).
 
     CPU: the mini-batch form."""
     P = pos_c.numel()
@@ -905,6 +911,12 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
         method = method or os.environ.get("FPS_SGNS_METHOD", "sorted")
         if method not in SGNS_METHODS:
             raise ValueError(f"sgns_standard: method must be one of {SGNS_METHODS}")
+        ob = d_out_bf16 is not None
+        if ob and (d_out_bf16.dtype != torch.bfloat16 or d_out_bf16.shape != d_out.shape):
+            raise ValueError("sgns_standard: d_out_bf16 must be bf16 and shaped as d_out")
+        direct_ob = ob and bf and method == "sorted" and wmap_out is None
+        if ob and not direct_ob:  # d_out is scratch: the deltas accumulate from zero, then narrow
+            d_out.zero_()
         if method == "sorted":
             lib = N.require()
             s = N.stream_ptr(rows_in.device)
@@ -919,19 +931,29 @@ def sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k: int, lr: float, d
             srow, perm = torch.sort(keys.to(torch.int32))
             N.check(lib.fps_sgns_rows(_c(srow).data_ptr(), _c(perm).data_ptr(), gbuf.data_ptr(), _c(pos_c).data_ptr(),
                                       k1, P * k1, _c(rows_in).data_ptr(), D, _c(d_out).data_ptr(), N.ptr(wmap_out), s,
-                                      int(bf)),
+                                      int(bf), _c(d_out_bf16).data_ptr() if direct_ob else None),
                     "sgns_rows")
+            if ob and not direct_ob:
+                d_out_bf16.copy_(d_out)
             return loss
         N.check(N.require().fps_sgns_standard(_c(rows_in).data_ptr(), _c(rows_out).data_ptr(), _c(pos_c).data_ptr(),
                                               _c(pos_o).data_ptr(), _c(pos_neg).data_ptr(), P, D, int(k), lr,
                                               _c(d_in).data_ptr(), _c(d_out).data_ptr(), N.ptr(wmap_in),
                                               N.ptr(wmap_out), N.ptr(loss), N.stream_ptr(rows_in.device), int(bf)),
                 "sgns_standard")
+        if ob:
+            d_out_bf16.copy_(d_out)
         return loss
     # CPU: the mini-batch form (every pair reads the rows as of the call); the
     # kernel's exact per-wave order is ``reference.sgns_standard`` (numerics tests)
     if rows_in.dtype != d_in.dtype or rows_out.dtype != d_out.dtype:  # bf16 wire rows: widened here
         rows_in, rows_out = rows_in.to(d_in.dtype), rows_out.to(d_out.dtype)
+    if d_out_bf16 is not None:  # d_out is scratch: accumulate from zero, return narrowed
+        d_out.zero_()
+        loss = sgns_standard(rows_in, rows_out, pos_c, pos_o, pos_neg, k, lr, d_in, d_out, with_loss, method,
+                             wmap_in, wmap_out)
+        d_out_bf16.copy_(d_out)
+        return loss
     if wmap_in is not None or wmap_out is not None:
         tmp_in = torch.zeros((rows_in.shape[0], D), dtype=d_in.dtype)
         tmp_out = torch.zeros((rows_out.shape[0], D), dtype=d_out.dtype)

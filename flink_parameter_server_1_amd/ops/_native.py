@@ -97,7 +97,7 @@ _SIGNATURES = {
                           c_vp, c_int],
     "fps_sgns_standard_coef": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_f32, c_vp, c_vp, c_vp, c_vp,
                                c_vp, c_int],
-    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_int],
+    "fps_sgns_rows": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
 }
 #: optional symbols (added by later kernel files); bound when present
 OPTIONAL = {}

@@ -12,42 +12,61 @@ import os
 from contextlib import contextmanager, nullcontext
 
 _ENABLED = os.environ.get("FPS_TRACE", "1") != "0"
+_NV = False  # False: not looked up yet; None: no roctx (no GPU, or FPS_TRACE=0)
 
 
 def _nvtx():
-    try:
-        import torch
+    """``torch.cuda.nvtx`` (roctx on ROCm) if a GPU is present, looked up once: every
+    pipeline stage opens a range, and a per-call ``torch.cuda.is_available()`` was
+    ~1/10 of a PS-path micro-batch's host time (profiles/r6_pa_host_profile.txt)."""
+    global _NV
+    if _NV is False:
+        _NV = None
+        if _ENABLED:
+            try:
+                import torch
 
-        if torch.cuda.is_available():
-            return torch.cuda.nvtx
-    except Exception:  # pragma: no cover
-        pass
-    return None
-
-
-@contextmanager
-def trace_range(name: str):
-    nv = _nvtx() if _ENABLED else None
-    if nv is None:
-        yield
-        return
-    nv.range_push(name)
-    try:
-        yield
-    finally:
-        nv.range_pop()
+                if torch.cuda.is_available():
+                    _NV = torch.cuda.nvtx
+            except Exception:  # pragma: no cover
+                pass
+    return _NV
 
 
-@contextmanager
-def stage(name: str, timer=None):
+class _Range:
+    """roctx range + optional ``utils.metrics.StageTimer`` stage as a plain context
+    manager (a generator-based one cost two frames per stage on the host)."""
+
+    __slots__ = ("name", "timer", "_nv", "_t")
+
+    def __init__(self, name: str, timer=None):
+        self.name, self.timer, self._t = name, timer, None
+        self._nv = _nvtx()
+
+    def __enter__(self):
+        if self._nv is not None:
+            self._nv.range_push(self.name)
+        if self.timer is not None:
+            self._t = self.timer.stage(self.name)
+            self._t.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._t is not None:
+            self._t.__exit__(*exc)
+        if self._nv is not None:
+            self._nv.range_pop()
+        return False
+
+
+def trace_range(name: str) -> _Range:
+    return _Range(name)
+
+
+def stage(name: str, timer=None) -> _Range:
     """A pipeline stage: roctx range (``rocprofv3 --marker-trace``) plus, when a
     ``utils.metrics.StageTimer`` is attached, HIP-event timing of the stage."""
-    if timer is None:
-        with trace_range(name):
-            yield
-        return
-    with trace_range(name), timer.stage(name):
-        yield
+    return _Range(name, timer)
 
 
 @contextmanager

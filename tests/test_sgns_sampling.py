@@ -253,6 +253,33 @@ def test_sgns_standard_bf16_rows_match_reference(D, method):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("D", [64, 300])
+@pytest.mark.parametrize("method", ["sorted", "atomic"])
+def test_sgns_standard_bf16_push_output(D, method):
+    """``d_out_bf16``: the output-row deltas leave the kernel in bf16 (the PS path's bf16
+    push) with ``d_out`` as unzeroed scratch.  A very hot context row spans many of the
+    rows kernel's 256-entry ranges (cut runs: zeroed, summed by atomics, narrowed after);
+    every row equals bf16 of the reference delta (within the fp32 sums' rounding)."""
+    torch.manual_seed(D + 7)
+    k, Uin, Uout, P = 5, 300, 400, 3000
+    rows_in = (torch.randn(Uin, D) * 0.3).bfloat16()
+    rows_out = (torch.randn(Uout, D) * 0.3).bfloat16()
+    pos_c = torch.sort(torch.randint(0, 60, (P,), dtype=torch.int32)).values
+    pos_o = torch.where(torch.rand(P) < 0.4, 7, torch.randint(0, Uout, (P,))).to(torch.int32)  # row 7: 1200 entries
+    pos_neg = torch.randint(0, Uout, (P * k,), dtype=torch.int32)
+    d_in_r, d_out_r = torch.zeros(Uin, D), torch.zeros(Uout, D)
+    R.sgns_standard(rows_in.float(), rows_out.float(), pos_c, pos_o, pos_neg, k, 0.05, d_in_r, d_out_r, method=method)
+    dev = "cuda"
+    d_in = torch.zeros(Uin, D, device=dev)
+    d_out = torch.full((Uout, D), 123.0, device=dev)  # scratch: garbage on entry
+    out_bf = torch.empty(Uout, D, dtype=torch.bfloat16, device=dev)
+    ops.sgns_standard(rows_in.to(dev), rows_out.to(dev), pos_c.to(dev), pos_o.to(dev), pos_neg.to(dev), k, 0.05,
+                      d_in, d_out, method=method, d_out_bf16=out_bf)
+    torch.testing.assert_close(d_in.cpu(), d_in_r, rtol=1e-4, atol=5e-6)
+    torch.testing.assert_close(out_bf.cpu().float(), d_out_r.bfloat16().float(), rtol=1.6e-2, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [64, 300])
 def test_sgns_standard_sorted_in_place_matches_reference(D):
     """Local path (d_in is rows_in, d_out is rows_out; a few very hot output rows
     shared by many waves): the sorted form equals its sequential reference -- the
