@@ -159,3 +159,37 @@ def test_kernel_operands_must_be_device_tensors():
     with pytest.raises(ValueError, match="expected a GPU tensor"):
         _native.ptr(torch.zeros(4))
     assert _native.ptr(None) is None
+
+
+def test_stage_ranges_time_and_propagate_exceptions():
+    """``utils.tracing.stage``: a roctx range (none without a GPU) plus the attached
+    StageTimer's stage, entered and left in order, exceptions passed through."""
+    import pytest as _pt
+
+    from flink_parameter_server_1_amd.utils import tracing
+
+    log = []
+
+    class _T:
+        def __init__(self, name):
+            self.name = name
+
+        def __enter__(self):
+            log.append(("in", self.name))
+
+        def __exit__(self, *exc):
+            log.append(("out", self.name, exc[0] is not None))
+            return False
+
+    class Timer:
+        def stage(self, name):
+            return _T(name)
+
+    with tracing.stage("a", Timer()):
+        with tracing.stage("b", None), tracing.trace_range("c"):
+            log.append("body")
+    assert log == [("in", "a"), "body", ("out", "a", False)]
+    with _pt.raises(KeyError):
+        with tracing.stage("d", Timer()):
+            raise KeyError("x")
+    assert log[-1] == ("out", "d", True)
