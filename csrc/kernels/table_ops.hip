@@ -809,25 +809,22 @@ __device__ __forceinline__ int64_t segment_src_row(const SegOffsets& so, int nse
   return r < k ? r : r % k;
 }
 
-// ROW_PER_THREAD: one thread per row (rows of a few words, e.g. PA's scalar weights); else
-// one wave per row, its lanes over the row's words (SGNS's 600-B rows)
-template <typename T, bool ROW_PER_THREAD>
+// LPR lanes per row (a power of two covering the row's words, at most 64): a wave
+// copies 64 / LPR rows at a time, so a 4-B row (PA's scalar weights) takes one lane,
+// a 128-B or 256-B row (config #5's bf16 / fp32 rows) 8 or 16 lanes and a 600-B row
+// (SGNS) the whole wave -- every lane busy with one 16-B (or smaller) word per step.
+template <typename T>
 __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_t wpr, T* __restrict__ out,
-                                    SegOffsets so, int nseg) {
+                                    SegOffsets so, int nseg, int lpr_shift) {
   const int64_t rows = so.off[nseg];
-  if constexpr (ROW_PER_THREAD) {
-    for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < rows;
-         row += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t r = segment_src_row(so, nseg, row, k);
-      for (int64_t c = 0; c < wpr; ++c) out[row * wpr + c] = src[r * wpr + c];
-    }
-  } else {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < rows; row += waves) {
-      const int64_t r = segment_src_row(so, nseg, row, k);
-      for (int64_t c = lane; c < wpr; c += 64) out[row * wpr + c] = src[r * wpr + c];
-    }
+  const int lane = threadIdx.x & 63;
+  const int lpr = 1 << lpr_shift, rpw = 64 >> lpr_shift;
+  const int sub = lane >> lpr_shift, c0 = lane & (lpr - 1);
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = wave * rpw + sub; row < rows; row += waves * rpw) {
+    const int64_t r = segment_src_row(so, nseg, row, k);
+    for (int64_t c = c0; c < wpr; c += lpr) out[row * wpr + c] = src[r * wpr + c];
   }
 }
 
@@ -835,13 +832,12 @@ template <typename T>
 void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* out, const SegOffsets& so, int nseg,
                          hipStream_t st) {
   const int64_t wpr = row_bytes / (int64_t)sizeof(T);
+  int sh = 0;
+  while (sh < 6 && (1ll << sh) < wpr) ++sh;
   const int64_t rows = so.off[nseg];
-  if (wpr < 16)
-    hipLaunchKernelGGL((segment_fill_kernel<T, true>), dim3(grid_for(rows, 256, 256 * 16)), dim3(256), 0, st,
-                       (const T*)src, k, wpr, (T*)out, so, nseg);
-  else
-    hipLaunchKernelGGL((segment_fill_kernel<T, false>), dim3(grid_for(rows, 4, 256 * 16)), dim3(256), 0, st,
-                       (const T*)src, k, wpr, (T*)out, so, nseg);
+  const int64_t waves = (rows + (64 >> sh) - 1) / (64 >> sh);
+  hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(waves, 4, 256 * 16)), dim3(256), 0, st, (const T*)src, k,
+                     wpr, (T*)out, so, nseg, sh);
 }
 }  // namespace
 
