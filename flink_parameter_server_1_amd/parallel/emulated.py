@@ -10,9 +10,11 @@ the same access pattern as on the real job (local keys ``key // N`` are valid ro
 of every shard) -- while each all-to-all's transfer is modelled on the device:
 
 * a posted exchange waits (on a high-priority link stream) for the posting
-  stream's event, spends ``latency + bytes to the busiest peer / link_gbps`` in a
+  stream's event and spends ``latency + bytes to the busiest peer / link_gbps`` in a
   one-wave device sleep (a fully connected xGMI node: one link per peer, all in
-  parallel), then copies the buffer on the device (the receive's HBM write);
+  parallel), while a second high-priority stream writes the receive buffer on the
+  device (one segment-fill kernel: the receive's HBM write, which RCCL's kernels do
+  chunk by chunk as the data crosses the links); the exchange is done when both are;
 * ``Work.wait()`` is a stream wait, as on RCCL; ``wait_ms()`` reports the time the
   compute stream waited with nothing else to run.
 
@@ -77,6 +79,7 @@ class SymmetricComm(Comm):
         self.link_gbps, self.latency_us = float(link_gbps), float(latency_us)
         self.cuda = self.device.type == "cuda"
         self._link = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
+        self._fill_stream = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
         #: exposed waits are those of this (compute) stream; an owner stream waiting for a
         #: transfer (``TensorPS.owner_stream``) idles no compute
         self._main = torch.cuda.current_stream(self.device) if self.cuda else None
@@ -148,14 +151,21 @@ class SymmetricComm(Comm):
         from .vworld import _Sleep
 
         us = (self.latency_us + (max(peer) if peer else 0) * 1e-3 / self.link_gbps) if self.world > 1 else 0.0
-        self._link.wait_stream(torch.cuda.current_stream(self.device))  # the send is ready in post order
+        posted = torch.cuda.Event()
+        posted.record(torch.cuda.current_stream(self.device))  # the send is ready in post order
+        self._link.wait_event(posted)
+        self._fill_stream.wait_event(posted)
+        with torch.cuda.stream(self._fill_stream):  # the receive's HBM write, during the transfer
+            self._fill(send, out, send_splits, recv_splits)
+            written = torch.cuda.Event()
+            written.record(self._fill_stream)
         with torch.cuda.stream(self._link):
             _Sleep.us(self.device, us)
-            self._fill(send, out, send_splits, recv_splits)
+            self._link.wait_event(written)
             done = torch.cuda.Event()
             done.record(self._link)
-        send.record_stream(self._link)
-        out.record_stream(self._link)
+        send.record_stream(self._fill_stream)
+        out.record_stream(self._fill_stream)
         self.transfers += 1
         return done
 
