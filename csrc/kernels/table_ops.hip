@@ -813,9 +813,17 @@ __device__ __forceinline__ int64_t segment_src_row(const SegOffsets& so, int nse
 // copies 64 / LPR rows at a time, so a 4-B row (PA's scalar weights) takes one lane,
 // a 128-B or 256-B row (config #5's bf16 / fp32 rows) 8 or 16 lanes and a 600-B row
 // (SGNS) the whole wave -- every lane busy with one 16-B (or smaller) word per step.
+//
+// min_ticks > 0 (the emulated link, parallel/emulated.py): the kernel also lasts at least
+// min_ticks of the 100 MHz s_memrealtime clock from the start of workgroup 0 -- its
+// first wave spins (s_sleep) after its share of the copy.  A transfer that writes its
+// receive buffer as the data arrives completes at max(link time, write time), in one
+// kernel on one stream.
 template <typename T>
 __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_t wpr, T* __restrict__ out,
-                                    SegOffsets so, int nseg, int lpr_shift) {
+                                    SegOffsets so, int nseg, int lpr_shift, uint64_t min_ticks) {
+  const bool timer = min_ticks > 0 && blockIdx.x == 0 && threadIdx.x < 64;  // wave-uniform
+  const uint64_t t0 = timer ? __builtin_amdgcn_s_memrealtime() : 0;
   const int64_t rows = so.off[nseg];
   const int lane = threadIdx.x & 63;
   const int lpr = 1 << lpr_shift, rpw = 64 >> lpr_shift;
@@ -826,24 +834,27 @@ __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_
     const int64_t r = segment_src_row(so, nseg, row, k);
     for (int64_t c = c0; c < wpr; c += lpr) out[row * wpr + c] = src[r * wpr + c];
   }
+  if (timer)
+    while (__builtin_amdgcn_s_memrealtime() - t0 < min_ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 template <typename T>
 void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* out, const SegOffsets& so, int nseg,
-                         hipStream_t st) {
+                         hipStream_t st, uint64_t min_ticks) {
   const int64_t wpr = row_bytes / (int64_t)sizeof(T);
   int sh = 0;
   while (sh < 6 && (1ll << sh) < wpr) ++sh;
   const int64_t rows = so.off[nseg];
   const int64_t waves = (rows + (64 >> sh) - 1) / (64 >> sh);
   hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(waves, 4, 256 * 16)), dim3(256), 0, st, (const T*)src, k,
-                     wpr, (T*)out, so, nseg, sh);
+                     wpr, (T*)out, so, nseg, sh, min_ticks);
 }
 }  // namespace
 
-// rows[nseg]: rows of each output segment (host array); src: k rows of row_bytes
+// rows[nseg]: rows of each output segment (host array); src: k rows of row_bytes;
+// min_us > 0: the kernel lasts at least that long (see segment_fill_kernel)
 FPS_API int fps_segment_fill(const void* src, int64_t k, int64_t row_bytes, void* out, const int64_t* rows, int nseg,
-                             void* stream) {
+                             void* stream, double min_us) {
   if (nseg <= 0 || nseg > FPS_FILL_MAX_SEGS || row_bytes <= 0) return (int)hipErrorInvalidValue;
   SegOffsets so;
   so.off[0] = 0;
@@ -851,17 +862,18 @@ FPS_API int fps_segment_fill(const void* src, int64_t k, int64_t row_bytes, void
     if (rows[j] < 0) return (int)hipErrorInvalidValue;
     so.off[j + 1] = so.off[j] + rows[j];
   }
-  if (so.off[nseg] == 0) return 0;
-  if (k <= 0) return (int)hipErrorInvalidValue;
+  const uint64_t min_ticks = min_us > 0 ? (uint64_t)(min_us * 100.0) : 0;  // s_memrealtime: 100 MHz
+  if (so.off[nseg] == 0 && min_ticks == 0) return 0;
+  if (so.off[nseg] > 0 && k <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   auto fits = [&](int64_t a) {
     return row_bytes % a == 0 && (uintptr_t)src % a == 0 && (uintptr_t)out % a == 0;
   };
-  if (fits(16)) segment_fill_launch<uint4>(src, k, row_bytes, out, so, nseg, st);
-  else if (fits(8)) segment_fill_launch<uint2>(src, k, row_bytes, out, so, nseg, st);
-  else if (fits(4)) segment_fill_launch<uint32_t>(src, k, row_bytes, out, so, nseg, st);
-  else if (fits(2)) segment_fill_launch<uint16_t>(src, k, row_bytes, out, so, nseg, st);
-  else segment_fill_launch<uint8_t>(src, k, row_bytes, out, so, nseg, st);
+  if (fits(16)) segment_fill_launch<uint4>(src, k, row_bytes, out, so, nseg, st, min_ticks);
+  else if (fits(8)) segment_fill_launch<uint2>(src, k, row_bytes, out, so, nseg, st, min_ticks);
+  else if (fits(4)) segment_fill_launch<uint32_t>(src, k, row_bytes, out, so, nseg, st, min_ticks);
+  else if (fits(2)) segment_fill_launch<uint16_t>(src, k, row_bytes, out, so, nseg, st, min_ticks);
+  else segment_fill_launch<uint8_t>(src, k, row_bytes, out, so, nseg, st, min_ticks);
   FPS_CHECK_LAUNCH();
   return 0;
 }

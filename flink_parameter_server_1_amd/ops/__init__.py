@@ -101,16 +101,18 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
     touched[r[r >= 0]] = 1
 
 
-def segment_fill(src: torch.Tensor, rows, out: torch.Tensor) -> None:
+def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0) -> None:
     """``out`` = the concatenation over ``j`` of ``src``'s first ``rows[j]`` rows, ``src``
     tiled where ``rows[j] > len(src)`` (row ``i`` of segment ``j`` is ``src[i % len(src)]``):
     the emulated all-to-all's receive (``parallel/emulated.py``), one launch on the GPU.
-    ``rows`` is a host sequence (<= 64 segments); ``out`` holds at least ``sum(rows)`` rows."""
+    ``rows`` is a host sequence (<= 64 segments); ``out`` holds at least ``sum(rows)`` rows.
+    ``min_us`` (GPU): the launch also lasts at least that long -- a modelled link
+    transfer that writes its receive as the data arrives (done at max(link, write))."""
     rows = [int(m) for m in rows]
     n_out, k = sum(rows), src.shape[0]
-    if n_out == 0:
+    if n_out == 0 and not (min_us > 0 and src.is_cuda):
         return
-    if k == 0:
+    if k == 0 and n_out:
         raise ValueError("segment_fill: nothing to tile (empty src)")
     if out.shape[0] < n_out or tuple(out.shape[1:]) != tuple(src.shape[1:]) or out.dtype != src.dtype:
         raise ValueError(f"segment_fill: out {tuple(out.shape)} {out.dtype} cannot take {n_out} rows of "
@@ -123,8 +125,11 @@ def segment_fill(src: torch.Tensor, rows, out: torch.Tensor) -> None:
         _c(src), _c(out)
 
         arr = (ctypes.c_int64 * len(rows))(*rows)
-        N.check(N.require().fps_segment_fill(src.data_ptr(), k, src[0].numel() * src.element_size(), out.data_ptr(),
-                                             ctypes.addressof(arr), len(rows), N.stream_ptr(src.device)),
+        row_bytes = src.element_size()
+        for d in src.shape[1:]:
+            row_bytes *= int(d)
+        N.check(N.require().fps_segment_fill(src.data_ptr(), k, row_bytes, out.data_ptr(), ctypes.addressof(arr),
+                                             len(rows), N.stream_ptr(src.device), float(min_us)),
                 "segment_fill")
         return
     off = 0

@@ -26,6 +26,7 @@ _err = None
 
 c_int, c_i64, c_f32, c_u32, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32, ctypes.c_void_p
 c_u64 = ctypes.c_uint64
+c_double = ctypes.c_double
 
 _SIGNATURES = {
     "fps_abi_version": [],
@@ -49,7 +50,7 @@ _SIGNATURES = {
     "fps_tile_partition_set_h16": [c_int],
     "fps_tile_partition_set_grid": [c_int],
     "fps_tile_partition_set_slim": [c_int],
-    "fps_segment_fill": [c_vp, c_i64, c_i64, c_vp, c_vp, c_int, c_vp],
+    "fps_segment_fill": [c_vp, c_i64, c_i64, c_vp, c_vp, c_int, c_vp, c_double],
     "fps_tile_partition_get_slim": [],
     "fps_tile_partition": [c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                            c_vp, c_vp, c_int, c_vp, c_vp],

@@ -10,11 +10,14 @@ the same access pattern as on the real job (local keys ``key // N`` are valid ro
 of every shard) -- while each all-to-all's transfer is modelled on the device:
 
 * a posted exchange waits (on a high-priority link stream) for the posting
-  stream's event and spends ``latency + bytes to the busiest peer / link_gbps`` in a
-  one-wave device sleep (a fully connected xGMI node: one link per peer, all in
-  parallel), while a second high-priority stream writes the receive buffer on the
-  device (one segment-fill kernel: the receive's HBM write, which RCCL's kernels do
-  chunk by chunk as the data crosses the links); the exchange is done when both are;
+  stream's event, then ONE segment-fill kernel writes the receive buffer on the device
+  and lasts at least ``latency + bytes to the busiest peer / link_gbps`` (a fully
+  connected xGMI node: one link per peer, all in parallel): RCCL's kernels write the
+  receive chunk by chunk as the data crosses the links, so a transfer completes at
+  max(link time, write time).  (Round 5 slept, then copied: the write sat on the
+  critical path after the link time.  A second stream for the write ran past the 4
+  hardware queues a process gets and serialised unrelated streams,
+  ``profiles/r6_link_model.md``.);
 * ``Work.wait()`` is a stream wait, as on RCCL; ``wait_ms()`` reports the time the
   compute stream waited with nothing else to run.
 
@@ -79,7 +82,6 @@ class SymmetricComm(Comm):
         self.link_gbps, self.latency_us = float(link_gbps), float(latency_us)
         self.cuda = self.device.type == "cuda"
         self._link = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
-        self._fill_stream = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
         #: exposed waits are those of this (compute) stream; an owner stream waiting for a
         #: transfer (``TensorPS.owner_stream``) idles no compute
         self._main = torch.cuda.current_stream(self.device) if self.cuda else None
@@ -88,13 +90,20 @@ class SymmetricComm(Comm):
 
     # ------------------------------------------------------------- link model
     def _fill(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
-              recv_splits: Sequence[int]) -> None:
+              recv_splits: Sequence[int], min_us: float = 0.0) -> bool:
         """The received buffer: this rank's own send buffer (symmetric), or every
-        incoming segment = this rank's self-segment tiled / cut (hot owner)."""
+        incoming segment = this rank's self-segment tiled / cut (hot owner).  On the GPU
+        one segment-fill kernel that also lasts ``min_us`` (the link time); returns
+        whether it did (else the caller models the link time itself)."""
+        from .. import ops
+
         if not self.hot_owner:
             n = int(sum(send_splits))
+            if n and send.is_cuda:
+                ops.segment_fill(send[:n].contiguous(), [n], out[:n], min_us=min_us)
+                return True
             out[:n].copy_(send[:n], non_blocking=True)
-            return
+            return False
         a = int(sum(send_splits[: self.rank]))
         own = send[a: a + int(send_splits[self.rank])]
         n_out = int(sum(recv_splits))
@@ -104,17 +113,15 @@ class SymmetricComm(Comm):
         # the real receive): every peer sends the self-segment (requests / pushes), or a
         # prefix of it (answers)
         if k and n_out and own.is_cuda:
-            from .. import ops
-
-            ops.segment_fill(own.contiguous(), rs, out[:n_out])
-            return
+            ops.segment_fill(own.contiguous(), rs, out[:n_out], min_us=min_us)
+            return True
         if k and n_out and all(m == k for m in rs):
             out[:n_out].view((len(rs),) + tuple(own.shape)).copy_(own.unsqueeze(0).expand((len(rs),) + tuple(own.shape)))
-            return
+            return False
         if k and n_out:
             src = own if max(rs) <= k else torch.cat([own] * -(-max(rs) // k))
             torch.cat([src[:m] for m in rs], out=out[:n_out])
-            return
+            return False
         off = 0
         for m in recv_splits:
             m = int(m)
@@ -132,6 +139,7 @@ class SymmetricComm(Comm):
                     out[off + done: off + done + k].copy_(own[:k], non_blocking=True)
                 done += k
             off += m
+        return False
 
     def _post(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
               recv_splits: Optional[Sequence[int]] = None) -> Optional[object]:
@@ -151,21 +159,14 @@ class SymmetricComm(Comm):
         from .vworld import _Sleep
 
         us = (self.latency_us + (max(peer) if peer else 0) * 1e-3 / self.link_gbps) if self.world > 1 else 0.0
-        posted = torch.cuda.Event()
-        posted.record(torch.cuda.current_stream(self.device))  # the send is ready in post order
-        self._link.wait_event(posted)
-        self._fill_stream.wait_event(posted)
-        with torch.cuda.stream(self._fill_stream):  # the receive's HBM write, during the transfer
-            self._fill(send, out, send_splits, recv_splits)
-            written = torch.cuda.Event()
-            written.record(self._fill_stream)
+        self._link.wait_stream(torch.cuda.current_stream(self.device))  # the send is ready in post order
         with torch.cuda.stream(self._link):
-            _Sleep.us(self.device, us)
-            self._link.wait_event(written)
+            if not self._fill(send, out, send_splits, recv_splits, min_us=us):  # the write, during the link time
+                _Sleep.us(self.device, us)
             done = torch.cuda.Event()
             done.record(self._link)
-        send.record_stream(self._fill_stream)
-        out.record_stream(self._fill_stream)
+        send.record_stream(self._link)
+        out.record_stream(self._link)
         self.transfers += 1
         return done
 

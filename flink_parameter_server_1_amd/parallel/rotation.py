@@ -301,15 +301,14 @@ class _SymmetricLinks:
     In a rotation every rank runs the same schedule on equal work, so the block a
     rank receives in sub-step ``s`` is posted by its neighbour when the neighbour's
     sub-step ``s - 1`` ends -- the moment this rank's own ``s - 1`` ends.  A posted
-    transfer waits for that compute-stream event, then spends ``latency + bytes /
-    link_gbps`` in a one-wave device sleep on a high-priority link stream (the two
-    rings' blocks travel on two different links, in parallel) while a second
-    high-priority stream runs a real device copy of the block (the send's HBM read and
-    the receive's HBM write of this GPU); the transfer is done when both are.  RCCL's
-    point-to-point kernels write the receive buffer chunk by chunk as the data crosses
-    the link, so the write overlaps the link time (round 5 ran the copy AFTER the
-    sleep: on a GPU busy with the SGD the copy took 0.1-0.3 ms and sat on every
-    sub-step's critical path, ``profiles/r6_link_model.md``).  Everything is enqueued at
+    transfer waits for that compute-stream event on a high-priority link stream, then
+    real device copies of the blocks (the send's HBM read and the receive's HBM write
+    of this GPU) run as segment-fill kernels, the last of which lasts at least
+    ``latency + bytes / link_gbps`` (the two rings' blocks travel on two different
+    links, in parallel).  RCCL's point-to-point kernels write the receive buffer chunk
+    by chunk as the data crosses the link, so the write overlaps the link time (round 5
+    slept, then copied: on a GPU busy with the SGD the copies took 0.1-0.3 ms and sat on
+    every sub-step's critical path, ``profiles/r6_link_model.md``).  Everything is enqueued at
     post time, so waiting on a transfer is a pure stream wait, as on RCCL (no host
     thread, no host block).  Only the emulated rank computes, at the full speed of its
     GPU: the measured wait is the exposure of the real schedule under rank symmetry,
@@ -323,20 +322,18 @@ class _SymmetricLinks:
         self.latency_us = float(latency_us)
         self.device = device
         self.stream = torch.cuda.Stream(device=device, priority=-1)
-        self.copy_stream = torch.cuda.Stream(device=device, priority=-1)
 
     def post(self, after: "torch.cuda.Event", copies, link_bytes: int) -> "torch.cuda.Event":
+        from .. import ops
+
         us = self.latency_us + link_bytes * self.us_per_byte
         self.stream.wait_event(after)
-        self.copy_stream.wait_event(after)
-        with torch.cuda.stream(self.copy_stream):  # the receive's HBM write, during the transfer
-            for dst, src in copies:
-                dst.copy_(src, non_blocking=True)
-            written = torch.cuda.Event()
-            written.record(self.copy_stream)
         with torch.cuda.stream(self.stream):
-            self._sleep.us(self.device, us)
-            self.stream.wait_event(written)
+            copies = [(d, s) for d, s in copies if s.shape[0]]
+            for j, (dst, src) in enumerate(copies):  # the last copy carries the link time
+                ops.segment_fill(src, [src.shape[0]], dst, min_us=us if j == len(copies) - 1 else 0.0)
+            if not copies:
+                self._sleep.us(self.device, us)
             done = torch.cuda.Event()
             done.record(self.stream)
         return done

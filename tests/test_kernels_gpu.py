@@ -676,3 +676,19 @@ def test_segment_fill_matches_torch(shape, dtype):
     ops.segment_fill(src.to(DEV), rows, out)
     assert torch.equal(out[:n].cpu(), ref)
     assert bool((out[n:].cpu() == 7).all())  # nothing past the segments is written
+
+
+def test_segment_fill_lasts_its_link_time():
+    """``segment_fill(min_us=...)`` (the emulated link): the launch lasts at least the
+    modelled transfer time, also with nothing to write, and still writes its rows."""
+    src = torch.arange(4096, dtype=torch.float32, device=DEV).view(1024, 4)
+    out = torch.zeros(2048, 4, device=DEV)
+    for rows, want_us in (([1024, 1024], 1500.0), ([0], 800.0)):
+        ops.segment_fill(src, rows, out, min_us=10.0)  # warm-up
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ops.segment_fill(src, rows, out, min_us=want_us)
+        b.record()
+        torch.cuda.synchronize()
+        assert a.elapsed_time(b) * 1e3 >= 0.95 * want_us
+    assert torch.equal(out, torch.cat([src, src]))
