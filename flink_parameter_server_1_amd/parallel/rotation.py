@@ -302,10 +302,10 @@ class _SymmetricLinks:
     rank receives in sub-step ``s`` is posted by its neighbour when the neighbour's
     sub-step ``s - 1`` ends -- the moment this rank's own ``s - 1`` ends.  A posted
     transfer waits for that compute-stream event on a high-priority link stream, then
-    real device copies of the blocks (the send's HBM read and the receive's HBM write
-    of this GPU) run as segment-fill kernels, the last of which lasts at least
-    ``latency + bytes / link_gbps`` (the two rings' blocks travel on two different
-    links, in parallel).  RCCL's point-to-point kernels write the receive buffer chunk
+    ONE segment-fill kernel moves the bytes of the sub-step's blocks (the send's HBM
+    read and the receive's HBM write of this GPU: every ring's block size, read from
+    the first block) and lasts at least ``latency + bytes / link_gbps`` (the two rings'
+    blocks travel on two different links, in parallel).  RCCL's point-to-point kernels write the receive buffer chunk
     by chunk as the data crosses the link, so the write overlaps the link time (round 5
     slept, then copied: on a GPU busy with the SGD the copies took 0.1-0.3 ms and sat on
     every sub-step's critical path, ``profiles/r6_link_model.md``).  Everything is enqueued at
@@ -322,17 +322,27 @@ class _SymmetricLinks:
         self.latency_us = float(latency_us)
         self.device = device
         self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self._scratch = None
 
     def post(self, after: "torch.cuda.Event", copies, link_bytes: int) -> "torch.cuda.Event":
+        """``copies``: ``(dst, src)`` of the blocks sent / received this sub-step; their
+        bytes are moved by one kernel (rows of every block, read from the first: the
+        same HBM traffic) into a scratch buffer that nothing reads."""
         from .. import ops
 
         us = self.latency_us + link_bytes * self.us_per_byte
+        srcs = [src for _, src in copies if src.shape[0]]
         self.stream.wait_event(after)
         with torch.cuda.stream(self.stream):
-            copies = [(d, s) for d, s in copies if s.shape[0]]
-            for j, (dst, src) in enumerate(copies):  # the last copy carries the link time
-                ops.segment_fill(src, [src.shape[0]], dst, min_us=us if j == len(copies) - 1 else 0.0)
-            if not copies:
+            if srcs:
+                rows = [x.shape[0] for x in srcs]
+                src = srcs[0]
+                if (self._scratch is None or self._scratch.shape[0] < sum(rows)
+                        or self._scratch.shape[1:] != src.shape[1:] or self._scratch.dtype != src.dtype):
+                    self._scratch = torch.empty((sum(rows),) + tuple(src.shape[1:]), dtype=src.dtype,
+                                                device=src.device)
+                ops.segment_fill(src.contiguous(), rows, self._scratch[:sum(rows)], min_us=us)
+            else:
                 self._sleep.us(self.device, us)
             done = torch.cuda.Event()
             done.record(self.stream)
@@ -372,7 +382,6 @@ class EmulatedRotation:
         self.bytes_sent = 0
         self.links = _SymmetricLinks(items.device, link_gbps, latency_us) \
             if link_gbps and items.is_cuda and world > 1 else None
-        self._scratch = None
         self._inflight = None
         self._events: List[tuple] = []
 
@@ -393,16 +402,12 @@ class EmulatedRotation:
         if self.links is not None and self.s >= 1:
             # sub-step s: each ring sends the block it finished in s - 1 and receives the
             # block it needs in s + 1 (posted when s - 1 ended, as the neighbour's is)
-            if self._scratch is None:
-                cap = max(b.shape[0] for b in self.blocks)
-                self._scratch = [torch.empty((cap, self.items.shape[1]), dtype=self.items.dtype,
-                                             device=self.items.device) for _ in self._ring_blocks(0)]
             after = torch.cuda.Event()
             after.record()
             copies, link_bytes = [], 0
-            for out_b, in_b, buf in zip(self._ring_blocks(self.s - 1), self._ring_blocks(self.s + 1), self._scratch):
+            for out_b, in_b in zip(self._ring_blocks(self.s - 1), self._ring_blocks(self.s + 1)):
                 n = min(self.blocks[out_b].shape[0], self.blocks[in_b].shape[0])
-                copies.append((buf[:n], self.blocks[out_b][:n]))
+                copies.append((None, self.blocks[out_b][:n]))  # the link's scratch receives the bytes
                 nbytes = self.blocks[in_b].numel() * self.blocks[in_b].element_size()
                 link_bytes = max(link_bytes, nbytes)  # the rings use different links: in parallel
                 self.bytes_sent += self.blocks[out_b].numel() * self.blocks[out_b].element_size()
