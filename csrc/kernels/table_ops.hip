@@ -846,8 +846,11 @@ void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* ou
   while (sh < 6 && (1ll << sh) < wpr) ++sh;
   const int64_t rows = so.off[nseg];
   const int64_t waves = (rows + (64 >> sh) - 1) / (64 >> sh);
-  hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(waves, 4, 256 * 16)), dim3(256), 0, st, (const T*)src, k,
-                     wpr, (T*)out, so, nseg, sh, min_ticks);
+  // a modelled link transfer (min_ticks > 0) writes with at most one workgroup per CU, as
+  // RCCL's copy kernels occupy a few CUs, not the whole GPU beside the compute
+  const int max_blocks = min_ticks > 0 ? 256 : 256 * 16;
+  hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(waves, 4, max_blocks)), dim3(256), 0, st, (const T*)src,
+                     k, wpr, (T*)out, so, nseg, sh, min_ticks);
 }
 }  // namespace
 

@@ -45,11 +45,17 @@ correctness is ``parallel/vworld.py``'s and ``tests/test_multigpu_nccl_gpu.py``'
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
 
 from .comm import Comm
+
+
+#: A/B switch of the link model (``FPS_EMU_LINK=serial``: sleep for the link time, then
+#: write the receive -- the round-5 model; default: one fill kernel lasting the link time)
+_SERIAL_LINK = os.environ.get("FPS_EMU_LINK", "") == "serial"
 
 
 class _LinkWork:
@@ -161,7 +167,10 @@ class SymmetricComm(Comm):
         us = (self.latency_us + (max(peer) if peer else 0) * 1e-3 / self.link_gbps) if self.world > 1 else 0.0
         self._link.wait_stream(torch.cuda.current_stream(self.device))  # the send is ready in post order
         with torch.cuda.stream(self._link):
-            if not self._fill(send, out, send_splits, recv_splits, min_us=us):  # the write, during the link time
+            if _SERIAL_LINK:  # A/B (FPS_EMU_LINK=serial): the round-5 model, sleep then write
+                _Sleep.us(self.device, us)
+                self._fill(send, out, send_splits, recv_splits)
+            elif not self._fill(send, out, send_splits, recv_splits, min_us=us):  # the write, during the link time
                 _Sleep.us(self.device, us)
             done = torch.cuda.Event()
             done.record(self._link)

@@ -295,6 +295,13 @@ class RingRotation:
         self.s = 0
 
 
+import os as _os
+
+#: A/B switch of the emulated link model (``FPS_EMU_LINK=serial``: sleep for the link
+#: time, then copy -- the round-5 model; default: one fill kernel lasting the link time)
+_SERIAL_LINK = _os.environ.get("FPS_EMU_LINK", "") == "serial"
+
+
 class _SymmetricLinks:
     """Device-timed xGMI links of the emulated rank (``EmulatedRotation(link_gbps=...)``).
 
@@ -334,7 +341,17 @@ class _SymmetricLinks:
         srcs = [src for _, src in copies if src.shape[0]]
         self.stream.wait_event(after)
         with torch.cuda.stream(self.stream):
-            if srcs:
+            if srcs and _SERIAL_LINK:  # A/B (FPS_EMU_LINK=serial): the round-5 model, sleep then copy
+                self._sleep.us(self.device, us)
+                rows = [x.shape[0] for x in srcs]
+                if self._scratch is None or self._scratch.shape[0] < sum(rows):
+                    self._scratch = torch.empty((sum(rows),) + tuple(srcs[0].shape[1:]), dtype=srcs[0].dtype,
+                                                device=srcs[0].device)
+                off = 0
+                for x in srcs:
+                    self._scratch[off:off + x.shape[0]].copy_(x, non_blocking=True)
+                    off += x.shape[0]
+            elif srcs:
                 rows = [x.shape[0] for x in srcs]
                 src = srcs[0]
                 if (self._scratch is None or self._scratch.shape[0] < sum(rows)
