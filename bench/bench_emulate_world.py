@@ -16,6 +16,12 @@ and ``comm_wait_ms_per_step`` is the time the compute stream waited for them.
     python bench/bench_emulate_world.py [--ws 1,2,4,8] [--steps 20 --warmup 5]
 
 One JSON line per N: ms_per_step, per-GPU updates/s, ratio to N = 1.
+
+Each N runs in a fresh child interpreter: a process that has already built models of
+other world sizes holds more HIP streams than the 4 hardware queues a process gets, and
+the queue an N-rank model's streams then share with each other is luck -- the same N = 8
+emulation measured 7.1 ms alone and 9.2 ms after N = 2 and 4 in one process
+(``profiles/r6_link_model.md``).
 """
 from __future__ import annotations
 
@@ -49,6 +55,25 @@ def main():
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                     help="sub-steps on alternating compute streams (MFConfig.overlap_substeps; auto: from 4 ranks)")
     a = ap.parse_args()
+    ws = [int(x) for x in a.ws.split(",")]
+    if len(ws) > 1:  # one fresh child per world size (module docstring); the parent never touches the GPU
+        import subprocess
+
+        base = None
+        for W in ws:
+            argv = [sys.executable, os.path.abspath(__file__)] + [x for x in _argv_without_ws(sys.argv[1:])] + \
+                ["--ws", str(W)]
+            r = subprocess.run(argv, stdout=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                sys.exit(r.returncode)
+            for line in r.stdout.splitlines():
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    base = base or d["ms_per_step"]
+                    d["ratio_to_n1"] = d["ms_per_step"] / base  # to the first N of the list, as before
+                    line = json.dumps(d)
+                print(line, flush=True)
+        return
 
     import torch
 
@@ -97,6 +122,21 @@ def main():
             m.rot.close()
         del m, data
         torch.cuda.empty_cache()
+
+
+def _argv_without_ws(argv):
+    out, skip = [], False
+    for x in argv:
+        if skip:
+            skip = False
+            continue
+        if x == "--ws":
+            skip = True
+            continue
+        if x.startswith("--ws="):
+            continue
+        out.append(x)
+    return out
 
 
 if __name__ == "__main__":
