@@ -42,6 +42,8 @@ run cap8 python bench/bench_capacity.py --steps 20 --warmup 3 --emulate-world 8
 run cap8_bf16 python bench/bench_capacity.py --steps 20 --warmup 3 --emulate-world 8 --wire bf16
 run w2v1_ps_bf16 python bench/bench_w2v.py --steps 10 --warmup 3 --ps-path --wire bf16
 run pa8_hash_b python bench/bench_pa.py --emulate-world 8 --steps 40 --warmup 5 --partition hash
+run pa8_hash_dedup python bench/bench_pa.py --emulate-world 8 --steps 40 --warmup 5 --partition hash --dedup on
+run pa8_range_dedup python bench/bench_pa.py --emulate-world 8 --steps 40 --warmup 5 --partition range --dedup on
 run mfps python bench.py --steps 20 --warmup 5 --force-ps-path --no-hogwild-probe --exact-steps 0
 timeout -k 10 200 python bench/bench_topk.py --steps 10 --warmup 3 > $O/topk.log 2>&1 || { tail -20 $O/topk.log; exit 1; }
 echo "topk $(tail -1 $O/topk.log | cut -c1-200)"
