@@ -156,6 +156,7 @@ def main(argv=None):
             "emulate_mode": a.emulate_mode if emu else None, "emulated_rank": a.emulate_rank if emu else None,
             "shard_key_shares": shares,
             "projected_whole_node": {"value": per_gpu * a.emulate_world, "measured": False} if emu else None,
+            "host_enqueue_ms_per_step": t_host / a.steps * 1e3,
             "exposed_wait_ms_per_step": wait_ms if emu else None, "link_gbps": a.link_gbps if emu else None,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": a.partition, "zipf": a.zipf, "wire_dtype": a.wire,
