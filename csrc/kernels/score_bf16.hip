@@ -87,7 +87,7 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 // q_f / |q|; cb: [N / 32][D] coordinate ranges); stats[0] / [1] count the (query
 // block, item block) pairs scored / skipped by the coordinate bound (pairs the length
 // bound skips by itself are in neither).
-template <int D, int QB, bool MASK = false, bool COORD = false>
+template <int D, int QB, bool MASK = false, bool COORD = false, bool ILV = false>
 __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xbm,
@@ -306,15 +306,40 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
                                                         __builtin_bit_cast(bf16x8, qv[b][s]), acc, 0, 0, 0);
         return acc;
       };
-#pragma unroll
-      for (int b = 0; b < QB; ++b) {
-        if (!block_live(b)) continue;
-        const floatx16 acc = mfma_block(b);
+      auto filter = [&](int b, const floatx16& acc) {
         const float thr = theta[b] - margin * ql[b] * bm;
         float m = acc[0];
 #pragma unroll
         for (int j = 1; j < 16; ++j) m = fmaxf(m, acc[j]);
         if (m > thr) emit(b, acc, thr);
+      };
+      bool lv[QB];
+      bool all_live = true;
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        lv[b] = block_live(b);
+        all_live = all_live && lv[b];
+      }
+      if (ILV && QB > 1 && all_live) {
+        // the QB chains interleaved k-step by k-step: independent MFMAs issue back to
+        // back instead of each waiting for its predecessor's result, and every block's
+        // filter runs after all the MFMAs (one chain + its max / emit at a time left the
+        // matrix core idle through each dependency and each epilogue)
+        floatx16 acc[QB];
+#pragma unroll
+        for (int b = 0; b < QB; ++b) acc[b] = floatx16{0};
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int b = 0; b < QB; ++b)
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, cur[s]),
+                                                             __builtin_bit_cast(bf16x8, qv[b][s]), acc[b], 0, 0, 0);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) filter(b, acc[b]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+          if (lv[b]) filter(b, mfma_block(b));
       }
     }
     if (more) lstore(buf ^ 1);  // every wave finished reading buf ^ 1 at the previous barrier
@@ -434,6 +459,9 @@ FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, i
 // 0: always SB_ITEMS items per workgroup (A/B knob, FPS_SB_MIN_WGS)
 static int g_sb_min_wgs = 512;
 FPS_API void fps_score_set_min_wgs(int v) { g_sb_min_wgs = v; }
+// interleaved MFMA chains of a wave's query blocks (ILV; A/B knob FPS_SB_ILV)
+static int g_sb_ilv = 1;
+FPS_API void fps_score_set_ilv(int v) { g_sb_ilv = v; }
 
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xbm, float margin, float slack,
@@ -454,14 +482,23 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
     while (ipw > 64 && nqt * ((N + ipw - 1) / ipw) < g_sb_min_wgs) ipw >>= 1;                             \
     const int64_t nit = (N + ipw - 1) / ipw;                                                                \
     if (nqt * nit > INT32_MAX) return (int)hipErrorInvalidValue;                                            \
-    if (coord)                                                                                              \
-      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true>), dim3((unsigned)(nqt * nit)),    \
-                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
-                         cap, qf, qbf, cb, stats, gate, ipw);                                               \
+    const dim3 grid((unsigned)(nqt * nit));                                                                 \
+    if (coord && g_sb_ilv)                                                                                  \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true, true>), grid, dim3(256), 0, s, Qb, \
+                         Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb,     \
+                         stats, gate, ipw);                                                                 \
+    else if (coord)                                                                                         \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true, false>), grid, dim3(256), 0, s, Qb,\
+                         Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb,     \
+                         stats, gate, ipw);                                                                 \
+    else if (g_sb_ilv)                                                                                      \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, true>), grid, dim3(256), 0, s,    \
+                         Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
+                         stats, gate, ipw);                                                                 \
     else                                                                                                    \
-      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false>), dim3((unsigned)(nqt * nit)),   \
-                         dim3(256), 0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt,  \
-                         cap, qf, qbf, cb, stats, gate, ipw);                                               \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, false>), grid, dim3(256), 0, s,   \
+                         Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
+                         stats, gate, ipw);                                                                 \
   }
   // D = 64: FPS_SB_QB64 query blocks per wave + the bit-mask epilogue (round 2: 4
   // blocks, the fastest of 1/2/4 with branch or mask epilogues, profiles/r2_bf16_topk.md;

@@ -1084,6 +1084,9 @@ def block_max32(xlen: torch.Tensor) -> torch.Tensor:
     return x.view(nb, 32).amax(1)
 
 
+_SB_KNOBS = False
+
+
 def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, cand_pos: torch.Tensor,
                       cnt: torch.Tensor, qlen: torch.Tensor, xlen: Optional[torch.Tensor], coord=None,
                       stats: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
@@ -1118,9 +1121,14 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
             check_index(qf, D, "score_filter_bf16 qf")
         qf, qbf, cb = _c(qf), _c(qbf.float()), _c(cb.float())
     slack = 1.0 + 1e-4 + D * 2.4e-7
-    mw = os.environ.get("FPS_SB_MIN_WGS")  # A/B switch: fewest workgroups per scorer launch (0: 1024 items each)
-    if mw is not None:
-        N.require().fps_score_set_min_wgs(int(mw))
+    global _SB_KNOBS
+    if not _SB_KNOBS:  # A/B switches, read once: FPS_SB_MIN_WGS = fewest workgroups per scorer launch (0: 1024
+        _SB_KNOBS = True  # items each); FPS_SB_ILV=0: one MFMA chain at a time (no interleaved query blocks)
+        mw, ilv = os.environ.get("FPS_SB_MIN_WGS"), os.environ.get("FPS_SB_ILV")
+        if mw is not None:
+            N.require().fps_score_set_min_wgs(int(mw))
+        if ilv is not None:
+            N.require().fps_score_set_ilv(int(ilv))
     N.check(N.require().fps_score_filter_bf16(
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
         _c(qlen.float()).data_ptr(), _c(xbm.float()).data_ptr(), bf16_score_margin(D), slack,
