@@ -459,8 +459,10 @@ FPS_API int fps_coord_gate(const int32_t* stats, int32_t* prev, int32_t* gate, i
 // 0: always SB_ITEMS items per workgroup (A/B knob, FPS_SB_MIN_WGS)
 static int g_sb_min_wgs = 512;
 FPS_API void fps_score_set_min_wgs(int v) { g_sb_min_wgs = v; }
-// interleaved MFMA chains of a wave's query blocks (ILV; A/B knob FPS_SB_ILV)
-static int g_sb_ilv = 1;
+// interleaved MFMA chains of a wave's query blocks (ILV; A/B knob FPS_SB_ILV=1): measured equal to one chain at a
+// time (MFMA busy 33.8 vs 33.6 %, profiles/r6_scorer_ilv_ab.txt) -- other waves already hide the dependency -- at
+// 8 more VGPRs, so off
+static int g_sb_ilv = 0;
 FPS_API void fps_score_set_ilv(int v) { g_sb_ilv = v; }
 
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,

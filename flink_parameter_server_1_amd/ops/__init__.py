@@ -1123,7 +1123,7 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     slack = 1.0 + 1e-4 + D * 2.4e-7
     global _SB_KNOBS
     if not _SB_KNOBS:  # A/B switches, read once: FPS_SB_MIN_WGS = fewest workgroups per scorer launch (0: 1024
-        _SB_KNOBS = True  # items each); FPS_SB_ILV=0: one MFMA chain at a time (no interleaved query blocks)
+        _SB_KNOBS = True  # items each); FPS_SB_ILV=1: interleaved MFMA chains of the query blocks
         mw, ilv = os.environ.get("FPS_SB_MIN_WGS"), os.environ.get("FPS_SB_ILV")
         if mw is not None:
             N.require().fps_score_set_min_wgs(int(mw))
