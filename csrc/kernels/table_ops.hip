@@ -889,6 +889,27 @@ FPS_API int fps_mark_rows(uint8_t* touched, const int32_t* rows, int64_t n, void
   return 0;
 }
 
+namespace {
+// The count message of a dynamic PS plan: row j = (2 counts[j] + request, flag).  One
+// launch instead of the cast / scale / offset / fill / concatenate chain (five torch
+// kernels and their host calls per micro-batch, TensorPS._pending).
+__global__ void pack_counts_kernel(const int32_t* __restrict__ counts, int W, int request, int flag,
+                                   int32_t* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= W) return;
+  out[2 * j] = counts[j] * 2 + request;
+  out[2 * j + 1] = flag;
+}
+}  // namespace
+
+FPS_API int fps_pack_counts(const int32_t* counts, int W, int request, int flag, int32_t* out, void* stream) {
+  if (W <= 0) return 0;
+  hipLaunchKernelGGL(pack_counts_kernel, dim3((W + 255) / 256), dim3(256), 0, (hipStream_t)stream, counts, W, request,
+                     flag, out);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
 FPS_API int fps_flip_masked(float* table, const uint8_t* mask, int64_t n_rows, int D, void* stream) {
   if (n_rows <= 0 || D <= 0) return 0;
   hipLaunchKernelGGL(flip_masked_kernel, dim3(grid_for(n_rows * D, 256, 256 * 16)), dim3(256), 0, (hipStream_t)stream,

@@ -78,11 +78,11 @@ class PAWorker(BatchedWorkerLogic):
         else:
             ps.push_unique(delta)
         B = indptr.numel() - 1
-        if ids is None:
-            ids = torch.arange(self._seen, self._seen + B, device=labels.device)
-        self._seen += B
         if self.emit_predictions:  # the unlabelled examples' predictions, compacted by the consumer (no sync)
+            if ids is None:
+                ids = torch.arange(self._seen, self._seen + B, device=labels.device)
             ps.output(MaskedPair(ids, pred, labels == (0 if self.kind == "binary" else -1)))
+        self._seen += B
         self.examples += B
         self.last = (pred, loss)
 

@@ -101,13 +101,27 @@ def mark_rows(touched: torch.Tensor, rows: torch.Tensor) -> None:
     touched[r[r >= 0]] = 1
 
 
-def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0) -> None:
+def pack_counts(counts: torch.Tensor, W: int, request: bool, flag: int) -> torch.Tensor:
+    """The count message of a dynamic PS plan, int32 ``[W, 2]``: row ``j`` =
+    ``(2 counts[j] + request, flag)`` (``TensorPS._wire_counts`` + the flag column);
+    one launch on the GPU."""
+    if _on_gpu(counts) and counts.dtype == torch.int32 and counts.is_contiguous() and counts.numel() >= W:
+        out = torch.empty((W, 2), dtype=torch.int32, device=counts.device)
+        N.check(N.require().fps_pack_counts(counts.data_ptr(), int(W), int(bool(request)), int(flag), out.data_ptr(),
+                                            N.stream_ptr(counts.device)), "pack_counts")
+        return out
+    c = counts[:W].view(W, 1).to(torch.int32) * 2 + int(bool(request))
+    return torch.cat([c, torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)], dim=1)
+
+
+def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0, stream=None) -> None:
     """``out`` = the concatenation over ``j`` of ``src``'s first ``rows[j]`` rows, ``src``
     tiled where ``rows[j] > len(src)`` (row ``i`` of segment ``j`` is ``src[i % len(src)]``):
     the emulated all-to-all's receive (``parallel/emulated.py``), one launch on the GPU.
     ``rows`` is a host sequence (<= 64 segments); ``out`` holds at least ``sum(rows)`` rows.
     ``min_us`` (GPU): the launch also lasts at least that long -- a modelled link
-    transfer that writes its receive as the data arrives (done at max(link, write))."""
+    transfer that writes its receive as the data arrives (done at max(link, write)).
+    ``stream`` (GPU): launch there instead of on the current stream."""
     rows = [int(m) for m in rows]
     n_out, k = sum(rows), src.shape[0]
     if n_out == 0 and not (min_us > 0 and src.is_cuda):
@@ -129,7 +143,8 @@ def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0
         for d in src.shape[1:]:
             row_bytes *= int(d)
         N.check(N.require().fps_segment_fill(src.data_ptr(), k, row_bytes, out.data_ptr(), ctypes.addressof(arr),
-                                             len(rows), N.stream_ptr(src.device), float(min_us)),
+                                             len(rows), N.stream_ptr(src.device) if stream is None else
+                                             stream.cuda_stream, float(min_us)),
                 "segment_fill")
         return
     off = 0
@@ -305,7 +320,20 @@ class DedupWorkspace:
             self.owner_slot_h = torch.empty(self.hash_cap, dtype=torch.int32, device=self.device)
             self.epoch = 0
 
-    def run(self, keys: torch.Tensor):
+    def _outputs(self, n: int, fresh: bool):
+        """(counts zeroed, prefix, uniq, pos) to write: the workspace's own, or -- ``fresh``
+        -- new tensors the caller may keep while later batches reuse the workspace (no
+        copy of ~2 x 4 B per request, ``TensorPS._pending``)."""
+        if not fresh:
+            self.counts.zero_()
+            return self.counts, self.prefix, self.uniq, self.pos
+        dev = self.device
+        return (torch.zeros(self.W, dtype=torch.int32, device=dev), torch.empty(self.W + 1, dtype=torch.int32, device=dev),
+                torch.empty(max(n, 1), dtype=torch.int32, device=dev), torch.empty(max(n, 1), dtype=torch.int32, device=dev))
+
+    def run(self, keys: torch.Tensor, fresh: bool = False):
+        """De-duplicate and group ``keys`` by owner: ``(counts, prefix, uniq, pos)``.
+        ``fresh``: outputs in new tensors instead of the reused workspace."""
         if self.device.type != "cuda":
             c, p, u, q = R.dedup(keys, self.W, self.part_kind, self.block)
             return self._widen(c, p) + (u, q)
@@ -317,7 +345,7 @@ class DedupWorkspace:
             (self.tab if self.hashed else self.map).zero_()
             if self.flag is not None:
                 self.flag.zero_()
-        self.counts.zero_()
+        counts, prefix, uniq, pos = self._outputs(n, fresh)
         lib = N.require()
         s = N.stream_ptr(self.device)
         use_flags = not self.hashed and (self.method == "flags" or
@@ -330,18 +358,18 @@ class DedupWorkspace:
                                         device=self.device)
             N.check(lib.fps_dedup_flags(_c(keys).data_ptr(), n, self.flag.data_ptr(), self.slot.data_ptr(),
                                         self.epoch, self.num_ids, self.W, self.part_kind, self.block,
-                                        self.bsum.data_ptr(), self.counts.data_ptr(), self.prefix.data_ptr(),
-                                        self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup_flags")
+                                        self.bsum.data_ptr(), counts.data_ptr(), prefix.data_ptr(),
+                                        uniq.data_ptr(), pos.data_ptr(), s), "dedup_flags")
         elif self.hashed:
             N.check(lib.fps_dedup_hashed(_c(keys).data_ptr(), n, self.tab.data_ptr(), self.hash_cap, self.epoch,
-                                         self.W, self.part_kind, self.block, self.counts.data_ptr(),
-                                         self.prefix.data_ptr(), self.hslot.data_ptr(), self.owner_slot_h.data_ptr(),
-                                         self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup_hashed")
+                                         self.W, self.part_kind, self.block, counts.data_ptr(),
+                                         prefix.data_ptr(), self.hslot.data_ptr(), self.owner_slot_h.data_ptr(),
+                                         uniq.data_ptr(), pos.data_ptr(), s), "dedup_hashed")
         else:
             N.check(lib.fps_dedup(_c(keys).data_ptr(), n, self.map.data_ptr(), self.epoch, self.W,
-                                  self.part_kind, self.block, self.counts.data_ptr(), self.prefix.data_ptr(),
-                                  self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(), s), "dedup")
-        return self._widen(self.counts, self.prefix) + (self.uniq, self.pos[:n])
+                                  self.part_kind, self.block, counts.data_ptr(), prefix.data_ptr(),
+                                  self.owner_slot.data_ptr(), uniq.data_ptr(), pos.data_ptr(), s), "dedup")
+        return self._widen(counts, prefix) + (uniq, pos[:n])
 
     def _widen(self, counts, prefix):
         """``(counts[out_world], prefix[out_world + 1])``: the shards' counts, then zeros
@@ -353,7 +381,7 @@ class DedupWorkspace:
         prefix = torch.cat([prefix[:self.W + 1], prefix[self.W:self.W + 1].expand(E)])
         return counts, prefix
 
-    def route(self, keys: torch.Tensor):
+    def route(self, keys: torch.Tensor, fresh: bool = False):
         """Like ``run`` but WITHOUT de-duplication: every request is its own entry of
         ``uniq`` (grouped by owning shard), ``pos`` a permutation of the requests.
         Same return layout as ``run``."""
@@ -362,12 +390,12 @@ class DedupWorkspace:
             return self._widen(c, p) + (u, q)
         n = keys.numel()
         self._grow(max(n, 1))
-        self.counts.zero_()
+        counts, prefix, uniq, pos = self._outputs(n, fresh)
         N.check(N.require().fps_route_requests(_c(keys).data_ptr(), n, self.W, self.part_kind, self.block,
-                                               self.counts.data_ptr(), self.prefix.data_ptr(),
-                                               self.owner_slot.data_ptr(), self.uniq.data_ptr(), self.pos.data_ptr(),
+                                               counts.data_ptr(), prefix.data_ptr(),
+                                               self.owner_slot.data_ptr(), uniq.data_ptr(), pos.data_ptr(),
                                                N.stream_ptr(self.device)), "route_requests")
-        return self._widen(self.counts, self.prefix) + (self.uniq, self.pos[:n])
+        return self._widen(counts, prefix) + (uniq, pos[:n])
 
     def reset_claims(self, keys: torch.Tensor) -> None:
         """Empty the claim entries of ``keys`` (the step's unique keys).  In

@@ -32,6 +32,7 @@ _SIGNATURES = {
     "fps_abi_version": [],
     "fps_init_rows": [c_vp, c_i64, c_int, c_i64, c_i64, c_f32, c_f32, c_u32, c_vp],
     "fps_mark_rows": [c_vp, c_vp, c_i64, c_vp],
+    "fps_pack_counts": [c_vp, c_int, c_int, c_int, c_vp, c_vp],
     "fps_static_plan": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_flip_masked": [c_vp, c_vp, c_i64, c_int, c_vp],
     "fps_dedup_flags": [c_vp, c_i64, c_vp, c_vp, c_u32, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -154,7 +155,18 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed with hipError {rc}")
 
 
+#: the current stream's raw handle without building a Stream object (the launch path's
+#: ``torch.cuda.current_stream(device)`` resolved the device index and wrapped the stream
+#: in Python on every kernel launch: ~1/10 of a PS micro-batch's host time)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    if _RAW_STREAM is not None:
+        if isinstance(device, torch.device) and device.type == "cuda":
+            return _RAW_STREAM(device.index if device.index is not None else torch.cuda.current_device())
+        if device is None:
+            return _RAW_STREAM(torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 

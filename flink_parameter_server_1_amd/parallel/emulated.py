@@ -96,56 +96,65 @@ class SymmetricComm(Comm):
 
     # ------------------------------------------------------------- link model
     def _fill(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
-              recv_splits: Sequence[int], min_us: float = 0.0) -> bool:
+              recv_splits: Sequence[int], min_us: float = 0.0, stream=None) -> bool:
         """The received buffer: this rank's own send buffer (symmetric), or every
         incoming segment = this rank's self-segment tiled / cut (hot owner).  On the GPU
-        one segment-fill kernel that also lasts ``min_us`` (the link time); returns
-        whether it did (else the caller models the link time itself)."""
+        one segment-fill kernel (on ``stream``, else the current one) that also lasts
+        ``min_us`` (the link time); returns whether it did (else the caller models the
+        link time itself)."""
         from .. import ops
 
         if not self.hot_owner:
             n = int(sum(send_splits))
             if n and send.is_cuda:
-                ops.segment_fill(send[:n].contiguous(), [n], out[:n], min_us=min_us)
+                ops.segment_fill(send[:n].contiguous(), [n], out[:n], min_us=min_us, stream=stream)
                 return True
-            out[:n].copy_(send[:n], non_blocking=True)
+            self._on(stream, lambda: out[:n].copy_(send[:n], non_blocking=True))
             return False
         a = int(sum(send_splits[: self.rank]))
         own = send[a: a + int(send_splits[self.rank])]
-        n_out = int(sum(recv_splits))
         rs = [int(m) for m in recv_splits]
-        k = own.shape[0]
+        n_out = sum(rs)
         # one kernel per exchange (the transfer model must not cost more device time than
         # the real receive): every peer sends the self-segment (requests / pushes), or a
         # prefix of it (answers)
-        if k and n_out and own.is_cuda:
-            ops.segment_fill(own.contiguous(), rs, out[:n_out], min_us=min_us)
+        if own.shape[0] and n_out and own.is_cuda:
+            ops.segment_fill(own.contiguous(), rs, out[:n_out], min_us=min_us, stream=stream)
             return True
+        self._on(stream, lambda: self._fill_torch(send, own, out, rs))
+        return False
+
+    @staticmethod
+    def _on(stream, fn) -> None:
+        if stream is None:
+            fn()
+        else:
+            with torch.cuda.stream(stream):
+                fn()
+
+    @staticmethod
+    def _fill_torch(send: torch.Tensor, own: torch.Tensor, out: torch.Tensor, rs: List[int]) -> None:
+        """The hot-owner receive with torch ops (CPU, or nothing of this rank's own to mirror)."""
+        n_out, k = sum(rs), own.shape[0]
         if k and n_out and all(m == k for m in rs):
             out[:n_out].view((len(rs),) + tuple(own.shape)).copy_(own.unsqueeze(0).expand((len(rs),) + tuple(own.shape)))
-            return False
+            return
         if k and n_out:
             src = own if max(rs) <= k else torch.cat([own] * -(-max(rs) // k))
             torch.cat([src[:m] for m in rs], out=out[:n_out])
-            return False
+            return
         off = 0
-        for m in recv_splits:
-            m = int(m)
-            done = 0
-            while done < m:
-                k = min(m - done, own.shape[0]) if own.shape[0] else 0
-                if k == 0:  # nothing to mirror: any valid rows of the send buffer
-                    src = send if send.shape[0] else None
-                    if src is None:
-                        out[off + done: off + m].zero_()
-                        break
-                    k = min(m - done, src.shape[0])
-                    out[off + done: off + done + k].copy_(src[:k], non_blocking=True)
+        for m in rs:
+            if m:  # nothing to mirror: any valid rows of the send buffer (zeros without any)
+                if send.shape[0]:
+                    done = 0
+                    while done < m:
+                        c = min(m - done, send.shape[0])
+                        out[off + done: off + done + c].copy_(send[:c], non_blocking=True)
+                        done += c
                 else:
-                    out[off + done: off + done + k].copy_(own[:k], non_blocking=True)
-                done += k
+                    out[off: off + m].zero_()
             off += m
-        return False
 
     def _post(self, send: torch.Tensor, out: torch.Tensor, send_splits: Sequence[int],
               recv_splits: Optional[Sequence[int]] = None) -> Optional[object]:
@@ -165,31 +174,36 @@ class SymmetricComm(Comm):
         from .vworld import _Sleep
 
         us = (self.latency_us + (max(peer) if peer else 0) * 1e-3 / self.link_gbps) if self.world > 1 else 0.0
-        self._link.wait_stream(torch.cuda.current_stream(self.device))  # the send is ready in post order
-        with torch.cuda.stream(self._link):
-            if _SERIAL_LINK:  # A/B (FPS_EMU_LINK=serial): the round-5 model, sleep then write
+        link = self._link
+        ready = torch.cuda.Event()  # the send is ready in post order
+        ready.record(torch.cuda.current_stream(self.device))
+        link.wait_event(ready)
+        if _SERIAL_LINK:  # A/B (FPS_EMU_LINK=serial): the round-5 model, sleep then write
+            with torch.cuda.stream(link):
                 _Sleep.us(self.device, us)
-                self._fill(send, out, send_splits, recv_splits)
-            elif not self._fill(send, out, send_splits, recv_splits, min_us=us):  # the write, during the link time
+            self._fill(send, out, send_splits, recv_splits, stream=link)
+        elif not self._fill(send, out, send_splits, recv_splits, min_us=us, stream=link):  # the write, during the link
+            with torch.cuda.stream(link):
                 _Sleep.us(self.device, us)
-            done = torch.cuda.Event()
-            done.record(self._link)
-        send.record_stream(self._link)
-        out.record_stream(self._link)
+        done = torch.cuda.Event()
+        done.record(link)
+        send.record_stream(link)
+        out.record_stream(link)
         self.transfers += 1
         return done
 
     def _wait(self, done) -> None:
         if done is None:
             return
-        if torch.cuda.current_stream(self.device) != self._main:
-            torch.cuda.current_stream(self.device).wait_event(done)
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self._main:
+            cur.wait_event(done)
             return
         e0 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        torch.cuda.current_stream(self.device).wait_event(done)
+        e0.record(cur)
+        cur.wait_event(done)
         e1 = torch.cuda.Event(enable_timing=True)
-        e1.record()
+        e1.record(cur)
         self._events.append((e0, e1))
 
     def wait_ms(self, reset: bool = True) -> float:

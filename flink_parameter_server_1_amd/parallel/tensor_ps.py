@@ -375,11 +375,13 @@ class TensorPS:
                                    None, int(flag), n_bound=n,
                                    unique=False, static=True)
             with stage("ps.route", self.timer):
-                counts, prefix, uniq, pos = self.dedup.route(keys)
+                counts, prefix, uniq, pos = self.dedup.route(keys, fresh=True)
             return n, counts, uniq, pos, False
+        static1 = W == 1 and self.static and not getattr(self.table, "sparse", False)
         with stage("ps.dedup", self.timer):
-            counts, prefix, uniq, pos = self.dedup.run(keys)
-        if W == 1 and self.static and not getattr(self.table, "sparse", False):
+            # a dynamic plan keeps its outputs across later plans: fresh tensors, no copy
+            counts, prefix, uniq, pos = self.dedup.run(keys, fresh=not static1)
+        if static1:
             nb = min(n, int(self.table.key_space))
             # padding slot j serves the real key uniq[j mod U]: real rows only (the
             # close-time dump stays exact) and spread over all of them (a single padding
@@ -391,6 +393,16 @@ class TensorPS:
                                static=True, push_rows=push_rows)
         return n, counts, uniq, pos, True
 
+    def _own(self, t: torch.Tensor) -> torch.Tensor:
+        """``t``, cloned if it lives in the dedup workspace (reused by the next plan)."""
+        ws = self.dedup
+        p = t.untyped_storage().data_ptr()
+        for a in ("counts", "prefix", "uniq", "pos"):
+            w = getattr(ws, a, None)
+            if w is not None and w.untyped_storage().data_ptr() == p:
+                return t.clone()
+        return t
+
     @staticmethod
     def _wire_counts(counts: torch.Tensor, W: int, unique: bool) -> torch.Tensor:
         """Per-peer counts as sent in the count exchange: ``2 * count + 1`` for a
@@ -400,10 +412,11 @@ class TensorPS:
     def _pending(self, n, counts, uniq, pos, unique: bool = True, flag: int = 0) -> PendingPlan:
         """Stage A's count exchange of a computed (de-duplicated or request) plan."""
         W = self.comm.world
-        # the workspace is reused by the next plan_begin: this plan keeps copies
-        counts = counts.clone()
-        uniq = uniq[:n].clone()
-        pos = pos.clone()
+        # the workspace is reused by the next plan_begin: this plan keeps copies of what
+        # lives there (a fresh-output dedup / the CPU twins return tensors of their own)
+        counts = self._own(counts)
+        uniq = self._own(uniq[:n])
+        pos = self._own(pos)
         if W == 1:  # no peers: only the count travels (device -> host), no exchange / packing ops
             if self._pinned:
                 host = torch.empty(1, dtype=torch.int32, pin_memory=True)
@@ -414,8 +427,7 @@ class TensorPS:
                 host, ev = counts[:1].to("cpu", torch.int32), None
             self._plan_seq += 1
             return PendingPlan(n, counts, uniq, pos, host, ev, int(flag), unique=unique, seq=self._plan_seq)
-        flags = torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)
-        send = torch.cat([self._wire_counts(counts, W, unique), flags], dim=1).contiguous()  # [W, 2]
+        send = ops.pack_counts(counts, W, not unique, flag)  # [W, 2]: 2 count + request, flag
         if (self.owner_stream is not None or self.async_exchange) and self._pinned:
             host, ev = self._counts_async(send)
         else:
@@ -524,7 +536,7 @@ class TensorPS:
             return out
         T, W = len(dyn), comm.world
         dev = staged[dyn[0]][1].device
-        counts = [staged[j][1].clone() for j in dyn]  # the workspaces are reused by the next plan
+        counts = [pss[j]._own(staged[j][1]) for j in dyn]  # the workspaces are reused by the next plan
         if W == 1:
             send = torch.cat([c[:1].to(torch.int32) for c in counts])  # [T]
             both = send
@@ -552,7 +564,7 @@ class TensorPS:
             n, _, uniq, pos, unique = staged[j]
             cols = (t, T, t, T) if W == 1 else (t, T, T + 1 + t, 2 * T + 1)
             pss[j]._plan_seq += 1
-            out[j] = PendingPlan(n, counts[t], uniq[:n].clone(), pos.clone(), host, ev, int(flag), unique=unique,
+            out[j] = PendingPlan(n, counts[t], pss[j]._own(uniq[:n]), pss[j]._own(pos), host, ev, int(flag), unique=unique,
                                  cols=cols, seq=pss[j]._plan_seq)
         return out
 

@@ -692,3 +692,10 @@ def test_segment_fill_lasts_its_link_time():
         torch.cuda.synchronize()
         assert a.elapsed_time(b) * 1e3 >= 0.95 * want_us
     assert torch.equal(out, torch.cat([src, src]))
+
+
+def test_pack_counts_kernel_matches_cpu():
+    c = torch.randint(0, 1 << 20, (300,), dtype=torch.int32)
+    for request, flag in ((False, 0), (True, 1), (True, 0)):
+        got = ops.pack_counts(c.to(DEV), 300, request, flag).cpu()
+        assert torch.equal(got, ops.pack_counts(c, 300, request, flag))

@@ -160,3 +160,15 @@ def test_poll_flags_reads_one_submit_late():
     assert pipe.all_flagged
     pipe.reset_flags()
     assert not pipe.all_flagged and pipe._flags_host is None and pipe._flags_dev is None
+
+
+def test_pack_counts_matches_wire_counts():
+    """``ops.pack_counts`` (one launch on the GPU) = ``TensorPS._wire_counts`` + the flag column."""
+    from flink_parameter_server_1_amd import ops
+    from flink_parameter_server_1_amd.parallel.tensor_ps import TensorPS
+
+    c = torch.tensor([5, 0, 7, 123456], dtype=torch.int32)
+    for request, flag in ((False, 0), (True, 1)):
+        want = torch.cat([TensorPS._wire_counts(c, 4, not request),
+                          torch.full((4, 1), flag, dtype=torch.int32)], dim=1)
+        assert torch.equal(ops.pack_counts(c, 4, request, flag), want)
