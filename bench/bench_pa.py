@@ -104,8 +104,18 @@ def main(argv=None):
     comm.barrier()
     sync()
     emu = a.emulate_world > 1
+    wait_ms = None
     if emu and dev.type == "cuda":
+        # the exposed link waits, timed in a pass of their own: the timing events cost host
+        # time a real RCCL job does not spend, so the timed loop below runs without them
         comm.wait_ms()  # drop the warm-up's waits
+        nw = max(4, a.steps // 4)
+        for s in range(nw):
+            m.train_step(*batches[s % 4])
+        m.flush()
+        sync()
+        wait_ms = comm.wait_ms() / nw
+        comm.time_waits = False
     prof = None
     if a.host_profile:
         import cProfile
@@ -134,7 +144,6 @@ def main(argv=None):
             f.write(f"host enqueue time per step: {t_host / a.steps * 1e3:.3f} ms; wall per step "
                     f"{dt / a.steps * 1e3:.3f} ms\n")
             f.write(buf.getvalue())
-    wait_ms = comm.wait_ms() / a.steps if emu and dev.type == "cuda" else 0.0
     ip, idx, val, lab = batches[0]  # accuracy on a trained batch (1B features: held-out rows share few features)
     pred = m.predict(ip, idx, val)
     acc = float(((pred.to(torch.int8) == lab) if a.kind == "binary" else (pred == lab)).float().mean())
@@ -157,7 +166,9 @@ def main(argv=None):
             "shard_key_shares": shares,
             "projected_whole_node": {"value": per_gpu * a.emulate_world, "measured": False} if emu else None,
             "host_enqueue_ms_per_step": t_host / a.steps * 1e3,
-            "exposed_wait_ms_per_step": wait_ms if emu else None, "link_gbps": a.link_gbps if emu else None,
+            "exposed_wait_ms_per_step": wait_ms if emu else None,
+            "exposed_wait_measured": "separate pass of max(4, steps/4) steps with timing events" if emu else None,
+            "link_gbps": a.link_gbps if emu else None,
             "config": {"model": f"PA-{a.kind} features={a.features} labels={a.labels}", "nnz": a.nnz,
                        "batch_per_gpu": a.batch, "partition": a.partition, "zipf": a.zipf, "wire_dtype": a.wire,
                        "dedup": a.dedup,

@@ -830,9 +830,34 @@ __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_
   const int sub = lane >> lpr_shift, c0 = lane & (lpr - 1);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t row = wave * rpw + sub; row < rows; row += waves * rpw) {
-    const int64_t r = segment_src_row(so, nseg, row, k);
-    for (int64_t c = c0; c < wpr; c += lpr) out[row * wpr + c] = src[r * wpr + c];
+  const int64_t stride = waves * rpw;
+  if (wpr <= lpr) {
+    // a row is at most one word per lane (PA's 4-B weights, 128-B rows, ...): FILL_UR rows
+    // per lane per trip, every load issued before the first store -- one dependent
+    // load / store pair per trip left a 256-workgroup launch latency-bound (a 16.8 MB
+    // receive of 4-B rows took 117 us beside the owner's gather)
+    constexpr int FILL_UR = 8;
+    const bool on = c0 < wpr;
+    for (int64_t row0 = wave * rpw + sub; row0 < rows; row0 += stride * FILL_UR) {
+      int64_t r[FILL_UR];
+      T v[FILL_UR];
+#pragma unroll
+      for (int u = 0; u < FILL_UR; ++u) {
+        const int64_t row = row0 + u * stride;
+        r[u] = on && row < rows ? segment_src_row(so, nseg, row, k) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < FILL_UR; ++u)
+        if (r[u] >= 0) v[u] = src[r[u] * wpr + c0];
+#pragma unroll
+      for (int u = 0; u < FILL_UR; ++u)
+        if (r[u] >= 0) out[(row0 + u * stride) * wpr + c0] = v[u];
+    }
+  } else {
+    for (int64_t row = wave * rpw + sub; row < rows; row += stride) {
+      const int64_t r = segment_src_row(so, nseg, row, k);
+      for (int64_t c = c0; c < wpr; c += lpr) out[row * wpr + c] = src[r * wpr + c];
+    }
   }
   if (timer)
     while (__builtin_amdgcn_s_memrealtime() - t0 < min_ticks) __builtin_amdgcn_s_sleep(8);

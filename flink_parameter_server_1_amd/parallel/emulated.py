@@ -92,6 +92,10 @@ class SymmetricComm(Comm):
         #: transfer (``TensorPS.owner_stream``) idles no compute
         self._main = torch.cuda.current_stream(self.device) if self.cuda else None
         self._events: List[tuple] = []  # (wait start, wait end) events of every exposed wait
+        #: time the compute stream's waits (two timing events per wait: ~1/10 of a PA
+        #: micro-batch's host time, which a real RCCL job does not spend -- a bench can
+        #: time its steps with this off and measure the waits in a pass of their own)
+        self.time_waits = True
         self.transfers = 0
 
     # ------------------------------------------------------------- link model
@@ -196,7 +200,7 @@ class SymmetricComm(Comm):
         if done is None:
             return
         cur = torch.cuda.current_stream(self.device)
-        if cur != self._main:
+        if not self.time_waits or cur != self._main:
             cur.wait_event(done)
             return
         e0 = torch.cuda.Event(enable_timing=True)

@@ -672,10 +672,11 @@ def test_segment_fill_matches_torch(shape, dtype):
         for i in range(0, m, max(1, m // 7)):
             assert torch.equal(ref[off + i], src[i % k])
         off += m
-    out = torch.full((n + 3,) + shape[1:], 7, dtype=dtype, device=DEV)
-    ops.segment_fill(src.to(DEV), rows, out)
-    assert torch.equal(out[:n].cpu(), ref)
-    assert bool((out[n:].cpu() == 7).all())  # nothing past the segments is written
+    for min_us in (0.0, 50.0):  # the timed (link) launch runs on at most 256 workgroups
+        out = torch.full((n + 3,) + shape[1:], 7, dtype=dtype, device=DEV)
+        ops.segment_fill(src.to(DEV), rows, out, min_us=min_us)
+        assert torch.equal(out[:n].cpu(), ref)
+        assert bool((out[n:].cpu() == 7).all())  # nothing past the segments is written
 
 
 def test_segment_fill_lasts_its_link_time():
