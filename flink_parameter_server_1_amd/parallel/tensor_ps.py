@@ -451,15 +451,19 @@ class TensorPS:
         communicator before it).  Returns ``(pinned host tensor, event)``."""
         with stage("ps.count-a2a", self.timer):
             recv, work = self.comm.exchange_counts_async(send)
+        host = torch.empty((send.shape[0], 2 * send.shape[1]), dtype=torch.int32, pin_memory=True)
+        if work is None:  # the counts are already on this stream (no transfer in flight): copy here
+            host.copy_(torch.cat([send, recv], dim=1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            return host, ev
         cur = torch.cuda.current_stream(send.device)
         if self._aux_stream is None:
             self._aux_stream = torch.cuda.Stream(send.device)
         aux = self._aux_stream
-        host = torch.empty((send.shape[0], 2 * send.shape[1]), dtype=torch.int32, pin_memory=True)
         with torch.cuda.stream(aux):
             aux.wait_stream(cur)  # send was written on the compute stream
-            if work is not None:
-                work.wait()
+            work.wait()
             send.record_stream(aux)
             recv.record_stream(aux)
             host.copy_(torch.cat([send, recv], dim=1), non_blocking=True)
