@@ -58,6 +58,8 @@ def main(argv=None):
                          "the first batch -- the owner the job waits for)")
     ap.add_argument("--host-profile", default=None,
                     help="write a cProfile summary of the timed loop's host (Python) time to this file")
+    ap.add_argument("--host-breakdown", action="store_true",
+                    help="print the timed loop's host time per PS stage (wall-clock wrappers, no profiler)")
     ap.add_argument("--link-gbps", type=float, default=50.0, help="--emulate-world: per-peer link rate (GB/s)")
     ap.add_argument("--latency-us", type=float, default=5.0, help="--emulate-world: per-message link latency")
     a = ap.parse_args(argv)
@@ -116,6 +118,7 @@ def main(argv=None):
         sync()
         wait_ms = comm.wait_ms() / nw
         comm.time_waits = False
+    breakdown = _wrap_stages(m, comm) if a.host_breakdown else None
     prof = None
     if a.host_profile:
         import cProfile
@@ -144,6 +147,9 @@ def main(argv=None):
             f.write(f"host enqueue time per step: {t_host / a.steps * 1e3:.3f} ms; wall per step "
                     f"{dt / a.steps * 1e3:.3f} ms\n")
             f.write(buf.getvalue())
+    if breakdown is not None:
+        for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1][0]):
+            print(f"host {k:40s} {v[0] / a.steps * 1e6:8.1f} us/step {v[1] / a.steps:5.2f} calls/step", file=sys.stderr)
     ip, idx, val, lab = batches[0]  # accuracy on a trained batch (1B features: held-out rows share few features)
     pred = m.predict(ip, idx, val)
     acc = float(((pred.to(torch.int8) == lab) if a.kind == "binary" else (pred == lab)).float().mean())
@@ -175,6 +181,45 @@ def main(argv=None):
                        "exchange": "local-direct" if m._direct else "ps", "staleness": m.cfg.staleness,
                        "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1)},
         }), flush=True)
+
+
+def _wrap_stages(m, comm):
+    """Wall-clock (inclusive) host time of the PS stages of the timed loop: {name: [s, calls]}."""
+    from flink_parameter_server_1_amd import ops
+
+    acc = {}
+
+    def wrap(obj, name, label):
+        f = getattr(obj, name)
+
+        def g(*args, **kw):
+            t = time.perf_counter()
+            try:
+                return f(*args, **kw)
+            finally:
+                e = acc.setdefault(label, [0.0, 0])
+                e[0] += time.perf_counter() - t
+                e[1] += 1
+        setattr(obj, name, g)
+
+    ps, pipe = m.ps, m.runtime.pipe
+    for n in ("plan_begin", "plan_end", "pull_planned", "push", "apply_pending", "_pending", "_stage_a", "serve",
+              "_counts_async"):
+        wrap(ps, n, "ps." + n)
+    for n in ("_plan_next", "_serve", "_finish", "poll_flags"):
+        wrap(pipe, n, "pipe." + n)
+    wrap(pipe, "compute", "pipe.compute")
+    for n in ("all_to_all_async", "all_to_all", "exchange_counts", "_wait", "_post"):
+        if hasattr(comm, n):
+            wrap(comm, n, "comm." + n)
+    wrap(m.worker, "on_pull_recv_batch", "worker.on_pull_recv_batch")
+    wrap(m.worker, "on_recv_batch", "worker.on_recv_batch")
+    wrap(m.runtime, "_submit_eager", "engine._submit_eager")
+    for n in ("segment_fill", "gather_rows", "apply_rows", "pa_binary", "pack_counts"):
+        wrap(ops, n, "ops." + n)
+    wrap(ps.dedup, "route", "dedup.route")
+    wrap(ps.dedup, "run", "dedup.run")
+    return acc
 
 
 if __name__ == "__main__":
