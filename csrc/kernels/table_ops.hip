@@ -863,6 +863,9 @@ __global__ void segment_fill_kernel(const T* __restrict__ src, int64_t k, int64_
     while (__builtin_amdgcn_s_memrealtime() - t0 < min_ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// workgroups of a fill that also times a link (A/B knob fps_segment_fill_set_link_wgs)
+int g_fill_link_wgs = 256;
+
 template <typename T>
 void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* out, const SegOffsets& so, int nseg,
                          hipStream_t st, uint64_t min_ticks) {
@@ -873,11 +876,13 @@ void segment_fill_launch(const void* src, int64_t k, int64_t row_bytes, void* ou
   const int64_t waves = (rows + (64 >> sh) - 1) / (64 >> sh);
   // a modelled link transfer (min_ticks > 0) writes with at most one workgroup per CU, as
   // RCCL's copy kernels occupy a few CUs, not the whole GPU beside the compute
-  const int max_blocks = min_ticks > 0 ? 256 : 256 * 16;
+  const int max_blocks = min_ticks > 0 ? g_fill_link_wgs : 256 * 16;
   hipLaunchKernelGGL(segment_fill_kernel<T>, dim3(grid_for(waves, 4, max_blocks)), dim3(256), 0, st, (const T*)src,
                      k, wpr, (T*)out, so, nseg, sh, min_ticks);
 }
 }  // namespace
+
+FPS_API void fps_segment_fill_set_link_wgs(int v) { g_fill_link_wgs = v > 0 ? v : 256; }
 
 // rows[nseg]: rows of each output segment (host array); src: k rows of row_bytes;
 // min_us > 0: the kernel lasts at least that long (see segment_fill_kernel)

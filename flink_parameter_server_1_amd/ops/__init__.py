@@ -114,6 +114,9 @@ def pack_counts(counts: torch.Tensor, W: int, request: bool, flag: int) -> torch
     return torch.cat([c, torch.full((W, 1), int(flag), dtype=torch.int32, device=counts.device)], dim=1)
 
 
+_FILL_KNOB = False
+
+
 def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0, stream=None) -> None:
     """``out`` = the concatenation over ``j`` of ``src``'s first ``rows[j]`` rows, ``src``
     tiled where ``rows[j] > len(src)`` (row ``i`` of segment ``j`` is ``src[i % len(src)]``):
@@ -134,6 +137,11 @@ def segment_fill(src: torch.Tensor, rows, out: torch.Tensor, min_us: float = 0.0
     if _on_gpu(src):
         import ctypes
 
+        global _FILL_KNOB
+        if not _FILL_KNOB:  # A/B: FPS_FILL_LINK_WGS = workgroups of a link-timed fill (default 256)
+            _FILL_KNOB = True
+            if os.environ.get("FPS_FILL_LINK_WGS"):
+                N.require().fps_segment_fill_set_link_wgs(int(os.environ["FPS_FILL_LINK_WGS"]))
         if len(rows) > 64:
             raise ValueError(f"segment_fill: {len(rows)} segments, the kernel takes <= 64")
         _c(src), _c(out)

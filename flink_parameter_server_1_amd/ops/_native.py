@@ -33,6 +33,7 @@ _SIGNATURES = {
     "fps_init_rows": [c_vp, c_i64, c_int, c_i64, c_i64, c_f32, c_f32, c_u32, c_vp],
     "fps_mark_rows": [c_vp, c_vp, c_i64, c_vp],
     "fps_pack_counts": [c_vp, c_int, c_int, c_int, c_vp, c_vp],
+    "fps_segment_fill_set_link_wgs": [c_int],
     "fps_static_plan": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_flip_masked": [c_vp, c_vp, c_i64, c_int, c_vp],
     "fps_dedup_flags": [c_vp, c_i64, c_vp, c_vp, c_u32, c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
