@@ -136,6 +136,7 @@ def main(argv=None):
                        "owner_stream": m.pipe.owner is not None, "interleaved": m.pipe.interleave,
                        "optimizer": a.optimizer, "wire_dtype": wire, "partition": "range", "zipf": a.zipf},
         }), flush=True)
+    comm.shutdown()  # every rank leaves the process group together
 
 
 if __name__ == "__main__":

@@ -114,6 +114,7 @@ def main(argv=None):
                        "seed_items": LempTopK.seed_items, "max_segment": LempTopK.max_segment,
                        "fused": not a.unfused, "fixed_plans": bool(a.capacity) and comm.world > 1},
         }), flush=True)
+    comm.shutdown()  # every rank leaves the process group together
 
 
 if __name__ == "__main__":

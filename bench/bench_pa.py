@@ -181,6 +181,7 @@ def main(argv=None):
                        "exchange": "local-direct" if m._direct else "ps", "staleness": m.cfg.staleness,
                        "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1)},
         }), flush=True)
+    comm.shutdown()  # every rank leaves the process group together
 
 
 def _wrap_stages(m, comm):

@@ -115,6 +115,7 @@ def main(argv=None):
             "config": {"items": a.items, "dim": a.dim, "k": a.k, "query_batch": a.queries, "bucket": a.bucket,
                        "strategy": a.strategy},
         }), flush=True)
+    comm.shutdown()  # every rank leaves the process group together
 
 
 if __name__ == "__main__":

@@ -149,6 +149,7 @@ def main(argv=None):
                        "fused_local_push": (not m._direct and m.cfg.fuse_local_push and comm.world == 1),
                        "pairs_per_gpu_step": a.pairs, "wire_dtype": a.wire},
         }), flush=True)
+    comm.shutdown()  # every rank leaves the process group together
 
 
 if __name__ == "__main__":

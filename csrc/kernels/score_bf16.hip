@@ -87,7 +87,7 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 // q_f / |q|; cb: [N / 32][D] coordinate ranges); stats[0] / [1] count the (query
 // block, item block) pairs scored / skipped by the coordinate bound (pairs the length
 // bound skips by itself are in neither).
-template <int D, int QB, bool MASK = false, bool COORD = false, bool ILV = false>
+template <int D, int QB, bool MASK = false, bool COORD = false, bool ILV = false, int PD = 1>
 __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xbm,
@@ -184,20 +184,24 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
   static_assert(ST * CPR % 256 == 0, "stage chunks must divide over the workgroup");
   __shared__ __attribute__((aligned(16))) unsigned char xs[2][ST * ROWB];
   const uint4* __restrict__ X16 = reinterpret_cast<const uint4*>(Xb);
-  uint4 ldv[LPT];
-  auto gload = [&](int s0) {
+  // PD = prefetch distance in stages: 1 = the next stage's rows are loaded during this
+  // stage's MFMAs (one register set); 2 = two register sets, the rows of stage st + 2
+  // are issued at the start of stage st and stored to LDS at the end of stage st + 1 --
+  // a stage (~16 MFMAs per wave) is shorter than an L2-miss round trip
+  uint4 ldA[LPT], ldB[LPT];
+  auto gload = [&](int s0, uint4 (&dst)[LPT]) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
       const int c = tid + 256 * u, row = c / CPR, col = c % CPR;
       const int i = s0 + row;
-      ldv[u] = i < i_end ? X16[(int64_t)i * CPR + col] : make_uint4(0, 0, 0, 0);
+      dst[u] = i < i_end ? X16[(int64_t)i * CPR + col] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const uint4 (&src)[LPT]) {
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
       const int c = tid + 256 * u, row = c / CPR, col = c % CPR;
-      *reinterpret_cast<uint4*>(&xs[buf][row * ROWB + col * 16]) = ldv[u];
+      *reinterpret_cast<uint4*>(&xs[buf][row * ROWB + col * 16]) = src[u];
     }
   };
   // the longest item of each of a stage's two blocks and (COORD) their coordinate
@@ -216,12 +220,15 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
       }
     }
   };
-  gload(i_begin);
+  gload(i_begin, ldA);
   cload(i_begin, cbn);
-  lstore(0);
+  if (PD == 2 && i_begin + ST < i_end) gload(i_begin + ST, ldB);
+  lstore(0, ldA);
   __syncthreads();
-  for (int s0 = i_begin, st = 0; s0 < i_end; s0 += ST, ++st) {
-    const int buf = st & 1;
+  // one stage: the MFMAs over LDS buffer `buf` (items s0 .. s0 + ST); nxt = the register
+  // set that receives (PD = 1) or already holds (PD = 2) stage s0 + ST, far (PD = 2) the
+  // free set that receives stage s0 + 2 ST
+  auto stage = [&](const int s0, const int buf, uint4 (&nxt)[LPT], uint4 (&far)[LPT]) {
     const bool more = s0 + ST < i_end;
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) bms[bi] = bmn[bi];
@@ -231,9 +238,11 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
 #pragma unroll
         for (int b = 0; b < QB; ++b) cbs[bi][b] = cbn[bi][b];
     }
-    if (more) {  // the next stage's rows are in flight during this stage's MFMAs
-      gload(s0 + ST);
-      cload(s0 + ST, cbn);
+    if (more) cload(s0 + ST, cbn);  // block bounds first: the next stage waits for them only
+    if (PD == 1) {
+      if (more) gload(s0 + ST, nxt);  // the next stage's rows are in flight during this stage's MFMAs
+    } else if (s0 + 2 * ST < i_end) {
+      gload(s0 + 2 * ST, far);
     }
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) {
@@ -342,8 +351,16 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
           if (lv[b]) filter(b, mfma_block(b));
       }
     }
-    if (more) lstore(buf ^ 1);  // every wave finished reading buf ^ 1 at the previous barrier
+    if (more) lstore(buf ^ 1, nxt);  // every wave finished reading buf ^ 1 at the previous barrier
     __syncthreads();
+  };
+  if (PD == 1) {
+    for (int s0 = i_begin, st = 0; s0 < i_end; s0 += ST, ++st) stage(s0, st & 1, ldA, ldB);
+  } else {
+    for (int s0 = i_begin; s0 < i_end; s0 += 2 * ST) {  // the register sets alternate: unrolled by 2
+      stage(s0, 0, ldB, ldA);
+      if (s0 + ST < i_end) stage(s0 + ST, 1, ldA, ldB);
+    }
   }
   if (COORD && use_coord && stats != nullptr && lane == 0) {
     atomicAdd(stats, scored);
@@ -464,6 +481,12 @@ FPS_API void fps_score_set_min_wgs(int v) { g_sb_min_wgs = v; }
 // 8 more VGPRs, so off
 static int g_sb_ilv = 0;
 FPS_API void fps_score_set_ilv(int v) { g_sb_ilv = v; }
+// prefetch distance of the LDS item stages (PD above; A/B knob FPS_SB_PD): 1 or 2
+#ifndef FPS_SB_PD_DEFAULT
+#define FPS_SB_PD_DEFAULT 1
+#endif
+static int g_sb_pd = FPS_SB_PD_DEFAULT;
+FPS_API void fps_score_set_pd(int v) { g_sb_pd = v == 2 ? 2 : 1; }
 
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xbm, float margin, float slack,
@@ -489,12 +512,20 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true, true>), grid, dim3(256), 0, s, Qb, \
                          Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb,     \
                          stats, gate, ipw);                                                                 \
+    else if (coord && g_sb_pd == 2)                                                                         \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true, false, 2>), grid, dim3(256), 0, s,  \
+                         Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
+                         stats, gate, ipw);                                                                 \
     else if (coord)                                                                                         \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, true, false>), grid, dim3(256), 0, s, Qb,\
                          Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb,     \
                          stats, gate, ipw);                                                                 \
     else if (g_sb_ilv)                                                                                      \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, true>), grid, dim3(256), 0, s,    \
+                         Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
+                         stats, gate, ipw);                                                                 \
+    else if (g_sb_pd == 2)                                                                                  \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, false, 2>), grid, dim3(256), 0, s,\
                          Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
                          stats, gate, ipw);                                                                 \
     else                                                                                                    \

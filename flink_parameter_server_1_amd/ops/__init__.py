@@ -1159,12 +1159,15 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     slack = 1.0 + 1e-4 + D * 2.4e-7
     global _SB_KNOBS
     if not _SB_KNOBS:  # A/B switches, read once: FPS_SB_MIN_WGS = fewest workgroups per scorer launch (0: 1024
-        _SB_KNOBS = True  # items each); FPS_SB_ILV=1: interleaved MFMA chains of the query blocks
-        mw, ilv = os.environ.get("FPS_SB_MIN_WGS"), os.environ.get("FPS_SB_ILV")
+        _SB_KNOBS = True  # items each); FPS_SB_ILV=1: interleaved MFMA chains of the query blocks;
+        # FPS_SB_PD = 1 / 2: prefetch distance of the LDS item stages
+        mw, ilv, pd = os.environ.get("FPS_SB_MIN_WGS"), os.environ.get("FPS_SB_ILV"), os.environ.get("FPS_SB_PD")
         if mw is not None:
             N.require().fps_score_set_min_wgs(int(mw))
         if ilv is not None:
             N.require().fps_score_set_ilv(int(ilv))
+        if pd is not None:
+            N.require().fps_score_set_pd(int(pd))
     N.check(N.require().fps_score_filter_bf16(
         _c(Qb).data_ptr(), _c(Xb).data_ptr(), B, n, D, _c(best_s).data_ptr(), best_s.shape[1],
         _c(qlen.float()).data_ptr(), _c(xbm.float()).data_ptr(), bf16_score_margin(D), slack,

@@ -218,3 +218,12 @@ class Comm:
         t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, group=self.group)
         return float(t.item())
+
+    def shutdown(self) -> None:
+        """End of a job: every rank reaches a barrier, then the default process group
+        is destroyed.  A rank that leaves while a peer still holds the group open
+        tears the backend down under it (gloo aborted a rank with
+        ``terminate called without an active exception`` at interpreter exit)."""
+        if self.world > 1 and dist.is_initialized():
+            self.barrier()
+            dist.destroy_process_group()
