@@ -32,7 +32,8 @@ def _entry(rank, world, port, fn, args, out_dir):
         res, err = None, traceback.format_exc()
     with open(os.path.join(out_dir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump((res, err), f)
-    dist.destroy_process_group()
+    if dist.is_initialized():  # fn may have left the group itself (Comm.shutdown)
+        dist.destroy_process_group()
 
 
 def run_ranks(fn, world, *args):
