@@ -559,6 +559,93 @@ __global__ void __launch_bounds__(RP_NT) round_plan_kernel(const int64_t* __rest
   }
 }
 
+// The plan of a batch of <= RPS_N users in ONE launch: the stable sort by user is a
+// bitonic sort of (user, entry) pairs in LDS (the pair order makes it stable), then the
+// run scans of round_plan_kernel over the sorted LDS copy.  The torch sort it replaces
+// (radixSortKVInPlace, one block per row) ran 41 us for 4096 int64 keys, and the
+// kernel above another 15 us reading the sorted keys back from memory
+// (profiles/r6_mf_topk_batch_timeline.md).
+constexpr int RPS_N = 4096;
+
+__global__ void __launch_bounds__(RP_NT) round_plan_small_kernel(const int64_t* __restrict__ users, int B,
+                                                                 int64_t* __restrict__ by_user,
+                                                                 int32_t* __restrict__ rnd,
+                                                                 int32_t* __restrict__ first,
+                                                                 int32_t* __restrict__ nu) {
+  __shared__ int64_t sk[RPS_N];
+  __shared__ int32_t sv[RPS_N];
+  __shared__ int32_t s_lo[RP_NT], s_hi[RP_NT];
+  const int t = threadIdx.x;
+  int n2 = 64;
+  while (n2 < B) n2 <<= 1;
+  for (int i = t; i < n2; i += RP_NT) {  // padding sorts last: (INT64_MAX, entry >= B)
+    sk[i] = i < B ? users[i] : INT64_MAX;
+    sv[i] = i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < n2; i += RP_NT) {
+        const int p = i ^ j;
+        if (p > i) {
+          const int64_t ka = sk[i], kb = sk[p];
+          const int32_t va = sv[i], vb = sv[p];
+          const bool gt = ka > kb || (ka == kb && va > vb);
+          if (gt == ((i & k) == 0)) {  // ascending where bit k of i is clear
+            sk[i] = kb; sk[p] = ka;
+            sv[i] = vb; sv[p] = va;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // runs of equal users over the sorted entries: each thread a contiguous chunk, the run
+  // start carried in by a max-scan from the left, the run end by a min-scan from the right
+  const int C = (B + RP_NT - 1) / RP_NT;
+  const int a = min(B, t * C), b = min(B, a + C);
+  int32_t last_start = -1, first_end = INT32_MAX;
+  for (int i = a; i < b; ++i)
+    if (i == 0 || sk[i] != sk[i - 1]) last_start = i;
+  for (int i = b - 1; i >= a; --i)
+    if (i + 1 == B || sk[i + 1] != sk[i]) first_end = i + 1;
+  s_lo[t] = last_start;
+  s_hi[t] = first_end;
+  __syncthreads();
+  for (int o = 1; o < RP_NT; o <<= 1) {
+    const int32_t lo = t >= o ? s_lo[t - o] : -1;
+    const int32_t hi = t + o < RP_NT ? s_hi[t + o] : INT32_MAX;
+    __syncthreads();
+    s_lo[t] = max(s_lo[t], lo);
+    s_hi[t] = min(s_hi[t], hi);
+    __syncthreads();
+  }
+  int32_t start = t > 0 ? s_lo[t - 1] : -1;
+  int32_t end = t + 1 < RP_NT ? s_hi[t + 1] : B;
+  if (end == INT32_MAX) end = B;
+  int32_t st[4];  // C <= RPS_N / RP_NT = 4
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = a + q;
+    if (i < b) {
+      if (i == 0 || sk[i] != sk[i - 1]) start = i;
+      st[q] = start;
+      const int32_t e = sv[i];
+      by_user[i] = e;
+      rnd[e] = i - start;
+      first[e] = start;
+    }
+  }
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    const int i = a + q;
+    if (i < b) {
+      if (i + 1 == B || sk[i + 1] != sk[i]) end = i + 1;
+      nu[sv[i]] = end - st[q];
+    }
+  }
+}
+
 // ---- fresh top-k of a short row: one wave per query (the seed segment of a scan).
 // The block kernel above spent ~100 us on the 4096 x 4096 seed merge (its three radix
 // levels and the bitonic sort each cost a dozen block barriers per row).  With an empty
@@ -751,6 +838,63 @@ FPS_API int fps_round_plan(const int64_t* su, const int64_t* by_user, int B, int
   if (B <= 0) return 0;
   if (B > (1 << 20)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(round_plan_kernel, dim3(1), dim3(RP_NT), 0, (hipStream_t)stream, su, by_user, B, rnd, first, nu);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// users [B] int64 (B <= 4096), unsorted: by_user [B] int64 and the three plans in one launch
+FPS_API int fps_round_plan_small(const int64_t* users, int B, int64_t* by_user, int32_t* rnd, int32_t* first,
+                                 int32_t* nu, void* stream) {
+  if (B <= 0) return 0;
+  if (B > RPS_N) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(round_plan_small_kernel, dim3(1), dim3(RP_NT), 0, (hipStream_t)stream, users, B, by_user, rnd,
+                     first, nu);
+  FPS_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- the per-scan set-up of a fused LEMP scan in ONE launch (topk_fast.LempTopK._scan):
+// |q| per query row, the bf16 copy of Q the filter reads (RNE), the running lists reset
+// (-inf / -1), the candidate counts and the overflow flag zeroed.  Replaces eight small
+// launches inside the scan's graph (square / sum / sqrt, bf16 cast, two fills, two zero
+// fills: ~40 us of a 0.6 ms LEMP batch, profiles/r6_mf_topk_batch_timeline.md).  One
+// wave per query row; the norm's summation order differs from torch's, which the
+// bounds allow (they carry a relative slack).
+namespace {
+__global__ void __launch_bounds__(256) topk_scan_prep_kernel(const float* __restrict__ Q, int B, int D, int k,
+                                                             float* __restrict__ qlen, uint16_t* __restrict__ Qb,
+                                                             float* __restrict__ best_s, int64_t* __restrict__ best_i,
+                                                             int32_t* __restrict__ cnt, int32_t* __restrict__ ovf) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row == 0 && lane == 0 && ovf != nullptr) ovf[0] = 0;
+  if (row >= B) return;
+  const float* q = Q + (int64_t)row * D;
+  float ss = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float v = q[d];
+    ss += v * v;
+    if (Qb != nullptr) Qb[(int64_t)row * D + d] = f32_to_bf16(v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (lane == 0) {
+    qlen[row] = sqrtf(ss);
+    if (cnt != nullptr) cnt[row] = 0;
+  }
+  for (int i = lane; i < k; i += 64) {
+    best_s[(int64_t)row * k + i] = -INFINITY;
+    best_i[(int64_t)row * k + i] = -1;
+  }
+}
+}  // namespace
+
+FPS_API int fps_topk_scan_prep(const float* Q, int B, int D, int k, float* qlen, uint16_t* Qb, float* best_s,
+                               int64_t* best_i, int32_t* cnt, int32_t* ovf, void* stream) {
+  if (B <= 0) return 0;
+  if (D <= 0 || k <= 0 || qlen == nullptr || best_s == nullptr || best_i == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_scan_prep_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, Q, B, D, k, qlen, Qb,
+                     best_s, best_i, cnt, ovf);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -329,7 +329,7 @@ class LempTopK:
         gc.disable()  # a collection on this thread inside the capture could free a pinned buffer / event
         try:
             with torch.cuda.graph(graph):
-                best_s, best_i, ovf = self._scan(q_in, _row_norms(q_in), k, capturing=True)[:3]
+                best_s, best_i, ovf = self._scan(q_in, None, k, capturing=True)[:3]
         except RuntimeError as e:  # a launch that cannot be captured: stay eager for this index
             import warnings
 
@@ -372,7 +372,19 @@ class LempTopK:
         runs from ``start`` to the next 32-item boundary, or is skipped)."""
         B, dev = Q.shape[0], Q.device
         N = self.vecs.shape[0]
-        if state is None:
+        # a fresh GPU scan's set-up (norms, bf16 queries, running lists, counts, flag) in
+        # one launch instead of eight (ops.topk_scan_prep)
+        prep = None
+        if state is None and Q.is_cuda and Q.dtype == torch.float32 and k <= ops.TOPK_MAX_K:
+            prep = ops.topk_scan_prep(Q, k, bf16=self.bf16)
+            if qlen is None:
+                qlen = prep[0]
+        elif qlen is None:
+            qlen = _row_norms(Q)
+        if prep is not None:
+            best_s, best_i = prep[2], prep[3]
+            seed = self.seed_items
+        elif state is None:
             best_s = torch.full((B, k), float("-inf"), device=dev)
             best_i = torch.full((B, k), -1, dtype=torch.long, device=dev)
             seed = self.seed_items
@@ -408,9 +420,12 @@ class LempTopK:
         cap = ops.TOPK_CAND_CAP
         ck = torch.empty((B, cap), dtype=torch.int32, device=dev)
         ci = torch.empty((B, cap), dtype=torch.long, device=dev)
-        cnt = torch.empty(B, dtype=torch.int32, device=dev)
-        ovf = torch.zeros(1, dtype=torch.int32, device=dev)
-        Qb = Q.bfloat16() if self.bf16 else None
+        if prep is not None:  # counts and flag zeroed, bf16 queries written by the set-up launch
+            Qb, cnt, ovf = prep[1], prep[4], prep[5]
+        else:
+            cnt = torch.empty(B, dtype=torch.int32, device=dev)
+            ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+            Qb = Q.bfloat16() if self.bf16 else None
         # the longest item of every 32-item block (the scorer's per-block length bound),
         # recomputed per scan: update_rows / refresh_from change the lengths in place
         xbm = ops.block_max32(self.lengths) if self.bf16 else None
@@ -419,7 +434,8 @@ class LempTopK:
             self._coord_gate.fill_(1)
             self._coord_prev.copy_(self.coord_stats)
             stats0 = self.coord_stats.clone()
-        cnt.zero_()  # then zeroed by each segment's merge (reset_cnt)
+        if prep is None:
+            cnt.zero_()  # then zeroed by each segment's merge (reset_cnt)
         for j, (s, e) in enumerate(zip(bounds[:-1], bounds[1:])):
             if self.break_check and j and j % self.break_check == 0 and not capturing and \
                     bool((qlen * self._bound(s) <= best_s[:, -1]).all()):

@@ -1110,6 +1110,28 @@ def coord_block_bounds(X: torch.Tensor, xlen: torch.Tensor) -> torch.Tensor:
     return torch.stack([xn.amin(1), xn.amax(1)], 2).contiguous()
 
 
+def topk_scan_prep(Q: torch.Tensor, k: int, bf16: bool = True):
+    """The set-up of a fresh fused top-K scan in ONE launch (``topk.hip``
+    ``topk_scan_prep_kernel``): ``(qlen [B] fp32 row norms, Qb [B, D] bf16 (RNE) or None,
+    best_s [B, k] = -inf, best_i [B, k] = -1, cnt [B] int32 = 0, ovf [1] int32 = 0)``."""
+    Q = _c(Q.float())
+    B, D = Q.shape
+    dev = Q.device
+    if not Q.is_cuda or k <= 0 or k > TOPK_MAX_K:
+        raise ValueError("topk_scan_prep: a cuda [B, D] query batch and 0 < k <= TOPK_MAX_K")
+    qlen = torch.empty(B, dtype=torch.float32, device=dev)
+    Qb = torch.empty((B, D), dtype=torch.bfloat16, device=dev) if bf16 else None
+    best_s = torch.empty((B, k), dtype=torch.float32, device=dev)
+    best_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cnt = torch.empty(B, dtype=torch.int32, device=dev)
+    ovf = torch.empty(1, dtype=torch.int32, device=dev)
+    N.check(N.require().fps_topk_scan_prep(Q.data_ptr(), B, D, k, qlen.data_ptr(),
+                                           Qb.data_ptr() if Qb is not None else None, best_s.data_ptr(),
+                                           best_i.data_ptr(), cnt.data_ptr(), ovf.data_ptr(),
+                                           N.stream_ptr(dev)), "topk_scan_prep")
+    return qlen, Qb, best_s, best_i, cnt, ovf
+
+
 def block_max32(xlen: torch.Tensor) -> torch.Tensor:
     """``[ceil(n / 32)]`` max of every 32 consecutive entries (the last block over its own)."""
     n = xlen.numel()
@@ -1260,6 +1282,10 @@ def index_refresh(rows: torch.Tensor, pos: torch.Tensor, W: torch.Tensor, vecs: 
                                           N.stream_ptr(W.device)), "index_refresh")
 
 
+#: batches up to this size are planned by ONE kernel (topk.hip round_plan_small_kernel)
+ROUND_PLAN_SMALL = 4096
+
+
 def round_plan(users: torch.Tensor):
     """``(by_user, rnd, first, nu)`` of a batch of users (GPU, one launch after the sort,
     ``topk.hip`` ``round_plan_kernel``): ``by_user`` = entries stably sorted by user,
@@ -1268,10 +1294,16 @@ def round_plan(users: torch.Tensor):
     B = users.numel()
     if not users.is_cuda or B > (1 << 20):
         raise ValueError("round_plan: a cuda tensor of at most 2^20 users")
-    su, by_user = torch.sort(users.long(), stable=True)
     rnd = torch.empty(B, dtype=torch.int32, device=users.device)
     first = torch.empty_like(rnd)
     nu = torch.empty_like(rnd)
+    if B <= ROUND_PLAN_SMALL:  # sort + plan in one launch (LDS bitonic sort of (user, entry) pairs)
+        by_user = torch.empty(B, dtype=torch.int64, device=users.device)
+        N.check(N.require().fps_round_plan_small(_c(users.long()).data_ptr(), B, by_user.data_ptr(), rnd.data_ptr(),
+                                                 first.data_ptr(), nu.data_ptr(), N.stream_ptr(users.device)),
+                "round_plan_small")
+        return by_user, rnd, first, nu
+    su, by_user = torch.sort(users.long(), stable=True)
     N.check(N.require().fps_round_plan(su.data_ptr(), by_user.data_ptr(), B, rnd.data_ptr(), first.data_ptr(),
                                        nu.data_ptr(), N.stream_ptr(users.device)), "round_plan")
     return by_user, rnd, first, nu

@@ -321,3 +321,20 @@ def test_pruned_lemp_gpu_equals_reference_semantics(strategy):
     sb, ib, _ = b._mask_scan(Q.float().contiguous(), k, settle=False)
     torch.testing.assert_close(sa, sb, rtol=0, atol=0)
     assert torch.equal(ia, ib)
+
+
+@pytest.mark.parametrize("B,D,k", [(1, 64, 1), (4096, 64, 100), (1000, 32, 75), (77, 128, 256)])
+def test_topk_scan_prep_matches_torch(B, D, k):
+    """The one-launch scan set-up == the torch ops it replaces: norms (summation order
+    free: close), the bf16 queries bit-equal to ``Q.bfloat16()``, -inf / -1 running
+    lists, zero counts and flag."""
+    g = torch.Generator(device="cuda").manual_seed(B + D)
+    Q = torch.randn(B, D, device="cuda", generator=g)
+    qlen, Qb, best_s, best_i, cnt, ovf = ops.topk_scan_prep(Q, k)
+    torch.testing.assert_close(qlen, Q.square().sum(1).sqrt(), rtol=2e-6, atol=0)
+    assert torch.equal(Qb.view(torch.int16), Q.bfloat16().view(torch.int16))
+    assert bool((best_s == float("-inf")).all()) and best_s.shape == (B, k)
+    assert bool((best_i == -1).all()) and best_i.dtype == torch.int64
+    assert int(cnt.abs().sum()) == 0 and int(ovf[0]) == 0
+    qlen2, Qb2 = ops.topk_scan_prep(Q, k, bf16=False)[:2]
+    assert Qb2 is None and torch.equal(qlen2, qlen)

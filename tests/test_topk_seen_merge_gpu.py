@@ -162,7 +162,7 @@ def test_online_learner_and_generator_gpu_matches_per_record():
         np.testing.assert_allclose([x[0] for x in lst], [x[0] for x in rlst], rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("B", [1, 5, 1000, 4096, 70_000])
+@pytest.mark.parametrize("B", [1, 5, 64, 1000, 3000, 4096, 4097, 70_000])
 def test_round_plan_kernel_equals_torch_plan(B):
     """``ops.round_plan`` (one workgroup after the sort) == the torch form of the fused
     RoundPlan, including long runs across thread chunks."""
