@@ -559,93 +559,6 @@ __global__ void __launch_bounds__(RP_NT) round_plan_kernel(const int64_t* __rest
   }
 }
 
-// The plan of a batch of <= RPS_N users in ONE launch: the stable sort by user is a
-// bitonic sort of (user, entry) pairs in LDS (the pair order makes it stable), then the
-// run scans of round_plan_kernel over the sorted LDS copy.  The torch sort it replaces
-// (radixSortKVInPlace, one block per row) ran 41 us for 4096 int64 keys, and the
-// kernel above another 15 us reading the sorted keys back from memory
-// (profiles/r6_mf_topk_batch_timeline.md).
-constexpr int RPS_N = 4096;
-
-__global__ void __launch_bounds__(RP_NT) round_plan_small_kernel(const int64_t* __restrict__ users, int B,
-                                                                 int64_t* __restrict__ by_user,
-                                                                 int32_t* __restrict__ rnd,
-                                                                 int32_t* __restrict__ first,
-                                                                 int32_t* __restrict__ nu) {
-  __shared__ int64_t sk[RPS_N];
-  __shared__ int32_t sv[RPS_N];
-  __shared__ int32_t s_lo[RP_NT], s_hi[RP_NT];
-  const int t = threadIdx.x;
-  int n2 = 64;
-  while (n2 < B) n2 <<= 1;
-  for (int i = t; i < n2; i += RP_NT) {  // padding sorts last: (INT64_MAX, entry >= B)
-    sk[i] = i < B ? users[i] : INT64_MAX;
-    sv[i] = i;
-  }
-  __syncthreads();
-  for (int k = 2; k <= n2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < n2; i += RP_NT) {
-        const int p = i ^ j;
-        if (p > i) {
-          const int64_t ka = sk[i], kb = sk[p];
-          const int32_t va = sv[i], vb = sv[p];
-          const bool gt = ka > kb || (ka == kb && va > vb);
-          if (gt == ((i & k) == 0)) {  // ascending where bit k of i is clear
-            sk[i] = kb; sk[p] = ka;
-            sv[i] = vb; sv[p] = va;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // runs of equal users over the sorted entries: each thread a contiguous chunk, the run
-  // start carried in by a max-scan from the left, the run end by a min-scan from the right
-  const int C = (B + RP_NT - 1) / RP_NT;
-  const int a = min(B, t * C), b = min(B, a + C);
-  int32_t last_start = -1, first_end = INT32_MAX;
-  for (int i = a; i < b; ++i)
-    if (i == 0 || sk[i] != sk[i - 1]) last_start = i;
-  for (int i = b - 1; i >= a; --i)
-    if (i + 1 == B || sk[i + 1] != sk[i]) first_end = i + 1;
-  s_lo[t] = last_start;
-  s_hi[t] = first_end;
-  __syncthreads();
-  for (int o = 1; o < RP_NT; o <<= 1) {
-    const int32_t lo = t >= o ? s_lo[t - o] : -1;
-    const int32_t hi = t + o < RP_NT ? s_hi[t + o] : INT32_MAX;
-    __syncthreads();
-    s_lo[t] = max(s_lo[t], lo);
-    s_hi[t] = min(s_hi[t], hi);
-    __syncthreads();
-  }
-  int32_t start = t > 0 ? s_lo[t - 1] : -1;
-  int32_t end = t + 1 < RP_NT ? s_hi[t + 1] : B;
-  if (end == INT32_MAX) end = B;
-  int32_t st[4];  // C <= RPS_N / RP_NT = 4
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int i = a + q;
-    if (i < b) {
-      if (i == 0 || sk[i] != sk[i - 1]) start = i;
-      st[q] = start;
-      const int32_t e = sv[i];
-      by_user[i] = e;
-      rnd[e] = i - start;
-      first[e] = start;
-    }
-  }
-#pragma unroll
-  for (int q = 3; q >= 0; --q) {
-    const int i = a + q;
-    if (i < b) {
-      if (i + 1 == B || sk[i + 1] != sk[i]) end = i + 1;
-      nu[sv[i]] = end - st[q];
-    }
-  }
-}
-
 // ---- fresh top-k of a short row: one wave per query (the seed segment of a scan).
 // The block kernel above spent ~100 us on the 4096 x 4096 seed merge (its three radix
 // levels and the bitonic sort each cost a dozen block barriers per row).  With an empty
@@ -838,17 +751,6 @@ FPS_API int fps_round_plan(const int64_t* su, const int64_t* by_user, int B, int
   if (B <= 0) return 0;
   if (B > (1 << 20)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(round_plan_kernel, dim3(1), dim3(RP_NT), 0, (hipStream_t)stream, su, by_user, B, rnd, first, nu);
-  FPS_CHECK_LAUNCH();
-  return 0;
-}
-
-// users [B] int64 (B <= 4096), unsorted: by_user [B] int64 and the three plans in one launch
-FPS_API int fps_round_plan_small(const int64_t* users, int B, int64_t* by_user, int32_t* rnd, int32_t* first,
-                                 int32_t* nu, void* stream) {
-  if (B <= 0) return 0;
-  if (B > RPS_N) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(round_plan_small_kernel, dim3(1), dim3(RP_NT), 0, (hipStream_t)stream, users, B, by_user, rnd,
-                     first, nu);
   FPS_CHECK_LAUNCH();
   return 0;
 }

@@ -1282,10 +1282,6 @@ def index_refresh(rows: torch.Tensor, pos: torch.Tensor, W: torch.Tensor, vecs: 
                                           N.stream_ptr(W.device)), "index_refresh")
 
 
-#: batches up to this size are planned by ONE kernel (topk.hip round_plan_small_kernel)
-ROUND_PLAN_SMALL = 4096
-
-
 def round_plan(users: torch.Tensor):
     """``(by_user, rnd, first, nu)`` of a batch of users (GPU, one launch after the sort,
     ``topk.hip`` ``round_plan_kernel``): ``by_user`` = entries stably sorted by user,
@@ -1297,12 +1293,6 @@ def round_plan(users: torch.Tensor):
     rnd = torch.empty(B, dtype=torch.int32, device=users.device)
     first = torch.empty_like(rnd)
     nu = torch.empty_like(rnd)
-    if B <= ROUND_PLAN_SMALL:  # sort + plan in one launch (LDS bitonic sort of (user, entry) pairs)
-        by_user = torch.empty(B, dtype=torch.int64, device=users.device)
-        N.check(N.require().fps_round_plan_small(_c(users.long()).data_ptr(), B, by_user.data_ptr(), rnd.data_ptr(),
-                                                 first.data_ptr(), nu.data_ptr(), N.stream_ptr(users.device)),
-                "round_plan_small")
-        return by_user, rnd, first, nu
     su, by_user = torch.sort(users.long(), stable=True)
     N.check(N.require().fps_round_plan(su.data_ptr(), by_user.data_ptr(), B, rnd.data_ptr(), first.data_ptr(),
                                        nu.data_ptr(), N.stream_ptr(users.device)), "round_plan")

@@ -63,7 +63,6 @@ _SIGNATURES = {
     "fps_mf_online_phase": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_index_refresh": [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
     "fps_round_plan": [c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
-    "fps_round_plan_small": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_topk_scan_prep": [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "fps_topk_seen_merge": [c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                             c_vp, c_vp, c_vp, c_vp],
