@@ -87,8 +87,8 @@ __device__ __forceinline__ bool coord_pass(float theta, float ql, float bm, floa
 // q_f / |q|; cb: [N / 32][D] coordinate ranges); stats[0] / [1] count the (query
 // block, item block) pairs scored / skipped by the coordinate bound (pairs the length
 // bound skips by itself are in neither).
-template <int D, int QB, bool MASK = false, bool COORD = false, bool ILV = false, int PD = 1>
-__global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
+template <int D, int QB, bool MASK = false, bool COORD = false, bool ILV = false, int PD = 1, bool CUR2 = false>
+__global__ void __launch_bounds__(256, COORD ? 2 : (CUR2 ? 4 : 3)) score_filter_bf16_kernel(
     const uint16_t* __restrict__ Qb, const uint16_t* __restrict__ Xb, int B, int N,
     const float* __restrict__ best_s, int k, const float* __restrict__ qlen, const float* __restrict__ xbm,
     float margin, float slack, int64_t* __restrict__ cand_pos, int32_t* __restrict__ cnt, int cap,
@@ -244,14 +244,30 @@ __global__ void __launch_bounds__(256, COORD ? 2 : 3) score_filter_bf16_kernel(
     } else if (s0 + 2 * ST < i_end) {
       gload(s0 + 2 * ST, far);
     }
+    // CUR2: every block's A operands read from LDS at the start of the stage (the reads of
+    // block bi + 1 in flight during block bi's MFMAs) instead of right before each block
+    uint4 cur_all[CUR2 ? NB : 1][S];
+    if constexpr (CUR2) {
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi) {
+        const unsigned char* rowp = &xs[buf][(32 * bi + r) * ROWB + h * D];
+#pragma unroll
+        for (int s = 0; s < S; ++s) cur_all[bi][s] = *reinterpret_cast<const uint4*>(rowp + 16 * s);
+      }
+    }
 #pragma unroll
     for (int bi = 0; bi < NB; ++bi) {
       const int i0 = s0 + 32 * bi;
       if (i0 >= i_end) break;  // uniform
       uint4 cur[S];
-      const unsigned char* rowp = &xs[buf][(32 * bi + r) * ROWB + h * D];  // half h = bytes [h D, h D + D)
+      if constexpr (CUR2) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) cur[s] = *reinterpret_cast<const uint4*>(rowp + 16 * s);
+        for (int s = 0; s < S; ++s) cur[s] = cur_all[bi][s];
+      } else {
+        const unsigned char* rowp = &xs[buf][(32 * bi + r) * ROWB + h * D];  // half h = bytes [h D, h D + D)
+#pragma unroll
+        for (int s = 0; s < S; ++s) cur[s] = *reinterpret_cast<const uint4*>(rowp + 16 * s);
+      }
       const float bm = bms[bi];  // longest item of this block
       // the passing scores of one (query block, 32-item block) into the block's LDS list
       auto emit = [&](int b, const floatx16& acc, float thr) {
@@ -487,6 +503,9 @@ FPS_API void fps_score_set_ilv(int v) { g_sb_ilv = v; }
 #endif
 static int g_sb_pd = FPS_SB_PD_DEFAULT;
 FPS_API void fps_score_set_pd(int v) { g_sb_pd = v == 2 ? 2 : 1; }
+// every block's LDS operand reads at the start of the stage (CUR2 above; A/B knob FPS_SB_CUR2=1, no COORD)
+static int g_sb_cur2 = 0;
+FPS_API void fps_score_set_cur2(int v) { g_sb_cur2 = v != 0; }
 
 FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B, int N, int D, const float* best_s,
                                   int k, const float* qlen, const float* xbm, float margin, float slack,
@@ -524,6 +543,10 @@ FPS_API int fps_score_filter_bf16(const uint16_t* Qb, const uint16_t* Xb, int B,
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, true>), grid, dim3(256), 0, s,    \
                          Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \
                          stats, gate, ipw);                                                                 \
+    else if (g_sb_cur2)                                                                                     \
+      hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, false, 1, true>), grid, dim3(256), \
+                         0, s, Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf,  \
+                         cb, stats, gate, ipw);                                                             \
     else if (g_sb_pd == 2)                                                                                  \
       hipLaunchKernelGGL((score_filter_bf16_kernel<D_, QB_, MASK_, false, false, 2>), grid, dim3(256), 0, s,\
                          Qb, Xb, B, N, best_s, k, qlen, xbm, margin, slack, cand_pos, cnt, cap, qf, qbf, cb, \

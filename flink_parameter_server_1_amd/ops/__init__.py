@@ -1182,8 +1182,11 @@ def score_filter_bf16(Qb: torch.Tensor, Xb: torch.Tensor, best_s: torch.Tensor, 
     global _SB_KNOBS
     if not _SB_KNOBS:  # A/B switches, read once: FPS_SB_MIN_WGS = fewest workgroups per scorer launch (0: 1024
         _SB_KNOBS = True  # items each); FPS_SB_ILV=1: interleaved MFMA chains of the query blocks;
-        # FPS_SB_PD = 1 / 2: prefetch distance of the LDS item stages
+        # FPS_SB_PD = 1 / 2: prefetch distance of the LDS item stages; FPS_SB_CUR2=1: a stage's LDS operand reads
+        # all issued at its start
         mw, ilv, pd = os.environ.get("FPS_SB_MIN_WGS"), os.environ.get("FPS_SB_ILV"), os.environ.get("FPS_SB_PD")
+        if os.environ.get("FPS_SB_CUR2") is not None:
+            N.require().fps_score_set_cur2(int(os.environ["FPS_SB_CUR2"]))
         if mw is not None:
             N.require().fps_score_set_min_wgs(int(mw))
         if ilv is not None:

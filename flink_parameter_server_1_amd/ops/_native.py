@@ -73,6 +73,7 @@ _SIGNATURES = {
     "fps_score_set_min_wgs": [c_int],
     "fps_score_set_ilv": [c_int],
     "fps_score_set_pd": [c_int],
+    "fps_score_set_cur2": [c_int],
     "fps_coord_gate": [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
     "fps_cand_rescore": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
     "fps_lock_acquire": [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp],
