@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6 session 3: bf16 scorer with every block's LDS operand reads issued at the start of the stage
-# (FPS_SB_CUR2=1; 128 VGPRs, 4 waves / SIMD, 12 B/lane spill) vs the default -- top-K tests under CUR2, same-box A/B.
+# (FPS_SB_CUR2=1; 128 VGPRs, 4 waves / SIMD, 12 B/lane spill) vs the default -- top-K tests under CUR2, same-box A/B;
+# then the whole GPU suite + smoke on this build.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r6s3e
@@ -15,4 +16,9 @@ for r in 1 2; do
     echo "mftopk cur2=$v $r $(tail -1 $O/mftopk_${v}_$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "%.4e" % d["value"])')"
   done
 done
+# the whole GPU suite and the smoke on this (final) build, default knobs
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/suite.log 2>&1 || { grep -E "FAILED|Error" $O/suite.log | head -20; tail -30 $O/suite.log; exit 1; }
+tail -1 $O/suite.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 echo ALLDONE
